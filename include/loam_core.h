@@ -1,0 +1,152 @@
+/*
+ * loam_core.h — C-ABI of the MI355X-native LOAM scan-matching core.
+ *
+ * Drop-in boundary for the hot path of liuzm-slam/VLOAM-NOTED src/lidar_odometry_mapping
+ * (paths below are relative to /root/reference/src/lidar_odometry_mapping/).  Every entry
+ * point cites the reference interface it replaces.  Plain pointers and sizes only; points
+ * are 4 floats (x, y, z, intensity) like pcl::PointXYZI (include/.../common.h:42); poses are
+ * double quaternions in xyzw storage order (para_q / parameters[0..3]) plus xyz translation.
+ *
+ * Threading: a handle is not thread-safe (neither is the reference: static broadcaster at
+ * laser_mapping.cpp:873, static work arrays at scan_registration.h:91-94).  Each handle owns
+ * one HIP stream on its device; calls block until their results are on the host.
+ *
+ * Errors: every function returns LOAM_OK (0) or a negative status.  Degenerate-but-valid
+ * situations the reference only logs (too few map points, laser_mapping.cpp:514-735; fewer
+ * than 10 correspondences, laser_odometry.cpp:493-496) return LOAM_OK and set flags in the
+ * stats structs, reproducing the reference's skip semantics instead of aborting.
+ */
+#ifndef LOAM_CORE_H
+#define LOAM_CORE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LOAM_OK 0
+#define LOAM_ERR_ARG (-1)       /* null handle / pointer, bad index or size */
+#define LOAM_ERR_HIP (-2)       /* HIP runtime error (message: loam_last_error) */
+#define LOAM_ERR_CAPACITY (-3)  /* a device buffer would overflow (see loam_params caps) */
+#define LOAM_ERR_STATE (-4)     /* call out of order (e.g. solve without input) */
+#define LOAM_ERR_NODEVICE (-5)  /* no HIP device / wrong architecture */
+
+/* ROS parameters of loam_velodyne_HDL_64_kitti.launch:3-16 + vloam_main.launch:4, plus
+ * device capacities.  loam_params_default() gives the KITTI launch values. */
+typedef struct loam_params {
+  int32_t scan_line;                /* 64 (scan_registration.cpp:50) */
+  double minimum_range;             /* 5.0 m (scan_registration.cpp:53) */
+  int32_t mapping_skip_frame;       /* 1 (laser_odometry.cpp:53) */
+  int32_t map_pub_number;           /* 20 (laser_mapping.cpp:127) */
+  double mapping_line_resolution;   /* 0.4 m (laser_mapping.cpp:99) */
+  double mapping_plane_resolution;  /* 0.8 m (laser_mapping.cpp:101) */
+  int32_t detach_vo_lo;             /* 1 (laser_odometry.cpp:47) */
+  int32_t verbose_level;            /* loam_verbose_level */
+  /* device capacities (per stream) */
+  int32_t max_input_points;         /* max points per input cloud (default 262144) */
+  int32_t max_map_points;           /* arena capacity per map (corner/surf) (default 4194304) */
+  int32_t max_submap_points;        /* 5x5x3-cube submap capacity per map (default 524288) */
+} loam_params;
+
+void loam_params_default(loam_params* p);
+const char* loam_last_error(void);
+int32_t loam_version(void);
+
+/* --------------------------------------------------------------------------------------
+ * Per-call statistics (the reference's TicToc probes, laser_mapping.cpp:502-811, and the
+ * Ceres summaries it discards).
+ * ------------------------------------------------------------------------------------ */
+typedef struct loam_lm_stats {
+  int32_t iterations;   /* trust-region steps (Ceres summary.iterations.size() - 1) */
+  int32_t successful;   /* accepted steps */
+  int32_t invalid;      /* steps with model_cost_change <= 0 */
+  int32_t termination;  /* 0 max-iter, 1 function tol, 2 parameter tol, 3 gradient tol,
+                           4 no residuals, 5 failure */
+  double initial_cost;
+  double final_cost;
+} loam_lm_stats;
+
+typedef struct loam_map_stats {
+  int32_t optimized;             /* 0: map too small, no optimisation (laser_mapping.cpp:514) */
+  int32_t corner_stack, surf_stack;
+  int32_t corner_map, surf_map;  /* submap sizes (laserCloudCornerFromMapNum, ...) */
+  int32_t corner_num[2], surf_num[2];  /* factors per outer round */
+  loam_lm_stats lm[2];
+  int32_t center[3];             /* centerCubeI/J/K after recentering */
+  int32_t valid_num;             /* laserCloudValidNum */
+  double ms_total;               /* device time of the whole solveMapping */
+  double ms_opt;                 /* device time of the optimisation block (:516-729) */
+} loam_map_stats;
+
+/* --------------------------------------------------------------------------------------
+ * LaserMapping (laser_mapping.h:85-100) — a handle holds n_streams independent mappers
+ * (independent sequences / vehicles) processed together by every launch.  n_streams = 1 is
+ * exactly the reference's single LaserMapping object.
+ * ------------------------------------------------------------------------------------ */
+typedef struct loam_mapper loam_mapper;
+
+/* LaserMapping::LaserMapping + init (laser_mapping.cpp:40-129) */
+int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_streams,
+                           loam_mapper** out);
+int32_t loam_mapper_destroy(loam_mapper* h);
+/* re-init all streams: empty maps, identity poses (laser_mapping.cpp:47-97) */
+int32_t loam_mapper_reset(loam_mapper* h);
+
+/* LaserMapping::input (laser_mapping.cpp:178-209): host clouds, deep-copied to HBM.
+ * corner = laserCloudCornerLast, surf = laserCloudSurfLast (4 floats / point). */
+int32_t loam_mapper_input(loam_mapper* h, int32_t stream, const float* corner, int32_t n_corner,
+                          const float* surf, int32_t n_surf, const double* q_wodom,
+                          const double* t_wodom, int32_t skip_frame);
+/* same, clouds already resident in HBM on the handle's device (device pointers) */
+int32_t loam_mapper_input_device(loam_mapper* h, int32_t stream, const float* d_corner,
+                                 int32_t n_corner, const float* d_surf, int32_t n_surf,
+                                 const double* q_wodom, const double* t_wodom,
+                                 int32_t skip_frame);
+/* LaserMapping::solveMapping (laser_mapping.cpp:212-814) for every stream that received an
+ * input since the last call (skip_frame inputs only update the high-frequency pose). */
+int32_t loam_mapper_solve(loam_mapper* h);
+/* pose after solveMapping: q_w_curr (xyzw), t_w_curr (laser_mapping.cpp:826-832) */
+int32_t loam_mapper_pose(loam_mapper* h, int32_t stream, double* q_w, double* t_w);
+int32_t loam_mapper_stats(loam_mapper* h, int32_t stream, loam_map_stats* st);
+
+/* map state (for teacher-forced parity and for the /laser_cloud_map publisher,
+ * laser_mapping.cpp:884-899).  cube = i + 21*j + 441*k; which: 0 corner, 1 surf. */
+int32_t loam_mapper_get_state(loam_mapper* h, int32_t stream, int32_t* cen,
+                              double* q_wmap_wodom, double* t_wmap_wodom);
+int32_t loam_mapper_set_state(loam_mapper* h, int32_t stream, const int32_t* cen,
+                              const double* q_wmap_wodom, const double* t_wmap_wodom);
+int32_t loam_mapper_cube_count(loam_mapper* h, int32_t stream, int32_t which, int32_t cube);
+int32_t loam_mapper_cube_copy(loam_mapper* h, int32_t stream, int32_t which, int32_t cube,
+                              float* out);
+int32_t loam_mapper_cube_set(loam_mapper* h, int32_t stream, int32_t which, int32_t cube,
+                             const float* pts, int32_t n);
+
+/* --------------------------------------------------------------------------------------
+ * Device LM engine on an explicit factor list (lidarFactor.hpp + Ceres TR-LM).  Factor
+ * record = 10 doubles: type (1 LidarEdgeFactor, 2 LidarPlaneFactor, 3 LidarPlaneNormFactor),
+ * curr_point[3], a[3], b[3] (edge: last_point_a/b; plane: j, unit normal ljm; plane-norm:
+ * unit normal, negative_OA_dot_norm in b[0]).  x = q(xyzw) + t, in/out.
+ * ------------------------------------------------------------------------------------ */
+int32_t loam_lm_solve(int32_t device, const double* factors, int32_t n_factors, double* x,
+                      int32_t max_iterations, loam_lm_stats* st);
+/* cost, J^T J (6x6 row-major) and J^T r of the Huber-corrected residuals at x, in the
+ * 6-dof local space of EigenQuaternionParameterization (unscaled) */
+int32_t loam_lm_normal_equations(int32_t device, const double* factors, int32_t n_factors,
+                                 const double* x, double* cost, double* jtj, double* jtr);
+
+/* --------------------------------------------------------------------------------------
+ * Primitives exposed for parity tests of the kernels behind the stages.
+ * ------------------------------------------------------------------------------------ */
+/* pcl::VoxelGrid<PointXYZI> (leaf metres) on one cloud; returns count in *n_out */
+int32_t loam_voxel_grid(int32_t device, const float* in, int32_t n, float leaf, float* out,
+                        int32_t* n_out);
+/* exact kNN (k <= 8) of queries against pts restricted to d2 < radius2 (1 m cells):
+ * idx/d2 sorted ascending; missing entries idx = -1 */
+int32_t loam_knn_radius(int32_t device, const float* pts, int32_t n, const float* queries,
+                        int32_t nq, int32_t k, float radius2, int32_t* idx, float* d2);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LOAM_CORE_H */

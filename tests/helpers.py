@@ -1,0 +1,57 @@
+"""Shared test helpers: synthetic sequences run through the CPU oracle, teacher-forcing
+snapshots of the oracle mapper, pose-difference metrics."""
+import numpy as np
+
+import loam_oracle as O
+from loam_amd import synth
+
+N_CUBES = 21 * 21 * 11
+
+
+def quat_angle(q1, q2):
+    """rotation angle (rad) of q1^-1 q2 (xyzw)"""
+    q1 = np.asarray(q1, dtype=np.float64)
+    q2 = np.asarray(q2, dtype=np.float64)
+    d = abs(float(np.dot(q1, q2))) / (np.linalg.norm(q1) * np.linalg.norm(q2))
+    return 2.0 * np.arccos(min(1.0, d))
+
+
+def snapshot(mp):
+    cen, q, t = mp.get_state()
+    return dict(cen=cen.copy(), q=q.copy(), t=t.copy(), corner=mp.cubes(0), surf=mp.cubes(1))
+
+
+def run_sequence(seed, n_frames, n_az=2000, snapshot_frames=(), keep_features=True):
+    """Oracle pipeline (scan registration -> odometry -> mapping) over a synthetic sequence.
+    For frames in snapshot_frames, the mapper state BEFORE solveMapping is recorded."""
+    sr, od, mp = O.ScanRegistration(), O.LaserOdometry(), O.LaserMapping()
+    frames = []
+    for f in range(n_frames):
+        xyz, gt = synth.frame(seed, f, n_az)
+        sr.input(xyz)
+        od.input(*sr.output())
+        od.solve()
+        q, t, _, _, _ = od.output()
+        corner, surf = od.cloud(0), od.cloud(1)
+        rec = dict(frame=f, q_wodom=q, t_wodom=t, gt=gt)
+        if keep_features:
+            rec.update(corner=corner, surf=surf)
+        if f in snapshot_frames:
+            rec["before"] = snapshot(mp)
+        mp.input(corner, surf, None, q, t)
+        mp.solve()
+        rec["pose"] = mp.pose()
+        rec["stats"] = mp.stats()
+        if f in snapshot_frames:
+            rec["after"] = snapshot(mp)
+            rec["factors"] = [mp.factors(0), mp.factors(1)]
+            rec["round_pose"] = [mp.round_pose(0), mp.round_pose(1)]
+        frames.append(rec)
+    return frames
+
+
+def load_state(mapper, stream, snap):
+    mapper.set_state(stream, snap["cen"], snap["q"], snap["t"])
+    for which, key in ((0, "corner"), (1, "surf")):
+        for cube, pts in snap[key].items():
+            mapper.set_cube(stream, which, cube, pts)

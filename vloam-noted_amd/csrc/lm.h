@@ -1,0 +1,409 @@
+// lm.h — device Levenberg-Marquardt engine for the 6-dof LiDAR pose problem.
+//
+// Residual blocks (lidarFactor.hpp):
+//   type 1 LidarEdgeFactor (3 rows)       r = (p' - a) x e,   e = (a - b)/|a - b|
+//            (== ((p'-a) x (p'-b))/|a-b| of lidarFactor.hpp:41-46, rearranged)
+//   type 2 LidarPlaneFactor (1 row)       r = (p' - j) . n    (lidarFactor.hpp:95)
+//   type 3 LidarPlaneNormFactor (1 row)   r = n . p' + d      (lidarFactor.hpp:130)
+// with p' = R(q) p + t (s = 1: DISTORTION = false, laser_odometry.h:90), analytic Jacobians in
+// the local space of EigenQuaternionParameterization: dp'/d(dtheta) = -2 [R p]_x, dp'/dt = I.
+// HuberLoss(0.1) + Ceres Corrector (rho'' <= 0 branch): rows scale by sqrt(rho'), so the
+// normal equations accumulate rho' J^T J and rho' J^T r, cost 1/2 sum rho(|r|^2).
+//
+// Solver: Ceres 2.0 TrustRegionMinimizer + LevenbergMarquardtStrategy with the reference's
+// options (laser_mapping.cpp:709-717, laser_odometry.cpp:500-509): radius0 1e4, Jacobi
+// scaling fixed at iteration 0, LM diagonal clamp [1e-6, 1e32], min_relative_decrease 1e-3,
+// function/parameter/gradient tolerances 1e-6/1e-8/1e-10, max 5 consecutive invalid steps,
+// max_num_iterations 4.  Ceres factorises [J_s; D] with Householder QR (DENSE_QR); here the
+// same least-squares step comes from the 6x6 normal equations (Cholesky in fp64), which is
+// what a device reduction produces.  Everything the step needs is a function of
+// (J^T J, J^T r, cost): one fused pass per trust-region iteration evaluates the candidate's
+// cost AND its normal equations (used only if the step is accepted), so an iteration costs
+// exactly one pass over the correspondences.
+#pragma once
+#include "common.h"
+#include "device_math.h"
+
+namespace loam {
+
+constexpr int LM_NACC = 29;  // 21 J^T J (upper, row-major) + 6 J^T r + cost + rows
+
+enum : int { LM_EVAL_X = 0, LM_EVAL_CAND = 1, LM_DONE = 2 };
+
+struct LmState {
+  double x[7], cand[7], best[7];
+  double jtj[21], g[6];
+  double cost, initial_cost, min_cost, mcc;
+  double scaling[6], diag[6];
+  double radius, decrease, x_norm, gmax;
+  int status, iteration, reuse_diag, consec_invalid;
+  int term, successful, invalid, max_iter;
+};
+
+__host__ __device__ inline int ut_index(int r, int c) {  // r <= c, upper triangle of 6x6
+  return r * 6 - (r * (r - 1)) / 2 + (c - r);
+}
+
+__host__ __device__ inline void lm_init(LmState& S, const double* x7, int max_iter, bool active) {
+  for (int i = 0; i < 7; ++i) {
+    S.x[i] = x7[i];
+    S.cand[i] = x7[i];
+    S.best[i] = x7[i];
+  }
+  for (int i = 0; i < 21; ++i) S.jtj[i] = 0;
+  for (int i = 0; i < 6; ++i) {
+    S.g[i] = 0;
+    S.scaling[i] = 1;
+    S.diag[i] = 0;
+  }
+  S.cost = S.initial_cost = S.mcc = 0;
+  S.min_cost = 1.7976931348623157e308;
+  S.radius = 1e4;
+  S.decrease = 2.0;
+  S.x_norm = S.gmax = 0;
+  S.status = active ? LM_EVAL_X : LM_DONE;
+  S.iteration = 0;
+  S.reuse_diag = 0;
+  S.consec_invalid = 0;
+  S.term = active ? 0 : 4;
+  S.successful = 0;
+  S.invalid = 0;
+  S.max_iter = max_iter;
+}
+
+// one residual block at X: accumulates rho' J^T J, rho' J^T r, 1/2 rho, rows
+__device__ inline void lm_accum(int type, float px, float py, float pz, double a0, double a1,
+                                double a2, double b0, double b1, double b2, const double* X,
+                                double* acc) {
+  dq q{X[0], X[1], X[2], X[3]};
+  d3 Rp = qrot(q, d3{(double)px, (double)py, (double)pz});
+  d3 lp{Rp.x + X[4], Rp.y + X[5], Rp.z + X[6]};
+  double J[3][6];
+  double r[3];
+  int m;
+  if (type == 1) {
+    // r = u x e ; dr/dlp = -[e]x ; J_rot = 2 [e]x [Rp]x ; J_t = -[e]x
+    d3 u{lp.x - a0, lp.y - a1, lp.z - a2};
+    r[0] = u.y * b2 - u.z * b1;
+    r[1] = u.z * b0 - u.x * b2;
+    r[2] = u.x * b1 - u.y * b0;
+    const double E[3][3] = {{0, -b2, b1}, {b2, 0, -b0}, {-b1, b0, 0}};
+    const double K[3][3] = {{0, -Rp.z, Rp.y}, {Rp.z, 0, -Rp.x}, {-Rp.y, Rp.x, 0}};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        J[i][c] = 2.0 * (E[i][0] * K[0][c] + E[i][1] * K[1][c] + E[i][2] * K[2][c]);
+        J[i][3 + c] = -E[i][c];
+      }
+    }
+    m = 3;
+  } else {
+    if (type == 2)
+      r[0] = ((lp.x - a0) * b0 + (lp.y - a1) * b1) + (lp.z - a2) * b2;  // n = b
+    else
+      r[0] = ((a0 * lp.x + a1 * lp.y) + a2 * lp.z) + b0;  // n = a, d = b0
+    const double nx = type == 2 ? b0 : a0, ny = type == 2 ? b1 : a1, nz = type == 2 ? b2 : a2;
+    // J_rot = 2 (Rp x n)^T, J_t = n^T
+    J[0][0] = 2.0 * (Rp.y * nz - Rp.z * ny);
+    J[0][1] = 2.0 * (Rp.z * nx - Rp.x * nz);
+    J[0][2] = 2.0 * (Rp.x * ny - Rp.y * nx);
+    J[0][3] = nx;
+    J[0][4] = ny;
+    J[0][5] = nz;
+    m = 1;
+  }
+  double s = 0;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    if (i < m) s += r[i] * r[i];
+  double rho0, rho1;
+  if (s > 0.01) {
+    const double sq = sqrt(s);
+    rho0 = 2.0 * 0.1 * sq - 0.01;
+    rho1 = fmax(2.2250738585072014e-308, 0.1 / sq);
+  } else {
+    rho0 = s;
+    rho1 = 1.0;
+  }
+  acc[27] += 0.5 * rho0;
+  acc[28] += (double)m;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    if (i >= m) break;
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      const double wa = rho1 * J[i][a];
+#pragma unroll
+      for (int b = a; b < 6; ++b) acc[k++] += wa * J[i][b];
+      acc[21 + a] += wa * r[i];
+    }
+  }
+}
+
+// EigenQuaternionParameterization::Plus + Euclidean t
+__host__ __device__ inline void lm_plus(const double* x, const double* d, double* out) {
+  double nd = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+  if (nd > 0.0) {
+    double s = sin(nd) / nd;
+    dq dqq{s * d[0], s * d[1], s * d[2], cos(nd)};
+    dq r = qmul(dqq, dq{x[0], x[1], x[2], x[3]});
+    out[0] = r.x;
+    out[1] = r.y;
+    out[2] = r.z;
+    out[3] = r.w;
+  } else {
+    out[0] = x[0];
+    out[1] = x[1];
+    out[2] = x[2];
+    out[3] = x[3];
+  }
+  out[4] = x[4] + d[3];
+  out[5] = x[5] + d[4];
+  out[6] = x[6] + d[5];
+}
+
+__host__ __device__ inline double lm_gradmax(const double* x, const double* g) {
+  double ng[6], pg[7];
+  for (int c = 0; c < 6; ++c) ng[c] = -g[c];
+  lm_plus(x, ng, pg);
+  double mx = 0.0;
+  for (int i = 0; i < 7; ++i) mx = fmax(mx, fabs(x[i] - pg[i]));
+  return mx;
+}
+
+__host__ __device__ inline double lm_norm7(const double* x) {
+  double s = 0;
+  for (int i = 0; i < 7; ++i) s += x[i] * x[i];
+  return sqrt(s);
+}
+
+// LM step: (S J^T J S + diag(D^2)) y = S J^T r, step = -y.  Returns false if not solvable.
+__host__ __device__ inline bool lm_solve_step(LmState& S, double* step) {
+  double A[6][6], b[6];
+  for (int i = 0; i < 6; ++i) {
+    if (!S.reuse_diag) {
+      double d = S.scaling[i] * S.scaling[i] * S.jtj[ut_index(i, i)];
+      S.diag[i] = fmin(fmax(d, 1e-6), 1e32);
+    }
+  }
+  for (int i = 0; i < 6; ++i) {
+    for (int j = 0; j < 6; ++j) {
+      int r = i < j ? i : j, c = i < j ? j : i;
+      A[i][j] = S.scaling[i] * S.jtj[ut_index(r, c)] * S.scaling[j];
+    }
+    double D = sqrt(S.diag[i] / S.radius);
+    A[i][i] += D * D;
+    b[i] = S.scaling[i] * S.g[i];
+  }
+  S.reuse_diag = 1;
+  // Cholesky A = L L^T
+  double L[6][6];
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j < 6; ++j) L[i][j] = 0;
+  for (int j = 0; j < 6; ++j) {
+    double s = A[j][j];
+    for (int k = 0; k < j; ++k) s -= L[j][k] * L[j][k];
+    if (!(s > 0.0)) return false;
+    double d = sqrt(s);
+    L[j][j] = d;
+    for (int i = j + 1; i < 6; ++i) {
+      double t = A[i][j];
+      for (int k = 0; k < j; ++k) t -= L[i][k] * L[j][k];
+      L[i][j] = t / d;
+    }
+  }
+  double z[6], y[6];
+  for (int i = 0; i < 6; ++i) {
+    double t = b[i];
+    for (int k = 0; k < i; ++k) t -= L[i][k] * z[k];
+    z[i] = t / L[i][i];
+  }
+  for (int i = 5; i >= 0; --i) {
+    double t = z[i];
+    for (int k = i + 1; k < 6; ++k) t -= L[k][i] * y[k];
+    y[i] = t / L[i][i];
+  }
+  for (int i = 0; i < 6; ++i) {
+    step[i] = -y[i];
+    if (!isfinite(step[i])) return false;
+  }
+  return true;
+}
+
+// Consume one reduced pass (red[LM_NACC]) and advance the trust-region state machine until
+// it needs another pass (status LM_EVAL_CAND) or terminates (LM_DONE, best in S.best).
+__host__ __device__ inline void lm_step(LmState& S, const double* red) {
+  if (S.status == LM_DONE) return;
+  bool step_ok;
+  if (S.status == LM_EVAL_X) {
+    for (int i = 0; i < 21; ++i) S.jtj[i] = red[i];
+    for (int i = 0; i < 6; ++i) S.g[i] = red[21 + i];
+    S.cost = red[27];
+    S.initial_cost = S.cost;
+    if (red[28] == 0.0) {  // no residual blocks: parameters untouched
+      S.term = 4;
+      S.min_cost = S.cost;
+      S.status = LM_DONE;
+      return;
+    }
+    for (int i = 0; i < 6; ++i) S.scaling[i] = 1.0 / (1.0 + sqrt(S.jtj[ut_index(i, i)]));
+    S.gmax = lm_gradmax(S.x, S.g);
+    S.x_norm = lm_norm7(S.x);
+    step_ok = true;
+  } else {
+    const double cand_cost = red[27];
+    const double cost_change = S.cost - cand_cost;
+    if (fabs(cost_change) <= 1e-6 * S.cost) {  // FunctionToleranceReached
+      S.term = 1;
+      S.status = LM_DONE;
+      return;
+    }
+    const double rel = cost_change / S.mcc;
+    if (rel > 1e-3) {  // HandleSuccessfulStep
+      for (int i = 0; i < 7; ++i) S.x[i] = S.cand[i];
+      for (int i = 0; i < 21; ++i) S.jtj[i] = red[i];
+      for (int i = 0; i < 6; ++i) S.g[i] = red[21 + i];
+      S.cost = cand_cost;
+      S.x_norm = lm_norm7(S.x);
+      S.gmax = lm_gradmax(S.x, S.g);
+      S.successful++;
+      double f = 2.0 * rel - 1.0;
+      S.radius = S.radius / fmax(1.0 / 3.0, 1.0 - f * f * f);
+      S.radius = fmin(1e16, S.radius);
+      S.decrease = 2.0;
+      S.reuse_diag = 0;
+      step_ok = true;
+    } else {  // HandleUnsuccessfulStep
+      S.radius = S.radius / S.decrease;
+      S.decrease *= 2.0;
+      S.reuse_diag = 1;
+      step_ok = false;
+    }
+  }
+  while (true) {  // FinalizeIterationAndCheckIfMinimizerCanContinue
+    if (step_ok && S.cost < S.min_cost) {
+      S.min_cost = S.cost;
+      for (int i = 0; i < 7; ++i) S.best[i] = S.x[i];
+    }
+    if (S.iteration >= S.max_iter) { S.term = 0; break; }
+    if (step_ok && S.gmax <= 1e-10) { S.term = 3; break; }
+    if (S.radius <= 1e-32) { S.term = 5; break; }
+    S.iteration++;
+    step_ok = false;
+    double step[6];
+    bool valid = lm_solve_step(S, step);
+    if (valid) {
+      // model_cost_change = -(step^T S g + 1/2 step^T (S JtJ S) step)
+      double lin = 0, quad = 0;
+      for (int i = 0; i < 6; ++i) {
+        lin += step[i] * S.scaling[i] * S.g[i];
+        for (int j = 0; j < 6; ++j) {
+          int r = i < j ? i : j, c = i < j ? j : i;
+          quad += step[i] * S.scaling[i] * S.jtj[ut_index(r, c)] * S.scaling[j] * step[j];
+        }
+      }
+      S.mcc = -(lin + 0.5 * quad);
+      valid = S.mcc > 0.0;
+    }
+    if (!valid) {  // HandleInvalidStep
+      S.invalid++;
+      if (++S.consec_invalid >= 5) { S.term = 5; break; }
+      S.radius = S.radius / S.decrease;
+      S.decrease *= 2.0;
+      S.reuse_diag = 1;
+      continue;
+    }
+    S.consec_invalid = 0;
+    double delta[6];
+    for (int i = 0; i < 6; ++i) delta[i] = step[i] * S.scaling[i];
+    lm_plus(S.x, delta, S.cand);
+    double sn = 0;
+    for (int i = 0; i < 7; ++i) sn += (S.x[i] - S.cand[i]) * (S.x[i] - S.cand[i]);
+    sn = sqrt(sn);
+    if (sn <= 1e-8 * (S.x_norm + 1e-8)) { S.term = 2; break; }  // ParameterToleranceReached
+    S.status = LM_EVAL_CAND;
+    return;
+  }
+  S.status = LM_DONE;
+}
+
+// ---------------------------------------------------------------------------------------
+// fused LM pass: evaluate at the state's evaluation point, per-workgroup partial of
+// (J^T J, J^T r, cost, rows), last-arriving workgroup of the stream reduces the partials
+// in chunk order (deterministic) and advances the trust-region state (lm_step).
+// Publish/consume follows the agent-scope release/acquire recipe (cdna_hip_programming.md
+// Guideline 16): plain stores -> vmcnt(0) -> barrier -> release fence -> ticket atomic;
+// the last arriver: acquire fence -> vmcnt(0) -> barrier -> plain loads.
+// ---------------------------------------------------------------------------------------
+template <int kThreads, int kPerThread>
+__device__ inline void lm_pass_body(const int* __restrict__ r_type, const float* __restrict__ r_px,
+                                    const float* __restrict__ r_py, const float* __restrict__ r_pz,
+                                    const double* __restrict__ a0, const double* __restrict__ a1,
+                                    const double* __restrict__ a2, const double* __restrict__ b0,
+                                    const double* __restrict__ b1, const double* __restrict__ b2,
+                                    int nrec, int chunk, int nchunks, LmState& S,
+                                    double* partials, uint32_t* ticket) {
+  __shared__ double red[kThreads / 64][LM_NACC];
+  __shared__ int last;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  const int status = S.status;
+  if (status == LM_DONE) return;  // uniform for every workgroup of the stream
+  double X[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) X[i] = status == LM_EVAL_X ? S.x[i] : S.cand[i];
+  double acc[LM_NACC];
+#pragma unroll
+  for (int i = 0; i < LM_NACC; ++i) acc[i] = 0.0;
+  constexpr int kChunk = kThreads * kPerThread;
+  const int base = chunk * kChunk;
+#pragma unroll
+  for (int it = 0; it < kPerThread; ++it) {
+    const int r = base + it * kThreads + tid;
+    if (r < nrec) {
+      const int t = r_type[r];
+      if (t != 0)
+        lm_accum(t, r_px[r], r_py[r], r_pz[r], a0[r], a1[r], a2[r], b0[r], b1[r], b2[r], X, acc);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < LM_NACC; ++i) {
+    double v = wave_sum_d(acc[i]);
+    if (lane == 0) red[wid][i] = v;
+  }
+  __syncthreads();
+  if (tid < LM_NACC) {
+    double v = 0.0;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; ++w) v += red[w][tid];
+    partials[(size_t)chunk * LM_NACC + tid] = v;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (prev == (uint32_t)nchunks - 1) ? 1 : 0;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (tid < LM_NACC) {
+    double v = 0.0;
+    for (int c = 0; c < nchunks; ++c) v += partials[(size_t)c * LM_NACC + tid];
+    red[0][tid] = v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    lm_step(S, red[0]);
+    *ticket = 0;
+  }
+}
+
+}  // namespace loam

@@ -1,0 +1,992 @@
+// mapper.hip — LaserMapping::solveMapping (laser_mapping.cpp:212-814) on MI355X.
+//
+// One handle = B independent mapping streams; every launch below covers all of them.
+// Per frame (all device resident, one host round-trip at the end for the poses):
+//   k_shift_cubes      ring-buffer recentering of the 21x21x11 cube grid (:252-444), rare
+//   k_stack_ds         VoxelGrid of laserCloudCornerLast (0.4 m) / SurfLast (0.8 m) (:492-500)
+//   k_submap_*         gather the 5x5x3 window cubes (:448-489) and build a 1 m-cell hash
+//                      (replaces the KD-tree build, :519-520); exact 5-NN because accepted
+//                      matches need all 5 neighbours within 1 m (:557, :642)
+//   2 x { k_correspond  5-NN + PCA line / QR plane fit -> factor records (:545-699)
+//         5 x k_lm_pass   fused: evaluate candidate (cost + J^T J + J^T r) -> last-arriving
+//                         workgroup of each stream reduces + runs the LM step (lm.h) }
+//   k_insert           transform stacks with the final pose, assign cubes (:741-788)
+//   k_revox            re-VoxelGrid every window cube (:795-808) into the map arena
+//
+// Map storage: per (stream, map) an append-only arena of float4 points + a cube table
+// (offset, count) for the 4851 cubes; window cubes are rewritten at the arena tail every
+// frame, the host compacts an arena when its tail passes half the capacity.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+#include "device_math.h"
+#include "cellhash.h"
+#include "lm.h"
+#include "voxel.h"
+
+namespace loam {
+
+constexpr int CW = 21, CH = 21, CD = 11, NCUBE = CW * CH * CD;
+constexpr int WIN_MAX = 125;
+constexpr int WIN_VALID_MAX = 75;
+constexpr int EXTRA_CAP = 64;
+constexpr int CORR_THREADS = 256;
+constexpr int LM_THREADS = 256;
+constexpr int LM_PER_THREAD = 4;
+constexpr int LM_CHUNK = LM_THREADS * LM_PER_THREAD;
+constexpr int SUBMAP_BLOCKS = 64;
+constexpr int MAP_ERR_SUBMAP = 4, MAP_ERR_EXTRA = 8, MAP_ERR_HASH = 16;
+
+struct StreamFrame {
+  double pose[7];  // in: initial guess (transformAssociateToMap); out: optimised pose
+  int active;
+  int nc_in, ns_in;
+  int nc_stack, ns_stack;
+  int sub_n[2];
+  int optimize;
+  int corner_num[2], surf_num[2];
+  int valid_num;
+  int window[WIN_MAX];
+  int sub_off[2][WIN_MAX + 1];
+  int center[3];
+  int cen[3];
+  int shift[3];
+  int origin[3];
+  uint32_t arena_tail[2];
+  int arena_active[2];
+  uint32_t scratch_tail[2];
+  uint32_t cursor[2];
+  int extra_n[2];
+  int extra_list[2][EXTRA_CAP];
+  int err;
+  LmState lm[2];
+};
+
+struct MapperDev {
+  int B;
+  int max_in, map_cap, sub_cap, hash_T, scratch_cap, max_chunks;
+  float leaf[2];
+  uint32_t epoch;
+  StreamFrame* fr;
+  float4* in_pts[2];
+  float4* stack[2];
+  float4* arena;  // [B][2 maps][2 arenas][map_cap]
+  uint2* cube_tab;  // [B][2 maps][NCUBE] (off, cnt) — current parity
+  uint32_t* extra_flag;  // [B][2][NCUBE]
+  unsigned long long* hkey;  // [B][2][T]
+  unsigned long long* hcnt;
+  uint32_t* hstart;
+  float4* sub_lin;  // [B][2][sub_cap] window-order submap
+  float4* spts;     // [B][2][sub_cap] cell-sorted submap (w = submap index bits)
+  uint32_t* pt_slot;
+  uint32_t* pt_rank;
+  // factor records (SoA) [B][2*max_in]
+  int* r_type;
+  float* r_px;
+  float* r_py;
+  float* r_pz;
+  double* r_a[3];
+  double* r_b[3];
+  float4* ins_pts;  // [B][2][max_in]
+  int* ins_tag;
+  float4* vx_pts;  // [B][2][scratch_cap]
+  int* vx_idx;
+  double* partials;  // [B][max_chunks][LM_NACC]
+  uint32_t* tickets;  // [B]
+  const int* corr_blk;  // [B+1] block prefix (k_correspond)
+  const int* lm_blk;    // [B+1] block prefix (k_lm_pass)
+};
+
+__device__ inline int find_stream(const int* blk, int B, int b) {
+  int lo = 0, hi = B;  // largest s with blk[s] <= b
+  while (hi - lo > 1) {
+    int mid = (lo + hi) >> 1;
+    if (blk[mid] <= b) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+__device__ inline size_t sm_index(int s, int m) { return (size_t)s * 2 + m; }
+
+__device__ inline float4* arena_base(const MapperDev& D, int s, int m, int active) {
+  return D.arena + ((sm_index(s, m) * 2 + active) * (size_t)D.map_cap);
+}
+
+// ---------------------------------------------------------------------------------------
+// ring-buffer recentering (laser_mapping.cpp:252-444): content moves by shift[axis] cube
+// indices, the slabs that wrap around are cleared.
+// ---------------------------------------------------------------------------------------
+__global__ void k_shift_cubes(MapperDev D, const uint2* __restrict__ old_tab, uint2* new_tab) {
+  int s = blockIdx.y;
+  const StreamFrame& F = D.fr[s];
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < 2 * NCUBE; t += gridDim.x * blockDim.x) {
+    int m = t / NCUBE, c = t % NCUBE;
+    int i = c % CW, j = (c / CW) % CH, k = c / (CW * CH);
+    int oi = i - F.shift[0], oj = j - F.shift[1], ok = k - F.shift[2];
+    uint2 v = make_uint2(0, 0);
+    if (oi >= 0 && oi < CW && oj >= 0 && oj < CH && ok >= 0 && ok < CD)
+      v = old_tab[sm_index(s, m) * NCUBE + oi + CW * oj + CW * CH * ok];
+    new_tab[sm_index(s, m) * NCUBE + c] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// VoxelGrid of the incoming feature clouds -> CornerStack / SurfStack (:492-500)
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
+  const int s = blockIdx.x >> 1, m = blockIdx.x & 1;
+  StreamFrame& F = D.fr[s];
+  if (!F.active) return;
+  VoxSeg S;
+  S.src0 = D.in_pts[m] + (size_t)s * D.max_in;
+  S.n0 = m == 0 ? F.nc_in : F.ns_in;
+  S.src1 = nullptr;
+  S.tag1 = nullptr;
+  S.n1 = 0;
+  S.tag = 0;
+  S.leaf = D.leaf[m];
+  S.append_only = 0;
+  S.out = D.stack[m] + (size_t)s * D.max_in;
+  S.tail = nullptr;
+  S.cap = D.max_in;
+  S.res_off = nullptr;
+  S.res_cnt = reinterpret_cast<uint32_t*>(m == 0 ? &F.nc_stack : &F.ns_stack);
+  S.scratch_pts = D.vx_pts + sm_index(s, m) * D.scratch_cap;
+  S.scratch_idx = D.vx_idx + sm_index(s, m) * D.scratch_cap;
+  S.scratch_tail = nullptr;
+  S.scratch_cap = D.scratch_cap;
+  S.err = &F.err;
+  voxel_segment(S, lds);
+}
+
+// ---------------------------------------------------------------------------------------
+// submap: offsets of the window cubes (laserCloudCornerFromMap concatenation order)
+// ---------------------------------------------------------------------------------------
+__global__ void k_submap_prep(MapperDev D) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= D.B) return;
+  StreamFrame& F = D.fr[s];
+  if (!F.active) return;
+  for (int m = 0; m < 2; ++m) {
+    uint32_t acc = 0;
+    const uint2* tab = D.cube_tab + sm_index(s, m) * NCUBE;
+    for (int w = 0; w < F.valid_num; ++w) {
+      F.sub_off[m][w] = acc;
+      acc += tab[F.window[w]].y;
+    }
+    F.sub_off[m][F.valid_num] = acc;
+    if (acc > (uint32_t)D.sub_cap) {
+      F.err |= MAP_ERR_SUBMAP;
+      acc = 0;
+      F.sub_off[m][F.valid_num] = 0;
+      for (int w = 0; w < F.valid_num; ++w) F.sub_off[m][w] = 0;
+    }
+    F.sub_n[m] = acc;
+    F.scratch_tail[m] = 0;
+    F.cursor[m] = 0;
+    F.extra_n[m] = 0;
+  }
+  // laser_mapping.cpp:514
+  F.optimize = (F.sub_n[0] > 10 && F.sub_n[1] > 50) ? 1 : 0;
+}
+
+// gather the window cubes into sub_lin and claim the cell slots; rank within the cell
+__global__ void k_submap_insert(MapperDev D) {
+  const int sm = blockIdx.y;
+  const int s = sm >> 1, m = sm & 1;
+  const StreamFrame& F = D.fr[s];
+  if (!F.active) return;
+  const uint32_t n = F.sub_n[m];
+  const uint2* tab = D.cube_tab + sm_index(s, m) * NCUBE;
+  const float4* ar = arena_base(D, s, m, F.arena_active[m]);
+  float4* lin = D.sub_lin + sm_index(s, m) * D.sub_cap;
+  unsigned long long* hk = D.hkey + sm_index(s, m) * D.hash_T;
+  unsigned long long* hc = D.hcnt + sm_index(s, m) * D.hash_T;
+  uint32_t* ps = D.pt_slot + sm_index(s, m) * D.sub_cap;
+  uint32_t* pr = D.pt_rank + sm_index(s, m) * D.sub_cap;
+  const uint32_t mask = D.hash_T - 1;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    int lo = 0, hi = F.valid_num;  // window slot: largest w with sub_off[w] <= i
+    while (hi - lo > 1) {
+      int mid = (lo + hi) >> 1;
+      if ((uint32_t)F.sub_off[m][mid] <= i) lo = mid; else hi = mid;
+    }
+    const uint2 cv = tab[F.window[lo]];
+    const float4 p = ar[cv.x + (i - F.sub_off[m][lo])];
+    lin[i] = p;
+    uint32_t slot, rank;
+    if (!hash_claim_rank(hk, hc, mask, D.epoch, cell_key_rel(p.x, p.y, p.z, F.origin), &slot, &rank)) {
+      atomicOr(&D.fr[s].err, MAP_ERR_HASH);
+      ps[i] = 0;
+      pr[i] = 0xFFFFFFFFu;
+      continue;
+    }
+    ps[i] = slot;
+    pr[i] = rank;
+  }
+}
+
+__global__ void k_submap_alloc(MapperDev D) {
+  const int sm = blockIdx.y;
+  const int s = sm >> 1, m = sm & 1;
+  StreamFrame& F = D.fr[s];
+  if (!F.active) return;
+  const uint32_t n = F.sub_n[m];
+  const unsigned long long* hc = D.hcnt + sm_index(s, m) * D.hash_T;
+  uint32_t* hs = D.hstart + sm_index(s, m) * D.hash_T;
+  const uint32_t* ps = D.pt_slot + sm_index(s, m) * D.sub_cap;
+  const uint32_t* pr = D.pt_rank + sm_index(s, m) * D.sub_cap;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    if (pr[i] == 0) {
+      uint32_t slot = ps[i];
+      uint32_t cnt = (uint32_t)(hc[slot] & 0xFFFFFFFFu);
+      hs[slot] = atomicAdd(&F.cursor[m], cnt);
+    }
+  }
+}
+
+__global__ void k_submap_scatter(MapperDev D) {
+  const int sm = blockIdx.y;
+  const int s = sm >> 1, m = sm & 1;
+  const StreamFrame& F = D.fr[s];
+  if (!F.active) return;
+  const uint32_t n = F.sub_n[m];
+  const uint32_t* hs = D.hstart + sm_index(s, m) * D.hash_T;
+  const uint32_t* ps = D.pt_slot + sm_index(s, m) * D.sub_cap;
+  const uint32_t* pr = D.pt_rank + sm_index(s, m) * D.sub_cap;
+  const float4* lin = D.sub_lin + sm_index(s, m) * D.sub_cap;
+  float4* sp = D.spts + sm_index(s, m) * D.sub_cap;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    if (pr[i] == 0xFFFFFFFFu) continue;
+    float4 p = lin[i];
+    sp[hs[ps[i]] + pr[i]] = make_float4(p.x, p.y, p.z, __int_as_float((int)i));
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// correspondences of one outer round (laser_mapping.cpp:545-699) -> factor records
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(CORR_THREADS) k_correspond(MapperDev D, int round) {
+  const int s = find_stream(D.corr_blk, D.B, blockIdx.x);
+  StreamFrame& F = D.fr[s];
+  if (!F.active) return;
+  const int local = (blockIdx.x - D.corr_blk[s]) * CORR_THREADS + threadIdx.x;
+  double X[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) X[i] = F.pose[i];
+  if (local == 0) lm_init(F.lm[round], X, 4, F.optimize != 0);
+  const int nc = F.nc_stack, ns = F.ns_stack;
+  if (local >= nc + ns) return;
+  const size_t rb = (size_t)s * 2 * D.max_in;
+  const int ridx = local;  // corners [0, nc), surfs [nc, nc + ns)
+  if (!F.optimize) {
+    D.r_type[rb + ridx] = 0;
+    return;
+  }
+  const int m = local < nc ? 0 : 1;
+  const int qi = m == 0 ? local : local - nc;
+  const float4 po = D.stack[m][(size_t)s * D.max_in + qi];
+  const float4 sel = to_map(X, po);
+  Top5 T;
+  knn5_hash(sel, F.origin, D.hkey + sm_index(s, m) * D.hash_T, D.hcnt + sm_index(s, m) * D.hash_T,
+            D.hstart + sm_index(s, m) * D.hash_T, D.spts + sm_index(s, m) * D.sub_cap,
+            D.hash_T - 1, D.epoch, 1.0f, T);
+  int type = 0;
+  double a[3] = {0, 0, 0}, b[3] = {0, 0, 0};
+  if (T.d[4] < 1.0f) {
+    float nb[5][3];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      nb[j][0] = T.x[j];
+      nb[j][1] = T.y[j];
+      nb[j][2] = T.z[j];
+    }
+    if (m == 0) {
+      d3 pa, pb;
+      if (edge_from_nbrs(nb, pa, pb)) {
+        type = 1;
+        d3 de{pa.x - pb.x, pa.y - pb.y, pa.z - pb.z};
+        double dn = sqrt(de.x * de.x + de.y * de.y + de.z * de.z);
+        a[0] = pa.x; a[1] = pa.y; a[2] = pa.z;
+        b[0] = de.x / dn; b[1] = de.y / dn; b[2] = de.z / dn;
+        atomicAdd(&F.corner_num[round], 1);
+      }
+    } else {
+      d3 n;
+      double d;
+      if (plane_from_nbrs(nb, n, d)) {
+        type = 3;
+        a[0] = n.x; a[1] = n.y; a[2] = n.z;
+        b[0] = d;
+        atomicAdd(&F.surf_num[round], 1);
+      }
+    }
+  }
+  D.r_type[rb + ridx] = type;
+  D.r_px[rb + ridx] = po.x;
+  D.r_py[rb + ridx] = po.y;
+  D.r_pz[rb + ridx] = po.z;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    D.r_a[k][rb + ridx] = a[k];
+    D.r_b[k][rb + ridx] = b[k];
+  }
+}
+
+__global__ void __launch_bounds__(LM_THREADS) k_lm_pass(MapperDev D, int round) {
+  const int s = find_stream(D.lm_blk, D.B, blockIdx.x);
+  StreamFrame& F = D.fr[s];
+  if (!F.active) return;
+  const int chunk = blockIdx.x - D.lm_blk[s];
+  const int nchunks = D.lm_blk[s + 1] - D.lm_blk[s];
+  const size_t rb = (size_t)s * 2 * D.max_in;
+  LmState& S = F.lm[round];
+  lm_pass_body<LM_THREADS, LM_PER_THREAD>(D.r_type + rb, D.r_px + rb, D.r_py + rb, D.r_pz + rb, D.r_a[0] + rb,
+                     D.r_a[1] + rb, D.r_a[2] + rb, D.r_b[0] + rb, D.r_b[1] + rb, D.r_b[2] + rb,
+                     F.nc_stack + F.ns_stack, chunk, nchunks, S,
+                     D.partials + (size_t)s * D.max_chunks * LM_NACC, D.tickets + s);
+}
+
+// copy the round's result into the stream pose (Ceres writes the best point back into
+// the parameter blocks, laser_mapping.cpp:535-536)
+__global__ void k_lm_finish(MapperDev D, int round) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= D.B) return;
+  StreamFrame& F = D.fr[s];
+  if (!F.active) return;
+  const LmState& S = F.lm[round];
+  for (int i = 0; i < 7; ++i) F.pose[i] = S.best[i];
+}
+
+// ---------------------------------------------------------------------------------------
+// insertion of the stacks into the cube grid with the final pose (laser_mapping.cpp:741-788)
+// ---------------------------------------------------------------------------------------
+__global__ void k_insert(MapperDev D) {
+  const int s = blockIdx.y;
+  StreamFrame& F = D.fr[s];
+  if (!F.active) return;
+  const int nc = F.nc_stack, ns = F.ns_stack;
+  double X[7];
+  for (int i = 0; i < 7; ++i) X[i] = F.pose[i];
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nc + ns; t += gridDim.x * blockDim.x) {
+    const int m = t < nc ? 0 : 1;
+    const int i = m == 0 ? t : t - nc;
+    const float4 sel = to_map(X, D.stack[m][(size_t)s * D.max_in + i]);
+    const int ci = cube_of(sel.x, F.cen[0]), cj = cube_of(sel.y, F.cen[1]), ck = cube_of(sel.z, F.cen[2]);
+    int tag = -1;
+    if (ci >= 0 && ci < CW && cj >= 0 && cj < CH && ck >= 0 && ck < CD) {
+      tag = ci + CW * cj + CW * CH * ck;
+      const bool in_window = ci >= F.center[0] - 2 && ci <= F.center[0] + 2 &&
+                             cj >= F.center[1] - 2 && cj <= F.center[1] + 2 &&
+                             ck >= F.center[2] - 1 && ck <= F.center[2] + 1;
+      if (!in_window) {
+        uint32_t* fl = D.extra_flag + sm_index(s, m) * NCUBE + tag;
+        if (atomicExch(fl, D.epoch) != D.epoch) {
+          int e = atomicAdd(&F.extra_n[m], 1);
+          if (e < EXTRA_CAP) F.extra_list[m][e] = tag;
+          else atomicOr(&F.err, MAP_ERR_EXTRA);
+        }
+      }
+    }
+    const size_t o = sm_index(s, m) * D.max_in + i;
+    D.ins_pts[o] = sel;
+    D.ins_tag[o] = tag;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// re-VoxelGrid of every window cube (old content ++ inserted points, :795-808); cubes outside
+// the window that received points get them appended raw (:762).  One workgroup per cube.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(VX_THREADS) k_revox(MapperDev D) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
+  constexpr int SLOTS = WIN_VALID_MAX + EXTRA_CAP;
+  const int slot = blockIdx.x % SLOTS;
+  const int sm = blockIdx.x / SLOTS;
+  const int s = sm >> 1, m = sm & 1;
+  StreamFrame& F = D.fr[s];
+  if (!F.active) return;
+  int cube;
+  int append;
+  if (slot < F.valid_num) {
+    cube = F.window[slot];
+    append = 0;
+  } else if (slot - F.valid_num < min(F.extra_n[m], EXTRA_CAP)) {
+    cube = F.extra_list[m][slot - F.valid_num];
+    append = 1;
+  } else {
+    return;
+  }
+  uint2* tab = D.cube_tab + sm_index(s, m) * NCUBE;
+  const uint2 cv = tab[cube];
+  float4* ar = arena_base(D, s, m, F.arena_active[m]);
+  const int nst = m == 0 ? F.nc_stack : F.ns_stack;
+  VoxSeg S;
+  S.src0 = ar + cv.x;
+  S.n0 = (int)cv.y;
+  S.src1 = D.ins_pts + sm_index(s, m) * D.max_in;
+  S.tag1 = D.ins_tag + sm_index(s, m) * D.max_in;
+  S.n1 = nst;
+  S.tag = cube;
+  S.leaf = D.leaf[m];
+  S.append_only = append;
+  S.out = ar;
+  S.tail = &F.arena_tail[m];
+  S.cap = D.map_cap;
+  S.res_off = &tab[cube].x;
+  S.res_cnt = &tab[cube].y;
+  S.scratch_pts = D.vx_pts + sm_index(s, m) * D.scratch_cap;
+  S.scratch_idx = D.vx_idx + sm_index(s, m) * D.scratch_cap;
+  S.scratch_tail = &F.scratch_tail[m];
+  S.scratch_cap = D.scratch_cap;
+  S.err = &F.err;
+  voxel_segment(S, lds);
+}
+
+// ---------------------------------------------------------------------------------------
+// arena compaction: live cubes copied, in cube order, into the other arena
+// ---------------------------------------------------------------------------------------
+__global__ void k_compact_scan(MapperDev D, const int* pairs, uint32_t* new_off) {
+  // one workgroup (1024 threads) per (stream, map) pair; pairs[b] = s*2 + m
+  __shared__ uint32_t ws[VX_WAVES + 1];
+  const int sm = pairs[blockIdx.x];
+  const uint2* tab = D.cube_tab + (size_t)sm * NCUBE;
+  uint32_t* no = new_off + (size_t)blockIdx.x * (NCUBE + 1);
+  constexpr int PER = (NCUBE + VX_THREADS - 1) / VX_THREADS;  // 5
+  uint32_t v[PER];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    int c = threadIdx.x * PER + k;
+    v[k] = c < NCUBE ? tab[c].y : 0u;
+    sum += v[k];
+  }
+  uint32_t total;
+  uint32_t pre = vx_block_scan(sum, ws, &total);
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    int c = threadIdx.x * PER + k;
+    if (c < NCUBE) no[c] = pre;
+    pre += v[k];
+  }
+  if (threadIdx.x == 0) no[NCUBE] = total;
+}
+
+__global__ void k_compact_copy(MapperDev D, const int* pairs, const uint32_t* new_off) {
+  const int p = blockIdx.y;
+  const int sm = pairs[p];
+  const int s = sm >> 1, m = sm & 1;
+  StreamFrame& F = D.fr[s];
+  uint2* tab = D.cube_tab + (size_t)sm * NCUBE;
+  const uint32_t* no = new_off + (size_t)p * (NCUBE + 1);
+  const float4* src = arena_base(D, s, m, F.arena_active[m]);
+  float4* dst = arena_base(D, s, m, 1 - F.arena_active[m]);
+  for (int c = blockIdx.x; c < NCUBE; c += gridDim.x) {
+    const uint2 cv = tab[c];
+    for (uint32_t i = threadIdx.x; i < cv.y; i += blockDim.x) dst[no[c] + i] = src[cv.x + i];
+  }
+}
+
+__global__ void k_compact_commit(MapperDev D, const int* pairs, int npairs, const uint32_t* new_off) {
+  const int p = blockIdx.x;
+  if (p >= npairs) return;
+  const int sm = pairs[p];
+  const int s = sm >> 1, m = sm & 1;
+  StreamFrame& F = D.fr[s];
+  uint2* tab = D.cube_tab + (size_t)sm * NCUBE;
+  const uint32_t* no = new_off + (size_t)p * (NCUBE + 1);
+  for (int c = threadIdx.x; c < NCUBE; c += blockDim.x) tab[c].x = no[c];
+  if (threadIdx.x == 0) {
+    F.arena_tail[m] = no[NCUBE];
+    F.arena_active[m] = 1 - F.arena_active[m];
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------
+struct HostStream {
+  double q_wmap_wodom[4] = {0, 0, 0, 1}, t_wmap_wodom[3] = {0, 0, 0};
+  double q_wodom[4] = {0, 0, 0, 1}, t_wodom[3] = {0, 0, 0};
+  double pose[7] = {0, 0, 0, 1, 0, 0, 0};
+  double q_hf[4] = {0, 0, 0, 1}, t_hf[3] = {0, 0, 0};
+  bool pending = false, skip = false;
+  int frame = 0;
+  loam_map_stats st{};
+};
+
+}  // namespace loam
+
+using namespace loam;
+
+struct loam_mapper {
+  loam_params P;
+  int dev = 0, B = 1;
+  hipStream_t st = nullptr;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  MapperDev D{};
+  std::vector<StreamFrame> hf;
+  std::vector<HostStream> hs;
+  std::vector<int> corr_blk, lm_blk;
+  int* d_corr_blk = nullptr;
+  int* d_lm_blk = nullptr;
+  uint2* cube_tab[2] = {nullptr, nullptr};
+  int parity = 0;
+  int* d_pairs = nullptr;
+  uint32_t* d_new_off = nullptr;
+  std::vector<void*> allocs;
+  uint32_t frame_counter = 0;
+};
+
+namespace {
+
+template <typename T>
+int32_t dalloc(loam_mapper* h, T** p, size_t count) {
+  void* q = nullptr;
+  size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+  LOAM_HIP(hipMalloc(&q, bytes));
+  LOAM_HIP(hipMemset(q, 0, bytes));
+  h->allocs.push_back(q);
+  *p = reinterpret_cast<T*>(q);
+  return LOAM_OK;
+}
+
+#define TRY(x)                   \
+  do {                           \
+    int32_t rc_ = (x);           \
+    if (rc_ != LOAM_OK) return rc_; \
+  } while (0)
+
+uint32_t next_pow2(uint32_t v) {
+  uint32_t p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+void free_all(loam_mapper* h) {
+  for (void* p : h->allocs) (void)hipFree(p);
+  h->allocs.clear();
+  for (auto& e : h->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->st) (void)hipStreamDestroy(h->st);
+}
+
+void host_initial_guess(HostStream& H, double* pose) {
+  // LaserMapping::input (laser_mapping.cpp:206-207)
+  dq qm{H.q_wmap_wodom[0], H.q_wmap_wodom[1], H.q_wmap_wodom[2], H.q_wmap_wodom[3]};
+  dq qo{H.q_wodom[0], H.q_wodom[1], H.q_wodom[2], H.q_wodom[3]};
+  dq q = qmul(qm, qo);
+  d3 r = qrot(qm, d3{H.t_wodom[0], H.t_wodom[1], H.t_wodom[2]});
+  pose[0] = q.x; pose[1] = q.y; pose[2] = q.z; pose[3] = q.w;
+  pose[4] = r.x + H.t_wmap_wodom[0];
+  pose[5] = r.y + H.t_wmap_wodom[1];
+  pose[6] = r.z + H.t_wmap_wodom[2];
+}
+
+void host_transform_update(HostStream& H) {
+  // LaserMapping::transformUpdate (laser_mapping.cpp:147-151)
+  dq qw{H.pose[0], H.pose[1], H.pose[2], H.pose[3]};
+  dq qo{H.q_wodom[0], H.q_wodom[1], H.q_wodom[2], H.q_wodom[3]};
+  dq qm = qmul(qw, qinv(qo));
+  d3 r = qrot(qm, d3{H.t_wodom[0], H.t_wodom[1], H.t_wodom[2]});
+  H.q_wmap_wodom[0] = qm.x; H.q_wmap_wodom[1] = qm.y; H.q_wmap_wodom[2] = qm.z; H.q_wmap_wodom[3] = qm.w;
+  H.t_wmap_wodom[0] = H.pose[4] - r.x;
+  H.t_wmap_wodom[1] = H.pose[5] - r.y;
+  H.t_wmap_wodom[2] = H.pose[6] - r.z;
+}
+
+int32_t check_stream(loam_mapper* h, int32_t s) {
+  if (!h) {
+    set_error("null mapper handle");
+    return LOAM_ERR_ARG;
+  }
+  if (s < 0 || s >= h->B) {
+    set_error("stream index out of range");
+    return LOAM_ERR_ARG;
+  }
+  return LOAM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_streams, loam_mapper** out) {
+  if (!out || n_streams <= 0) {
+    set_error("loam_mapper_create: bad arguments");
+    return LOAM_ERR_ARG;
+  }
+  *out = nullptr;
+  TRY(ensure_device(device));
+  LOAM_HIP(hipSetDevice(device));
+  auto* h = new loam_mapper;
+  if (p) h->P = *p; else loam_params_default(&h->P);
+  h->dev = device;
+  h->B = n_streams;
+  MapperDev& D = h->D;
+  D.B = n_streams;
+  D.max_in = h->P.max_input_points;
+  D.map_cap = h->P.max_map_points;
+  D.sub_cap = h->P.max_submap_points;
+  D.hash_T = (int)next_pow2((uint32_t)D.sub_cap);
+  D.scratch_cap = D.sub_cap + D.max_in;
+  D.max_chunks = (2 * D.max_in + LM_CHUNK - 1) / LM_CHUNK;
+  D.leaf[0] = (float)h->P.mapping_line_resolution;
+  D.leaf[1] = (float)h->P.mapping_plane_resolution;
+  const size_t B = n_streams;
+  auto fail = [&](int32_t rc) {
+    free_all(h);
+    delete h;
+    return rc;
+  };
+  int32_t rc = LOAM_OK;
+#define ALLOC(ptr, n) \
+  if ((rc = dalloc(h, &(ptr), (n))) != LOAM_OK) return fail(rc)
+  if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess) return fail(LOAM_ERR_HIP);
+  for (auto& e : h->ev)
+    if (hipEventCreate(&e) != hipSuccess) return fail(LOAM_ERR_HIP);
+  ALLOC(D.fr, B);
+  for (int m = 0; m < 2; ++m) {
+    ALLOC(D.in_pts[m], B * D.max_in);
+    ALLOC(D.stack[m], B * D.max_in);
+  }
+  ALLOC(D.arena, B * 2 * 2 * (size_t)D.map_cap);
+  ALLOC(h->cube_tab[0], B * 2 * NCUBE);
+  ALLOC(h->cube_tab[1], B * 2 * NCUBE);
+  ALLOC(D.extra_flag, B * 2 * NCUBE);
+  ALLOC(D.hkey, B * 2 * (size_t)D.hash_T);
+  ALLOC(D.hcnt, B * 2 * (size_t)D.hash_T);
+  ALLOC(D.hstart, B * 2 * (size_t)D.hash_T);
+  ALLOC(D.sub_lin, B * 2 * (size_t)D.sub_cap);
+  ALLOC(D.spts, B * 2 * (size_t)D.sub_cap);
+  ALLOC(D.pt_slot, B * 2 * (size_t)D.sub_cap);
+  ALLOC(D.pt_rank, B * 2 * (size_t)D.sub_cap);
+  ALLOC(D.r_type, B * 2 * (size_t)D.max_in);
+  ALLOC(D.r_px, B * 2 * (size_t)D.max_in);
+  ALLOC(D.r_py, B * 2 * (size_t)D.max_in);
+  ALLOC(D.r_pz, B * 2 * (size_t)D.max_in);
+  for (int k = 0; k < 3; ++k) {
+    ALLOC(D.r_a[k], B * 2 * (size_t)D.max_in);
+    ALLOC(D.r_b[k], B * 2 * (size_t)D.max_in);
+  }
+  ALLOC(D.ins_pts, B * 2 * (size_t)D.max_in);
+  ALLOC(D.ins_tag, B * 2 * (size_t)D.max_in);
+  ALLOC(D.vx_pts, B * 2 * (size_t)D.scratch_cap);
+  ALLOC(D.vx_idx, B * 2 * (size_t)D.scratch_cap);
+  ALLOC(D.partials, B * (size_t)D.max_chunks * LM_NACC);
+  ALLOC(D.tickets, B);
+  ALLOC(h->d_corr_blk, B + 1);
+  ALLOC(h->d_lm_blk, B + 1);
+  ALLOC(h->d_pairs, B * 2);
+  ALLOC(h->d_new_off, B * 2 * (NCUBE + 1));
+#undef ALLOC
+  D.cube_tab = h->cube_tab[0];
+  D.corr_blk = h->d_corr_blk;
+  D.lm_blk = h->d_lm_blk;
+  h->hf.assign(B, StreamFrame{});
+  h->hs.assign(B, HostStream{});
+  for (size_t s = 0; s < B; ++s) {
+    StreamFrame& F = h->hf[s];
+    F.cen[0] = 10; F.cen[1] = 10; F.cen[2] = 5;
+    F.pose[3] = 1.0;
+  }
+  *out = h;
+  return LOAM_OK;
+}
+
+int32_t loam_mapper_destroy(loam_mapper* h) {
+  if (!h) return LOAM_ERR_ARG;
+  (void)hipSetDevice(h->dev);
+  free_all(h);
+  delete h;
+  return LOAM_OK;
+}
+
+int32_t loam_mapper_reset(loam_mapper* h) {
+  if (!h) return LOAM_ERR_ARG;
+  LOAM_HIP(hipSetDevice(h->dev));
+  for (int p = 0; p < 2; ++p)
+    LOAM_HIP(hipMemsetAsync(h->cube_tab[p], 0, sizeof(uint2) * h->B * 2 * NCUBE, h->st));
+  LOAM_HIP(hipStreamSynchronize(h->st));
+  for (int s = 0; s < h->B; ++s) {
+    h->hf[s] = StreamFrame{};
+    h->hf[s].cen[0] = 10; h->hf[s].cen[1] = 10; h->hf[s].cen[2] = 5;
+    h->hf[s].pose[3] = 1.0;
+    h->hs[s] = HostStream{};
+  }
+  return LOAM_OK;
+}
+
+static int32_t mapper_input_common(loam_mapper* h, int32_t s, const float* corner, int32_t nc,
+                                   const float* surf, int32_t ns, const double* q_wodom,
+                                   const double* t_wodom, int32_t skip, hipMemcpyKind kind) {
+  TRY(check_stream(h, s));
+  if (!q_wodom || !t_wodom || nc < 0 || ns < 0 || (nc > 0 && !corner) || (ns > 0 && !surf)) {
+    set_error("loam_mapper_input: bad arguments");
+    return LOAM_ERR_ARG;
+  }
+  if (nc > h->D.max_in || ns > h->D.max_in) {
+    set_error("loam_mapper_input: cloud larger than max_input_points");
+    return LOAM_ERR_CAPACITY;
+  }
+  LOAM_HIP(hipSetDevice(h->dev));
+  HostStream& H = h->hs[s];
+  for (int i = 0; i < 4; ++i) H.q_wodom[i] = q_wodom[i];
+  for (int i = 0; i < 3; ++i) H.t_wodom[i] = t_wodom[i];
+  H.skip = skip != 0;
+  if (H.skip) {  // laser_mapping.cpp:197-201: high-frequency pose only
+    double pose[7];
+    host_initial_guess(H, pose);
+    for (int i = 0; i < 4; ++i) H.q_hf[i] = pose[i];
+    for (int i = 0; i < 3; ++i) H.t_hf[i] = pose[4 + i];
+    H.pending = false;
+    return LOAM_OK;
+  }
+  StreamFrame& F = h->hf[s];
+  F.nc_in = nc;
+  F.ns_in = ns;
+  if (nc)
+    LOAM_HIP(hipMemcpyAsync(h->D.in_pts[0] + (size_t)s * h->D.max_in, corner, sizeof(float4) * nc, kind, h->st));
+  if (ns)
+    LOAM_HIP(hipMemcpyAsync(h->D.in_pts[1] + (size_t)s * h->D.max_in, surf, sizeof(float4) * ns, kind, h->st));
+  host_initial_guess(H, H.pose);
+  H.pending = true;
+  return LOAM_OK;
+}
+
+int32_t loam_mapper_input(loam_mapper* h, int32_t s, const float* corner, int32_t nc, const float* surf,
+                          int32_t ns, const double* q_wodom, const double* t_wodom, int32_t skip) {
+  return mapper_input_common(h, s, corner, nc, surf, ns, q_wodom, t_wodom, skip, hipMemcpyHostToDevice);
+}
+
+int32_t loam_mapper_input_device(loam_mapper* h, int32_t s, const float* corner, int32_t nc,
+                                 const float* surf, int32_t ns, const double* q_wodom,
+                                 const double* t_wodom, int32_t skip) {
+  return mapper_input_common(h, s, corner, nc, surf, ns, q_wodom, t_wodom, skip, hipMemcpyDeviceToDevice);
+}
+
+int32_t loam_mapper_solve(loam_mapper* h) {
+  if (!h) return LOAM_ERR_ARG;
+  LOAM_HIP(hipSetDevice(h->dev));
+  MapperDev& D = h->D;
+  const int B = h->B;
+  bool any = false, any_shift = false;
+  h->corr_blk.assign(B + 1, 0);
+  h->lm_blk.assign(B + 1, 0);
+  for (int s = 0; s < B; ++s) {
+    StreamFrame& F = h->hf[s];
+    HostStream& H = h->hs[s];
+    F.active = H.pending ? 1 : 0;
+    F.shift[0] = F.shift[1] = F.shift[2] = 0;
+    F.err = 0;
+    F.nc_stack = F.ns_stack = 0;
+    F.corner_num[0] = F.corner_num[1] = F.surf_num[0] = F.surf_num[1] = 0;
+    F.sub_n[0] = F.sub_n[1] = 0;
+    F.optimize = 0;
+    int nrec = 0;
+    if (F.active) {
+      any = true;
+      for (int i = 0; i < 7; ++i) F.pose[i] = H.pose[i];
+      // centerCube + recentering (laser_mapping.cpp:228-444)
+      int cI = cube_of(F.pose[4], F.cen[0]), cJ = cube_of(F.pose[5], F.cen[1]), cK = cube_of(F.pose[6], F.cen[2]);
+      const int dims[3] = {CW, CH, CD};
+      int c3[3] = {cI, cJ, cK};
+      for (int a = 0; a < 3; ++a) {
+        while (c3[a] < 3) { c3[a]++; F.cen[a]++; F.shift[a]++; }
+        while (c3[a] >= dims[a] - 3) { c3[a]--; F.cen[a]--; F.shift[a]--; }
+        if (F.shift[a]) any_shift = true;
+      }
+      F.center[0] = c3[0]; F.center[1] = c3[1]; F.center[2] = c3[2];
+      int vn = 0;
+      for (int i = c3[0] - 2; i <= c3[0] + 2; i++)
+        for (int j = c3[1] - 2; j <= c3[1] + 2; j++)
+          for (int k = c3[2] - 1; k <= c3[2] + 1; k++)
+            if (i >= 0 && i < CW && j >= 0 && j < CH && k >= 0 && k < CD) F.window[vn++] = i + CW * j + CW * CH * k;
+      F.valid_num = vn;
+      // hash cell origin: world metres of the window's low corner, minus a 2-cell margin
+      F.origin[0] = (c3[0] - 2 - F.cen[0]) * 50 - 25 - 2;
+      F.origin[1] = (c3[1] - 2 - F.cen[1]) * 50 - 25 - 2;
+      F.origin[2] = (c3[2] - 1 - F.cen[2]) * 50 - 25 - 2;
+      nrec = F.nc_in + F.ns_in;
+    }
+    h->corr_blk[s + 1] = h->corr_blk[s] + (F.active ? std::max(1, (nrec + CORR_THREADS - 1) / CORR_THREADS) : 0);
+    h->lm_blk[s + 1] = h->lm_blk[s] + std::max(1, (nrec + LM_CHUNK - 1) / LM_CHUNK) * (F.active ? 1 : 0);
+  }
+  if (!any) return LOAM_OK;
+  h->frame_counter++;
+  D.epoch = h->frame_counter;
+  D.cube_tab = h->cube_tab[h->parity];
+  hipStream_t st = h->st;
+  LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(StreamFrame) * B, hipMemcpyHostToDevice, st));
+  LOAM_HIP(hipMemcpyAsync(h->d_corr_blk, h->corr_blk.data(), sizeof(int) * (B + 1), hipMemcpyHostToDevice, st));
+  LOAM_HIP(hipMemcpyAsync(h->d_lm_blk, h->lm_blk.data(), sizeof(int) * (B + 1), hipMemcpyHostToDevice, st));
+  LOAM_HIP(hipEventRecord(h->ev[0], st));
+  if (any_shift) {
+    k_shift_cubes<<<dim3(16, B), 256, 0, st>>>(D, h->cube_tab[h->parity], h->cube_tab[1 - h->parity]);
+    h->parity ^= 1;
+    D.cube_tab = h->cube_tab[h->parity];
+  }
+  k_stack_ds<<<B * 2, VX_THREADS, 0, st>>>(D);
+  k_submap_prep<<<(B + 63) / 64, 64, 0, st>>>(D);
+  LOAM_HIP(hipEventRecord(h->ev[1], st));
+  k_submap_insert<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D);
+  k_submap_alloc<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D);
+  k_submap_scatter<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D);
+  const int ncorr = h->corr_blk[B], nlm = h->lm_blk[B];
+  for (int round = 0; round < 2; ++round) {
+    if (ncorr > 0) k_correspond<<<ncorr, CORR_THREADS, 0, st>>>(D, round);
+    for (int it = 0; it < 5; ++it) k_lm_pass<<<nlm, LM_THREADS, 0, st>>>(D, round);
+    k_lm_finish<<<(B + 63) / 64, 64, 0, st>>>(D, round);
+  }
+  LOAM_HIP(hipEventRecord(h->ev[2], st));
+  k_insert<<<dim3(16, B), 256, 0, st>>>(D);
+  k_revox<<<B * 2 * (WIN_VALID_MAX + EXTRA_CAP), VX_THREADS, 0, st>>>(D);
+  LOAM_HIP(hipGetLastError());
+  LOAM_HIP(hipEventRecord(h->ev[3], st));
+  LOAM_HIP(hipMemcpyAsync(h->hf.data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
+  LOAM_HIP(hipStreamSynchronize(st));
+  float ms_total = 0, ms_opt = 0;
+  LOAM_HIP(hipEventElapsedTime(&ms_total, h->ev[0], h->ev[3]));
+  LOAM_HIP(hipEventElapsedTime(&ms_opt, h->ev[1], h->ev[2]));
+  // host bookkeeping + compaction decisions
+  std::vector<int> pairs;
+  int32_t status = LOAM_OK;
+  for (int s = 0; s < B; ++s) {
+    StreamFrame& F = h->hf[s];
+    HostStream& H = h->hs[s];
+    if (!F.active) continue;
+    H.pending = false;
+    for (int i = 0; i < 7; ++i) H.pose[i] = F.pose[i];
+    host_transform_update(H);
+    H.frame++;
+    loam_map_stats& S = H.st;
+    S.optimized = F.optimize;
+    S.corner_stack = F.nc_stack;
+    S.surf_stack = F.ns_stack;
+    S.corner_map = F.sub_n[0];
+    S.surf_map = F.sub_n[1];
+    for (int r = 0; r < 2; ++r) {
+      S.corner_num[r] = F.corner_num[r];
+      S.surf_num[r] = F.surf_num[r];
+      const LmState& L = F.lm[r];
+      S.lm[r].iterations = F.optimize ? L.iteration : 0;
+      S.lm[r].successful = L.successful;
+      S.lm[r].invalid = L.invalid;
+      S.lm[r].termination = L.term;
+      S.lm[r].initial_cost = L.initial_cost;
+      S.lm[r].final_cost = L.min_cost;
+    }
+    for (int a = 0; a < 3; ++a) S.center[a] = F.center[a];
+    S.valid_num = F.valid_num;
+    S.ms_total = ms_total;
+    S.ms_opt = ms_opt;
+    if (F.err) {
+      set_error("loam_mapper_solve: device capacity exceeded (err flags " + std::to_string(F.err) + ")");
+      status = LOAM_ERR_CAPACITY;
+    }
+    for (int m = 0; m < 2; ++m)
+      if (F.arena_tail[m] > (uint32_t)D.map_cap / 2) pairs.push_back(s * 2 + m);
+  }
+  if (!pairs.empty()) {
+    const int np = (int)pairs.size();
+    LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(StreamFrame) * B, hipMemcpyHostToDevice, st));
+    LOAM_HIP(hipMemcpyAsync(h->d_pairs, pairs.data(), sizeof(int) * np, hipMemcpyHostToDevice, st));
+    k_compact_scan<<<np, VX_THREADS, 0, st>>>(D, h->d_pairs, h->d_new_off);
+    k_compact_copy<<<dim3(256, np), 256, 0, st>>>(D, h->d_pairs, h->d_new_off);
+    k_compact_commit<<<np, 256, 0, st>>>(D, h->d_pairs, np, h->d_new_off);
+    LOAM_HIP(hipGetLastError());
+    LOAM_HIP(hipMemcpyAsync(h->hf.data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
+    LOAM_HIP(hipStreamSynchronize(st));
+    for (int p : pairs) {
+      const StreamFrame& F = h->hf[p >> 1];
+      if (F.arena_tail[p & 1] > (uint32_t)D.map_cap / 2) {
+        set_error("loam_mapper_solve: live map exceeds half of max_map_points");
+        status = LOAM_ERR_CAPACITY;
+      }
+    }
+  }
+  return status;
+}
+
+int32_t loam_mapper_pose(loam_mapper* h, int32_t s, double* q_w, double* t_w) {
+  TRY(check_stream(h, s));
+  if (!q_w || !t_w) return LOAM_ERR_ARG;
+  const HostStream& H = h->hs[s];
+  if (H.skip) {
+    for (int i = 0; i < 4; ++i) q_w[i] = H.q_hf[i];
+    for (int i = 0; i < 3; ++i) t_w[i] = H.t_hf[i];
+  } else {
+    for (int i = 0; i < 4; ++i) q_w[i] = H.pose[i];
+    for (int i = 0; i < 3; ++i) t_w[i] = H.pose[4 + i];
+  }
+  return LOAM_OK;
+}
+
+int32_t loam_mapper_stats(loam_mapper* h, int32_t s, loam_map_stats* st) {
+  TRY(check_stream(h, s));
+  if (!st) return LOAM_ERR_ARG;
+  *st = h->hs[s].st;
+  return LOAM_OK;
+}
+
+int32_t loam_mapper_get_state(loam_mapper* h, int32_t s, int32_t* cen, double* q, double* t) {
+  TRY(check_stream(h, s));
+  if (!cen || !q || !t) return LOAM_ERR_ARG;
+  for (int a = 0; a < 3; ++a) cen[a] = h->hf[s].cen[a];
+  for (int i = 0; i < 4; ++i) q[i] = h->hs[s].q_wmap_wodom[i];
+  for (int i = 0; i < 3; ++i) t[i] = h->hs[s].t_wmap_wodom[i];
+  return LOAM_OK;
+}
+
+int32_t loam_mapper_set_state(loam_mapper* h, int32_t s, const int32_t* cen, const double* q, const double* t) {
+  TRY(check_stream(h, s));
+  if (!cen || !q || !t) return LOAM_ERR_ARG;
+  for (int a = 0; a < 3; ++a) h->hf[s].cen[a] = cen[a];
+  for (int i = 0; i < 4; ++i) h->hs[s].q_wmap_wodom[i] = q[i];
+  for (int i = 0; i < 3; ++i) h->hs[s].t_wmap_wodom[i] = t[i];
+  return LOAM_OK;
+}
+
+int32_t loam_mapper_cube_count(loam_mapper* h, int32_t s, int32_t which, int32_t cube) {
+  TRY(check_stream(h, s));
+  if (which < 0 || which > 1 || cube < 0 || cube >= NCUBE) return LOAM_ERR_ARG;
+  LOAM_HIP(hipSetDevice(h->dev));
+  uint2 v;
+  LOAM_HIP(hipMemcpy(&v, h->cube_tab[h->parity] + ((size_t)s * 2 + which) * NCUBE + cube, sizeof(uint2), hipMemcpyDeviceToHost));
+  return (int32_t)v.y;
+}
+
+int32_t loam_mapper_cube_copy(loam_mapper* h, int32_t s, int32_t which, int32_t cube, float* out) {
+  TRY(check_stream(h, s));
+  if (which < 0 || which > 1 || cube < 0 || cube >= NCUBE || !out) return LOAM_ERR_ARG;
+  LOAM_HIP(hipSetDevice(h->dev));
+  uint2 v;
+  LOAM_HIP(hipMemcpy(&v, h->cube_tab[h->parity] + ((size_t)s * 2 + which) * NCUBE + cube, sizeof(uint2), hipMemcpyDeviceToHost));
+  const float4* base = h->D.arena + (((size_t)s * 2 + which) * 2 + h->hf[s].arena_active[which]) * (size_t)h->D.map_cap;
+  if (v.y) LOAM_HIP(hipMemcpy(out, base + v.x, sizeof(float4) * v.y, hipMemcpyDeviceToHost));
+  return (int32_t)v.y;
+}
+
+int32_t loam_mapper_cube_set(loam_mapper* h, int32_t s, int32_t which, int32_t cube, const float* pts, int32_t n) {
+  TRY(check_stream(h, s));
+  if (which < 0 || which > 1 || cube < 0 || cube >= NCUBE || n < 0 || (n > 0 && !pts)) return LOAM_ERR_ARG;
+  LOAM_HIP(hipSetDevice(h->dev));
+  StreamFrame& F = h->hf[s];
+  uint32_t& tail = F.arena_tail[which];
+  if (tail + (uint32_t)n > (uint32_t)h->D.map_cap) {
+    set_error("loam_mapper_cube_set: arena full");
+    return LOAM_ERR_CAPACITY;
+  }
+  float4* base = h->D.arena + (((size_t)s * 2 + which) * 2 + F.arena_active[which]) * (size_t)h->D.map_cap;
+  if (n) LOAM_HIP(hipMemcpy(base + tail, pts, sizeof(float4) * n, hipMemcpyHostToDevice));
+  uint2 v = make_uint2(tail, (uint32_t)n);
+  tail += n;
+  LOAM_HIP(hipMemcpy(h->cube_tab[h->parity] + ((size_t)s * 2 + which) * NCUBE + cube, &v, sizeof(uint2), hipMemcpyHostToDevice));
+  return LOAM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,381 @@
+// prims.hip — standalone entry points of the kernels behind the stages (include/loam_core.h):
+// the device LM engine on an explicit factor list, the VoxelGrid workgroup routine on one
+// cloud, and the radius-bounded kNN over the 1 m cell hash.  They share the kernels' code
+// with the stage pipelines and exist so that each kernel can be parity-tested on its own.
+#include <cmath>
+#include <vector>
+
+#include "cellhash.h"
+#include "common.h"
+#include "lm.h"
+#include "voxel.h"
+
+namespace loam {
+
+constexpr int P_LM_THREADS = 256;
+constexpr int P_LM_PER_THREAD = 4;
+constexpr int P_LM_CHUNK = P_LM_THREADS * P_LM_PER_THREAD;
+
+struct LmRecDev {
+  int* type;
+  float *px, *py, *pz;
+  double *a0, *a1, *a2, *b0, *b1, *b2;
+};
+
+__global__ void __launch_bounds__(P_LM_THREADS)
+    k_lm_pass_single(LmRecDev R, int nrec, LmState* S, double* partials, uint32_t* ticket) {
+  lm_pass_body<P_LM_THREADS, P_LM_PER_THREAD>(R.type, R.px, R.py, R.pz, R.a0, R.a1, R.a2, R.b0,
+                                              R.b1, R.b2, nrec, blockIdx.x, gridDim.x, *S,
+                                              partials, ticket);
+}
+
+// one evaluation at x: partial sums per workgroup (no state machine)
+__global__ void __launch_bounds__(P_LM_THREADS)
+    k_lm_eval(LmRecDev R, int nrec, const double* x, double* partials) {
+  __shared__ double red[P_LM_THREADS / 64][LM_NACC];
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  double X[7];
+  for (int i = 0; i < 7; ++i) X[i] = x[i];
+  double acc[LM_NACC];
+#pragma unroll
+  for (int i = 0; i < LM_NACC; ++i) acc[i] = 0.0;
+  for (int it = 0; it < P_LM_PER_THREAD; ++it) {
+    const int r = blockIdx.x * P_LM_CHUNK + it * P_LM_THREADS + tid;
+    if (r < nrec && R.type[r] != 0)
+      lm_accum(R.type[r], R.px[r], R.py[r], R.pz[r], R.a0[r], R.a1[r], R.a2[r], R.b0[r], R.b1[r],
+               R.b2[r], X, acc);
+  }
+#pragma unroll
+  for (int i = 0; i < LM_NACC; ++i) {
+    double v = wave_sum_d(acc[i]);
+    if (lane == 0) red[wid][i] = v;
+  }
+  __syncthreads();
+  if (tid < LM_NACC) {
+    double v = 0.0;
+    for (int w = 0; w < P_LM_THREADS / 64; ++w) v += red[w][tid];
+    partials[(size_t)blockIdx.x * LM_NACC + tid] = v;
+  }
+}
+
+__global__ void __launch_bounds__(VX_THREADS) k_voxel_one(VoxSeg S) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
+  voxel_segment(S, lds);
+}
+
+// standalone cell hash (one point set)
+__global__ void k_hash_insert(const float4* pts, int n, const int* origin, unsigned long long* hk,
+                              unsigned long long* hc, uint32_t mask, uint32_t epoch, uint32_t* ps,
+                              uint32_t* pr, int* err) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float4 p = pts[i];
+    uint32_t slot, rank;
+    if (!hash_claim_rank(hk, hc, mask, epoch, cell_key_rel(p.x, p.y, p.z, origin), &slot, &rank)) {
+      atomicOr(err, 1);
+      pr[i] = 0xFFFFFFFFu;
+      continue;
+    }
+    ps[i] = slot;
+    pr[i] = rank;
+  }
+}
+
+__global__ void k_hash_alloc(int n, const unsigned long long* hc, uint32_t* hs, const uint32_t* ps,
+                             const uint32_t* pr, uint32_t* cursor) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    if (pr[i] == 0) hs[ps[i]] = atomicAdd(cursor, (uint32_t)(hc[ps[i]] & 0xFFFFFFFFu));
+}
+
+__global__ void k_hash_scatter(const float4* pts, int n, const uint32_t* hs, const uint32_t* ps,
+                               const uint32_t* pr, float4* sp) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    if (pr[i] == 0xFFFFFFFFu) continue;
+    const float4 p = pts[i];
+    sp[hs[ps[i]] + pr[i]] = make_float4(p.x, p.y, p.z, __int_as_float(i));
+  }
+}
+
+__global__ void k_knn_query(const float4* q, int nq, int k, float radius2, const int* origin,
+                            const unsigned long long* hk, const unsigned long long* hc,
+                            const uint32_t* hs, const float4* sp, uint32_t mask, uint32_t epoch,
+                            int* idx, float* d2) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += gridDim.x * blockDim.x) {
+    Top5 T;
+    knn5_hash(q[i], origin, hk, hc, hs, sp, mask, epoch, radius2, T);
+    for (int j = 0; j < k; ++j) {
+      const bool ok = T.d[j] < radius2;
+      idx[(size_t)i * k + j] = ok ? T.id[j] : -1;
+      d2[(size_t)i * k + j] = ok ? T.d[j] : INFINITY;
+    }
+  }
+}
+
+// host helpers
+struct DevBuf {
+  void* p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+template <typename T>
+hipError_t dmalloc(DevBuf& b, size_t n) {
+  hipError_t e = hipMalloc(&b.p, std::max<size_t>(n, 1) * sizeof(T));
+  if (e == hipSuccess) e = hipMemset(b.p, 0, std::max<size_t>(n, 1) * sizeof(T));
+  return e;
+}
+
+struct LmHostRecs {
+  DevBuf type, px, py, pz, a0, a1, a2, b0, b1, b2;
+  LmRecDev view() {
+    return LmRecDev{(int*)type.p, (float*)px.p, (float*)py.p, (float*)pz.p, (double*)a0.p,
+                    (double*)a1.p, (double*)a2.p, (double*)b0.p, (double*)b1.p, (double*)b2.p};
+  }
+};
+
+// factor rows (10 doubles) -> device SoA records (edge: a, unit (a-b)/|a-b|)
+int32_t upload_factors(const double* f, int n, LmHostRecs& R) {
+  std::vector<int> type(n);
+  std::vector<float> px(n), py(n), pz(n);
+  std::vector<double> A[3], Bv[3];
+  for (int k = 0; k < 3; ++k) {
+    A[k].resize(n);
+    Bv[k].resize(n);
+  }
+  for (int i = 0; i < n; ++i) {
+    const double* r = f + (size_t)i * 10;
+    type[i] = (int)r[0];
+    px[i] = (float)r[1];
+    py[i] = (float)r[2];
+    pz[i] = (float)r[3];
+    if (type[i] == 1) {
+      double de[3] = {r[4] - r[7], r[5] - r[8], r[6] - r[9]};
+      double dn = std::sqrt(de[0] * de[0] + de[1] * de[1] + de[2] * de[2]);
+      for (int k = 0; k < 3; ++k) {
+        A[k][i] = r[4 + k];
+        Bv[k][i] = de[k] / dn;
+      }
+    } else {
+      for (int k = 0; k < 3; ++k) {
+        A[k][i] = r[4 + k];
+        Bv[k][i] = r[7 + k];
+      }
+    }
+  }
+  LOAM_HIP(dmalloc<int>(R.type, n));
+  LOAM_HIP(dmalloc<float>(R.px, n));
+  LOAM_HIP(dmalloc<float>(R.py, n));
+  LOAM_HIP(dmalloc<float>(R.pz, n));
+  LOAM_HIP(dmalloc<double>(R.a0, n));
+  LOAM_HIP(dmalloc<double>(R.a1, n));
+  LOAM_HIP(dmalloc<double>(R.a2, n));
+  LOAM_HIP(dmalloc<double>(R.b0, n));
+  LOAM_HIP(dmalloc<double>(R.b1, n));
+  LOAM_HIP(dmalloc<double>(R.b2, n));
+  if (n) {
+    LOAM_HIP(hipMemcpy(R.type.p, type.data(), sizeof(int) * n, hipMemcpyHostToDevice));
+    LOAM_HIP(hipMemcpy(R.px.p, px.data(), sizeof(float) * n, hipMemcpyHostToDevice));
+    LOAM_HIP(hipMemcpy(R.py.p, py.data(), sizeof(float) * n, hipMemcpyHostToDevice));
+    LOAM_HIP(hipMemcpy(R.pz.p, pz.data(), sizeof(float) * n, hipMemcpyHostToDevice));
+    LOAM_HIP(hipMemcpy(R.a0.p, A[0].data(), sizeof(double) * n, hipMemcpyHostToDevice));
+    LOAM_HIP(hipMemcpy(R.a1.p, A[1].data(), sizeof(double) * n, hipMemcpyHostToDevice));
+    LOAM_HIP(hipMemcpy(R.a2.p, A[2].data(), sizeof(double) * n, hipMemcpyHostToDevice));
+    LOAM_HIP(hipMemcpy(R.b0.p, Bv[0].data(), sizeof(double) * n, hipMemcpyHostToDevice));
+    LOAM_HIP(hipMemcpy(R.b1.p, Bv[1].data(), sizeof(double) * n, hipMemcpyHostToDevice));
+    LOAM_HIP(hipMemcpy(R.b2.p, Bv[2].data(), sizeof(double) * n, hipMemcpyHostToDevice));
+  }
+  return LOAM_OK;
+}
+
+}  // namespace loam
+
+using namespace loam;
+
+extern "C" {
+
+int32_t loam_lm_solve(int32_t device, const double* factors, int32_t n, double* x, int32_t max_it,
+                      loam_lm_stats* st) {
+  if (n < 0 || !x || (n > 0 && !factors) || max_it < 0) {
+    set_error("loam_lm_solve: bad arguments");
+    return LOAM_ERR_ARG;
+  }
+  int32_t rc = ensure_device(device);
+  if (rc != LOAM_OK) return rc;
+  LOAM_HIP(hipSetDevice(device));
+  LmHostRecs R;
+  rc = upload_factors(factors, n, R);
+  if (rc != LOAM_OK) return rc;
+  const int nchunks = std::max(1, (n + P_LM_CHUNK - 1) / P_LM_CHUNK);
+  LmState hS;
+  lm_init(hS, x, max_it, true);
+  DevBuf dS, dpart, dtick;
+  LOAM_HIP(dmalloc<LmState>(dS, 1));
+  LOAM_HIP(dmalloc<double>(dpart, (size_t)nchunks * LM_NACC));
+  LOAM_HIP(dmalloc<uint32_t>(dtick, 1));
+  LOAM_HIP(hipMemcpy(dS.p, &hS, sizeof(LmState), hipMemcpyHostToDevice));
+  for (int it = 0; it <= max_it; ++it)
+    k_lm_pass_single<<<nchunks, P_LM_THREADS>>>(R.view(), n, (LmState*)dS.p, (double*)dpart.p,
+                                                 (uint32_t*)dtick.p);
+  LOAM_HIP(hipGetLastError());
+  LOAM_HIP(hipMemcpy(&hS, dS.p, sizeof(LmState), hipMemcpyDeviceToHost));
+  if (hS.status != LM_DONE) {
+    set_error("loam_lm_solve: state machine did not terminate");
+    return LOAM_ERR_STATE;
+  }
+  for (int i = 0; i < 7; ++i) x[i] = hS.best[i];
+  if (st) {
+    st->iterations = hS.iteration;
+    st->successful = hS.successful;
+    st->invalid = hS.invalid;
+    st->termination = hS.term;
+    st->initial_cost = hS.initial_cost;
+    st->final_cost = hS.min_cost;
+  }
+  return LOAM_OK;
+}
+
+int32_t loam_lm_normal_equations(int32_t device, const double* factors, int32_t n, const double* x,
+                                 double* cost, double* jtj, double* jtr) {
+  if (n < 0 || !x || !cost || !jtj || !jtr || (n > 0 && !factors)) {
+    set_error("loam_lm_normal_equations: bad arguments");
+    return LOAM_ERR_ARG;
+  }
+  int32_t rc = ensure_device(device);
+  if (rc != LOAM_OK) return rc;
+  LOAM_HIP(hipSetDevice(device));
+  LmHostRecs R;
+  rc = upload_factors(factors, n, R);
+  if (rc != LOAM_OK) return rc;
+  const int nchunks = std::max(1, (n + P_LM_CHUNK - 1) / P_LM_CHUNK);
+  DevBuf dx, dpart;
+  LOAM_HIP(dmalloc<double>(dx, 7));
+  LOAM_HIP(dmalloc<double>(dpart, (size_t)nchunks * LM_NACC));
+  LOAM_HIP(hipMemcpy(dx.p, x, sizeof(double) * 7, hipMemcpyHostToDevice));
+  k_lm_eval<<<nchunks, P_LM_THREADS>>>(R.view(), n, (const double*)dx.p, (double*)dpart.p);
+  LOAM_HIP(hipGetLastError());
+  std::vector<double> part((size_t)nchunks * LM_NACC);
+  LOAM_HIP(hipMemcpy(part.data(), dpart.p, sizeof(double) * part.size(), hipMemcpyDeviceToHost));
+  double red[LM_NACC] = {0};
+  for (int c = 0; c < nchunks; ++c)
+    for (int i = 0; i < LM_NACC; ++i) red[i] += part[(size_t)c * LM_NACC + i];
+  *cost = red[27];
+  for (int r = 0; r < 6; ++r)
+    for (int c = 0; c < 6; ++c) jtj[r * 6 + c] = red[ut_index(r < c ? r : c, r < c ? c : r)];
+  for (int i = 0; i < 6; ++i) jtr[i] = red[21 + i];
+  return (int32_t)red[28];
+}
+
+int32_t loam_voxel_grid(int32_t device, const float* in, int32_t n, float leaf, float* out, int32_t* n_out) {
+  if (n < 0 || (n > 0 && (!in || !out)) || !n_out || !(leaf > 0.f)) {
+    set_error("loam_voxel_grid: bad arguments");
+    return LOAM_ERR_ARG;
+  }
+  int32_t rc = ensure_device(device);
+  if (rc != LOAM_OK) return rc;
+  LOAM_HIP(hipSetDevice(device));
+  DevBuf din, dout, dsp, dsi, dcnt, derr;
+  LOAM_HIP(dmalloc<float4>(din, n));
+  LOAM_HIP(dmalloc<float4>(dout, n));
+  LOAM_HIP(dmalloc<float4>(dsp, n));
+  LOAM_HIP(dmalloc<int>(dsi, n));
+  LOAM_HIP(dmalloc<uint32_t>(dcnt, 1));
+  LOAM_HIP(dmalloc<int>(derr, 1));
+  if (n) LOAM_HIP(hipMemcpy(din.p, in, sizeof(float4) * n, hipMemcpyHostToDevice));
+  VoxSeg S{};
+  S.src0 = (const float4*)din.p;
+  S.n0 = n;
+  S.leaf = leaf;
+  S.out = (float4*)dout.p;
+  S.cap = (uint32_t)n;
+  S.res_cnt = (uint32_t*)dcnt.p;
+  S.scratch_pts = (float4*)dsp.p;
+  S.scratch_idx = (int*)dsi.p;
+  S.scratch_cap = (uint32_t)n;
+  S.err = (int*)derr.p;
+  k_voxel_one<<<1, VX_THREADS>>>(S);
+  LOAM_HIP(hipGetLastError());
+  uint32_t cnt = 0;
+  int err = 0;
+  LOAM_HIP(hipMemcpy(&cnt, dcnt.p, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  LOAM_HIP(hipMemcpy(&err, derr.p, sizeof(int), hipMemcpyDeviceToHost));
+  if (err) {
+    set_error("loam_voxel_grid: more unique voxels than the LDS capacity");
+    return LOAM_ERR_CAPACITY;
+  }
+  if (cnt) LOAM_HIP(hipMemcpy(out, dout.p, sizeof(float4) * cnt, hipMemcpyDeviceToHost));
+  *n_out = (int32_t)cnt;
+  return LOAM_OK;
+}
+
+int32_t loam_knn_radius(int32_t device, const float* pts, int32_t n, const float* queries, int32_t nq,
+                        int32_t k, float radius2, int32_t* idx, float* d2) {
+  if (n < 0 || nq < 0 || k < 1 || k > 5 || !(radius2 > 0.f) || radius2 > 1.0f ||
+      (n > 0 && !pts) || (nq > 0 && (!queries || !idx || !d2))) {
+    set_error("loam_knn_radius: bad arguments (k in 1..5, 0 < radius2 <= 1)");
+    return LOAM_ERR_ARG;
+  }
+  int32_t rc = ensure_device(device);
+  if (rc != LOAM_OK) return rc;
+  LOAM_HIP(hipSetDevice(device));
+  // origin: 2-cell margin below the bounding box of points and queries; 9-bit cells
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int i = 0; i < n; ++i)
+    for (int a = 0; a < 3; ++a) {
+      mn[a] = std::min(mn[a], pts[i * 4 + a]);
+      mx[a] = std::max(mx[a], pts[i * 4 + a]);
+    }
+  int origin[3];
+  for (int a = 0; a < 3; ++a) {
+    origin[a] = n ? (int)std::floor(mn[a]) - 2 : 0;
+    if (n && std::floor(mx[a]) - origin[a] > 509) {
+      set_error("loam_knn_radius: point cloud spans more than 509 m");
+      return LOAM_ERR_ARG;
+    }
+  }
+  uint32_t T = 1;
+  while (T < (uint32_t)std::max(2 * n, 64)) T <<= 1;
+  DevBuf dp, dq, dorig, dhk, dhc, dhs, dps, dpr, dsp, dcur, derr, didx, dd2;
+  LOAM_HIP(dmalloc<float4>(dp, n));
+  LOAM_HIP(dmalloc<float4>(dq, nq));
+  LOAM_HIP(dmalloc<int>(dorig, 3));
+  LOAM_HIP(dmalloc<unsigned long long>(dhk, T));
+  LOAM_HIP(dmalloc<unsigned long long>(dhc, T));
+  LOAM_HIP(dmalloc<uint32_t>(dhs, T));
+  LOAM_HIP(dmalloc<uint32_t>(dps, n));
+  LOAM_HIP(dmalloc<uint32_t>(dpr, n));
+  LOAM_HIP(dmalloc<float4>(dsp, n));
+  LOAM_HIP(dmalloc<uint32_t>(dcur, 1));
+  LOAM_HIP(dmalloc<int>(derr, 1));
+  LOAM_HIP(dmalloc<int>(didx, (size_t)nq * k));
+  LOAM_HIP(dmalloc<float>(dd2, (size_t)nq * k));
+  if (n) LOAM_HIP(hipMemcpy(dp.p, pts, sizeof(float4) * n, hipMemcpyHostToDevice));
+  if (nq) LOAM_HIP(hipMemcpy(dq.p, queries, sizeof(float4) * nq, hipMemcpyHostToDevice));
+  LOAM_HIP(hipMemcpy(dorig.p, origin, sizeof(origin), hipMemcpyHostToDevice));
+  const uint32_t epoch = 1;
+  const int blocks = 256;
+  k_hash_insert<<<blocks, 256>>>((const float4*)dp.p, n, (const int*)dorig.p, (unsigned long long*)dhk.p,
+                                 (unsigned long long*)dhc.p, T - 1, epoch, (uint32_t*)dps.p,
+                                 (uint32_t*)dpr.p, (int*)derr.p);
+  k_hash_alloc<<<blocks, 256>>>(n, (const unsigned long long*)dhc.p, (uint32_t*)dhs.p,
+                                (const uint32_t*)dps.p, (const uint32_t*)dpr.p, (uint32_t*)dcur.p);
+  k_hash_scatter<<<blocks, 256>>>((const float4*)dp.p, n, (const uint32_t*)dhs.p, (const uint32_t*)dps.p,
+                                  (const uint32_t*)dpr.p, (float4*)dsp.p);
+  k_knn_query<<<blocks, 256>>>((const float4*)dq.p, nq, k, radius2, (const int*)dorig.p,
+                               (const unsigned long long*)dhk.p, (const unsigned long long*)dhc.p,
+                               (const uint32_t*)dhs.p, (const float4*)dsp.p, T - 1, epoch, (int*)didx.p,
+                               (float*)dd2.p);
+  LOAM_HIP(hipGetLastError());
+  if (nq) {
+    LOAM_HIP(hipMemcpy(idx, didx.p, sizeof(int) * (size_t)nq * k, hipMemcpyDeviceToHost));
+    LOAM_HIP(hipMemcpy(d2, dd2.p, sizeof(float) * (size_t)nq * k, hipMemcpyDeviceToHost));
+  }
+  int err = 0;
+  LOAM_HIP(hipMemcpy(&err, derr.p, sizeof(int), hipMemcpyDeviceToHost));
+  if (err) {
+    set_error("loam_knn_radius: hash table full");
+    return LOAM_ERR_CAPACITY;
+  }
+  return LOAM_OK;
+}
+
+}  // extern "C"

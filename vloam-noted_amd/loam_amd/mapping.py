@@ -1,0 +1,135 @@
+"""LaserMapping on MI355X — host mirror of the reference interface.
+
+Mirrors ``vloam::LaserMapping`` (src/lidar_odometry_mapping/include/lidar_odometry_mapping/
+laser_mapping.h:85-100): ``init`` / ``reset`` / ``input`` / ``solveMapping`` / ``output``,
+same argument meaning (clouds are (n, 4) float32 x, y, z, intensity = pcl::PointXYZI;
+quaternions xyzw like ``parameters[0..3]``).  The ROS publishers are not part of the core:
+``output`` returns what ``publish`` would send (laser_mapping.cpp:816-911).
+
+``BatchMapper`` exposes the batched form: n independent streams per handle, one set of
+kernel launches per ``solve`` for all of them.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _core
+from ._core import check, f32x4, lib, ptr
+
+N_CUBES = 21 * 21 * 11
+
+
+class BatchMapper:
+    def __init__(self, n_streams=1, device=0, params=None, **param_overrides):
+        self.params = params if params is not None else _core.default_params(**param_overrides)
+        self.n_streams = n_streams
+        self.device = device
+        h = ctypes.c_void_p()
+        check(lib().loam_mapper_create(ctypes.byref(self.params), device, n_streams, ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().loam_mapper_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self):
+        check(lib().loam_mapper_reset(self.h))
+
+    def input(self, stream, corner, surf, q_wodom, t_wodom, skip_frame=False):
+        c, s = f32x4(corner), f32x4(surf)
+        q = np.ascontiguousarray(q_wodom, dtype=np.float64)
+        t = np.ascontiguousarray(t_wodom, dtype=np.float64)
+        check(lib().loam_mapper_input(self.h, stream, ptr(c), len(c), ptr(s), len(s),
+                                      ptr(q), ptr(t), int(skip_frame)))
+
+    def input_device(self, stream, corner_ptr, n_corner, surf_ptr, n_surf, q_wodom, t_wodom,
+                     skip_frame=False):
+        q = np.ascontiguousarray(q_wodom, dtype=np.float64)
+        t = np.ascontiguousarray(t_wodom, dtype=np.float64)
+        check(lib().loam_mapper_input_device(self.h, stream, corner_ptr, n_corner, surf_ptr,
+                                             n_surf, ptr(q), ptr(t), int(skip_frame)))
+
+    def solve(self):
+        check(lib().loam_mapper_solve(self.h))
+
+    def pose(self, stream=0):
+        q = np.empty(4)
+        t = np.empty(3)
+        check(lib().loam_mapper_pose(self.h, stream, ptr(q), ptr(t)))
+        return q, t
+
+    def stats(self, stream=0):
+        st = _core.MapStats()
+        check(lib().loam_mapper_stats(self.h, stream, ctypes.byref(st)))
+        return st
+
+    def get_state(self, stream=0):
+        cen = np.empty(3, dtype=np.int32)
+        q = np.empty(4)
+        t = np.empty(3)
+        check(lib().loam_mapper_get_state(self.h, stream, ptr(cen), ptr(q), ptr(t)))
+        return cen, q, t
+
+    def set_state(self, stream, cen, q_wmap_wodom, t_wmap_wodom):
+        cen = np.ascontiguousarray(cen, dtype=np.int32)
+        q = np.ascontiguousarray(q_wmap_wodom, dtype=np.float64)
+        t = np.ascontiguousarray(t_wmap_wodom, dtype=np.float64)
+        check(lib().loam_mapper_set_state(self.h, stream, ptr(cen), ptr(q), ptr(t)))
+
+    def cube(self, stream, which, cube):
+        n = check(lib().loam_mapper_cube_count(self.h, stream, which, cube))
+        out = np.empty((n, 4), dtype=np.float32)
+        if n:
+            check(lib().loam_mapper_cube_copy(self.h, stream, which, cube, ptr(out)))
+        return out
+
+    def set_cube(self, stream, which, cube, pts):
+        pts = f32x4(pts)
+        check(lib().loam_mapper_cube_set(self.h, stream, which, cube, ptr(pts), len(pts)))
+
+    def cubes(self, stream, which):
+        out = {}
+        for c in range(N_CUBES):
+            if check(lib().loam_mapper_cube_count(self.h, stream, which, c)) > 0:
+                out[c] = self.cube(stream, which, c)
+        return out
+
+
+class LaserMapping:
+    """Single-stream drop-in with the reference method names."""
+
+    def __init__(self, device=0, **param_overrides):
+        self._m = BatchMapper(1, device, **param_overrides)
+        self._skip = False
+
+    def init(self):
+        self._m.reset()
+
+    def reset(self):  # laser_mapping.cpp:132-136 — per-frame submap counters only
+        pass
+
+    def input(self, laserCloudCornerLast, laserCloudSurfLast, laserCloudFullRes, q_wodom_curr,
+              t_wodom_curr, skip_frame=False):
+        self._skip = bool(skip_frame)
+        self._m.input(0, laserCloudCornerLast, laserCloudSurfLast, q_wodom_curr, t_wodom_curr,
+                      skip_frame)
+
+    def solveMapping(self):
+        self._m.solve()
+
+    def output(self):
+        return self._m.pose(0)
+
+    def stats(self):
+        return self._m.stats(0)
+
+    @property
+    def batch(self):
+        return self._m
