@@ -80,6 +80,30 @@ typedef struct loam_map_stats {
 } loam_map_stats;
 
 /* --------------------------------------------------------------------------------------
+ * ScanRegistration (scan_registration.h:64-81): one frame per call, outputs stay in HBM.
+ * ------------------------------------------------------------------------------------ */
+typedef struct loam_scanreg loam_scanreg;
+
+/* ScanRegistration::init (scan_registration.cpp:42-92); scan_line 16/32/64 */
+int32_t loam_scanreg_create(const loam_params* p, int32_t device, loam_scanreg** out);
+int32_t loam_scanreg_destroy(loam_scanreg* h);
+/* ScanRegistration::input (scan_registration.cpp:144-513): n points, `stride` floats per
+ * point (x, y, z first), host or device memory */
+int32_t loam_scanreg_input(loam_scanreg* h, const float* xyz, int32_t n, int32_t stride);
+int32_t loam_scanreg_input_device(loam_scanreg* h, const float* d_xyz, int32_t n, int32_t stride);
+/* ScanRegistration::output (scan_registration.cpp:566-577): which = 0 laserCloud,
+ * 1 cornerPointsSharp, 2 cornerPointsLessSharp, 3 surfPointsFlat, 4 surfPointsLessFlat */
+int32_t loam_scanreg_counts(loam_scanreg* h, int32_t* counts5);
+/* copies cloud `which` (4 floats / point) into out (capacity cap points); returns count */
+int32_t loam_scanreg_copy(loam_scanreg* h, int32_t which, float* out, int32_t cap);
+/* device pointer of cloud `which`, valid until the next input; returns count */
+int32_t loam_scanreg_device_ptr(loam_scanreg* h, int32_t which, const float** ptr);
+/* per-point curvature and label of laserCloud (cloudCurvature / cloudLabel) */
+int32_t loam_scanreg_curvature(loam_scanreg* h, float* curv, int32_t* label, int32_t cap);
+/* device time of the last input (ms) */
+double loam_scanreg_ms(loam_scanreg* h);
+
+/* --------------------------------------------------------------------------------------
  * LaserMapping (laser_mapping.h:85-100) — a handle holds n_streams independent mappers
  * (independent sequences / vehicles) processed together by every launch.  n_streams = 1 is
  * exactly the reference's single LaserMapping object.

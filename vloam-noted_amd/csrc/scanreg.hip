@@ -1,0 +1,689 @@
+// scanreg.hip — ScanRegistration::input (scan_registration.cpp:144-513) on MI355X.
+//
+// Kernels (one frame per call; all buffers HBM-resident, outputs stay on the device for the
+// odometry / mapping stages):
+//   k_sr_valid      NaN + minimum-range filter (:168-176, :107-141); first/last valid index
+//                   -> startOri / endOri (:185-197)
+//   k_sr_ring       elevation -> scanID (:217-259), azimuth branch-1 test; the halfPassed
+//                   latch (:265-292) = first ring-valid point whose branch-1 azimuth passes
+//                   startOri + pi (atomicMin); per-block ring histograms
+//   k_sr_ring_scan  exclusive scan of the (ring, block) histogram -> stable counting sort
+//                   offsets = laserCloudScans concatenation (:308-315)
+//   k_sr_scatter    stable scatter into the ring-major cloud, intensity = scanID + 0.1*relTime
+//   k_sr_curv       11-tap curvature over the concatenated cloud (:323-346), crossing rings
+//   k_sr_select     one workgroup per ring: 6 sectors, LDS bitonic sort by curvature, greedy
+//                   sharp / lessSharp / flat picks with +-5 neighbour suppression (:352-493);
+//                   one wave runs the (inherently sequential) greedy scan with 64-wide ballots
+//   k_sr_ringvox    VoxelGrid 0.2 m of each ring's lessFlat candidates (:497-503)
+//   k_sr_gather     concatenation of the per-ring outputs in ring order
+// The reference sorts each sector with std::sort (unstable); the kernel sorts by
+// (curvature, index), which is the same order whenever curvatures are distinct.
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "common.h"
+#include "voxel.h"
+
+namespace loam {
+
+constexpr int SR_MAX_RINGS = 64;
+constexpr int SR_BLOCK = 256;
+constexpr int SR_RING_CAP = 16384;  // points per ring handled in LDS
+constexpr int SR_SECT_CAP = 4096;   // points per sector (bitonic in LDS)
+constexpr int SR_SHARP = 2, SR_LESS_SHARP = 20, SR_FLAT = 4;
+constexpr int SR_ERR_RING = 1, SR_ERR_VOXEL = 2;
+
+struct SrFrame {
+  int n_in;
+  int first, last;  // first / last valid raw index
+  int latch;        // raw index of the halfPassed latch (INT_MAX: never)
+  float start_ori, end_ori;
+  int n_cloud;
+  int ring_off[SR_MAX_RINGS + 1];
+  int ring_cnt[SR_MAX_RINGS];
+  int n_sharp[SR_MAX_RINGS], n_less_sharp[SR_MAX_RINGS], n_flat[SR_MAX_RINGS];
+  int n_less_flat_scan[SR_MAX_RINGS];
+  uint32_t n_less_flat[SR_MAX_RINGS];
+  int out_n[5];
+  int err;
+};
+
+struct SrDev {
+  int cap;  // max input points
+  int n_scans;
+  float min_range;
+  int stride;
+  const float* xyz;      // raw input (stride floats per point)
+  SrFrame* fr;
+  int* ring_of;          // [cap] scanID per raw point (-1 dropped)
+  int* blk_hist;         // [SR_MAX_RINGS][nblocks]
+  int* blk_off;          // [SR_MAX_RINGS][nblocks]
+  float4* cloud;         // [cap] laserCloud
+  float* curv;           // [cap]
+  int* sort_ind;         // [cap] debug: label per point
+  int* label;            // [cap]
+  int* ring_sharp;       // [SR_MAX_RINGS][6*SR_SHARP] cloud indices
+  int* ring_less_sharp;  // [SR_MAX_RINGS][6*SR_LESS_SHARP]
+  int* ring_flat;        // [SR_MAX_RINGS][6*SR_FLAT]
+  float4* less_flat_scan;  // [cap] ring-local regions
+  float4* less_flat_ds;    // [cap]
+  float4* vx_pts;
+  int* vx_idx;
+  float4* out[5];        // laserCloud alias, sharp, lessSharp, flat, lessFlat
+};
+
+// scan_registration.cpp:217-259 (float atan/sqrt like the reference's float overloads)
+__device__ inline int sr_scan_id(float x, float y, float z, int n_scans) {
+  // float atan(float) * 180 -> float, / M_PI -> double, stored as float
+  const float angle = (float)((double)(atanf(z / sqrtf(x * x + y * y)) * 180) / M_PI);
+  int scanID = 0;
+  if (n_scans == 16) {
+    scanID = int((angle + 15) / 2 + 0.5);
+    if (scanID > (n_scans - 1) || scanID < 0) return -1;
+  } else if (n_scans == 32) {
+    scanID = int((angle + 92.0 / 3.0) * 3.0 / 4.0);
+    if (scanID > (n_scans - 1) || scanID < 0) return -1;
+  } else {
+    if (angle >= -8.83) scanID = int((2 - angle) * 3.0 + 0.5);
+    else scanID = n_scans / 2 + int((-8.83 - angle) * 2.0 + 0.5);
+    if (angle > 2 || angle < -24.33 || scanID > 50 || scanID < 0) return -1;
+  }
+  return scanID;
+}
+
+__global__ void k_sr_valid(SrDev D) {
+  SrFrame& F = *D.fr;
+  const float thr2 = D.min_range * D.min_range;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < F.n_in; i += gridDim.x * blockDim.x) {
+    const float x = D.xyz[(size_t)i * D.stride], y = D.xyz[(size_t)i * D.stride + 1],
+                z = D.xyz[(size_t)i * D.stride + 2];
+    const bool ok = isfinite(x) && isfinite(y) && isfinite(z) && !(x * x + y * y + z * z < thr2);
+    D.ring_of[i] = ok ? 0 : -2;  // -2: removed before the ring rule
+    if (ok) {
+      atomicMin(&F.first, i);
+      atomicMax(&F.last, i);
+    }
+  }
+}
+
+__device__ inline float sr_ori_branch1(float ori, float startOri) {
+  if (ori < startOri - M_PI / 2) ori += 2 * M_PI;
+  else if (ori > startOri + M_PI * 3 / 2) ori -= 2 * M_PI;
+  return ori;
+}
+
+// per raw point: ring (or -1), branch-1 latch test; per-block ring histogram
+__global__ void __launch_bounds__(SR_BLOCK) k_sr_ring(SrDev D, int nblocks) {
+  __shared__ int hist[SR_MAX_RINGS];
+  SrFrame& F = *D.fr;
+  for (int r = threadIdx.x; r < SR_MAX_RINGS; r += SR_BLOCK) hist[r] = 0;
+  __syncthreads();
+  const int i = blockIdx.x * SR_BLOCK + threadIdx.x;
+  if (i < F.n_in && D.ring_of[i] == 0) {
+    const float x = D.xyz[(size_t)i * D.stride], y = D.xyz[(size_t)i * D.stride + 1],
+                z = D.xyz[(size_t)i * D.stride + 2];
+    const int sid = sr_scan_id(x, y, z, D.n_scans);
+    D.ring_of[i] = sid;
+    if (sid >= 0) {
+      atomicAdd(&hist[sid], 1);
+      const float ori = sr_ori_branch1(-atan2f(y, x), F.start_ori);
+      if (ori - F.start_ori > M_PI) atomicMin(&F.latch, i);
+    }
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < SR_MAX_RINGS; r += SR_BLOCK) D.blk_hist[r * nblocks + blockIdx.x] = hist[r];
+}
+
+__global__ void k_sr_oris(SrDev D) {
+  // startOri / endOri (scan_registration.cpp:185-197)
+  SrFrame& F = *D.fr;
+  if (F.first > F.last) return;
+  const float* p0 = D.xyz + (size_t)F.first * D.stride;
+  const float* p1 = D.xyz + (size_t)F.last * D.stride;
+  float startOri = -atan2f(p0[1], p0[0]);
+  float endOri = (float)(-atan2f(p1[1], p1[0]) + 2 * M_PI);
+  if (endOri - startOri > 3 * M_PI) endOri = (float)(endOri - 2 * M_PI);
+  else if (endOri - startOri < M_PI) endOri = (float)(endOri + 2 * M_PI);
+  F.start_ori = startOri;
+  F.end_ori = endOri;
+}
+
+// exclusive scan of blk_hist in ring-major order (one 1024-thread workgroup)
+__global__ void __launch_bounds__(1024) k_sr_ring_scan(SrDev D, int nblocks) {
+  __shared__ uint32_t ws[VX_WAVES + 1];
+  __shared__ int ring_tot[SR_MAX_RINGS];
+  SrFrame& F = *D.fr;
+  const int total = SR_MAX_RINGS * nblocks;
+  const int per = (total + 1023) / 1024;
+  const int b0 = threadIdx.x * per;
+  uint32_t sum = 0;
+  for (int k = 0; k < per; ++k)
+    if (b0 + k < total) sum += D.blk_hist[b0 + k];
+  uint32_t tot;
+  uint32_t pre = vx_block_scan(sum, ws, &tot);
+  for (int k = 0; k < per; ++k) {
+    int e = b0 + k;
+    if (e < total) {
+      D.blk_off[e] = pre;
+      pre += D.blk_hist[e];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < SR_MAX_RINGS) {
+    int r = threadIdx.x, c = 0;
+    for (int b = 0; b < nblocks; ++b) c += D.blk_hist[r * nblocks + b];
+    ring_tot[r] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int r = 0; r < SR_MAX_RINGS; ++r) {
+      F.ring_off[r] = acc;
+      F.ring_cnt[r] = ring_tot[r];
+      acc += ring_tot[r];
+    }
+    F.ring_off[SR_MAX_RINGS] = acc;
+    F.n_cloud = acc;
+  }
+}
+
+// stable scatter: rank within the block by wave peeling, intensity = scanID + 0.1 * relTime
+__global__ void __launch_bounds__(SR_BLOCK) k_sr_scatter(SrDev D, int nblocks) {
+  __shared__ int wcnt[SR_BLOCK / 64][SR_MAX_RINGS];
+  const SrFrame& F = *D.fr;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  for (int k = tid; k < (SR_BLOCK / 64) * SR_MAX_RINGS; k += SR_BLOCK) (&wcnt[0][0])[k] = 0;
+  __syncthreads();
+  const int i = blockIdx.x * SR_BLOCK + tid;
+  const int sid = (i < F.n_in) ? D.ring_of[i] : -1;
+  // wave-local stable rank among equal rings
+  uint64_t active = __ballot(sid >= 0);
+  int rank = 0;
+  while (active) {
+    const int leader = __ffsll((long long)active) - 1;
+    const int r = __shfl(sid, leader, 64);
+    const uint64_t mask = __ballot(sid == r);
+    if (sid == r) rank = __popcll(mask & lanemask_lt());
+    if (lane == leader) wcnt[wid][r] = __popcll(mask);
+    active &= ~mask;
+  }
+  __syncthreads();
+  if (sid < 0) return;
+  int before = 0;
+  for (int w = 0; w < wid; ++w) before += wcnt[w][sid];
+  const int pos = D.blk_off[sid * nblocks + blockIdx.x] + before + rank;
+  const float x = D.xyz[(size_t)i * D.stride], y = D.xyz[(size_t)i * D.stride + 1],
+              z = D.xyz[(size_t)i * D.stride + 2];
+  float ori = -atan2f(y, x);
+  const float startOri = F.start_ori, endOri = F.end_ori;
+  if (i <= F.latch) {
+    ori = sr_ori_branch1(ori, startOri);
+  } else {
+    ori = (float)(ori + 2 * M_PI);
+    if (ori < endOri - M_PI * 3 / 2) ori = (float)(ori + 2 * M_PI);
+    else if (ori > endOri + M_PI / 2) ori = (float)(ori - 2 * M_PI);
+  }
+  const float relTime = (ori - startOri) / (endOri - startOri);
+  const float intensity = (float)(sid + 0.1 * relTime);
+  D.cloud[pos] = make_float4(x, y, z, intensity);
+}
+
+__global__ void k_sr_curv(SrDev D) {
+  const SrFrame& F = *D.fr;
+  const int n = F.n_cloud;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    D.label[i] = 0;
+    if (i < 5 || i >= n - 5) {
+      D.curv[i] = 0.f;
+      continue;
+    }
+    const float4* L = D.cloud;
+    float dx = L[i - 5].x + L[i - 4].x + L[i - 3].x + L[i - 2].x + L[i - 1].x - 10 * L[i].x +
+               L[i + 1].x + L[i + 2].x + L[i + 3].x + L[i + 4].x + L[i + 5].x;
+    float dy = L[i - 5].y + L[i - 4].y + L[i - 3].y + L[i - 2].y + L[i - 1].y - 10 * L[i].y +
+               L[i + 1].y + L[i + 2].y + L[i + 3].y + L[i + 4].y + L[i + 5].y;
+    float dz = L[i - 5].z + L[i - 4].z + L[i - 3].z + L[i - 2].z + L[i - 1].z - 10 * L[i].z +
+               L[i + 1].z + L[i + 2].z + L[i + 3].z + L[i + 4].z + L[i + 5].z;
+    D.curv[i] = dx * dx + dy * dy + dz * dz;
+  }
+}
+
+// +-5 neighbour suppression while consecutive squared gaps stay <= 0.05 (:406-429)
+__device__ inline void sr_suppress(const float4* L, uint8_t* picked, int base, int ind) {
+  for (int l = 1; l <= 5; l++) {
+    float dX = L[ind + l].x - L[ind + l - 1].x;
+    float dY = L[ind + l].y - L[ind + l - 1].y;
+    float dZ = L[ind + l].z - L[ind + l - 1].z;
+    if (dX * dX + dY * dY + dZ * dZ > 0.05) break;
+    picked[ind + l - base] = 1;
+  }
+  for (int l = -1; l >= -5; l--) {
+    float dX = L[ind + l].x - L[ind + l + 1].x;
+    float dY = L[ind + l].y - L[ind + l + 1].y;
+    float dZ = L[ind + l].z - L[ind + l + 1].z;
+    if (dX * dX + dY * dY + dZ * dZ > 0.05) break;
+    picked[ind + l - base] = 1;
+  }
+}
+
+__global__ void __launch_bounds__(SR_BLOCK) k_sr_select(SrDev D) {
+  __shared__ uint64_t keys[SR_SECT_CAP];
+  __shared__ uint8_t picked[SR_RING_CAP];
+  __shared__ int8_t lab[SR_RING_CAP];
+  __shared__ uint32_t ws[8];
+  const int r = blockIdx.x;
+  SrFrame& F = *D.fr;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  const int base = F.ring_off[r], n = F.ring_cnt[r];
+  const int s = base + 5, e = base + n - 6;
+  if (tid == 0) {
+    F.n_sharp[r] = F.n_less_sharp[r] = F.n_flat[r] = F.n_less_flat_scan[r] = 0;
+  }
+  if (e - s < 6) return;  // :355-356
+  if (n > SR_RING_CAP) {
+    if (tid == 0) atomicOr(&F.err, SR_ERR_RING);
+    return;
+  }
+  const float4* L = D.cloud;
+  for (int k = tid; k < n; k += SR_BLOCK) {
+    picked[k] = 0;
+    lab[k] = 0;
+  }
+  int nsh = 0, nls = 0, nfl = 0, nlf = 0;  // valid in thread 0 / wave 0
+  __syncthreads();
+  for (int j = 0; j < 6; j++) {
+    const int sp = s + (e - s) * j / 6;
+    const int ep = s + (e - s) * (j + 1) / 6 - 1;
+    const int len = ep - sp + 1;
+    if (len > SR_SECT_CAP) {
+      if (tid == 0) atomicOr(&F.err, SR_ERR_RING);
+      return;
+    }
+    int pad = 1;
+    while (pad < len) pad <<= 1;
+    for (int k = tid; k < pad; k += SR_BLOCK)
+      keys[k] = k < len ? (((uint64_t)__float_as_uint(D.curv[sp + k]) << 32) | (uint32_t)(sp + k))
+                        : 0xFFFFFFFFFFFFFFFFull;
+    __syncthreads();
+    for (int kk = 2; kk <= pad; kk <<= 1) {
+      for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+        for (int i = tid; i < pad; i += SR_BLOCK) {
+          int ixj = i ^ jj;
+          if (ixj > i) {
+            uint64_t a = keys[i], b = keys[ixj];
+            bool asc = (i & kk) == 0;
+            if ((a > b) == asc) {
+              keys[i] = b;
+              keys[ixj] = a;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    if (wid == 0) {
+      // sharp / lessSharp: descending curvature (:371-431)
+      int largest = 0;
+      int pos = len - 1;
+      while (pos >= 0) {
+        const int k = pos - lane;
+        bool cond = false, low = false;
+        int ind = 0;
+        if (k >= 0) {
+          const uint64_t key = keys[k];
+          ind = (int)(key & 0xFFFFFFFFu);
+          const float c = __uint_as_float((uint32_t)(key >> 32));
+          cond = picked[ind - base] == 0 && c > 0.1f;
+          low = !(c > 0.1f);
+        }
+        const uint64_t bc = __ballot(cond);
+        const uint64_t bl = __ballot(low);
+        const int fc = bc ? __ffsll((long long)bc) - 1 : 64;
+        const int fl = bl ? __ffsll((long long)bl) - 1 : 64;
+        if (fc < fl) {
+          const int pind = __shfl(ind, fc, 64);
+          largest++;
+          if (largest > SR_LESS_SHARP) break;
+          if (lane == 0) {
+            if (largest <= SR_SHARP) {
+              lab[pind - base] = 2;
+              D.ring_sharp[r * 6 * SR_SHARP + nsh++] = pind;
+              D.ring_less_sharp[r * 6 * SR_LESS_SHARP + nls++] = pind;
+            } else {
+              lab[pind - base] = 1;
+              D.ring_less_sharp[r * 6 * SR_LESS_SHARP + nls++] = pind;
+            }
+            picked[pind - base] = 1;
+            sr_suppress(L, picked, base, pind);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          pos = pos - fc - 1;
+        } else if (fl < 64) {
+          break;  // every remaining curvature <= 0.1
+        } else {
+          pos -= 64;
+        }
+      }
+      // flat: ascending curvature (:439-483)
+      int smallest = 0;
+      pos = 0;
+      while (pos < len) {
+        const int k = pos + lane;
+        bool cond = false, high = false;
+        int ind = 0;
+        if (k < len) {
+          const uint64_t key = keys[k];
+          ind = (int)(key & 0xFFFFFFFFu);
+          const float c = __uint_as_float((uint32_t)(key >> 32));
+          cond = picked[ind - base] == 0 && c < 0.1f;
+          high = !(c < 0.1f);
+        }
+        const uint64_t bc = __ballot(cond);
+        const uint64_t bh = __ballot(high);
+        const int fc = bc ? __ffsll((long long)bc) - 1 : 64;
+        const int fh = bh ? __ffsll((long long)bh) - 1 : 64;
+        if (fc < fh) {
+          const int pind = __shfl(ind, fc, 64);
+          if (lane == 0) {
+            lab[pind - base] = -1;
+            D.ring_flat[r * 6 * SR_FLAT + nfl++] = pind;
+          }
+          smallest++;
+          if (smallest >= SR_FLAT) break;
+          if (lane == 0) {
+            picked[pind - base] = 1;
+            sr_suppress(L, picked, base, pind);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          pos = pos + fc + 1;
+        } else if (fh < 64) {
+          break;
+        } else {
+          pos += 64;
+        }
+      }
+    }
+    __syncthreads();
+    // lessFlat candidates: label <= 0 in index order (:486-493), stable block compaction
+    for (int c = sp; c <= ep; c += SR_BLOCK) {
+      const int k = c + tid;
+      const bool pred = k <= ep && lab[k - base] <= 0;
+      const uint64_t bal = __ballot(pred);
+      const uint32_t pre = __popcll(bal & lanemask_lt());
+      if (lane == 0) ws[wid] = __popcll(bal);
+      __syncthreads();
+      uint32_t off = 0, tot = 0;
+      for (int w = 0; w < SR_BLOCK / 64; ++w) {
+        if (w < wid) off += ws[w];
+        tot += ws[w];
+      }
+      if (pred) D.less_flat_scan[base + nlf + off + pre] = L[k];
+      nlf += tot;
+      __syncthreads();
+    }
+  }
+  for (int k = tid; k < n; k += SR_BLOCK) D.label[base + k] = lab[k];
+  if (tid == 0) {
+    F.n_sharp[r] = nsh;
+    F.n_less_sharp[r] = nls;
+    F.n_flat[r] = nfl;
+    F.n_less_flat_scan[r] = nlf;
+  }
+}
+
+__global__ void __launch_bounds__(VX_THREADS) k_sr_ringvox(SrDev D) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
+  const int r = blockIdx.x;
+  SrFrame& F = *D.fr;
+  const int base = F.ring_off[r];
+  const int n = F.n_less_flat_scan[r];
+  if (threadIdx.x == 0) F.n_less_flat[r] = 0;
+  if (n == 0) return;
+  __syncthreads();
+  VoxSeg S{};
+  S.src0 = D.less_flat_scan + base;
+  S.n0 = n;
+  S.leaf = 0.2f;
+  S.out = D.less_flat_ds + base;
+  S.cap = (uint32_t)n;
+  S.res_cnt = &F.n_less_flat[r];
+  S.scratch_pts = D.vx_pts + base;
+  S.scratch_idx = D.vx_idx + base;
+  S.scratch_cap = (uint32_t)n;
+  S.err = &F.err;
+  voxel_segment(S, lds);
+}
+
+// concatenation of the per-ring outputs in ring order
+__global__ void k_sr_gather(SrDev D) {
+  const int r = blockIdx.x;
+  SrFrame& F = *D.fr;
+  int o1 = 0, o2 = 0, o3 = 0, o4 = 0;
+  for (int q = 0; q < r; ++q) {
+    o1 += F.n_sharp[q];
+    o2 += F.n_less_sharp[q];
+    o3 += F.n_flat[q];
+    o4 += (int)F.n_less_flat[q];
+  }
+  const float4* L = D.cloud;
+  for (int k = threadIdx.x; k < F.n_sharp[r]; k += blockDim.x)
+    D.out[1][o1 + k] = L[D.ring_sharp[r * 6 * SR_SHARP + k]];
+  for (int k = threadIdx.x; k < F.n_less_sharp[r]; k += blockDim.x)
+    D.out[2][o2 + k] = L[D.ring_less_sharp[r * 6 * SR_LESS_SHARP + k]];
+  for (int k = threadIdx.x; k < F.n_flat[r]; k += blockDim.x)
+    D.out[3][o3 + k] = L[D.ring_flat[r * 6 * SR_FLAT + k]];
+  const int base = F.ring_off[r];
+  for (int k = threadIdx.x; k < (int)F.n_less_flat[r]; k += blockDim.x)
+    D.out[4][o4 + k] = D.less_flat_ds[base + k];
+  if (r == SR_MAX_RINGS - 1 && threadIdx.x == 0) {
+    F.out_n[0] = F.n_cloud;
+    F.out_n[1] = o1 + F.n_sharp[r];
+    F.out_n[2] = o2 + F.n_less_sharp[r];
+    F.out_n[3] = o3 + F.n_flat[r];
+    F.out_n[4] = o4 + (int)F.n_less_flat[r];
+  }
+}
+
+}  // namespace loam
+
+using namespace loam;
+
+struct loam_scanreg {
+  loam_params P;
+  int dev = 0;
+  hipStream_t st = nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  SrDev D{};
+  SrFrame hf{};
+  float* d_in = nullptr;
+  std::vector<void*> allocs;
+  float ms = 0.f;
+};
+
+namespace {
+template <typename T>
+int32_t sralloc(loam_scanreg* h, T** p, size_t n) {
+  void* q = nullptr;
+  LOAM_HIP(hipMalloc(&q, std::max<size_t>(n, 1) * sizeof(T)));
+  LOAM_HIP(hipMemset(q, 0, std::max<size_t>(n, 1) * sizeof(T)));
+  h->allocs.push_back(q);
+  *p = reinterpret_cast<T*>(q);
+  return LOAM_OK;
+}
+void sr_free(loam_scanreg* h) {
+  for (void* p : h->allocs) (void)hipFree(p);
+  h->allocs.clear();
+  for (auto& e : h->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->st) (void)hipStreamDestroy(h->st);
+}
+}  // namespace
+
+extern "C" {
+
+int32_t loam_scanreg_create(const loam_params* p, int32_t device, loam_scanreg** out) {
+  if (!out) return LOAM_ERR_ARG;
+  *out = nullptr;
+  int32_t rc = ensure_device(device);
+  if (rc != LOAM_OK) return rc;
+  LOAM_HIP(hipSetDevice(device));
+  auto* h = new loam_scanreg;
+  if (p) h->P = *p; else loam_params_default(&h->P);
+  if (h->P.scan_line != 16 && h->P.scan_line != 32 && h->P.scan_line != 64) {
+    delete h;
+    set_error("only support velodyne with 16, 32 or 64 scan line (scan_registration.cpp:58-61)");
+    return LOAM_ERR_ARG;
+  }
+  h->dev = device;
+  const int cap = h->P.max_input_points;
+  SrDev& D = h->D;
+  D.cap = cap;
+  D.n_scans = h->P.scan_line;
+  D.min_range = (float)h->P.minimum_range;
+  const int nblocks = (cap + SR_BLOCK - 1) / SR_BLOCK;
+  auto fail = [&](int32_t r) {
+    sr_free(h);
+    delete h;
+    return r;
+  };
+  if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess) return fail(LOAM_ERR_HIP);
+  for (auto& e : h->ev)
+    if (hipEventCreate(&e) != hipSuccess) return fail(LOAM_ERR_HIP);
+#define SRA(ptr, n) \
+  if ((rc = sralloc(h, &(ptr), (n))) != LOAM_OK) return fail(rc)
+  SRA(h->d_in, (size_t)cap * 4);
+  SRA(D.fr, 1);
+  SRA(D.ring_of, cap);
+  SRA(D.blk_hist, (size_t)SR_MAX_RINGS * nblocks);
+  SRA(D.blk_off, (size_t)SR_MAX_RINGS * nblocks);
+  SRA(D.cloud, cap);
+  SRA(D.curv, cap);
+  SRA(D.label, cap);
+  SRA(D.ring_sharp, SR_MAX_RINGS * 6 * SR_SHARP);
+  SRA(D.ring_less_sharp, SR_MAX_RINGS * 6 * SR_LESS_SHARP);
+  SRA(D.ring_flat, SR_MAX_RINGS * 6 * SR_FLAT);
+  SRA(D.less_flat_scan, cap);
+  SRA(D.less_flat_ds, cap);
+  SRA(D.vx_pts, cap);
+  SRA(D.vx_idx, cap);
+  for (int k = 1; k < 5; ++k) SRA(D.out[k], cap);
+#undef SRA
+  D.out[0] = D.cloud;
+  D.sort_ind = nullptr;
+  *out = h;
+  return LOAM_OK;
+}
+
+int32_t loam_scanreg_destroy(loam_scanreg* h) {
+  if (!h) return LOAM_ERR_ARG;
+  (void)hipSetDevice(h->dev);
+  sr_free(h);
+  delete h;
+  return LOAM_OK;
+}
+
+static int32_t sr_run(loam_scanreg* h, const float* xyz, int32_t n, int32_t stride, bool on_device) {
+  if (!h || n < 0 || (n > 0 && !xyz) || stride < 3) {
+    set_error("loam_scanreg_input: bad arguments");
+    return LOAM_ERR_ARG;
+  }
+  if (n > h->D.cap) {
+    set_error("loam_scanreg_input: more points than max_input_points");
+    return LOAM_ERR_CAPACITY;
+  }
+  LOAM_HIP(hipSetDevice(h->dev));
+  hipStream_t st = h->st;
+  SrDev D = h->D;
+  D.stride = stride;
+  if (on_device) {
+    D.xyz = xyz;
+  } else {
+    if (stride != 4 && (size_t)n * stride > (size_t)h->D.cap * 4) {
+      set_error("loam_scanreg_input: stride too large for the staging buffer");
+      return LOAM_ERR_CAPACITY;
+    }
+    if (n) LOAM_HIP(hipMemcpyAsync(h->d_in, xyz, sizeof(float) * (size_t)n * stride, hipMemcpyHostToDevice, st));
+    D.xyz = h->d_in;
+  }
+  SrFrame f{};
+  f.n_in = n;
+  f.first = 0x7FFFFFFF;
+  f.last = -1;
+  f.latch = 0x7FFFFFFF;
+  LOAM_HIP(hipEventRecord(h->ev[0], st));
+  LOAM_HIP(hipMemcpyAsync(D.fr, &f, sizeof(SrFrame), hipMemcpyHostToDevice, st));
+  const int nblocks = std::max(1, (n + SR_BLOCK - 1) / SR_BLOCK);
+  if (n > 0) {
+    k_sr_valid<<<std::min(nblocks, 1024), SR_BLOCK, 0, st>>>(D);
+    k_sr_oris<<<1, 1, 0, st>>>(D);
+    k_sr_ring<<<nblocks, SR_BLOCK, 0, st>>>(D, nblocks);
+    k_sr_ring_scan<<<1, 1024, 0, st>>>(D, nblocks);
+    k_sr_scatter<<<nblocks, SR_BLOCK, 0, st>>>(D, nblocks);
+    k_sr_curv<<<std::min(nblocks, 1024), SR_BLOCK, 0, st>>>(D);
+    k_sr_select<<<SR_MAX_RINGS, SR_BLOCK, 0, st>>>(D);
+    k_sr_ringvox<<<SR_MAX_RINGS, VX_THREADS, 0, st>>>(D);
+    k_sr_gather<<<SR_MAX_RINGS, 256, 0, st>>>(D);
+    LOAM_HIP(hipGetLastError());
+  }
+  LOAM_HIP(hipEventRecord(h->ev[1], st));
+  LOAM_HIP(hipMemcpyAsync(&h->hf, D.fr, sizeof(SrFrame), hipMemcpyDeviceToHost, st));
+  LOAM_HIP(hipStreamSynchronize(st));
+  LOAM_HIP(hipEventElapsedTime(&h->ms, h->ev[0], h->ev[1]));
+  h->D.xyz = D.xyz;
+  h->D.stride = stride;
+  if (h->hf.err) {
+    set_error("loam_scanreg_input: ring or sector larger than the LDS capacity (err " +
+              std::to_string(h->hf.err) + ")");
+    return LOAM_ERR_CAPACITY;
+  }
+  return LOAM_OK;
+}
+
+int32_t loam_scanreg_input(loam_scanreg* h, const float* xyz, int32_t n, int32_t stride) {
+  return sr_run(h, xyz, n, stride, false);
+}
+
+int32_t loam_scanreg_input_device(loam_scanreg* h, const float* d_xyz, int32_t n, int32_t stride) {
+  return sr_run(h, d_xyz, n, stride, true);
+}
+
+int32_t loam_scanreg_counts(loam_scanreg* h, int32_t* counts) {
+  if (!h || !counts) return LOAM_ERR_ARG;
+  for (int k = 0; k < 5; ++k) counts[k] = h->hf.n_in > 0 ? h->hf.out_n[k] : 0;
+  return LOAM_OK;
+}
+
+int32_t loam_scanreg_copy(loam_scanreg* h, int32_t which, float* out, int32_t cap) {
+  if (!h || which < 0 || which > 4 || (cap > 0 && !out)) return LOAM_ERR_ARG;
+  LOAM_HIP(hipSetDevice(h->dev));
+  const int n = h->hf.n_in > 0 ? h->hf.out_n[which] : 0;
+  if (n > cap) {
+    set_error("loam_scanreg_copy: output buffer too small");
+    return LOAM_ERR_CAPACITY;
+  }
+  if (n) LOAM_HIP(hipMemcpy(out, h->D.out[which], sizeof(float4) * n, hipMemcpyDeviceToHost));
+  return n;
+}
+
+int32_t loam_scanreg_device_ptr(loam_scanreg* h, int32_t which, const float** ptr) {
+  if (!h || which < 0 || which > 4 || !ptr) return LOAM_ERR_ARG;
+  *ptr = reinterpret_cast<const float*>(h->D.out[which]);
+  return h->hf.n_in > 0 ? h->hf.out_n[which] : 0;
+}
+
+int32_t loam_scanreg_curvature(loam_scanreg* h, float* curv, int32_t* label, int32_t cap) {
+  if (!h || (cap > 0 && (!curv || !label))) return LOAM_ERR_ARG;
+  LOAM_HIP(hipSetDevice(h->dev));
+  const int n = h->hf.n_in > 0 ? h->hf.n_cloud : 0;
+  if (n > cap) return LOAM_ERR_CAPACITY;
+  if (n) {
+    LOAM_HIP(hipMemcpy(curv, h->D.curv, sizeof(float) * n, hipMemcpyDeviceToHost));
+    LOAM_HIP(hipMemcpy(label, h->D.label, sizeof(int) * n, hipMemcpyDeviceToHost));
+  }
+  return n;
+}
+
+double loam_scanreg_ms(loam_scanreg* h) { return h ? (double)h->ms : 0.0; }
+
+}  // extern "C"

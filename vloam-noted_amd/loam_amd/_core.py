@@ -52,6 +52,15 @@ SIGNATURES = {
     "loam_params_default": (None, [ctypes.POINTER(Params)]),
     "loam_last_error": (ctypes.c_char_p, []),
     "loam_version": (c_i32, []),
+    "loam_scanreg_create": (c_i32, [ctypes.POINTER(Params), c_i32, ctypes.POINTER(vp)]),
+    "loam_scanreg_destroy": (c_i32, [vp]),
+    "loam_scanreg_input": (c_i32, [vp, vp, c_i32, c_i32]),
+    "loam_scanreg_input_device": (c_i32, [vp, vp, c_i32, c_i32]),
+    "loam_scanreg_counts": (c_i32, [vp, vp]),
+    "loam_scanreg_copy": (c_i32, [vp, c_i32, vp, c_i32]),
+    "loam_scanreg_device_ptr": (c_i32, [vp, c_i32, ctypes.POINTER(vp)]),
+    "loam_scanreg_curvature": (c_i32, [vp, vp, vp, c_i32]),
+    "loam_scanreg_ms": (c_d, [vp]),
     "loam_mapper_create": (c_i32, [ctypes.POINTER(Params), c_i32, c_i32, ctypes.POINTER(vp)]),
     "loam_mapper_destroy": (c_i32, [vp]),
     "loam_mapper_reset": (c_i32, [vp]),

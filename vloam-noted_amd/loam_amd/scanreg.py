@@ -1,0 +1,78 @@
+"""ScanRegistration on MI355X — host mirror of vloam::ScanRegistration
+(src/lidar_odometry_mapping/include/lidar_odometry_mapping/scan_registration.h:64-81).
+
+``input(cloud)`` takes an (n, >=3) float32 array (pcl::PointXYZ fields first); ``output()``
+returns the five clouds of ScanRegistration::output (scan_registration.cpp:566-577) as
+(n, 4) float32 arrays (x, y, z, intensity = scanID + 0.1 * relTime).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _core
+from ._core import check, lib, ptr
+
+CLOUDS = ("laserCloud", "cornerPointsSharp", "cornerPointsLessSharp", "surfPointsFlat",
+          "surfPointsLessFlat")
+
+
+class ScanRegistration:
+    def __init__(self, device=0, params=None, **param_overrides):
+        self.params = params if params is not None else _core.default_params(**param_overrides)
+        h = ctypes.c_void_p()
+        check(lib().loam_scanreg_create(ctypes.byref(self.params), device, ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().loam_scanreg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def init(self):
+        pass
+
+    def reset(self):
+        pass
+
+    def input(self, cloud):
+        xyz = np.ascontiguousarray(cloud, dtype=np.float32)
+        check(lib().loam_scanreg_input(self.h, ptr(xyz), len(xyz), xyz.shape[1]))
+
+    def input_device(self, d_ptr, n, stride):
+        check(lib().loam_scanreg_input_device(self.h, d_ptr, n, stride))
+
+    def counts(self):
+        c = np.zeros(5, dtype=np.int32)
+        check(lib().loam_scanreg_counts(self.h, ptr(c)))
+        return c
+
+    def cloud(self, which):
+        n = int(self.counts()[which])
+        out = np.empty((n, 4), dtype=np.float32)
+        check(lib().loam_scanreg_copy(self.h, which, ptr(out), n))
+        return out
+
+    def output(self):
+        return tuple(self.cloud(i) for i in range(5))
+
+    def device_ptr(self, which):
+        p = ctypes.c_void_p()
+        n = check(lib().loam_scanreg_device_ptr(self.h, which, ctypes.byref(p)))
+        return p.value, n
+
+    def curvature(self):
+        n = int(self.counts()[0])
+        c = np.empty(n, dtype=np.float32)
+        lab = np.empty(n, dtype=np.int32)
+        check(lib().loam_scanreg_curvature(self.h, ptr(c), ptr(lab), n))
+        return c, lab
+
+    @property
+    def ms(self):
+        return lib().loam_scanreg_ms(self.h)
