@@ -1,0 +1,238 @@
+"""bench.py — scan-to-map LM iterations/sec on 64-ring KITTI-shaped clouds (BASELINE.json).
+
+Workload (BASELINE.json configs[3]): LaserMapping::solveMapping (laser_mapping.cpp:212-814)
+over a synthetic HDL-64E street sequence, voxel-hashed local map resident in HBM.  A step is
+one full solveMapping frame — map window / recentering, stack VoxelGrid, submap hash build,
+2 x (correspondences + <= 4 LM iterations), insertion and per-cube re-VoxelGrid — for each
+of `--streams` independent mapping streams held by one handle (one launch sequence per step).
+LM iterations are counted like Ceres' summary.iterations.size() - 1 (trust-region steps).
+
+Inputs are produced before the timed region, on the GPU: synthetic raw scans
+(vloam-noted_amd/csrc/synth.cpp) -> HIP ScanRegistration -> lessSharp / lessFlat clouds kept
+in HBM; the odometry pose prior is ground truth plus a seeded random-walk drift.  Stream b
+replays the sequence from frame b * --stride.
+
+value = sum of LM iterations of all streams on all ranks / max over ranks of the timed
+wall time.  roofline: the kernel family with the largest device time, algorithmic bytes /
+its average launch duration (HIP events around every launch inside the library, on the
+library's stream, over the timed region).  cpu_baseline (rank 0, N = 1): the CPU oracle
+(single-threaded restatement of the reference: PCL KD-tree + VoxelGrid + Ceres-LM
+semantics) timed on the same frames of stream 0.
+
+Usage: python bench.py [--gpus N --steps K --warmup W --streams B]; for N > 1 launch with
+torch.distributed.run, one rank per GPU (streams shard across ranks, no data-path
+collective: "scaling": "weak").
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "vloam-noted_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--streams", type=int, default=32, help="mapping streams per GPU")
+    ap.add_argument("--stride", type=int, default=3, help="frame offset between streams")
+    ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--n-az", type=int, default=2000)
+    ap.add_argument("--cpu-frames", type=int, default=150, help="cpu_baseline sample (frames)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-prof", action="store_true", help="no per-launch HIP events")
+    ap.add_argument("--single-stream", action="store_true",
+                    help="also time a single stream (latency view) and report it")
+    return ap.parse_args()
+
+
+def drift_priors(seed, n, q_gt, t_gt):
+    """odometry-like prior: ground truth composed with a random-walk drift (2 cm, 0.03 deg / frame)"""
+    from scipy.spatial.transform import Rotation as R
+    rng = np.random.default_rng(seed + 99)
+    dt = np.cumsum(rng.normal(0, 0.02, (n, 3)), axis=0)
+    dr = np.cumsum(rng.normal(0, np.radians(0.03), (n, 3)), axis=0)
+    q = np.empty((n, 4))
+    t = np.empty((n, 3))
+    for i in range(n):
+        rq = R.from_rotvec(dr[i]) * R.from_quat(q_gt[i])
+        q[i] = rq.as_quat()
+        t[i] = t_gt[i] + dt[i]
+    return q, t
+
+
+def make_frames(seed, n_frames, n_az, device):
+    """raw scans (threads) -> HIP ScanRegistration -> features in HBM (torch tensors)"""
+    import torch
+    from loam_amd import synth
+    from loam_amd.scanreg import ScanRegistration
+
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4)) as ex:
+        raw = list(ex.map(lambda f: synth.frame(seed, f, n_az), range(n_frames)))
+    sr = ScanRegistration(device=device)
+    frames = []
+    for xyz, gt in raw:
+        sr.input(xyz)
+        corner = sr.cloud(2)  # cornerPointsLessSharp -> laserCloudCornerLast
+        surf = sr.cloud(4)    # surfPointsLessFlat   -> laserCloudSurfLast
+        frames.append(dict(corner=torch.from_numpy(corner).to(f"cuda:{device}"),
+                           surf=torch.from_numpy(surf).to(f"cuda:{device}"),
+                           gt=gt, raw=xyz))
+    sr.close()
+    q_gt = np.array([f["gt"][:4] for f in frames])
+    t_gt = np.array([f["gt"][4:] for f in frames])
+    q, t = drift_priors(seed, n_frames, q_gt, t_gt)
+    for i, f in enumerate(frames):
+        f["q"], f["t"] = q[i], t[i]
+    torch.cuda.synchronize(device)
+    return frames
+
+
+def run_steps(mapper, frames, streams, stride, first, count):
+    """count solveMapping steps; stream b consumes frame b*stride + step"""
+    iters = 0
+    for k in range(first, first + count):
+        for b in range(streams):
+            f = frames[b * stride + k]
+            mapper.input_device(b, f["corner"].data_ptr(), len(f["corner"]), f["surf"].data_ptr(),
+                                len(f["surf"]), f["q"], f["t"])
+        mapper.solve()
+        for b in range(streams):
+            st = mapper.stats(b)
+            iters += st.lm[0].iterations + st.lm[1].iterations
+    return iters
+
+
+def cpu_baseline(frames, n):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import loam_oracle as O
+    sr, mp = O.ScanRegistration(), O.LaserMapping()
+    iters, ms = 0, 0.0
+    for f in frames[:n]:
+        sr.input(f["raw"])
+        mp.input(sr.cloud(2), sr.cloud(4), None, f["q"], f["t"])
+        mp.solve()
+        st = mp.stats()
+        iters += st.lm[0].iterations + st.lm[1].iterations
+        ms += st.ms_total
+    return iters, ms
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    torch.cuda.set_device(local)
+
+    from loam_amd.mapping import BatchMapper
+
+    B, K, W = args.streams, args.steps, args.warmup
+    n_frames = (B - 1) * args.stride + W + K
+    frames = make_frames(args.seed + 1000 * rank, max(n_frames, args.cpu_frames if rank == 0 else 0),
+                         args.n_az, local)
+    mapper = BatchMapper(B, device=local)
+
+    def barrier():
+        torch.cuda.synchronize(local)
+        if world > 1:
+            dist.barrier()
+
+    run_steps(mapper, frames, B, args.stride, 0, W)
+    if not args.no_prof:
+        mapper.set_profiling(True)
+    mapper.reset_kernel_times()
+    barrier()
+    t0 = time.perf_counter()
+    iters = run_steps(mapper, frames, B, args.stride, W, K)
+    barrier()
+    dt = time.perf_counter() - t0
+    kt = mapper.kernel_times()
+    mapper.set_profiling(False)
+
+    tot = torch.tensor([float(iters), dt], dtype=torch.float64, device=f"cuda:{local}")
+    if world > 1:
+        it_t = tot[:1].clone()
+        dist.all_reduce(it_t, op=dist.ReduceOp.SUM)
+        dt_t = tot[1:].clone()
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+        iters_all, dt_max = float(it_t.item()), float(dt_t.item())
+    else:
+        iters_all, dt_max = float(iters), dt
+
+    single = None
+    if args.single_stream and rank == 0:
+        m1 = BatchMapper(1, device=local)
+        run_steps(m1, frames, 1, args.stride, 0, W)
+        torch.cuda.synchronize(local)
+        t1 = time.perf_counter()
+        it1 = run_steps(m1, frames, 1, args.stride, W, K)
+        torch.cuda.synchronize(local)
+        d1 = time.perf_counter() - t1
+        single = {"value": it1 / d1, "ms_per_frame": 1e3 * d1 / K, "iterations": it1}
+        m1.close()
+
+    if rank == 0:
+        dom = max(kt, key=lambda k: kt[k]["ms"])
+        d = kt[dom]
+        achieved = d["bytes"] / (d["ms"] * 1e-3) / 1e9 if d["ms"] > 0 else 0.0
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                    "launches": d["launches"], "avg_launch_us": round(1e3 * d["ms"] / max(1, d["launches"]), 3),
+                    "algorithmic_bytes_per_launch": round(d["bytes"] / max(1, d["launches"]), 1)}
+        cpu = None
+        if not args.no_cpu and world == 1:
+            ci, cms = cpu_baseline(frames, args.cpu_frames)
+            cpu = {"value": round(ci / (cms * 1e-3), 3), "unit": "LM iters/s", "cores": 1, "kind": "port",
+                   "sample": f"{args.cpu_frames} frames of stream 0: oracle solveMapping (KD-tree, VoxelGrid, "
+                             f"Ceres-LM/DENSE_QR restatement), {ci} LM iterations in {cms / 1e3:.2f} s",
+                   "ms_per_frame": round(cms / args.cpu_frames, 3)}
+        out = {
+            "metric": "scan-to-map LM iters/sec on 64-ring KITTI-shaped cloud",
+            "value": round(iters_all / dt_max, 3),
+            "unit": "LM iters/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": round(1e3 * dt_max / K, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp64 pose/normal equations, fp32 points",
+            "data": "synthetic HDL-64E street sequence (64 rings x 2000 azimuths), GPU scan registration "
+                    "features, ground-truth + random-walk odometry prior",
+            "config": {"workload": "laserMapping solveMapping, voxel-hashed map resident in HBM "
+                                   "(BASELINE configs[3])",
+                       "streams_per_gpu": B, "frames_per_step": B * world, "n_az": args.n_az,
+                       "parallelism": f"{world} GPU x {B} independent streams"},
+            "lm_iterations": int(iters_all),
+            "kernel_ms_per_step": {k: round(v["ms"] / K, 4) for k, v in kt.items()},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        if single is not None:
+            out["single_stream"] = {k: round(v, 4) for k, v in single.items()}
+        if cpu:
+            out["speedup_vs_cpu_baseline"] = round(out["value"] / cpu["value"], 2)
+        print(json.dumps(out), flush=True)
+    mapper.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

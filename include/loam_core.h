@@ -122,7 +122,8 @@ int32_t loam_mapper_reset(loam_mapper* h);
 int32_t loam_mapper_input(loam_mapper* h, int32_t stream, const float* corner, int32_t n_corner,
                           const float* surf, int32_t n_surf, const double* q_wodom,
                           const double* t_wodom, int32_t skip_frame);
-/* same, clouds already resident in HBM on the handle's device (device pointers) */
+/* same, clouds already resident in HBM on the handle's device (device pointers, read in place:
+ * they must stay valid until loam_mapper_solve returns) */
 int32_t loam_mapper_input_device(loam_mapper* h, int32_t stream, const float* d_corner,
                                  int32_t n_corner, const float* d_surf, int32_t n_surf,
                                  const double* q_wodom, const double* t_wodom,
@@ -133,6 +134,21 @@ int32_t loam_mapper_solve(loam_mapper* h);
 /* pose after solveMapping: q_w_curr (xyzw), t_w_curr (laser_mapping.cpp:826-832) */
 int32_t loam_mapper_pose(loam_mapper* h, int32_t stream, double* q_w, double* t_w);
 int32_t loam_mapper_stats(loam_mapper* h, int32_t stream, loam_map_stats* st);
+
+/* kernel-level timing: with profiling on, every launch of loam_mapper_solve is bracketed by
+ * HIP events on the handle's stream; times, launches and algorithmic bytes (DESIGN.md,
+ * "Kernels") accumulate per kernel family until reset.  Families: 0 stack VoxelGrid,
+ * 1 submap hash build, 2 correspondences (kNN + PCA/plane fit), 3 fused LM pass,
+ * 4 insertion, 5 window-cube re-VoxelGrid, 6 other (prep / finish / shift / compaction). */
+#define LOAM_KFAM_COUNT 8
+typedef struct loam_kernel_times {
+  double ms[LOAM_KFAM_COUNT];
+  int64_t launches[LOAM_KFAM_COUNT];
+  double bytes[LOAM_KFAM_COUNT];
+} loam_kernel_times;
+int32_t loam_mapper_set_profiling(loam_mapper* h, int32_t enable);
+int32_t loam_mapper_kernel_times(loam_mapper* h, loam_kernel_times* out);
+int32_t loam_mapper_reset_kernel_times(loam_mapper* h);
 
 /* map state (for teacher-forced parity and for the /laser_cloud_map publisher,
  * laser_mapping.cpp:884-899).  cube = i + 21*j + 441*k; which: 0 corner, 1 surf. */

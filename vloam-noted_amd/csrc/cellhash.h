@@ -102,7 +102,7 @@ __device__ inline void top5_offer(Top5& T, float d, int id, float px, float py, 
 __device__ inline void knn5_hash(const float4 q, const int* origin, const unsigned long long* hk,
                                  const unsigned long long* hc, const uint32_t* hs,
                                  const float4* sp, uint32_t mask, uint32_t epoch, float radius2,
-                                 Top5& T) {
+                                 Top5& T, uint32_t* ncand = nullptr) {
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
     T.d[k] = INFINITY;
@@ -140,6 +140,7 @@ __device__ inline void knn5_hash(const float4 q, const int* origin, const unsign
           if (cur == want) {
             const uint32_t cnt = (uint32_t)(hc[h] & 0xFFFFFFFFu);
             const uint32_t st = hs[h];
+            if (ncand) *ncand += cnt;
             for (uint32_t j = 0; j < cnt; ++j) {
               const float4 p = sp[st + j];
               const float d = fdist2(q.x, q.y, q.z, p.x, p.y, p.z);

@@ -38,6 +38,7 @@ struct LmState {
   double radius, decrease, x_norm, gmax;
   int status, iteration, reuse_diag, consec_invalid;
   int term, successful, invalid, max_iter;
+  int passes;  // evaluation passes consumed (iteration 0 + candidates)
 };
 
 __host__ __device__ inline int ut_index(int r, int c) {  // r <= c, upper triangle of 6x6
@@ -69,6 +70,7 @@ __host__ __device__ inline void lm_init(LmState& S, const double* x7, int max_it
   S.successful = 0;
   S.invalid = 0;
   S.max_iter = max_iter;
+  S.passes = 0;
 }
 
 // one residual block at X: accumulates rho' J^T J, rho' J^T r, 1/2 rho, rows
@@ -236,6 +238,7 @@ __host__ __device__ inline bool lm_solve_step(LmState& S, double* step) {
 // it needs another pass (status LM_EVAL_CAND) or terminates (LM_DONE, best in S.best).
 __host__ __device__ inline void lm_step(LmState& S, const double* red) {
   if (S.status == LM_DONE) return;
+  S.passes++;
   bool step_ok;
   if (S.status == LM_EVAL_X) {
     for (int i = 0; i < 21; ++i) S.jtj[i] = red[i];

@@ -62,6 +62,8 @@ struct StreamFrame {
   int extra_n[2];
   int extra_list[2][EXTRA_CAP];
   int err;
+  const float4* in_ptr[2];        // input clouds (mapper staging buffer or caller's HBM)
+  unsigned long long cand[2];     // map points examined by the kNN of each round
   LmState lm[2];
 };
 
@@ -142,7 +144,7 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
   VoxSeg S;
-  S.src0 = D.in_pts[m] + (size_t)s * D.max_in;
+  S.src0 = F.in_ptr[m];
   S.n0 = m == 0 ? F.nc_in : F.ns_in;
   S.src1 = nullptr;
   S.tag1 = nullptr;
@@ -292,9 +294,16 @@ __global__ void __launch_bounds__(CORR_THREADS) k_correspond(MapperDev D, int ro
   const float4 po = D.stack[m][(size_t)s * D.max_in + qi];
   const float4 sel = to_map(X, po);
   Top5 T;
+  uint32_t ncand = 0;
   knn5_hash(sel, F.origin, D.hkey + sm_index(s, m) * D.hash_T, D.hcnt + sm_index(s, m) * D.hash_T,
             D.hstart + sm_index(s, m) * D.hash_T, D.spts + sm_index(s, m) * D.sub_cap,
-            D.hash_T - 1, D.epoch, 1.0f, T);
+            D.hash_T - 1, D.epoch, 1.0f, T, &ncand);
+  {
+    unsigned long long wsum = ncand;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) wsum += __shfl_xor(wsum, o, 64);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&F.cand[round], wsum);
+  }
   int type = 0;
   double a[3] = {0, 0, 0}, b[3] = {0, 0, 0};
   if (T.d[4] < 1.0f) {
@@ -523,8 +532,15 @@ struct HostStream {
 
 using namespace loam;
 
+enum : int { FAM_STACK = 0, FAM_HASH, FAM_CORR, FAM_LM, FAM_INSERT, FAM_REVOX, FAM_OTHER, NFAM };
+
 struct loam_mapper {
   loam_params P;
+  bool prof = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<int> ev_fam;  // family of each recorded (start, stop) pair
+  double fam_ms[NFAM] = {0}, fam_bytes[NFAM] = {0};
+  long long fam_launches[NFAM] = {0};
   int dev = 0, B = 1;
   hipStream_t st = nullptr;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -570,6 +586,8 @@ uint32_t next_pow2(uint32_t v) {
 void free_all(loam_mapper* h) {
   for (void* p : h->allocs) (void)hipFree(p);
   h->allocs.clear();
+  for (auto& e : h->ev_pool) (void)hipEventDestroy(e);
+  h->ev_pool.clear();
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
   if (h->st) (void)hipStreamDestroy(h->st);
@@ -749,10 +767,18 @@ static int32_t mapper_input_common(loam_mapper* h, int32_t s, const float* corne
   StreamFrame& F = h->hf[s];
   F.nc_in = nc;
   F.ns_in = ns;
-  if (nc)
-    LOAM_HIP(hipMemcpyAsync(h->D.in_pts[0] + (size_t)s * h->D.max_in, corner, sizeof(float4) * nc, kind, h->st));
-  if (ns)
-    LOAM_HIP(hipMemcpyAsync(h->D.in_pts[1] + (size_t)s * h->D.max_in, surf, sizeof(float4) * ns, kind, h->st));
+  if (kind == hipMemcpyHostToDevice) {
+    // LaserMapping::input deep-copies the clouds (laser_mapping.cpp:188-190)
+    F.in_ptr[0] = h->D.in_pts[0] + (size_t)s * h->D.max_in;
+    F.in_ptr[1] = h->D.in_pts[1] + (size_t)s * h->D.max_in;
+    if (nc) LOAM_HIP(hipMemcpyAsync((void*)F.in_ptr[0], corner, sizeof(float4) * nc, kind, h->st));
+    if (ns) LOAM_HIP(hipMemcpyAsync((void*)F.in_ptr[1], surf, sizeof(float4) * ns, kind, h->st));
+  } else {
+    // HBM-resident clouds are read in place: they must stay valid until loam_mapper_solve
+    // returns (no copy, like the output() aliasing of scan_registration.cpp:572-576)
+    F.in_ptr[0] = reinterpret_cast<const float4*>(corner);
+    F.in_ptr[1] = reinterpret_cast<const float4*>(surf);
+  }
   host_initial_guess(H, H.pose);
   H.pending = true;
   return LOAM_OK;
@@ -769,8 +795,35 @@ int32_t loam_mapper_input_device(loam_mapper* h, int32_t s, const float* corner,
   return mapper_input_common(h, s, corner, nc, surf, ns, q_wodom, t_wodom, skip, hipMemcpyDeviceToDevice);
 }
 
+// HIP events around each launch when profiling is on (accumulated per kernel family)
+static hipError_t prof_begin(loam_mapper* h, int fam, hipEvent_t* stop) {
+  *stop = nullptr;
+  if (!h->prof) return hipSuccess;
+  size_t k = h->ev_fam.size() * 2;
+  while (h->ev_pool.size() < k + 2) {
+    hipEvent_t e;
+    hipError_t err = hipEventCreate(&e);
+    if (err != hipSuccess) return err;
+    h->ev_pool.push_back(e);
+  }
+  h->ev_fam.push_back(fam);
+  *stop = h->ev_pool[k + 1];
+  return hipEventRecord(h->ev_pool[k], h->st);
+}
+static hipError_t prof_end(loam_mapper* h, hipEvent_t stop) {
+  return (h->prof && stop) ? hipEventRecord(stop, h->st) : hipSuccess;
+}
+#define LAUNCH(fam, ...)                              \
+  do {                                                \
+    hipEvent_t stop_;                                 \
+    LOAM_HIP(prof_begin(h, (fam), &stop_));           \
+    __VA_ARGS__;                                      \
+    LOAM_HIP(prof_end(h, stop_));                     \
+  } while (0)
+
 int32_t loam_mapper_solve(loam_mapper* h) {
   if (!h) return LOAM_ERR_ARG;
+  h->ev_fam.clear();
   LOAM_HIP(hipSetDevice(h->dev));
   MapperDev& D = h->D;
   const int B = h->B;
@@ -819,6 +872,12 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   if (!any) return LOAM_OK;
   h->frame_counter++;
   D.epoch = h->frame_counter;
+  std::vector<uint32_t> tail0(2 * B);
+  for (int s = 0; s < B; ++s) {
+    tail0[2 * s] = h->hf[s].arena_tail[0];
+    tail0[2 * s + 1] = h->hf[s].arena_tail[1];
+    h->hf[s].cand[0] = h->hf[s].cand[1] = 0;
+  }
   D.cube_tab = h->cube_tab[h->parity];
   hipStream_t st = h->st;
   LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(StreamFrame) * B, hipMemcpyHostToDevice, st));
@@ -826,25 +885,25 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   LOAM_HIP(hipMemcpyAsync(h->d_lm_blk, h->lm_blk.data(), sizeof(int) * (B + 1), hipMemcpyHostToDevice, st));
   LOAM_HIP(hipEventRecord(h->ev[0], st));
   if (any_shift) {
-    k_shift_cubes<<<dim3(16, B), 256, 0, st>>>(D, h->cube_tab[h->parity], h->cube_tab[1 - h->parity]);
+    LAUNCH(FAM_OTHER, k_shift_cubes<<<dim3(16, B), 256, 0, st>>>(D, h->cube_tab[h->parity], h->cube_tab[1 - h->parity]));
     h->parity ^= 1;
     D.cube_tab = h->cube_tab[h->parity];
   }
-  k_stack_ds<<<B * 2, VX_THREADS, 0, st>>>(D);
-  k_submap_prep<<<(B + 63) / 64, 64, 0, st>>>(D);
+  LAUNCH(FAM_STACK, k_stack_ds<<<B * 2, VX_THREADS, 0, st>>>(D));
+  LAUNCH(FAM_OTHER, k_submap_prep<<<(B + 63) / 64, 64, 0, st>>>(D));
   LOAM_HIP(hipEventRecord(h->ev[1], st));
-  k_submap_insert<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D);
-  k_submap_alloc<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D);
-  k_submap_scatter<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D);
+  LAUNCH(FAM_HASH, k_submap_insert<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D));
+  LAUNCH(FAM_HASH, k_submap_alloc<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D));
+  LAUNCH(FAM_HASH, k_submap_scatter<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D));
   const int ncorr = h->corr_blk[B], nlm = h->lm_blk[B];
   for (int round = 0; round < 2; ++round) {
-    if (ncorr > 0) k_correspond<<<ncorr, CORR_THREADS, 0, st>>>(D, round);
-    for (int it = 0; it < 5; ++it) k_lm_pass<<<nlm, LM_THREADS, 0, st>>>(D, round);
-    k_lm_finish<<<(B + 63) / 64, 64, 0, st>>>(D, round);
+    if (ncorr > 0) LAUNCH(FAM_CORR, k_correspond<<<ncorr, CORR_THREADS, 0, st>>>(D, round));
+    for (int it = 0; it < 5; ++it) LAUNCH(FAM_LM, k_lm_pass<<<nlm, LM_THREADS, 0, st>>>(D, round));
+    LAUNCH(FAM_OTHER, k_lm_finish<<<(B + 63) / 64, 64, 0, st>>>(D, round));
   }
   LOAM_HIP(hipEventRecord(h->ev[2], st));
-  k_insert<<<dim3(16, B), 256, 0, st>>>(D);
-  k_revox<<<B * 2 * (WIN_VALID_MAX + EXTRA_CAP), VX_THREADS, 0, st>>>(D);
+  LAUNCH(FAM_INSERT, k_insert<<<dim3(16, B), 256, 0, st>>>(D));
+  LAUNCH(FAM_REVOX, k_revox<<<B * 2 * (WIN_VALID_MAX + EXTRA_CAP), VX_THREADS, 0, st>>>(D));
   LOAM_HIP(hipGetLastError());
   LOAM_HIP(hipEventRecord(h->ev[3], st));
   LOAM_HIP(hipMemcpyAsync(h->hf.data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
@@ -852,6 +911,31 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   float ms_total = 0, ms_opt = 0;
   LOAM_HIP(hipEventElapsedTime(&ms_total, h->ev[0], h->ev[3]));
   LOAM_HIP(hipEventElapsedTime(&ms_opt, h->ev[1], h->ev[2]));
+  if (h->prof) {
+    for (size_t k = 0; k < h->ev_fam.size(); ++k) {
+      float ms = 0;
+      LOAM_HIP(hipEventElapsedTime(&ms, h->ev_pool[2 * k], h->ev_pool[2 * k + 1]));
+      h->fam_ms[h->ev_fam[k]] += ms;
+      h->fam_launches[h->ev_fam[k]]++;
+    }
+    // algorithmic bytes (DESIGN.md "Kernels"): what each family must read / write
+    for (int s = 0; s < B; ++s) {
+      const StreamFrame& F = h->hf[s];
+      if (!F.active) continue;
+      const double nst = (double)F.nc_stack + F.ns_stack;
+      h->fam_bytes[FAM_STACK] += 16.0 * ((double)F.nc_in + F.ns_in + nst);
+      h->fam_bytes[FAM_HASH] += 32.0 * ((double)F.sub_n[0] + F.sub_n[1]);
+      h->fam_bytes[FAM_INSERT] += 36.0 * nst;
+      if (F.optimize) {
+        for (int r = 0; r < 2; ++r) {
+          const double ne = F.corner_num[r], npl = F.surf_num[r], ninv = nst - ne - npl;
+          const double rec = 60.0 * ne + 44.0 * npl + 4.0 * ninv;
+          h->fam_bytes[FAM_CORR] += 16.0 * nst + 16.0 * (double)F.cand[r] + rec;
+          h->fam_bytes[FAM_LM] += (double)F.lm[r].passes * rec;
+        }
+      }
+    }
+  }
   // host bookkeeping + compaction decisions
   std::vector<int> pairs;
   int32_t status = LOAM_OK;
@@ -884,6 +968,10 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     S.valid_num = F.valid_num;
     S.ms_total = ms_total;
     S.ms_opt = ms_opt;
+    if (h->prof) {  // window content read + stacks read + new content written
+      const double written = (double)(F.arena_tail[0] - tail0[2 * s]) + (double)(F.arena_tail[1] - tail0[2 * s + 1]);
+      h->fam_bytes[FAM_REVOX] += 16.0 * ((double)F.sub_n[0] + F.sub_n[1] + F.nc_stack + F.ns_stack + written);
+    }
     if (F.err) {
       set_error("loam_mapper_solve: device capacity exceeded (err flags " + std::to_string(F.err) + ")");
       status = LOAM_ERR_CAPACITY;
@@ -910,6 +998,31 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     }
   }
   return status;
+}
+
+int32_t loam_mapper_set_profiling(loam_mapper* h, int32_t enable) {
+  if (!h) return LOAM_ERR_ARG;
+  h->prof = enable != 0;
+  return LOAM_OK;
+}
+
+int32_t loam_mapper_kernel_times(loam_mapper* h, loam_kernel_times* out) {
+  if (!h || !out) return LOAM_ERR_ARG;
+  for (int f = 0; f < LOAM_KFAM_COUNT; ++f) {
+    out->ms[f] = f < NFAM ? h->fam_ms[f] : 0.0;
+    out->launches[f] = f < NFAM ? h->fam_launches[f] : 0;
+    out->bytes[f] = f < NFAM ? h->fam_bytes[f] : 0.0;
+  }
+  return LOAM_OK;
+}
+
+int32_t loam_mapper_reset_kernel_times(loam_mapper* h) {
+  if (!h) return LOAM_ERR_ARG;
+  for (int f = 0; f < NFAM; ++f) {
+    h->fam_ms[f] = h->fam_bytes[f] = 0.0;
+    h->fam_launches[f] = 0;
+  }
+  return LOAM_OK;
 }
 
 int32_t loam_mapper_pose(loam_mapper* h, int32_t s, double* q_w, double* t_w) {

@@ -47,6 +47,14 @@ class MapStats(ctypes.Structure):
                 ("valid_num", c_i32), ("ms_total", c_d), ("ms_opt", c_d)]
 
 
+KFAM = ("stack_voxelgrid", "submap_hash_build", "correspondence", "lm_pass", "insert",
+        "cube_revoxel", "other")
+
+
+class KernelTimes(ctypes.Structure):
+    _fields_ = [("ms", c_d * 8), ("launches", ctypes.c_int64 * 8), ("bytes", c_d * 8)]
+
+
 # name -> (restype, argtypes); must cover every function declared in include/loam_core.h
 SIGNATURES = {
     "loam_params_default": (None, [ctypes.POINTER(Params)]),
@@ -68,6 +76,9 @@ SIGNATURES = {
     "loam_mapper_input_device": (c_i32, [vp, c_i32, vp, c_i32, vp, c_i32, vp, vp, c_i32]),
     "loam_mapper_solve": (c_i32, [vp]),
     "loam_mapper_pose": (c_i32, [vp, c_i32, vp, vp]),
+    "loam_mapper_set_profiling": (c_i32, [vp, c_i32]),
+    "loam_mapper_kernel_times": (c_i32, [vp, ctypes.POINTER(KernelTimes)]),
+    "loam_mapper_reset_kernel_times": (c_i32, [vp]),
     "loam_mapper_stats": (c_i32, [vp, c_i32, ctypes.POINTER(MapStats)]),
     "loam_mapper_get_state": (c_i32, [vp, c_i32, vp, vp, vp]),
     "loam_mapper_set_state": (c_i32, [vp, c_i32, vp, vp, vp]),

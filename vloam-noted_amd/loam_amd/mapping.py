@@ -59,6 +59,18 @@ class BatchMapper:
     def solve(self):
         check(lib().loam_mapper_solve(self.h))
 
+    def set_profiling(self, enable=True):
+        check(lib().loam_mapper_set_profiling(self.h, int(enable)))
+
+    def kernel_times(self):
+        kt = _core.KernelTimes()
+        check(lib().loam_mapper_kernel_times(self.h, ctypes.byref(kt)))
+        return {name: dict(ms=kt.ms[i], launches=int(kt.launches[i]), bytes=kt.bytes[i])
+                for i, name in enumerate(_core.KFAM)}
+
+    def reset_kernel_times(self):
+        check(lib().loam_mapper_reset_kernel_times(self.h))
+
     def pose(self, stream=0):
         q = np.empty(4)
         t = np.empty(3)
