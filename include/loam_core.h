@@ -128,12 +128,20 @@ int32_t loam_mapper_input_device(loam_mapper* h, int32_t stream, const float* d_
                                  int32_t n_corner, const float* d_surf, int32_t n_surf,
                                  const double* q_wodom, const double* t_wodom,
                                  int32_t skip_frame);
+/* loam_mapper_input_device for n streams at once: streams[i], device pointers (as integers),
+ * sizes, q_wodom (n x 4), t_wodom (n x 3); skip_frame = 0 */
+int32_t loam_mapper_input_device_batch(loam_mapper* h, int32_t n, const int32_t* streams,
+                                       const uint64_t* d_corner, const int32_t* n_corner,
+                                       const uint64_t* d_surf, const int32_t* n_surf,
+                                       const double* q_wodom, const double* t_wodom);
 /* LaserMapping::solveMapping (laser_mapping.cpp:212-814) for every stream that received an
  * input since the last call (skip_frame inputs only update the high-frequency pose). */
 int32_t loam_mapper_solve(loam_mapper* h);
 /* pose after solveMapping: q_w_curr (xyzw), t_w_curr (laser_mapping.cpp:826-832) */
 int32_t loam_mapper_pose(loam_mapper* h, int32_t stream, double* q_w, double* t_w);
 int32_t loam_mapper_stats(loam_mapper* h, int32_t stream, loam_map_stats* st);
+/* stats of streams 0..n-1 */
+int32_t loam_mapper_stats_all(loam_mapper* h, loam_map_stats* out, int32_t n);
 
 /* kernel-level timing: with profiling on, every launch of loam_mapper_solve is bracketed by
  * HIP events on the handle's stream; times, launches and algorithmic bytes (DESIGN.md,

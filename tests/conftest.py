@@ -26,6 +26,10 @@ def pytest_configure(config):
     if not os.path.exists(os.path.join(ROOT, "vloam-noted_amd", "loam_amd", "_lib", "libloam_synth.so")):
         subprocess.run(["make", "-C", os.path.join(ROOT, "vloam-noted_amd"), "synth"], check=True,
                        stdout=subprocess.DEVNULL)
+    # the HIP library (hipcc cross-compiles gfx950 without a GPU): the ABI tests load it
+    if not os.path.exists(os.path.join(ROOT, "vloam-noted_amd", "loam_amd", "_lib", "libloam_core.so")):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "vloam-noted_amd"), "-j4"], check=True,
+                       stdout=subprocess.DEVNULL)
 
 
 def gpu_available():

@@ -333,23 +333,25 @@ __host__ __device__ inline void lm_step(LmState& S, const double* red) {
 }
 
 // ---------------------------------------------------------------------------------------
-// fused LM pass: evaluate at the state's evaluation point, per-workgroup partial of
-// (J^T J, J^T r, cost, rows), last-arriving workgroup of the stream reduces the partials
-// in chunk order (deterministic) and advances the trust-region state (lm_step).
-// Publish/consume follows the agent-scope release/acquire recipe (cdna_hip_programming.md
-// Guideline 16): plain stores -> vmcnt(0) -> barrier -> release fence -> ticket atomic;
-// the last arriver: acquire fence -> vmcnt(0) -> barrier -> plain loads.
+// LM pass, split in two launches per trust-region iteration:
+//   lm_eval_block  (many workgroups per stream)  evaluate every residual block at the state's
+//                  evaluation point, grid-stride over the records, one partial
+//                  (J^T J, J^T r, cost, rows) per workgroup in a fixed slot;
+//   lm_step_wave   (one wave per stream)  sum the partials in a fixed order (lane-strided,
+//                  then a shuffle tree: deterministic), run lm_step on lane 0.
+// Keeping the trust-region logic out of the evaluation kernel keeps its register budget (and
+// occupancy) that of the residual arithmetic alone.
 // ---------------------------------------------------------------------------------------
-template <int kThreads, int kPerThread>
-__device__ inline void lm_pass_body(const int* __restrict__ r_type, const float* __restrict__ r_px,
-                                    const float* __restrict__ r_py, const float* __restrict__ r_pz,
-                                    const double* __restrict__ a0, const double* __restrict__ a1,
-                                    const double* __restrict__ a2, const double* __restrict__ b0,
-                                    const double* __restrict__ b1, const double* __restrict__ b2,
-                                    int nrec, int chunk, int nchunks, LmState& S,
-                                    double* partials, uint32_t* ticket) {
+struct LmRecView {
+  const int* type;
+  const float *px, *py, *pz;
+  const double *a0, *a1, *a2, *b0, *b1, *b2;
+};
+
+template <int kThreads>
+__device__ inline void lm_eval_block(const LmRecView& R, int nrec, const LmState& S, int blk,
+                                     int nblk, double* partial_out) {
   __shared__ double red[kThreads / 64][LM_NACC];
-  __shared__ int last;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int status = S.status;
   if (status == LM_DONE) return;  // uniform for every workgroup of the stream
@@ -359,16 +361,11 @@ __device__ inline void lm_pass_body(const int* __restrict__ r_type, const float*
   double acc[LM_NACC];
 #pragma unroll
   for (int i = 0; i < LM_NACC; ++i) acc[i] = 0.0;
-  constexpr int kChunk = kThreads * kPerThread;
-  const int base = chunk * kChunk;
-#pragma unroll
-  for (int it = 0; it < kPerThread; ++it) {
-    const int r = base + it * kThreads + tid;
-    if (r < nrec) {
-      const int t = r_type[r];
-      if (t != 0)
-        lm_accum(t, r_px[r], r_py[r], r_pz[r], a0[r], a1[r], a2[r], b0[r], b1[r], b2[r], X, acc);
-    }
+  for (int r = blk * kThreads + tid; r < nrec; r += nblk * kThreads) {
+    const int t = R.type[r];
+    if (t != 0)
+      lm_accum(t, R.px[r], R.py[r], R.pz[r], R.a0[r], R.a1[r], R.a2[r], R.b0[r], R.b1[r],
+               R.b2[r], X, acc);
   }
 #pragma unroll
   for (int i = 0; i < LM_NACC; ++i) {
@@ -380,33 +377,39 @@ __device__ inline void lm_pass_body(const int* __restrict__ r_type, const float*
     double v = 0.0;
 #pragma unroll
     for (int w = 0; w < kThreads / 64; ++w) v += red[w][tid];
-    partials[(size_t)chunk * LM_NACC + tid] = v;
+    partial_out[tid] = v;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = (prev == (uint32_t)nchunks - 1) ? 1 : 0;
-  }
-  __syncthreads();
-  if (!last) return;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  if (tid < LM_NACC) {
+}
+
+// one wave: reduce nblk partials, advance the state; returns true (lane 0) if the state
+// terminated in this step
+__device__ inline bool lm_step_wave(const double* partials, int nblk, LmState& S,
+                                    double* best_out = nullptr) {
+  const int lane = threadIdx.x & 63;
+  if (S.status == LM_DONE) return false;
+  __shared__ double sred[LM_NACC];
+  // the state is staged in LDS: lm_step is a long dependent chain, and every access to the
+  // global copy would pay a memory round trip
+  __shared__ LmState ls;
+  static_assert(sizeof(LmState) % 8 == 0, "LmState copy granularity");
+  constexpr int NW = sizeof(LmState) / 8;
+  const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&S);
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(&ls);
+  for (int w = lane; w < NW; w += 64) dst[w] = src[w];
+  for (int i = 0; i < LM_NACC; ++i) {
     double v = 0.0;
-    for (int c = 0; c < nchunks; ++c) v += partials[(size_t)c * LM_NACC + tid];
-    red[0][tid] = v;
+    for (int c = lane; c < nblk; c += 64) v += partials[(size_t)c * LM_NACC + i];
+    v = wave_sum_d(v);
+    if (lane == 0) sred[i] = v;
   }
   __syncthreads();
-  if (tid == 0) {
-    lm_step(S, red[0]);
-    *ticket = 0;
-  }
+  if (lane == 0) lm_step(ls, sred);
+  __syncthreads();
+  unsigned long long* back = reinterpret_cast<unsigned long long*>(&S);
+  for (int w = lane; w < NW; w += 64) back[w] = dst[w];
+  const bool done = ls.status == LM_DONE;
+  if (done && best_out && lane < 7) best_out[lane] = ls.best[lane];
+  return done;
 }
 
 }  // namespace loam

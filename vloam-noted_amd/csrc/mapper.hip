@@ -7,9 +7,10 @@
 //   k_submap_*         gather the 5x5x3 window cubes (:448-489) and build a 1 m-cell hash
 //                      (replaces the KD-tree build, :519-520); exact 5-NN because accepted
 //                      matches need all 5 neighbours within 1 m (:557, :642)
-//   2 x { k_correspond  5-NN + PCA line / QR plane fit -> factor records (:545-699)
-//         5 x k_lm_pass   fused: evaluate candidate (cost + J^T J + J^T r) -> last-arriving
-//                         workgroup of each stream reduces + runs the LM step (lm.h) }
+//   2 x { k_knn         exact 5-NN of every query in the cell hash (:554, :633)
+//         k_geom        PCA line / QR plane fit of the neighbours -> factor records (:557-699)
+//         5 x { k_lm_eval  candidate cost + J^T J + J^T r, per-workgroup partials (lm.h)
+//               k_lm_step  one wave per stream: reduce partials, Ceres TR-LM step } }
 //   k_insert           transform stacks with the final pose, assign cubes (:741-788)
 //   k_revox            re-VoxelGrid every window cube (:795-808) into the map arena
 //
@@ -34,9 +35,9 @@ constexpr int WIN_MAX = 125;
 constexpr int WIN_VALID_MAX = 75;
 constexpr int EXTRA_CAP = 64;
 constexpr int CORR_THREADS = 256;
+constexpr int CORR_BLK = 64;    // correspondence workgroups per stream (grid-stride)
 constexpr int LM_THREADS = 256;
-constexpr int LM_PER_THREAD = 4;
-constexpr int LM_CHUNK = LM_THREADS * LM_PER_THREAD;
+constexpr int LM_EBLK = 32;     // LM evaluation workgroups per stream (grid-stride)
 constexpr int SUBMAP_BLOCKS = 64;
 constexpr int MAP_ERR_SUBMAP = 4, MAP_ERR_EXTRA = 8, MAP_ERR_HASH = 16;
 
@@ -59,6 +60,7 @@ struct StreamFrame {
   int arena_active[2];
   uint32_t scratch_tail[2];
   uint32_t cursor[2];
+  uint32_t hmask[2];              // this frame's cell-hash size - 1 (>= 2x the submap points)
   int extra_n[2];
   int extra_list[2][EXTRA_CAP];
   int err;
@@ -81,6 +83,9 @@ struct MapperDev {
   unsigned long long* hkey;  // [B][2][T]
   unsigned long long* hcnt;
   uint32_t* hstart;
+  uint4* qtab;      // [B][2][T] packed query entries {key, epoch, start, count}
+  int* knn_id;      // [5][B][2*max_in] neighbour ids (submap index) per query, -1: none
+  size_t knn_stride;
   float4* sub_lin;  // [B][2][sub_cap] window-order submap
   float4* spts;     // [B][2][sub_cap] cell-sorted submap (w = submap index bits)
   uint32_t* pt_slot;
@@ -98,18 +103,7 @@ struct MapperDev {
   int* vx_idx;
   double* partials;  // [B][max_chunks][LM_NACC]
   uint32_t* tickets;  // [B]
-  const int* corr_blk;  // [B+1] block prefix (k_correspond)
-  const int* lm_blk;    // [B+1] block prefix (k_lm_pass)
 };
-
-__device__ inline int find_stream(const int* blk, int B, int b) {
-  int lo = 0, hi = B;  // largest s with blk[s] <= b
-  while (hi - lo > 1) {
-    int mid = (lo + hi) >> 1;
-    if (blk[mid] <= b) lo = mid; else hi = mid;
-  }
-  return lo;
-}
 
 __device__ inline size_t sm_index(int s, int m) { return (size_t)s * 2 + m; }
 
@@ -168,32 +162,40 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
 // ---------------------------------------------------------------------------------------
 // submap: offsets of the window cubes (laserCloudCornerFromMap concatenation order)
 // ---------------------------------------------------------------------------------------
-__global__ void k_submap_prep(MapperDev D) {
-  int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= D.B) return;
+__global__ void __launch_bounds__(128) k_submap_prep(MapperDev D) {
+  // one wave per map; window slots 2*lane, 2*lane+1 (valid_num <= 75 <= 128)
+  const int s = blockIdx.x;
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
-  for (int m = 0; m < 2; ++m) {
-    uint32_t acc = 0;
-    const uint2* tab = D.cube_tab + sm_index(s, m) * NCUBE;
-    for (int w = 0; w < F.valid_num; ++w) {
-      F.sub_off[m][w] = acc;
-      acc += tab[F.window[w]].y;
+  const int m = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint2* tab = D.cube_tab + sm_index(s, m) * NCUBE;
+  const int vn = F.valid_num;
+  const int w0 = 2 * lane, w1 = 2 * lane + 1;
+  const uint32_t c0 = w0 < vn ? tab[F.window[w0]].y : 0u;
+  const uint32_t c1 = w1 < vn ? tab[F.window[w1]].y : 0u;
+  const uint32_t inc = wave_incl_scan_u(c0 + c1);
+  uint32_t total = __shfl(inc, 63, 64);
+  const bool over = total > (uint32_t)D.sub_cap;
+  const uint32_t ex = over ? 0u : inc - (c0 + c1);
+  if (w0 < vn) F.sub_off[m][w0] = ex;
+  if (w1 < vn) F.sub_off[m][w1] = over ? 0u : ex + c0;
+  if (lane == 0) {
+    if (over) {
+      atomicOr(&F.err, MAP_ERR_SUBMAP);
+      total = 0;
     }
-    F.sub_off[m][F.valid_num] = acc;
-    if (acc > (uint32_t)D.sub_cap) {
-      F.err |= MAP_ERR_SUBMAP;
-      acc = 0;
-      F.sub_off[m][F.valid_num] = 0;
-      for (int w = 0; w < F.valid_num; ++w) F.sub_off[m][w] = 0;
-    }
-    F.sub_n[m] = acc;
+    F.sub_off[m][vn] = total;
+    F.sub_n[m] = total;
     F.scratch_tail[m] = 0;
     F.cursor[m] = 0;
     F.extra_n[m] = 0;
+    uint32_t T = 1024;
+    while (T < 2 * total && T < (uint32_t)D.hash_T) T <<= 1;
+    F.hmask[m] = T - 1;
   }
+  __syncthreads();
   // laser_mapping.cpp:514
-  F.optimize = (F.sub_n[0] > 10 && F.sub_n[1] > 50) ? 1 : 0;
+  if (threadIdx.x == 0) F.optimize = (F.sub_n[0] > 10 && F.sub_n[1] > 50) ? 1 : 0;
 }
 
 // gather the window cubes into sub_lin and claim the cell slots; rank within the cell
@@ -210,7 +212,7 @@ __global__ void k_submap_insert(MapperDev D) {
   unsigned long long* hc = D.hcnt + sm_index(s, m) * D.hash_T;
   uint32_t* ps = D.pt_slot + sm_index(s, m) * D.sub_cap;
   uint32_t* pr = D.pt_rank + sm_index(s, m) * D.sub_cap;
-  const uint32_t mask = D.hash_T - 1;
+  const uint32_t mask = F.hmask[m];
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     int lo = 0, hi = F.valid_num;  // window slot: largest w with sub_off[w] <= i
     while (hi - lo > 1) {
@@ -238,16 +240,17 @@ __global__ void k_submap_alloc(MapperDev D) {
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
   const uint32_t n = F.sub_n[m];
+  const unsigned long long* hk = D.hkey + sm_index(s, m) * D.hash_T;
   const unsigned long long* hc = D.hcnt + sm_index(s, m) * D.hash_T;
   uint32_t* hs = D.hstart + sm_index(s, m) * D.hash_T;
+  uint4* qt = D.qtab + sm_index(s, m) * D.hash_T;
   const uint32_t* ps = D.pt_slot + sm_index(s, m) * D.sub_cap;
   const uint32_t* pr = D.pt_rank + sm_index(s, m) * D.sub_cap;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    if (pr[i] == 0) {
-      uint32_t slot = ps[i];
-      uint32_t cnt = (uint32_t)(hc[slot] & 0xFFFFFFFFu);
-      hs[slot] = atomicAdd(&F.cursor[m], cnt);
-    }
+  // block-uniform trip count: hash_alloc_cell needs whole waves
+  for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < n; b0 += gridDim.x * blockDim.x) {
+    const uint32_t i = b0 + threadIdx.x;
+    const bool first = i < n && pr[i] == 0;
+    hash_alloc_cell(first, first ? ps[i] : 0u, hk, hc, D.epoch, hs, qt, &F.cursor[m]);
   }
 }
 
@@ -272,103 +275,129 @@ __global__ void k_submap_scatter(MapperDev D) {
 // ---------------------------------------------------------------------------------------
 // correspondences of one outer round (laser_mapping.cpp:545-699) -> factor records
 // ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(CORR_THREADS) k_correspond(MapperDev D, int round) {
-  const int s = find_stream(D.corr_blk, D.B, blockIdx.x);
+// pass 1: exact 5-NN of every query in the cell hash -> neighbour ids (laser_mapping.cpp:554,
+// :633, accepted only if the 5th is within 1 m: :557, :642)
+__global__ void __launch_bounds__(CORR_THREADS) k_knn(MapperDev D, int round) {
+  const int s = blockIdx.x / CORR_BLK, blk = blockIdx.x % CORR_BLK;
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
-  const int local = (blockIdx.x - D.corr_blk[s]) * CORR_THREADS + threadIdx.x;
   double X[7];
 #pragma unroll
   for (int i = 0; i < 7; ++i) X[i] = F.pose[i];
-  if (local == 0) lm_init(F.lm[round], X, 4, F.optimize != 0);
+  if (blk == 0 && threadIdx.x == 0) lm_init(F.lm[round], X, 4, F.optimize != 0);
+  if (!F.optimize) return;  // k_geom types every record 0
   const int nc = F.nc_stack, ns = F.ns_stack;
-  if (local >= nc + ns) return;
   const size_t rb = (size_t)s * 2 * D.max_in;
-  const int ridx = local;  // corners [0, nc), surfs [nc, nc + ns)
-  if (!F.optimize) {
-    D.r_type[rb + ridx] = 0;
-    return;
-  }
-  const int m = local < nc ? 0 : 1;
-  const int qi = m == 0 ? local : local - nc;
-  const float4 po = D.stack[m][(size_t)s * D.max_in + qi];
-  const float4 sel = to_map(X, po);
-  Top5 T;
   uint32_t ncand = 0;
-  knn5_hash(sel, F.origin, D.hkey + sm_index(s, m) * D.hash_T, D.hcnt + sm_index(s, m) * D.hash_T,
-            D.hstart + sm_index(s, m) * D.hash_T, D.spts + sm_index(s, m) * D.sub_cap,
-            D.hash_T - 1, D.epoch, 1.0f, T, &ncand);
-  {
-    unsigned long long wsum = ncand;
+  for (int ridx = blk * CORR_THREADS + threadIdx.x; ridx < nc + ns; ridx += CORR_BLK * CORR_THREADS) {
+    const int m = ridx < nc ? 0 : 1;  // corners [0, nc), surfs [nc, nc + ns)
+    const int qi = m == 0 ? ridx : ridx - nc;
+    const float4 sel = to_map(X, D.stack[m][(size_t)s * D.max_in + qi]);
+    Top5 T;
+    knn5_hash(sel, F.origin, D.qtab + sm_index(s, m) * D.hash_T, D.spts + sm_index(s, m) * D.sub_cap,
+              F.hmask[m], D.epoch, 1.0f, T, &ncand);
+    const bool ok = T.d[4] < 1.0f;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) wsum += __shfl_xor(wsum, o, 64);
-    if ((threadIdx.x & 63) == 0) atomicAdd(&F.cand[round], wsum);
+    for (int k = 0; k < 5; ++k) D.knn_id[k * D.knn_stride + rb + ridx] = ok ? T.id[k] : -1;
   }
-  int type = 0;
-  double a[3] = {0, 0, 0}, b[3] = {0, 0, 0};
-  if (T.d[4] < 1.0f) {
-    float nb[5][3];
+  unsigned long long wc = ncand;
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      nb[j][0] = T.x[j];
-      nb[j][1] = T.y[j];
-      nb[j][2] = T.z[j];
-    }
-    if (m == 0) {
-      d3 pa, pb;
-      if (edge_from_nbrs(nb, pa, pb)) {
-        type = 1;
-        d3 de{pa.x - pb.x, pa.y - pb.y, pa.z - pb.z};
-        double dn = sqrt(de.x * de.x + de.y * de.y + de.z * de.z);
-        a[0] = pa.x; a[1] = pa.y; a[2] = pa.z;
-        b[0] = de.x / dn; b[1] = de.y / dn; b[2] = de.z / dn;
-        atomicAdd(&F.corner_num[round], 1);
-      }
-    } else {
-      d3 n;
-      double d;
-      if (plane_from_nbrs(nb, n, d)) {
-        type = 3;
-        a[0] = n.x; a[1] = n.y; a[2] = n.z;
-        b[0] = d;
-        atomicAdd(&F.surf_num[round], 1);
-      }
-    }
-  }
-  D.r_type[rb + ridx] = type;
-  D.r_px[rb + ridx] = po.x;
-  D.r_py[rb + ridx] = po.y;
-  D.r_pz[rb + ridx] = po.z;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    D.r_a[k][rb + ridx] = a[k];
-    D.r_b[k][rb + ridx] = b[k];
-  }
+  for (int o = 32; o > 0; o >>= 1) wc += __shfl_xor(wc, o, 64);
+  if ((threadIdx.x & 63) == 0 && wc) atomicAdd(&F.cand[round], wc);
 }
 
-__global__ void __launch_bounds__(LM_THREADS) k_lm_pass(MapperDev D, int round) {
-  const int s = find_stream(D.lm_blk, D.B, blockIdx.x);
+// pass 2: line PCA / plane fit of the 5 neighbours -> factor records (laser_mapping.cpp:557-603,
+// :642-680)
+__global__ void __launch_bounds__(CORR_THREADS) k_geom(MapperDev D, int round) {
+  const int s = blockIdx.x / CORR_BLK, blk = blockIdx.x % CORR_BLK;
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
-  const int chunk = blockIdx.x - D.lm_blk[s];
-  const int nchunks = D.lm_blk[s + 1] - D.lm_blk[s];
+  const int nc = F.nc_stack, ns = F.ns_stack;
   const size_t rb = (size_t)s * 2 * D.max_in;
-  LmState& S = F.lm[round];
-  lm_pass_body<LM_THREADS, LM_PER_THREAD>(D.r_type + rb, D.r_px + rb, D.r_py + rb, D.r_pz + rb, D.r_a[0] + rb,
-                     D.r_a[1] + rb, D.r_a[2] + rb, D.r_b[0] + rb, D.r_b[1] + rb, D.r_b[2] + rb,
-                     F.nc_stack + F.ns_stack, chunk, nchunks, S,
-                     D.partials + (size_t)s * D.max_chunks * LM_NACC, D.tickets + s);
+  uint32_t n_edge = 0, n_plane = 0;  // reduced once per wave after the loop
+  for (int ridx = blk * CORR_THREADS + threadIdx.x; ridx < nc + ns; ridx += CORR_BLK * CORR_THREADS) {
+    if (!F.optimize) {
+      D.r_type[rb + ridx] = 0;
+      continue;
+    }
+    const int m = ridx < nc ? 0 : 1;
+    const int qi = m == 0 ? ridx : ridx - nc;
+    const float4 po = D.stack[m][(size_t)s * D.max_in + qi];
+    int type = 0;
+    double a[3] = {0, 0, 0}, b[3] = {0, 0, 0};
+    if (D.knn_id[rb + ridx] >= 0) {
+      const float4* lin = D.sub_lin + sm_index(s, m) * D.sub_cap;
+      float nb[5][3];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const float4 p = lin[D.knn_id[j * D.knn_stride + rb + ridx]];
+        nb[j][0] = p.x;
+        nb[j][1] = p.y;
+        nb[j][2] = p.z;
+      }
+      if (m == 0) {
+        d3 pa, pb;
+        if (edge_from_nbrs(nb, pa, pb)) {
+          type = 1;
+          d3 de{pa.x - pb.x, pa.y - pb.y, pa.z - pb.z};
+          double dn = sqrt(de.x * de.x + de.y * de.y + de.z * de.z);
+          a[0] = pa.x; a[1] = pa.y; a[2] = pa.z;
+          b[0] = de.x / dn; b[1] = de.y / dn; b[2] = de.z / dn;
+          ++n_edge;
+        }
+      } else {
+        d3 n;
+        double d;
+        if (plane_from_nbrs(nb, n, d)) {
+          type = 3;
+          a[0] = n.x; a[1] = n.y; a[2] = n.z;
+          b[0] = d;
+          ++n_plane;
+        }
+      }
+    }
+    D.r_type[rb + ridx] = type;
+    D.r_px[rb + ridx] = po.x;
+    D.r_py[rb + ridx] = po.y;
+    D.r_pz[rb + ridx] = po.z;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      D.r_a[k][rb + ridx] = a[k];
+      D.r_b[k][rb + ridx] = b[k];
+    }
+  }
+  uint32_t we = n_edge, wp = n_plane;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    we += __shfl_xor(we, o, 64);
+    wp += __shfl_xor(wp, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (we) atomicAdd(&F.corner_num[round], (int)we);
+    if (wp) atomicAdd(&F.surf_num[round], (int)wp);
+  }
 }
 
-// copy the round's result into the stream pose (Ceres writes the best point back into
-// the parameter blocks, laser_mapping.cpp:535-536)
-__global__ void k_lm_finish(MapperDev D, int round) {
-  int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= D.B) return;
+// LM evaluation pass at the state's evaluation point (lm.h)
+__global__ void __launch_bounds__(LM_THREADS) k_lm_eval(MapperDev D, int round) {
+  const int s = blockIdx.x / LM_EBLK, blk = blockIdx.x % LM_EBLK;
+  const StreamFrame& F = D.fr[s];
+  if (!F.active) return;
+  const size_t rb = (size_t)s * 2 * D.max_in;
+  const LmRecView R{D.r_type + rb, D.r_px + rb, D.r_py + rb, D.r_pz + rb, D.r_a[0] + rb,
+                    D.r_a[1] + rb, D.r_a[2] + rb, D.r_b[0] + rb, D.r_b[1] + rb, D.r_b[2] + rb};
+  lm_eval_block<LM_THREADS>(R, F.nc_stack + F.ns_stack, F.lm[round], blk, LM_EBLK,
+                            D.partials + ((size_t)s * LM_EBLK + blk) * LM_NACC);
+}
+
+// LM step: one wave per stream; on termination the best point becomes the stream pose
+// (Ceres writes it back into the parameter blocks, laser_mapping.cpp:535-536)
+__global__ void __launch_bounds__(64) k_lm_step(MapperDev D, int round) {
+  const int s = blockIdx.x;
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
-  const LmState& S = F.lm[round];
-  for (int i = 0; i < 7; ++i) F.pose[i] = S.best[i];
+  LmState& S = F.lm[round];
+  lm_step_wave(D.partials + (size_t)s * LM_EBLK * LM_NACC, LM_EBLK, S, F.pose);  // pose = best when done
 }
 
 // ---------------------------------------------------------------------------------------
@@ -547,9 +576,6 @@ struct loam_mapper {
   MapperDev D{};
   std::vector<StreamFrame> hf;
   std::vector<HostStream> hs;
-  std::vector<int> corr_blk, lm_blk;
-  int* d_corr_blk = nullptr;
-  int* d_lm_blk = nullptr;
   uint2* cube_tab[2] = {nullptr, nullptr};
   int parity = 0;
   int* d_pairs = nullptr;
@@ -652,7 +678,7 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
   D.sub_cap = h->P.max_submap_points;
   D.hash_T = (int)next_pow2((uint32_t)D.sub_cap);
   D.scratch_cap = D.sub_cap + D.max_in;
-  D.max_chunks = (2 * D.max_in + LM_CHUNK - 1) / LM_CHUNK;
+  D.max_chunks = LM_EBLK;
   D.leaf[0] = (float)h->P.mapping_line_resolution;
   D.leaf[1] = (float)h->P.mapping_plane_resolution;
   const size_t B = n_streams;
@@ -679,6 +705,9 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
   ALLOC(D.hkey, B * 2 * (size_t)D.hash_T);
   ALLOC(D.hcnt, B * 2 * (size_t)D.hash_T);
   ALLOC(D.hstart, B * 2 * (size_t)D.hash_T);
+  ALLOC(D.qtab, B * 2 * (size_t)D.hash_T);
+  D.knn_stride = B * 2 * (size_t)D.max_in;
+  ALLOC(D.knn_id, 5 * D.knn_stride);
   ALLOC(D.sub_lin, B * 2 * (size_t)D.sub_cap);
   ALLOC(D.spts, B * 2 * (size_t)D.sub_cap);
   ALLOC(D.pt_slot, B * 2 * (size_t)D.sub_cap);
@@ -697,14 +726,10 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
   ALLOC(D.vx_idx, B * 2 * (size_t)D.scratch_cap);
   ALLOC(D.partials, B * (size_t)D.max_chunks * LM_NACC);
   ALLOC(D.tickets, B);
-  ALLOC(h->d_corr_blk, B + 1);
-  ALLOC(h->d_lm_blk, B + 1);
   ALLOC(h->d_pairs, B * 2);
   ALLOC(h->d_new_off, B * 2 * (NCUBE + 1));
 #undef ALLOC
   D.cube_tab = h->cube_tab[0];
-  D.corr_blk = h->d_corr_blk;
-  D.lm_blk = h->d_lm_blk;
   h->hf.assign(B, StreamFrame{});
   h->hs.assign(B, HostStream{});
   for (size_t s = 0; s < B; ++s) {
@@ -821,6 +846,29 @@ static hipError_t prof_end(loam_mapper* h, hipEvent_t stop) {
     LOAM_HIP(prof_end(h, stop_));                     \
   } while (0)
 
+int32_t loam_mapper_input_device_batch(loam_mapper* h, int32_t n, const int32_t* streams,
+                                       const uint64_t* d_corner, const int32_t* n_corner,
+                                       const uint64_t* d_surf, const int32_t* n_surf,
+                                       const double* q_wodom, const double* t_wodom) {
+  if (!h || n < 0 || (n > 0 && (!streams || !d_corner || !n_corner || !d_surf || !n_surf || !q_wodom || !t_wodom))) {
+    set_error("loam_mapper_input_device_batch: bad arguments");
+    return LOAM_ERR_ARG;
+  }
+  for (int i = 0; i < n; ++i) {
+    int32_t rc = mapper_input_common(h, streams[i], reinterpret_cast<const float*>(d_corner[i]), n_corner[i],
+                                     reinterpret_cast<const float*>(d_surf[i]), n_surf[i], q_wodom + 4 * i,
+                                     t_wodom + 3 * i, 0, hipMemcpyDeviceToDevice);
+    if (rc != LOAM_OK) return rc;
+  }
+  return LOAM_OK;
+}
+
+int32_t loam_mapper_stats_all(loam_mapper* h, loam_map_stats* out, int32_t n) {
+  if (!h || !out || n < 0 || n > h->B) return LOAM_ERR_ARG;
+  for (int s = 0; s < n; ++s) out[s] = h->hs[s].st;
+  return LOAM_OK;
+}
+
 int32_t loam_mapper_solve(loam_mapper* h) {
   if (!h) return LOAM_ERR_ARG;
   h->ev_fam.clear();
@@ -828,8 +876,6 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   MapperDev& D = h->D;
   const int B = h->B;
   bool any = false, any_shift = false;
-  h->corr_blk.assign(B + 1, 0);
-  h->lm_blk.assign(B + 1, 0);
   for (int s = 0; s < B; ++s) {
     StreamFrame& F = h->hf[s];
     HostStream& H = h->hs[s];
@@ -840,7 +886,6 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     F.corner_num[0] = F.corner_num[1] = F.surf_num[0] = F.surf_num[1] = 0;
     F.sub_n[0] = F.sub_n[1] = 0;
     F.optimize = 0;
-    int nrec = 0;
     if (F.active) {
       any = true;
       for (int i = 0; i < 7; ++i) F.pose[i] = H.pose[i];
@@ -864,10 +909,7 @@ int32_t loam_mapper_solve(loam_mapper* h) {
       F.origin[0] = (c3[0] - 2 - F.cen[0]) * 50 - 25 - 2;
       F.origin[1] = (c3[1] - 2 - F.cen[1]) * 50 - 25 - 2;
       F.origin[2] = (c3[2] - 1 - F.cen[2]) * 50 - 25 - 2;
-      nrec = F.nc_in + F.ns_in;
     }
-    h->corr_blk[s + 1] = h->corr_blk[s] + (F.active ? std::max(1, (nrec + CORR_THREADS - 1) / CORR_THREADS) : 0);
-    h->lm_blk[s + 1] = h->lm_blk[s] + std::max(1, (nrec + LM_CHUNK - 1) / LM_CHUNK) * (F.active ? 1 : 0);
   }
   if (!any) return LOAM_OK;
   h->frame_counter++;
@@ -881,8 +923,6 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   D.cube_tab = h->cube_tab[h->parity];
   hipStream_t st = h->st;
   LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(StreamFrame) * B, hipMemcpyHostToDevice, st));
-  LOAM_HIP(hipMemcpyAsync(h->d_corr_blk, h->corr_blk.data(), sizeof(int) * (B + 1), hipMemcpyHostToDevice, st));
-  LOAM_HIP(hipMemcpyAsync(h->d_lm_blk, h->lm_blk.data(), sizeof(int) * (B + 1), hipMemcpyHostToDevice, st));
   LOAM_HIP(hipEventRecord(h->ev[0], st));
   if (any_shift) {
     LAUNCH(FAM_OTHER, k_shift_cubes<<<dim3(16, B), 256, 0, st>>>(D, h->cube_tab[h->parity], h->cube_tab[1 - h->parity]));
@@ -890,16 +930,18 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     D.cube_tab = h->cube_tab[h->parity];
   }
   LAUNCH(FAM_STACK, k_stack_ds<<<B * 2, VX_THREADS, 0, st>>>(D));
-  LAUNCH(FAM_OTHER, k_submap_prep<<<(B + 63) / 64, 64, 0, st>>>(D));
+  LAUNCH(FAM_OTHER, k_submap_prep<<<B, 128, 0, st>>>(D));
   LOAM_HIP(hipEventRecord(h->ev[1], st));
   LAUNCH(FAM_HASH, k_submap_insert<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D));
   LAUNCH(FAM_HASH, k_submap_alloc<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D));
   LAUNCH(FAM_HASH, k_submap_scatter<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D));
-  const int ncorr = h->corr_blk[B], nlm = h->lm_blk[B];
   for (int round = 0; round < 2; ++round) {
-    if (ncorr > 0) LAUNCH(FAM_CORR, k_correspond<<<ncorr, CORR_THREADS, 0, st>>>(D, round));
-    for (int it = 0; it < 5; ++it) LAUNCH(FAM_LM, k_lm_pass<<<nlm, LM_THREADS, 0, st>>>(D, round));
-    LAUNCH(FAM_OTHER, k_lm_finish<<<(B + 63) / 64, 64, 0, st>>>(D, round));
+    LAUNCH(FAM_CORR, k_knn<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round));
+    LAUNCH(FAM_CORR, k_geom<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round));
+    for (int it = 0; it < 5; ++it) {  // iteration 0 + max_num_iterations = 4 candidates
+      LAUNCH(FAM_LM, k_lm_eval<<<B * LM_EBLK, LM_THREADS, 0, st>>>(D, round));
+      LAUNCH(FAM_LM, k_lm_step<<<B, 64, 0, st>>>(D, round));
+    }
   }
   LOAM_HIP(hipEventRecord(h->ev[2], st));
   LAUNCH(FAM_INSERT, k_insert<<<dim3(16, B), 256, 0, st>>>(D));

@@ -22,11 +22,14 @@ struct LmRecDev {
   double *a0, *a1, *a2, *b0, *b1, *b2;
 };
 
-__global__ void __launch_bounds__(P_LM_THREADS)
-    k_lm_pass_single(LmRecDev R, int nrec, LmState* S, double* partials, uint32_t* ticket) {
-  lm_pass_body<P_LM_THREADS, P_LM_PER_THREAD>(R.type, R.px, R.py, R.pz, R.a0, R.a1, R.a2, R.b0,
-                                              R.b1, R.b2, nrec, blockIdx.x, gridDim.x, *S,
-                                              partials, ticket);
+__global__ void __launch_bounds__(P_LM_THREADS) k_lm_eval_single(LmRecDev R, int nrec, const LmState* S,
+                                                                 double* partials) {
+  const LmRecView V{R.type, R.px, R.py, R.pz, R.a0, R.a1, R.a2, R.b0, R.b1, R.b2};
+  lm_eval_block<P_LM_THREADS>(V, nrec, *S, blockIdx.x, gridDim.x, partials + (size_t)blockIdx.x * LM_NACC);
+}
+
+__global__ void __launch_bounds__(64) k_lm_step_single(const double* partials, int nblk, LmState* S) {
+  lm_step_wave(partials, nblk, *S);
 }
 
 // one evaluation at x: partial sums per workgroup (no state machine)
@@ -80,10 +83,14 @@ __global__ void k_hash_insert(const float4* pts, int n, const int* origin, unsig
   }
 }
 
-__global__ void k_hash_alloc(int n, const unsigned long long* hc, uint32_t* hs, const uint32_t* ps,
+__global__ void k_hash_alloc(int n, const unsigned long long* hk, const unsigned long long* hc,
+                             uint32_t epoch, uint32_t* hs, uint4* qt, const uint32_t* ps,
                              const uint32_t* pr, uint32_t* cursor) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    if (pr[i] == 0) hs[ps[i]] = atomicAdd(cursor, (uint32_t)(hc[ps[i]] & 0xFFFFFFFFu));
+  for (int b0 = blockIdx.x * blockDim.x; b0 < n; b0 += gridDim.x * blockDim.x) {  // whole waves
+    const int i = b0 + threadIdx.x;
+    const bool first = i < n && pr[i] == 0;
+    hash_alloc_cell(first, first ? ps[i] : 0u, hk, hc, epoch, hs, qt, cursor);
+  }
 }
 
 __global__ void k_hash_scatter(const float4* pts, int n, const uint32_t* hs, const uint32_t* ps,
@@ -96,12 +103,11 @@ __global__ void k_hash_scatter(const float4* pts, int n, const uint32_t* hs, con
 }
 
 __global__ void k_knn_query(const float4* q, int nq, int k, float radius2, const int* origin,
-                            const unsigned long long* hk, const unsigned long long* hc,
-                            const uint32_t* hs, const float4* sp, uint32_t mask, uint32_t epoch,
+                            const uint4* qt, const float4* sp, uint32_t mask, uint32_t epoch,
                             int* idx, float* d2) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += gridDim.x * blockDim.x) {
     Top5 T;
-    knn5_hash(q[i], origin, hk, hc, hs, sp, mask, epoch, radius2, T);
+    knn5_hash(q[i], origin, qt, sp, mask, epoch, radius2, T);
     for (int j = 0; j < k; ++j) {
       const bool ok = T.d[j] < radius2;
       idx[(size_t)i * k + j] = ok ? T.id[j] : -1;
@@ -205,17 +211,17 @@ int32_t loam_lm_solve(int32_t device, const double* factors, int32_t n, double* 
   LmHostRecs R;
   rc = upload_factors(factors, n, R);
   if (rc != LOAM_OK) return rc;
-  const int nchunks = std::max(1, (n + P_LM_CHUNK - 1) / P_LM_CHUNK);
+  const int nblk = 32;
   LmState hS;
   lm_init(hS, x, max_it, true);
-  DevBuf dS, dpart, dtick;
+  DevBuf dS, dpart;
   LOAM_HIP(dmalloc<LmState>(dS, 1));
-  LOAM_HIP(dmalloc<double>(dpart, (size_t)nchunks * LM_NACC));
-  LOAM_HIP(dmalloc<uint32_t>(dtick, 1));
+  LOAM_HIP(dmalloc<double>(dpart, (size_t)nblk * LM_NACC));
   LOAM_HIP(hipMemcpy(dS.p, &hS, sizeof(LmState), hipMemcpyHostToDevice));
-  for (int it = 0; it <= max_it; ++it)
-    k_lm_pass_single<<<nchunks, P_LM_THREADS>>>(R.view(), n, (LmState*)dS.p, (double*)dpart.p,
-                                                 (uint32_t*)dtick.p);
+  for (int it = 0; it <= max_it; ++it) {
+    k_lm_eval_single<<<nblk, P_LM_THREADS>>>(R.view(), n, (const LmState*)dS.p, (double*)dpart.p);
+    k_lm_step_single<<<1, 64>>>((const double*)dpart.p, nblk, (LmState*)dS.p);
+  }
   LOAM_HIP(hipGetLastError());
   LOAM_HIP(hipMemcpy(&hS, dS.p, sizeof(LmState), hipMemcpyDeviceToHost));
   if (hS.status != LM_DONE) {
@@ -334,13 +340,14 @@ int32_t loam_knn_radius(int32_t device, const float* pts, int32_t n, const float
   }
   uint32_t T = 1;
   while (T < (uint32_t)std::max(2 * n, 64)) T <<= 1;
-  DevBuf dp, dq, dorig, dhk, dhc, dhs, dps, dpr, dsp, dcur, derr, didx, dd2;
+  DevBuf dp, dq, dorig, dhk, dhc, dhs, dqt, dps, dpr, dsp, dcur, derr, didx, dd2;
   LOAM_HIP(dmalloc<float4>(dp, n));
   LOAM_HIP(dmalloc<float4>(dq, nq));
   LOAM_HIP(dmalloc<int>(dorig, 3));
   LOAM_HIP(dmalloc<unsigned long long>(dhk, T));
   LOAM_HIP(dmalloc<unsigned long long>(dhc, T));
   LOAM_HIP(dmalloc<uint32_t>(dhs, T));
+  LOAM_HIP(dmalloc<uint4>(dqt, T));
   LOAM_HIP(dmalloc<uint32_t>(dps, n));
   LOAM_HIP(dmalloc<uint32_t>(dpr, n));
   LOAM_HIP(dmalloc<float4>(dsp, n));
@@ -356,13 +363,13 @@ int32_t loam_knn_radius(int32_t device, const float* pts, int32_t n, const float
   k_hash_insert<<<blocks, 256>>>((const float4*)dp.p, n, (const int*)dorig.p, (unsigned long long*)dhk.p,
                                  (unsigned long long*)dhc.p, T - 1, epoch, (uint32_t*)dps.p,
                                  (uint32_t*)dpr.p, (int*)derr.p);
-  k_hash_alloc<<<blocks, 256>>>(n, (const unsigned long long*)dhc.p, (uint32_t*)dhs.p,
-                                (const uint32_t*)dps.p, (const uint32_t*)dpr.p, (uint32_t*)dcur.p);
+  k_hash_alloc<<<blocks, 256>>>(n, (const unsigned long long*)dhk.p, (const unsigned long long*)dhc.p, epoch,
+                                (uint32_t*)dhs.p, (uint4*)dqt.p, (const uint32_t*)dps.p,
+                                (const uint32_t*)dpr.p, (uint32_t*)dcur.p);
   k_hash_scatter<<<blocks, 256>>>((const float4*)dp.p, n, (const uint32_t*)dhs.p, (const uint32_t*)dps.p,
                                   (const uint32_t*)dpr.p, (float4*)dsp.p);
   k_knn_query<<<blocks, 256>>>((const float4*)dq.p, nq, k, radius2, (const int*)dorig.p,
-                               (const unsigned long long*)dhk.p, (const unsigned long long*)dhc.p,
-                               (const uint32_t*)dhs.p, (const float4*)dsp.p, T - 1, epoch, (int*)didx.p,
+                               (const uint4*)dqt.p, (const float4*)dsp.p, T - 1, epoch, (int*)didx.p,
                                (float*)dd2.p);
   LOAM_HIP(hipGetLastError());
   if (nq) {

@@ -14,7 +14,8 @@
 //   2. bbox reduction
 //   3. LDS open-addressing hash of the voxel idx -> per-voxel counts (ds atomics)
 //   4. compact the U unique voxels, bitonic-sort them in LDS by idx
-//   5. exclusive scan of counts -> output slots; member lists scattered to global scratch
+//   5. exclusive scan of counts -> output slots; member lists (u16 in LDS when they fit,
+//      else int in global scratch)
 //   6. per voxel: members sorted by input index (insertion sort, lists are short and nearly
 //      ordered), float sums in that order, centroid -> output
 // Capacity: U <= VX_UCAP unique voxels per segment (else *err |= VX_ERR_CAPACITY).
@@ -116,13 +117,65 @@ constexpr int VX_HIST_WORD = 3 * VX_UCAP;      // LDS words [36864, 38912): buck
 constexpr int VX_GEND_WORD = VX_HIST_WORD + VX_NB;  // [38912, 40704): group ends
 constexpr int VX_MAX_GROUPS = VX_LDS_WORDS - 256 - VX_GEND_WORD;
 
+// Member lists (chunk by chunk: members of earlier chunks precede later ones), then per
+// voxel: members sorted by input index, float sums in that order, centroid -> out[j].
+template <typename MT>
+__device__ inline void vx_centroids(const VxGeom& g, const VxSrc& P, uint32_t N, MT* members,
+                                    uint32_t klo, uint32_t khi, uint32_t U, const uint32_t* ukey,
+                                    const uint32_t* uoff, uint32_t* ufill, float4* out) {
+  const int tid = threadIdx.x;
+  for (uint32_t c = 0; c < N; c += VX_THREADS) {
+    uint32_t i = c + tid;
+    if (i < N) {
+      uint32_t k = vx_key(g, P(i));
+      if (k >= klo && k < khi) {
+        uint32_t lo = 0, hi = U;  // lower_bound
+        while (lo < hi) {
+          uint32_t mid = (lo + hi) >> 1;
+          if (ukey[mid] < k) lo = mid + 1; else hi = mid;
+        }
+        uint32_t pos = uoff[lo] + atomicAdd(&ufill[lo], 1u);
+        members[pos] = (MT)i;
+      }
+    }
+    __syncthreads();
+  }
+  for (uint32_t j = tid; j < U; j += VX_THREADS) {
+    const uint32_t b = uoff[j];
+    const uint32_t n = ufill[j];
+    for (uint32_t a = 1; a < n; ++a) {  // insertion sort (lists are short and nearly ordered)
+      const MT v = members[b + a];
+      uint32_t q = a;
+      while (q > 0 && members[b + q - 1] > v) {
+        members[b + q] = members[b + q - 1];
+        --q;
+      }
+      members[b + q] = v;
+    }
+    float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
+    for (uint32_t a = 0; a < n; a += 4) {  // gathers issued together, summed in order
+      float4 p[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (a + u < n) p[u] = P((uint32_t)members[b + a + u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (a + u < n) {
+          sx += p[u].x; sy += p[u].y; sz += p[u].z; si += p[u].w;
+        }
+    }
+    const float fn = (float)n;
+    out[j] = make_float4(sx / fn, sy / fn, sz / fn, si / fn);
+  }
+}
+
 // Steps 3-6 for the points whose voxel idx lies in [klo, khi): LDS hash -> sorted unique
 // voxels -> member lists -> centroids written at out[base + j].  out_base == VX_ALLOC:
 // allocate exactly U (at *tail or at 0) once U is known.  Returns U, or VX_OVERFLOW (no side
 // effects on the output) when the unique voxels do not fit the LDS.
 __device__ inline uint32_t vx_group(const VoxSeg& S, const VxGeom& g, const VxSrc& P, uint32_t N,
                                     int* members, uint32_t klo, uint32_t khi, uint32_t out_base,
-                                    uint32_t* lds, uint32_t* ws, VxMisc& M) {
+                                    uint32_t lds_limit, uint32_t* lds, uint32_t* ws, VxMisc& M) {
   const int tid = threadIdx.x;
   uint32_t* hkey = lds;
   uint32_t* hcnt = lds + VX_HASH;
@@ -205,9 +258,9 @@ __device__ inline uint32_t vx_group(const VoxSeg& S, const VxGeom& g, const VxSr
   }
   uint32_t tot;
   uint32_t cpre = vx_block_scan(csum, ws, &tot);  // its barriers order the s64 reads
-  uint32_t* ukey = lds;
-  uint32_t* uoff = lds + VX_UCAP;
-  uint32_t* ufill = lds + 2 * VX_UCAP;
+  uint32_t* ukey = lds;  // packed: ukey[U] | uoff[U] | ufill[U] | LDS member lists
+  uint32_t* uoff = lds + U;
+  uint32_t* ufill = lds + 2 * U;
 #pragma unroll
   for (int e = 0; e < EPT; ++e) {
     uint32_t j = tid * EPT + e;
@@ -219,23 +272,6 @@ __device__ inline uint32_t vx_group(const VoxSeg& S, const VxGeom& g, const VxSr
     cpre += cc[e];
   }
   __syncthreads();
-  // member lists, chunk by chunk (members of earlier chunks precede later ones)
-  for (uint32_t c = 0; c < N; c += VX_THREADS) {
-    uint32_t i = c + tid;
-    if (i < N) {
-      uint32_t k = vx_key(g, P(i));
-      if (k >= klo && k < khi) {
-        uint32_t lo = 0, hi = U;  // lower_bound
-        while (lo < hi) {
-          uint32_t mid = (lo + hi) >> 1;
-          if (ukey[mid] < k) lo = mid + 1; else hi = mid;
-        }
-        uint32_t pos = uoff[lo] + atomicAdd(&ufill[lo], 1u);
-        members[pos] = (int)i;
-      }
-    }
-    __syncthreads();
-  }
   uint32_t ob = out_base;
   if (out_base == VX_ALLOC) {
     if (tid == 0) {
@@ -250,27 +286,12 @@ __device__ inline uint32_t vx_group(const VoxSeg& S, const VxGeom& g, const VxSr
     ob = M.sbase[1];
     if (ob == 0xFFFFFFFFu) return 0;
   }
-  // centroids in input order
-  for (uint32_t j = tid; j < U; j += VX_THREADS) {
-    uint32_t b = uoff[j];
-    uint32_t n = ufill[j];
-    for (uint32_t a = 1; a < n; ++a) {  // insertion sort of the member list by input index
-      int v = members[b + a];
-      uint32_t q = a;
-      while (q > 0 && members[b + q - 1] > v) {
-        members[b + q] = members[b + q - 1];
-        --q;
-      }
-      members[b + q] = v;
-    }
-    float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
-    for (uint32_t a = 0; a < n; ++a) {
-      float4 p = P((uint32_t)members[b + a]);
-      sx += p.x; sy += p.y; sz += p.z; si += p.w;
-    }
-    const float fn = (float)n;
-    S.out[ob + j] = make_float4(sx / fn, sy / fn, sz / fn, si / fn);
-  }
+  // member lists in LDS as u16 point indices when they fit, else in global scratch
+  if (N <= 65536u && 3 * U + (tot + 1) / 2 <= lds_limit)
+    vx_centroids(g, P, N, reinterpret_cast<uint16_t*>(lds + 3 * U), klo, khi, U, ukey, uoff, ufill,
+                 S.out + ob);
+  else
+    vx_centroids(g, P, N, members, klo, khi, U, ukey, uoff, ufill, S.out + ob);
   if (out_base == VX_ALLOC && tid == 0) {
     if (S.res_off) *S.res_off = ob;
     if (S.res_cnt) *S.res_cnt = U;
@@ -331,7 +352,7 @@ __device__ inline void vx_grouped(const VoxSeg& S, const VxGeom& g, const VxSrc&
   for (int gi = 0; gi < ng; ++gi) {
     const int ge = (int)gend[gi];
     const uint32_t U = vx_group(S, g, P, N, members, blo(gstart), ge >= VX_NB ? 0xFFFFFFFFu : blo(ge),
-                                ob + acc, lds, ws, M);
+                                ob + acc, VX_HIST_WORD, lds, ws, M);
     if (U == VX_OVERFLOW) {
       if (tid == 0) atomicOr(S.err, VX_ERR_CAPACITY);
       return;
@@ -495,7 +516,8 @@ __device__ inline void voxel_segment(const VoxSeg& S, uint32_t* lds) {
 
   // ---- 3-6 in one LDS pass when the unique voxels fit, else in idx-range groups
   const VxSrc src{S.src0, n0, sec};
-  uint32_t U = vx_group(S, g, src, N, members, 0u, 0xFFFFFFFFu, VX_ALLOC, lds, ws, M);
+  uint32_t U = vx_group(S, g, src, N, members, 0u, 0xFFFFFFFFu, VX_ALLOC, VX_LDS_WORDS - 256, lds, ws,
+                        M);
   if (U != VX_OVERFLOW) return;
   vx_grouped(S, g, src, N, members, lds, ws, M);
 }

@@ -56,6 +56,23 @@ class BatchMapper:
         check(lib().loam_mapper_input_device(self.h, stream, corner_ptr, n_corner, surf_ptr,
                                              n_surf, ptr(q), ptr(t), int(skip_frame)))
 
+    def input_device_batch(self, streams, corner_ptrs, n_corner, surf_ptrs, n_surf, q_wodom, t_wodom):
+        """n streams at once: arrays of stream ids, device pointers (uint64) and sizes"""
+        st = np.ascontiguousarray(streams, dtype=np.int32)
+        cp = np.ascontiguousarray(corner_ptrs, dtype=np.uint64)
+        cn = np.ascontiguousarray(n_corner, dtype=np.int32)
+        sp = np.ascontiguousarray(surf_ptrs, dtype=np.uint64)
+        sn = np.ascontiguousarray(n_surf, dtype=np.int32)
+        q = np.ascontiguousarray(q_wodom, dtype=np.float64).reshape(-1, 4)
+        t = np.ascontiguousarray(t_wodom, dtype=np.float64).reshape(-1, 3)
+        check(lib().loam_mapper_input_device_batch(self.h, len(st), ptr(st), ptr(cp), ptr(cn), ptr(sp),
+                                                   ptr(sn), ptr(q), ptr(t)))
+
+    def stats_all(self):
+        out = (_core.MapStats * self.n_streams)()
+        check(lib().loam_mapper_stats_all(self.h, out, self.n_streams))
+        return list(out)
+
     def solve(self):
         check(lib().loam_mapper_solve(self.h))
 

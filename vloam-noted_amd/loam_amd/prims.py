@@ -1,0 +1,55 @@
+"""Standalone HIP primitives behind the mapping stage (C-ABI, include/loam_core.h).
+
+Same argument meaning as the pieces of the reference they replace:
+  voxel_grid   pcl::VoxelGrid<PointXYZI>::filter (laser_mapping.cpp:492-500, :795-808)
+  knn_radius   pcl::KdTreeFLANN::nearestKSearch restricted to d2 < radius2 (:554, :633)
+  lm_solve     ceres::Solve with the reference's options (:709-717) on factor records
+  lm_normal_equations  cost, J^T J, J^T r at x (Huber-corrected, local 6-dof)
+Every call runs on the GPU; there is no CPU fallback.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _core
+from ._core import check, f32x4, lib, ptr
+
+
+def voxel_grid(pts, leaf, device=0):
+    pts = f32x4(pts)
+    out = np.empty_like(pts)
+    n = _core.c_i32()
+    check(lib().loam_voxel_grid(device, ptr(pts), len(pts), float(leaf), ptr(out), ctypes.byref(n)))
+    return out[: n.value].copy()
+
+
+def knn_radius(pts, queries, k=5, radius2=1.0, device=0):
+    pts, q = f32x4(pts), f32x4(queries)
+    idx = np.empty((len(q), k), dtype=np.int32)
+    d2 = np.empty((len(q), k), dtype=np.float32)
+    check(lib().loam_knn_radius(device, ptr(pts), len(pts), ptr(q), len(q), k, float(radius2),
+                                ptr(idx), ptr(d2)))
+    return idx, d2
+
+
+def _factors(f):
+    f = np.ascontiguousarray(f, dtype=np.float64)
+    return f.reshape(-1, 10)
+
+
+def lm_solve(factors, x, max_iterations=4, device=0):
+    f = _factors(factors)
+    x = np.array(x, dtype=np.float64).copy()
+    st = _core.LMStats()
+    check(lib().loam_lm_solve(device, ptr(f), len(f), ptr(x), max_iterations, ctypes.byref(st)))
+    return x, st
+
+
+def lm_normal_equations(factors, x, device=0):
+    f = _factors(factors)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    cost = np.empty(1)
+    jtj = np.empty(36)
+    jtr = np.empty(6)
+    check(lib().loam_lm_normal_equations(device, ptr(f), len(f), ptr(x), ptr(cost), ptr(jtj), ptr(jtr)))
+    return float(cost[0]), jtj.reshape(6, 6), jtr
