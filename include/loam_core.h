@@ -45,7 +45,7 @@ typedef struct loam_params {
   int32_t verbose_level;            /* loam_verbose_level */
   /* device capacities (per stream) */
   int32_t max_input_points;         /* max points per input cloud (default 262144) */
-  int32_t max_map_points;           /* arena capacity per map (corner/surf) (default 4194304) */
+  int32_t max_map_points;           /* arena capacity per map (corner/surf) (default 2097152) */
   int32_t max_submap_points;        /* 5x5x3-cube submap capacity per map (default 524288) */
 } loam_params;
 
@@ -189,7 +189,13 @@ int32_t loam_lm_normal_equations(int32_t device, const double* factors, int32_t 
 /* pcl::VoxelGrid<PointXYZI> (leaf metres) on one cloud; returns count in *n_out */
 int32_t loam_voxel_grid(int32_t device, const float* in, int32_t n, float leaf, float* out,
                         int32_t* n_out);
-/* exact kNN (k <= 8) of queries against pts restricted to d2 < radius2 (1 m cells):
+/* VoxelGrid of fixed ++ added where `fixed` is already a VoxelGrid output of the same leaf
+ * whose centroids stayed in their voxels (the per-cube map update, laser_mapping.cpp:795-808):
+ * same result as loam_voxel_grid on the concatenation.  *merged = 1 if the merge path ran
+ * (n1 <= 4096), 0 if the full filter did.  out holds n0 + n1 points. */
+int32_t loam_voxel_merge(int32_t device, const float* fixed, int32_t n0, const float* added, int32_t n1,
+                         float leaf, float* out, int32_t* n_out, int32_t* merged);
+/* exact kNN (k <= 5) of queries against pts restricted to d2 < radius2 (1 m cells):
  * idx/d2 sorted ascending; missing entries idx = -1 */
 int32_t loam_knn_radius(int32_t device, const float* pts, int32_t n, const float* queries,
                         int32_t nq, int32_t k, float radius2, int32_t* idx, float* d2);

@@ -1,0 +1,142 @@
+// loam_core.hpp — header-only C++ shim over the C-ABI (loam_core.h) with the reference's
+// class and method names, for the lidar_odometry_mapping nodes:
+//   vloam::ScanRegistration  scan_registration.h:64-81   -> loam_amd::ScanRegistration
+//   vloam::LaserMapping      laser_mapping.h:85-100      -> loam_amd::LaserMapping
+// Clouds cross the boundary as packed float4 (x, y, z, intensity) arrays. pcl::PointXYZI
+// is 32 bytes, so the node packs and unpacks it (INTEGRATION.md shows the adapter). Errors
+// throw loam_amd::Error carrying the LOAM_ERR_* code and loam_last_error(). There is no
+// CPU fallback.
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "loam_core.h"
+
+namespace loam_amd {
+
+class Error : public std::runtime_error {
+ public:
+  Error(int32_t rc, const std::string& msg) : std::runtime_error(msg), rc_(rc) {}
+  int32_t code() const { return rc_; }
+
+ private:
+  int32_t rc_;
+};
+
+inline int32_t check(int32_t rc) {
+  if (rc < 0) throw Error(rc, std::string("loam: ") + loam_last_error());
+  return rc;
+}
+
+inline loam_params default_params() {
+  loam_params p;
+  loam_params_default(&p);
+  return p;
+}
+
+using Cloud = std::vector<float>;  // 4 floats per point
+
+// ScanRegistration::input / output (scan_registration.cpp:144-577)
+class ScanRegistration {
+ public:
+  explicit ScanRegistration(const loam_params& p = default_params(), int32_t device = 0) {
+    check(loam_scanreg_create(&p, device, &h_));
+  }
+  ~ScanRegistration() { loam_scanreg_destroy(h_); }
+  ScanRegistration(const ScanRegistration&) = delete;
+  ScanRegistration& operator=(const ScanRegistration&) = delete;
+
+  void init() {}
+  void reset() {}
+  // laserCloudIn: n points, `stride` floats apart (pcl::PointXYZ: stride 4)
+  void input(const float* xyz, int32_t n, int32_t stride = 4) { check(loam_scanreg_input(h_, xyz, n, stride)); }
+  // laserCloud, cornerPointsSharp, cornerPointsLessSharp, surfPointsFlat, surfPointsLessFlat
+  void output(Cloud& full, Cloud& sharp, Cloud& less_sharp, Cloud& flat, Cloud& less_flat) const {
+    Cloud* out[5] = {&full, &sharp, &less_sharp, &flat, &less_flat};
+    int32_t n[5];
+    check(loam_scanreg_counts(h_, n));
+    for (int k = 0; k < 5; ++k) {
+      out[k]->resize(static_cast<size_t>(n[k]) * 4);
+      if (n[k]) check(loam_scanreg_copy(h_, k, out[k]->data(), n[k]));
+    }
+  }
+  // device pointer + count of one output cloud (stays valid until the next input)
+  std::pair<const float*, int32_t> device_cloud(int32_t which) const {
+    const float* p = nullptr;
+    const int32_t n = check(loam_scanreg_device_ptr(h_, which, &p));
+    return {p, n};
+  }
+  double ms() const { return loam_scanreg_ms(h_); }
+  loam_scanreg* handle() const { return h_; }
+
+ private:
+  loam_scanreg* h_ = nullptr;
+};
+
+// B independent LaserMapping instances in one handle (one launch sequence per solve)
+class BatchMapper {
+ public:
+  BatchMapper(int32_t n_streams, const loam_params& p = default_params(), int32_t device = 0) : n_(n_streams) {
+    check(loam_mapper_create(&p, device, n_streams, &h_));
+  }
+  ~BatchMapper() { loam_mapper_destroy(h_); }
+  BatchMapper(const BatchMapper&) = delete;
+  BatchMapper& operator=(const BatchMapper&) = delete;
+
+  void reset() { check(loam_mapper_reset(h_)); }
+  void input(int32_t stream, const Cloud& corner, const Cloud& surf, const double q_wodom[4],
+             const double t_wodom[3], bool skip_frame = false) {
+    check(loam_mapper_input(h_, stream, corner.data(), static_cast<int32_t>(corner.size() / 4), surf.data(),
+                            static_cast<int32_t>(surf.size() / 4), q_wodom, t_wodom, skip_frame ? 1 : 0));
+  }
+  void input_device(int32_t stream, const float* corner, int32_t nc, const float* surf, int32_t ns,
+                    const double q_wodom[4], const double t_wodom[3], bool skip_frame = false) {
+    check(loam_mapper_input_device(h_, stream, corner, nc, surf, ns, q_wodom, t_wodom, skip_frame ? 1 : 0));
+  }
+  void solve() { check(loam_mapper_solve(h_)); }
+  void pose(int32_t stream, double q_w[4], double t_w[3]) const { check(loam_mapper_pose(h_, stream, q_w, t_w)); }
+  loam_map_stats stats(int32_t stream) const {
+    loam_map_stats st;
+    check(loam_mapper_stats(h_, stream, &st));
+    return st;
+  }
+  Cloud cube(int32_t stream, int32_t which, int32_t cube) const {
+    const int32_t n = check(loam_mapper_cube_count(h_, stream, which, cube));
+    Cloud out(static_cast<size_t>(n) * 4);
+    if (n) check(loam_mapper_cube_copy(h_, stream, which, cube, out.data()));
+    return out;
+  }
+  int32_t streams() const { return n_; }
+  loam_mapper* handle() const { return h_; }
+
+ private:
+  loam_mapper* h_ = nullptr;
+  int32_t n_ = 0;
+};
+
+// LaserMapping::init / reset / input / solveMapping / output (laser_mapping.cpp:147-814)
+class LaserMapping {
+ public:
+  explicit LaserMapping(const loam_params& p = default_params(), int32_t device = 0) : m_(1, p, device) {}
+  void init() { m_.reset(); }
+  void reset() {}  // laser_mapping.cpp:132-136 clears per-frame buffers only
+  // laserCloudCornerLast, laserCloudSurfLast, q_wodom_curr, t_wodom_curr, skip_frame
+  void input(const Cloud& corner_last, const Cloud& surf_last, const double q_wodom_curr[4],
+             const double t_wodom_curr[3], bool skip_frame) {
+    m_.input(0, corner_last, surf_last, q_wodom_curr, t_wodom_curr, skip_frame);
+  }
+  void solveMapping() { m_.solve(); }
+  // q_w_curr / t_w_curr: what publish() sends on /aft_mapped_to_init (laser_mapping.cpp:816-874)
+  void output(double q_w_curr[4], double t_w_curr[3]) const { m_.pose(0, q_w_curr, t_w_curr); }
+  loam_map_stats stats() const { return m_.stats(0); }
+  BatchMapper& batch() { return m_; }
+
+ private:
+  BatchMapper m_;
+};
+
+}  // namespace loam_amd

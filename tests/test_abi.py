@@ -72,3 +72,17 @@ def test_no_device_fails_loudly():
     from loam_amd import prims
     with pytest.raises(_core.LoamError):
         prims.voxel_grid([[0, 0, 0, 0]], 0.4)
+
+
+def test_cxx_shim_compiles_and_links(tmp_path):
+    """include/loam_core.hpp with plain g++ (the reference nodes' compiler), linked to the library"""
+    import subprocess
+    lib_dir = os.path.dirname(_core.LIB_PATH)
+    exe = str(tmp_path / "shim_check")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cxx", "shim_check.cpp"), "-o", exe, "-L", lib_dir,
+                    "-lloam_core", f"-Wl,-rpath,{lib_dir}", "-Wl,-rpath,/opt/rocm/lib"],
+                   check=True, capture_output=True, text=True)
+    r = subprocess.run([exe, "1" if gpu_available() else "0"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "version" in r.stdout

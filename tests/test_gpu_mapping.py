@@ -95,3 +95,19 @@ def test_skip_frame_pose(seq):
     m.solve()
     q, t = m.pose(0)
     assert np.allclose(q, rec["q_wodom"]) and np.allclose(t, rec["t_wodom"])
+
+
+@pytest.mark.parametrize("persistent", ["1", "0"])
+def test_lm_paths_many_streams(seq, monkeypatch, persistent):
+    """both LM implementations (one persistent launch per round / eval + step kernels per pass)
+    on 24 streams: each stream is one of the snapshot frames"""
+    monkeypatch.setenv("LOAM_LM_PERSISTENT", persistent)
+    m = BatchMapper(24)
+    for s in range(24):
+        fi = SNAP[s % len(SNAP)]
+        load_state(m, s, seq[fi]["before"])
+        m.input(s, seq[fi]["corner"], seq[fi]["surf"], seq[fi]["q_wodom"], seq[fi]["t_wodom"])
+    m.solve()
+    for s in range(24):
+        _check_frame(m, s, seq[SNAP[s % len(SNAP)]])
+    m.close()

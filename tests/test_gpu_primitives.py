@@ -142,3 +142,26 @@ def test_voxel_grid_many_unique_voxels():
     got = gpu_voxel(pts, 0.5)
     assert len(ref) > 12288
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("leaf,n_new", [(0.4, 300), (0.8, 1500), (0.4, 4096), (0.4, 5000)])
+def test_voxel_merge_bit_exact(frame_clouds, leaf, n_new):
+    """map update path: VoxelGrid(fixed ++ added) with `fixed` a VoxelGrid fixed point; the merge
+    kernel (n_new <= 4096) must equal the full filter bit for bit"""
+    from loam_amd import prims
+    fixed = O.voxel_grid(frame_clouds[4], leaf)
+    if not np.array_equal(O.voxel_grid(fixed, leaf), fixed):
+        pytest.skip("content is not a fixed point")
+    rng = np.random.default_rng(n_new)
+    # half the new points land in occupied voxels (jittered copies), half anywhere nearby
+    pick = fixed[rng.integers(0, len(fixed), n_new // 2)].copy()
+    pick[:, :3] += rng.uniform(-0.05, 0.05, (len(pick), 3)).astype(np.float32)
+    lo, hi = fixed[:, :3].min(0), fixed[:, :3].max(0)
+    far = np.concatenate([rng.uniform(lo, hi, (n_new - len(pick), 3)),
+                          rng.uniform(0, 64, (n_new - len(pick), 1))], 1).astype(np.float32)
+    added = np.concatenate([pick, far]).astype(np.float32)
+    got, merged = prims.voxel_merge(fixed, added, leaf)
+    ref = O.voxel_grid(np.concatenate([fixed, added]), leaf)
+    assert merged == (n_new <= 4096)
+    assert got.shape == ref.shape
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))

@@ -148,8 +148,10 @@ __device__ inline void lm_accum(int type, float px, float py, float pz, double a
 __host__ __device__ inline void lm_plus(const double* x, const double* d, double* out) {
   double nd = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
   if (nd > 0.0) {
-    double s = sin(nd) / nd;
-    dq dqq{s * d[0], s * d[1], s * d[2], cos(nd)};
+    double sn, cs;
+    sincos(nd, &sn, &cs);
+    double s = sn / nd;
+    dq dqq{s * d[0], s * d[1], s * d[2], cs};
     dq r = qmul(dqq, dq{x[0], x[1], x[2], x[3]});
     out[0] = r.x;
     out[1] = r.y;
@@ -166,7 +168,14 @@ __host__ __device__ inline void lm_plus(const double* x, const double* d, double
   out[6] = x[6] + d[5];
 }
 
+// max_i |x_i - Plus(x, -g)_i| (Ceres' gradient max norm).  Its only use is the test
+// gmax <= gradient_tolerance (1e-10): the translation terms are computed exactly as in the
+// full expression, so when one of them already exceeds the tolerance the rotation terms
+// (two transcendentals) cannot change the outcome and are skipped.
 __host__ __device__ inline double lm_gradmax(const double* x, const double* g) {
+  double mt = 0.0;
+  for (int c = 0; c < 3; ++c) mt = fmax(mt, fabs(x[4 + c] - (x[4 + c] + -g[3 + c])));
+  if (mt > 1e-10) return mt;
   double ng[6], pg[7];
   for (int c = 0; c < 6; ++c) ng[c] = -g[c];
   lm_plus(x, ng, pg);
@@ -348,24 +357,36 @@ struct LmRecView {
   const double *a0, *a1, *a2, *b0, *b1, *b2;
 };
 
+// residual sums of records r = blk*kThreads + tid + k*nblk*kThreads at X; the block total
+// is left in sum[LM_NACC] (LDS) for tid < LM_NACC after the trailing barrier.  Two records per
+// thread are loaded before either is evaluated, so their loads are in flight together.
 template <int kThreads>
-__device__ inline void lm_eval_block(const LmRecView& R, int nrec, const LmState& S, int blk,
-                                     int nblk, double* partial_out) {
+__device__ inline void lm_eval_sum(const LmRecView& R, int nrec, const double* X, int blk, int nblk,
+                                   double* sum) {
   __shared__ double red[kThreads / 64][LM_NACC];
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const int status = S.status;
-  if (status == LM_DONE) return;  // uniform for every workgroup of the stream
-  double X[7];
-#pragma unroll
-  for (int i = 0; i < 7; ++i) X[i] = status == LM_EVAL_X ? S.x[i] : S.cand[i];
   double acc[LM_NACC];
 #pragma unroll
   for (int i = 0; i < LM_NACC; ++i) acc[i] = 0.0;
-  for (int r = blk * kThreads + tid; r < nrec; r += nblk * kThreads) {
-    const int t = R.type[r];
-    if (t != 0)
-      lm_accum(t, R.px[r], R.py[r], R.pz[r], R.a0[r], R.a1[r], R.a2[r], R.b0[r], R.b1[r],
-               R.b2[r], X, acc);
+  const int stride = nblk * kThreads;
+  for (int r = blk * kThreads + tid; r < nrec; r += 2 * stride) {
+    int t[2];
+    float px[2], py[2], pz[2];
+    double a0[2], a1[2], a2[2], b0[2], b1[2], b2[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int rr = r + u * stride;
+      t[u] = 0;
+      if (rr < nrec) {
+        t[u] = R.type[rr];
+        px[u] = R.px[rr]; py[u] = R.py[rr]; pz[u] = R.pz[rr];
+        a0[u] = R.a0[rr]; a1[u] = R.a1[rr]; a2[u] = R.a2[rr];
+        b0[u] = R.b0[rr]; b1[u] = R.b1[rr]; b2[u] = R.b2[rr];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (t[u] != 0) lm_accum(t[u], px[u], py[u], pz[u], a0[u], a1[u], a2[u], b0[u], b1[u], b2[u], X, acc);
   }
 #pragma unroll
   for (int i = 0; i < LM_NACC; ++i) {
@@ -377,8 +398,22 @@ __device__ inline void lm_eval_block(const LmRecView& R, int nrec, const LmState
     double v = 0.0;
 #pragma unroll
     for (int w = 0; w < kThreads / 64; ++w) v += red[w][tid];
-    partial_out[tid] = v;
+    sum[tid] = v;
   }
+  __syncthreads();
+}
+
+template <int kThreads>
+__device__ inline void lm_eval_block(const LmRecView& R, int nrec, const LmState& S, int blk,
+                                     int nblk, double* partial_out) {
+  __shared__ double bsum[LM_NACC];
+  const int status = S.status;
+  if (status == LM_DONE) return;  // uniform for every workgroup of the stream
+  double X[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) X[i] = status == LM_EVAL_X ? S.x[i] : S.cand[i];
+  lm_eval_sum<kThreads>(R, nrec, X, blk, nblk, bsum);
+  if (threadIdx.x < LM_NACC) partial_out[threadIdx.x] = bsum[threadIdx.x];
 }
 
 // one wave: reduce nblk partials, advance the state; returns true (lane 0) if the state
@@ -396,14 +431,24 @@ __device__ inline bool lm_step_wave(const double* partials, int nblk, LmState& S
   const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&S);
   unsigned long long* dst = reinterpret_cast<unsigned long long*>(&ls);
   for (int w = lane; w < NW; w += 64) dst[w] = src[w];
+  double v[LM_NACC];
+#pragma unroll
+  for (int i = 0; i < LM_NACC; ++i) v[i] = 0.0;
+  for (int c = lane; c < nblk; c += 64) {  // all loads of a block row in flight together
+#pragma unroll
+    for (int i = 0; i < LM_NACC; ++i) v[i] += partials[(size_t)c * LM_NACC + i];
+  }
+#pragma unroll
   for (int i = 0; i < LM_NACC; ++i) {
-    double v = 0.0;
-    for (int c = lane; c < nblk; c += 64) v += partials[(size_t)c * LM_NACC + i];
-    v = wave_sum_d(v);
-    if (lane == 0) sred[i] = v;
+    const double t = wave_sum_d(v[i]);
+    if (lane == 0) sred[i] = t;
   }
   __syncthreads();
-  if (lane == 0) lm_step(ls, sred);
+  if (lane == 0) {
+    LmState L = ls;  // registers for the dependent chain
+    lm_step(L, sred);
+    ls = L;
+  }
   __syncthreads();
   unsigned long long* back = reinterpret_cast<unsigned long long*>(&S);
   for (int w = lane; w < NW; w += 64) back[w] = dst[w];

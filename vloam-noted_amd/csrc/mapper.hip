@@ -19,6 +19,7 @@
 // frame, the host compacts an arena when its tail passes half the capacity.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -39,7 +40,10 @@ constexpr int CORR_BLK = 64;    // correspondence workgroups per stream (grid-st
 constexpr int LM_THREADS = 256;
 constexpr int LM_EBLK = 32;     // LM evaluation workgroups per stream (grid-stride)
 constexpr int SUBMAP_BLOCKS = 64;
-constexpr int MAP_ERR_SUBMAP = 4, MAP_ERR_EXTRA = 8, MAP_ERR_HASH = 16;
+constexpr int INS_SLOTS = WIN_VALID_MAX + EXTRA_CAP;
+constexpr int LM_MAX_PASSES = 8;          // a round needs <= 1 + max_num_iterations = 5
+constexpr uint32_t LM_SPIN_LIMIT = 1u << 21;
+constexpr int MAP_ERR_SUBMAP = 4, MAP_ERR_EXTRA = 8, MAP_ERR_HASH = 16, MAP_ERR_LM_SYNC = 32;
 
 struct StreamFrame {
   double pose[7];  // in: initial guess (transformAssociateToMap); out: optimised pose
@@ -99,9 +103,15 @@ struct MapperDev {
   double* r_b[3];
   float4* ins_pts;  // [B][2][max_in]
   int* ins_tag;
+  float4* ins_sorted;    // [B][2][max_in] inserted points grouped by target cube (input order kept)
+  uint32_t* ins_off;     // [B][2][INS_SLOTS + 1] group offsets: window slots, then extra cubes
+  uint32_t* stable_tok;  // [B][2][NCUBE] arena offset + 1 of content known to be a VoxelGrid
+                         // fixed point (re-filtering it is the identity), else 0
   float4* vx_pts;  // [B][2][scratch_cap]
   int* vx_idx;
   double* partials;  // [B][max_chunks][LM_NACC]
+  uint32_t* lm_sync;   // [B][2 rounds][4]: worker arrivals, eval-point generation, status
+  double* lm_xpub;     // [B][2 rounds][8]: eval point published to the workers
   uint32_t* tickets;  // [B]
 };
 
@@ -284,6 +294,7 @@ __global__ void __launch_bounds__(CORR_THREADS) k_knn(MapperDev D, int round) {
   double X[7];
 #pragma unroll
   for (int i = 0; i < 7; ++i) X[i] = F.pose[i];
+  if (blk == 0 && threadIdx.x < 4) D.lm_sync[((size_t)s * 2 + round) * 4 + threadIdx.x] = 0;
   if (blk == 0 && threadIdx.x == 0) lm_init(F.lm[round], X, 4, F.optimize != 0);
   if (!F.optimize) return;  // k_geom types every record 0
   const int nc = F.nc_stack, ns = F.ns_stack;
@@ -401,6 +412,147 @@ __global__ void __launch_bounds__(64) k_lm_step(MapperDev D, int round) {
 }
 
 // ---------------------------------------------------------------------------------------
+// One launch per outer round: all <= 5 LM passes of every stream.  G workgroups per stream
+// evaluate a share of the records each; the stream's leader (g = 0) keeps the trust-region
+// state in its LDS, reduces the workers' partials and runs the step.  Hand-offs follow the
+// agent-scope release/acquire recipe (cdna_hip_programming.md §6 Guideline 16): partials are
+// plain stores + drain + release fence + relaxed ticket; the eval point is published with sc1
+// (atomic) stores + drain + a relaxed flag; every consumer polls relaxed and acquires once.
+// The grid is sized on the host so that every workgroup is resident, and every spin is
+// bounded (MAP_ERR_LM_SYNC, the stream's LM then stops).
+// ---------------------------------------------------------------------------------------
+#define RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+
+__device__ inline bool lm_spin_ge(uint32_t* w, uint32_t target) {
+  for (uint32_t spins = 0;; ++spins) {
+    if (__hip_atomic_load(w, RLX_AGENT) >= target) return true;
+    if (spins >= LM_SPIN_LIMIT) return false;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+__global__ void __launch_bounds__(LM_THREADS) k_lm_round(MapperDev D, int round, int G) {
+  __shared__ LmState ls;
+  __shared__ double sx[7];
+  __shared__ double bsum[LM_NACC];
+  __shared__ double sred[LM_NACC];
+  __shared__ int sstat;
+  const int s = blockIdx.x / G, g = blockIdx.x % G;
+  StreamFrame& F = D.fr[s];
+  if (!F.active) return;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  LmState& S = F.lm[round];
+  const int nrec = F.nc_stack + F.ns_stack;
+  const size_t rb = (size_t)s * 2 * D.max_in;
+  const LmRecView R{D.r_type + rb, D.r_px + rb, D.r_py + rb, D.r_pz + rb, D.r_a[0] + rb, D.r_a[1] + rb,
+                    D.r_a[2] + rb, D.r_b[0] + rb, D.r_b[1] + rb, D.r_b[2] + rb};
+  uint32_t* sync = D.lm_sync + ((size_t)s * 2 + round) * 4;  // [0] arrivals, [1] generation
+  double* xpub = D.lm_xpub + ((size_t)s * 2 + round) * 8;
+  double* part = D.partials + (size_t)s * D.max_chunks * LM_NACC;
+  if (g == 0) {  // state written by k_knn (earlier launch): plain loads
+    constexpr int NW = sizeof(LmState) / 8;
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&S);
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(&ls);
+    for (int w = tid; w < NW; w += LM_THREADS) dst[w] = src[w];
+  }
+  __syncthreads();
+  bool aborted = false;
+  for (int pass = 0; pass < LM_MAX_PASSES; ++pass) {
+    // ---- evaluation point of this pass
+    if (g == 0) {
+      if (tid == 0) {
+        sstat = ls.status;
+        for (int i = 0; i < 7; ++i) sx[i] = ls.status == LM_EVAL_X ? ls.x[i] : ls.cand[i];
+      }
+      __syncthreads();
+      if (G > 1 && wid == 0) {  // publish: sc1 stores, drain, relaxed flag
+        if (lane < 7) __hip_atomic_store(&xpub[lane], sx[lane], RLX_AGENT);
+        if (lane == 7) __hip_atomic_store(&sync[2], (uint32_t)sstat, RLX_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(&sync[1], (uint32_t)(pass + 1), RLX_AGENT);
+      }
+    } else {
+      if (tid == 0) {
+        if (lm_spin_ge(&sync[1], (uint32_t)(pass + 1))) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          sstat = (int)__hip_atomic_load(&sync[2], RLX_AGENT);
+          for (int i = 0; i < 7; ++i) sx[i] = __hip_atomic_load(&xpub[i], RLX_AGENT);
+        } else {
+          atomicOr(&F.err, MAP_ERR_LM_SYNC);
+          sstat = LM_DONE;
+        }
+      }
+      __syncthreads();
+    }
+    if (sstat == LM_DONE) break;
+    double X[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) X[i] = sx[i];
+    // ---- evaluation of this workgroup's share
+    lm_eval_sum<LM_THREADS>(R, nrec, X, g, G, bsum);
+    if (g != 0) {  // publish the partial: plain stores, drain, release, relaxed ticket
+      if (tid < LM_NACC) part[(size_t)g * LM_NACC + tid] = bsum[tid];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(&sync[0], 1u, RLX_AGENT);
+      }
+      continue;
+    }
+    // ---- leader: gather the partials, step
+    if (tid == 0 && G > 1) {
+      if (lm_spin_ge(&sync[0], (uint32_t)(pass + 1) * (uint32_t)(G - 1))) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        atomicOr(&F.err, MAP_ERR_LM_SYNC);
+        sstat = -1;
+      }
+    }
+    __syncthreads();
+    if (sstat == -1) {
+      aborted = true;
+      break;
+    }
+    if (wid == 0) {
+      double v[LM_NACC];
+#pragma unroll
+      for (int i = 0; i < LM_NACC; ++i) v[i] = lane == 0 ? bsum[i] : 0.0;
+      for (int c = lane; c < G; c += 64) {
+        if (c == 0) continue;
+#pragma unroll
+        for (int i = 0; i < LM_NACC; ++i) v[i] += part[(size_t)c * LM_NACC + i];
+      }
+#pragma unroll
+      for (int i = 0; i < LM_NACC; ++i) {
+        const double t = wave_sum_d(v[i]);
+        if (lane == 0) sred[i] = t;
+      }
+      if (lane == 0) {
+        LmState L = ls;  // registers for the dependent chain
+        lm_step(L, sred);
+        ls = L;
+      }
+    }
+    __syncthreads();
+  }
+  if (g != 0) return;
+  if (aborted && tid == 0) {  // stop this stream's LM where it is (best so far)
+    ls.term = 6;
+    ls.status = LM_DONE;
+  }
+  __syncthreads();
+  if (ls.status == LM_DONE && tid < 7) F.pose[tid] = ls.best[tid];
+  constexpr int NW = sizeof(LmState) / 8;
+  const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&ls);
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(&S);
+  for (int w = tid; w < NW; w += LM_THREADS) dst[w] = src[w];
+}
+
+// ---------------------------------------------------------------------------------------
 // insertion of the stacks into the cube grid with the final pose (laser_mapping.cpp:741-788)
 // ---------------------------------------------------------------------------------------
 __global__ void k_insert(MapperDev D) {
@@ -437,6 +589,85 @@ __global__ void k_insert(MapperDev D) {
 }
 
 // ---------------------------------------------------------------------------------------
+// group the inserted points by target cube (stable counting sort, one workgroup per (stream,
+// map)): each re-VoxelGrid workgroup then reads one contiguous run, in input order
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(VX_THREADS) k_bucket(MapperDev D) {
+  __shared__ int cslot[NCUBE];
+  __shared__ uint32_t base[INS_SLOTS];
+  __shared__ uint32_t wcnt[VX_WAVES][INS_SLOTS];
+  const int sm = blockIdx.x, s = sm >> 1, m = sm & 1;
+  const StreamFrame& F = D.fr[s];
+  if (!F.active) return;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  const int n = m == 0 ? F.nc_stack : F.ns_stack;
+  const int* tag = D.ins_tag + sm_index(s, m) * D.max_in;
+  const float4* pts = D.ins_pts + sm_index(s, m) * D.max_in;
+  float4* out = D.ins_sorted + sm_index(s, m) * D.max_in;
+  uint32_t* off = D.ins_off + sm_index(s, m) * (INS_SLOTS + 1);
+  for (int c = tid; c < NCUBE; c += VX_THREADS) cslot[c] = -1;
+  for (int k = tid; k < INS_SLOTS; k += VX_THREADS) base[k] = 0;
+  __syncthreads();
+  const int vn = F.valid_num, ne = min(F.extra_n[m], EXTRA_CAP);
+  if (tid < vn) cslot[F.window[tid]] = tid;
+  if (tid < ne) cslot[F.extra_list[m][tid]] = WIN_VALID_MAX + tid;
+  __syncthreads();
+  for (int i = tid; i < n; i += VX_THREADS) {
+    const int t = tag[i];
+    const int sl = t >= 0 ? cslot[t] : -1;
+    if (sl >= 0) atomicAdd(&base[sl], 1u);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (int k = 0; k < INS_SLOTS; ++k) {
+      const uint32_t c = base[k];
+      base[k] = acc;
+      off[k] = acc;
+      acc += c;
+    }
+    off[INS_SLOTS] = acc;
+  }
+  __syncthreads();
+  for (int c0 = 0; c0 < n; c0 += VX_THREADS) {
+    const int i = c0 + tid;
+    const int t = i < n ? tag[i] : -1;
+    const int sl = t >= 0 ? cslot[t] : -1;
+    for (int k = tid; k < VX_WAVES * INS_SLOTS; k += VX_THREADS) (&wcnt[0][0])[k] = 0;
+    __syncthreads();
+    // rank among the lanes of this wave with the same slot (peel one slot value per pass)
+    uint32_t rank = 0;
+    bool pending = sl >= 0;
+    while (true) {
+      const uint64_t live = __ballot(pending);
+      if (!live) break;
+      const int leader = __ffsll((unsigned long long)live) - 1;
+      const int lsl = __shfl(sl, leader, 64);
+      const bool mine = pending && sl == lsl;
+      const uint64_t mk = __ballot(mine);
+      if (mine) {
+        rank = __popcll(mk & lanemask_lt());
+        pending = false;
+      }
+      if (lane == 0) wcnt[wid][lsl] = __popcll(mk);
+    }
+    __syncthreads();
+    if (tid < INS_SLOTS) {  // wave prefix per slot, advance the slot base
+      uint32_t acc = base[tid];
+      for (int w = 0; w < VX_WAVES; ++w) {
+        const uint32_t c = wcnt[w][tid];
+        wcnt[w][tid] = acc;
+        acc += c;
+      }
+      base[tid] = acc;
+    }
+    __syncthreads();
+    if (sl >= 0) out[wcnt[wid][sl] + rank] = pts[i];
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // re-VoxelGrid of every window cube (old content ++ inserted points, :795-808); cubes outside
 // the window that received points get them appended raw (:762).  One workgroup per cube.
 // ---------------------------------------------------------------------------------------
@@ -453,22 +684,27 @@ __global__ void __launch_bounds__(VX_THREADS) k_revox(MapperDev D) {
   if (slot < F.valid_num) {
     cube = F.window[slot];
     append = 0;
-  } else if (slot - F.valid_num < min(F.extra_n[m], EXTRA_CAP)) {
-    cube = F.extra_list[m][slot - F.valid_num];
+  } else if (slot >= WIN_VALID_MAX && slot - WIN_VALID_MAX < min(F.extra_n[m], EXTRA_CAP)) {
+    cube = F.extra_list[m][slot - WIN_VALID_MAX];
     append = 1;
   } else {
     return;
   }
+  const uint32_t* ioff = D.ins_off + sm_index(s, m) * (INS_SLOTS + 1);
+  const uint32_t i0 = ioff[slot], n_new = ioff[slot + 1] - i0;
+  uint32_t* tok = D.stable_tok + sm_index(s, m) * NCUBE + cube;
   uint2* tab = D.cube_tab + sm_index(s, m) * NCUBE;
   const uint2 cv = tab[cube];
+  // a cube that received nothing and whose content is a VoxelGrid fixed point keeps it:
+  // re-filtering it (laser_mapping.cpp:795-808) would reproduce it bit for bit
+  if (!append && n_new == 0 && (cv.y == 0 || *tok == cv.x + 1)) return;
   float4* ar = arena_base(D, s, m, F.arena_active[m]);
-  const int nst = m == 0 ? F.nc_stack : F.ns_stack;
   VoxSeg S;
   S.src0 = ar + cv.x;
   S.n0 = (int)cv.y;
-  S.src1 = D.ins_pts + sm_index(s, m) * D.max_in;
-  S.tag1 = D.ins_tag + sm_index(s, m) * D.max_in;
-  S.n1 = nst;
+  S.src1 = D.ins_sorted + sm_index(s, m) * D.max_in + i0;
+  S.tag1 = nullptr;
+  S.n1 = (int)n_new;
   S.tag = cube;
   S.leaf = D.leaf[m];
   S.append_only = append;
@@ -477,11 +713,16 @@ __global__ void __launch_bounds__(VX_THREADS) k_revox(MapperDev D) {
   S.cap = D.map_cap;
   S.res_off = &tab[cube].x;
   S.res_cnt = &tab[cube].y;
+  S.stable_out = tok;
   S.scratch_pts = D.vx_pts + sm_index(s, m) * D.scratch_cap;
   S.scratch_idx = D.vx_idx + sm_index(s, m) * D.scratch_cap;
   S.scratch_tail = &F.scratch_tail[m];
   S.scratch_cap = D.scratch_cap;
   S.err = &F.err;
+  if (!append && n_new > 0 && n_new <= VX_MERGE_CAP && cv.y > 0 && *tok == cv.x + 1) {
+    if (vx_merge_fixed_point(S, lds)) return;
+    __syncthreads();  // grid overflow: full filter below
+  }
   voxel_segment(S, lds);
 }
 
@@ -537,7 +778,12 @@ __global__ void k_compact_commit(MapperDev D, const int* pairs, int npairs, cons
   StreamFrame& F = D.fr[s];
   uint2* tab = D.cube_tab + (size_t)sm * NCUBE;
   const uint32_t* no = new_off + (size_t)p * (NCUBE + 1);
-  for (int c = threadIdx.x; c < NCUBE; c += blockDim.x) tab[c].x = no[c];
+  uint32_t* tok = D.stable_tok + (size_t)sm * NCUBE;
+  for (int c = threadIdx.x; c < NCUBE; c += blockDim.x) {
+    const bool stable = tok[c] != 0 && tok[c] == tab[c].x + 1;  // content moves verbatim
+    tab[c].x = no[c];
+    tok[c] = stable ? no[c] + 1 : 0u;
+  }
   if (threadIdx.x == 0) {
     F.arena_tail[m] = no[NCUBE];
     F.arena_active[m] = 1 - F.arena_active[m];
@@ -572,6 +818,8 @@ struct loam_mapper {
   long long fam_launches[NFAM] = {0};
   int dev = 0, B = 1;
   hipStream_t st = nullptr;
+  hipStream_t st2 = nullptr;  // stack VoxelGrid, concurrent with the submap / hash build
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   MapperDev D{};
   std::vector<StreamFrame> hf;
@@ -582,6 +830,7 @@ struct loam_mapper {
   uint32_t* d_new_off = nullptr;
   std::vector<void*> allocs;
   uint32_t frame_counter = 0;
+  int lm_G = 0;  // workgroups per stream of k_lm_round (0: two-kernel path k_lm_eval / k_lm_step)
 };
 
 namespace {
@@ -591,7 +840,9 @@ int32_t dalloc(loam_mapper* h, T** p, size_t count) {
   void* q = nullptr;
   size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
   LOAM_HIP(hipMalloc(&q, bytes));
-  LOAM_HIP(hipMemset(q, 0, bytes));
+  // zero on the handle's own (non-blocking) stream: a null-stream memset is not ordered
+  // before this stream's kernels; create() synchronizes the stream before returning
+  LOAM_HIP(hipMemsetAsync(q, 0, bytes, h->st));
   h->allocs.push_back(q);
   *p = reinterpret_cast<T*>(q);
   return LOAM_OK;
@@ -616,7 +867,10 @@ void free_all(loam_mapper* h) {
   h->ev_pool.clear();
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
+  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->st) (void)hipStreamDestroy(h->st);
+  if (h->st2) (void)hipStreamDestroy(h->st2);
 }
 
 void host_initial_guess(HostStream& H, double* pose) {
@@ -679,6 +933,18 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
   D.hash_T = (int)next_pow2((uint32_t)D.sub_cap);
   D.scratch_cap = D.sub_cap + D.max_in;
   D.max_chunks = LM_EBLK;
+  {
+    // k_lm_round needs every workgroup resident: G per stream with B * G <= CUs x blocks/CU.
+    // LOAM_LM_PERSISTENT=0 selects the two-kernel path (tests cover both).
+    int occ = 0, cus = 0;
+    const char* env = std::getenv("LOAM_LM_PERSISTENT");
+    const bool allow = !(env && env[0] == '0');
+    if (allow && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_lm_round, LM_THREADS, 0) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess) {
+      const int cap = occ * cus;
+      h->lm_G = std::min(LM_EBLK, std::min(16, cap / n_streams));
+    }
+  }
   D.leaf[0] = (float)h->P.mapping_line_resolution;
   D.leaf[1] = (float)h->P.mapping_plane_resolution;
   const size_t B = n_streams;
@@ -691,6 +957,10 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
 #define ALLOC(ptr, n) \
   if ((rc = dalloc(h, &(ptr), (n))) != LOAM_OK) return fail(rc)
   if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess) return fail(LOAM_ERR_HIP);
+  if (hipStreamCreateWithFlags(&h->st2, hipStreamNonBlocking) != hipSuccess) return fail(LOAM_ERR_HIP);
+  if (hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess)
+    return fail(LOAM_ERR_HIP);
   for (auto& e : h->ev)
     if (hipEventCreate(&e) != hipSuccess) return fail(LOAM_ERR_HIP);
   ALLOC(D.fr, B);
@@ -722,9 +992,14 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
   }
   ALLOC(D.ins_pts, B * 2 * (size_t)D.max_in);
   ALLOC(D.ins_tag, B * 2 * (size_t)D.max_in);
+  ALLOC(D.ins_sorted, B * 2 * (size_t)D.max_in);
+  ALLOC(D.ins_off, B * 2 * (size_t)(INS_SLOTS + 1));
+  ALLOC(D.stable_tok, B * 2 * (size_t)NCUBE);
   ALLOC(D.vx_pts, B * 2 * (size_t)D.scratch_cap);
   ALLOC(D.vx_idx, B * 2 * (size_t)D.scratch_cap);
   ALLOC(D.partials, B * (size_t)D.max_chunks * LM_NACC);
+  ALLOC(D.lm_sync, B * 2 * 4);
+  ALLOC(D.lm_xpub, B * 2 * 8);
   ALLOC(D.tickets, B);
   ALLOC(h->d_pairs, B * 2);
   ALLOC(h->d_new_off, B * 2 * (NCUBE + 1));
@@ -737,6 +1012,7 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
     F.cen[0] = 10; F.cen[1] = 10; F.cen[2] = 5;
     F.pose[3] = 1.0;
   }
+  if (hipStreamSynchronize(h->st) != hipSuccess) return fail(LOAM_ERR_HIP);  // zero-fills done
   *out = h;
   return LOAM_OK;
 }
@@ -754,6 +1030,7 @@ int32_t loam_mapper_reset(loam_mapper* h) {
   LOAM_HIP(hipSetDevice(h->dev));
   for (int p = 0; p < 2; ++p)
     LOAM_HIP(hipMemsetAsync(h->cube_tab[p], 0, sizeof(uint2) * h->B * 2 * NCUBE, h->st));
+  LOAM_HIP(hipMemsetAsync(h->D.stable_tok, 0, sizeof(uint32_t) * h->B * 2 * NCUBE, h->st));
   LOAM_HIP(hipStreamSynchronize(h->st));
   for (int s = 0; s < h->B; ++s) {
     h->hf[s] = StreamFrame{};
@@ -821,7 +1098,7 @@ int32_t loam_mapper_input_device(loam_mapper* h, int32_t s, const float* corner,
 }
 
 // HIP events around each launch when profiling is on (accumulated per kernel family)
-static hipError_t prof_begin(loam_mapper* h, int fam, hipEvent_t* stop) {
+static hipError_t prof_begin(loam_mapper* h, int fam, hipEvent_t* stop, hipStream_t st) {
   *stop = nullptr;
   if (!h->prof) return hipSuccess;
   size_t k = h->ev_fam.size() * 2;
@@ -833,18 +1110,19 @@ static hipError_t prof_begin(loam_mapper* h, int fam, hipEvent_t* stop) {
   }
   h->ev_fam.push_back(fam);
   *stop = h->ev_pool[k + 1];
-  return hipEventRecord(h->ev_pool[k], h->st);
+  return hipEventRecord(h->ev_pool[k], st);
 }
-static hipError_t prof_end(loam_mapper* h, hipEvent_t stop) {
-  return (h->prof && stop) ? hipEventRecord(stop, h->st) : hipSuccess;
+static hipError_t prof_end(loam_mapper* h, hipEvent_t stop, hipStream_t st) {
+  return (h->prof && stop) ? hipEventRecord(stop, st) : hipSuccess;
 }
-#define LAUNCH(fam, ...)                              \
+#define LAUNCH_ON(stream, fam, ...)                   \
   do {                                                \
     hipEvent_t stop_;                                 \
-    LOAM_HIP(prof_begin(h, (fam), &stop_));           \
+    LOAM_HIP(prof_begin(h, (fam), &stop_, (stream))); \
     __VA_ARGS__;                                      \
-    LOAM_HIP(prof_end(h, stop_));                     \
+    LOAM_HIP(prof_end(h, stop_, (stream)));           \
   } while (0)
+#define LAUNCH(fam, ...) LAUNCH_ON(h->st, fam, __VA_ARGS__)
 
 int32_t loam_mapper_input_device_batch(loam_mapper* h, int32_t n, const int32_t* streams,
                                        const uint64_t* d_corner, const int32_t* n_corner,
@@ -924,28 +1202,39 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   hipStream_t st = h->st;
   LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(StreamFrame) * B, hipMemcpyHostToDevice, st));
   LOAM_HIP(hipEventRecord(h->ev[0], st));
+  // stack VoxelGrid (reads only this frame's inputs) on the second stream, overlapping the
+  // cube shift, submap gather and hash build; joined before the correspondences
+  LOAM_HIP(hipEventRecord(h->ev_fork, st));
+  LOAM_HIP(hipStreamWaitEvent(h->st2, h->ev_fork, 0));
+  LAUNCH_ON(h->st2, FAM_STACK, k_stack_ds<<<B * 2, VX_THREADS, 0, h->st2>>>(D));
+  LOAM_HIP(hipEventRecord(h->ev_join, h->st2));
   if (any_shift) {
     LAUNCH(FAM_OTHER, k_shift_cubes<<<dim3(16, B), 256, 0, st>>>(D, h->cube_tab[h->parity], h->cube_tab[1 - h->parity]));
     h->parity ^= 1;
     D.cube_tab = h->cube_tab[h->parity];
   }
-  LAUNCH(FAM_STACK, k_stack_ds<<<B * 2, VX_THREADS, 0, st>>>(D));
   LAUNCH(FAM_OTHER, k_submap_prep<<<B, 128, 0, st>>>(D));
   LOAM_HIP(hipEventRecord(h->ev[1], st));
   LAUNCH(FAM_HASH, k_submap_insert<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D));
   LAUNCH(FAM_HASH, k_submap_alloc<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D));
   LAUNCH(FAM_HASH, k_submap_scatter<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D));
+  LOAM_HIP(hipStreamWaitEvent(st, h->ev_join, 0));
   for (int round = 0; round < 2; ++round) {
     LAUNCH(FAM_CORR, k_knn<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round));
     LAUNCH(FAM_CORR, k_geom<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round));
-    for (int it = 0; it < 5; ++it) {  // iteration 0 + max_num_iterations = 4 candidates
-      LAUNCH(FAM_LM, k_lm_eval<<<B * LM_EBLK, LM_THREADS, 0, st>>>(D, round));
-      LAUNCH(FAM_LM, k_lm_step<<<B, 64, 0, st>>>(D, round));
+    if (h->lm_G > 0) {
+      LAUNCH(FAM_LM, k_lm_round<<<B * h->lm_G, LM_THREADS, 0, st>>>(D, round, h->lm_G));
+    } else {
+      for (int it = 0; it < 5; ++it) {  // iteration 0 + max_num_iterations = 4 candidates
+        LAUNCH(FAM_LM, k_lm_eval<<<B * LM_EBLK, LM_THREADS, 0, st>>>(D, round));
+        LAUNCH(FAM_LM, k_lm_step<<<B, 64, 0, st>>>(D, round));
+      }
     }
   }
   LOAM_HIP(hipEventRecord(h->ev[2], st));
   LAUNCH(FAM_INSERT, k_insert<<<dim3(16, B), 256, 0, st>>>(D));
-  LAUNCH(FAM_REVOX, k_revox<<<B * 2 * (WIN_VALID_MAX + EXTRA_CAP), VX_THREADS, 0, st>>>(D));
+  LAUNCH(FAM_INSERT, k_bucket<<<B * 2, VX_THREADS, 0, st>>>(D));
+  LAUNCH(FAM_REVOX, k_revox<<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D));
   LOAM_HIP(hipGetLastError());
   LOAM_HIP(hipEventRecord(h->ev[3], st));
   LOAM_HIP(hipMemcpyAsync(h->hf.data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
@@ -1141,6 +1430,8 @@ int32_t loam_mapper_cube_set(loam_mapper* h, int32_t s, int32_t which, int32_t c
   uint2 v = make_uint2(tail, (uint32_t)n);
   tail += n;
   LOAM_HIP(hipMemcpy(h->cube_tab[h->parity] + ((size_t)s * 2 + which) * NCUBE + cube, &v, sizeof(uint2), hipMemcpyHostToDevice));
+  const uint32_t zero = 0;  // caller content: not known to be a VoxelGrid fixed point
+  LOAM_HIP(hipMemcpy(h->D.stable_tok + ((size_t)s * 2 + which) * NCUBE + cube, &zero, sizeof(zero), hipMemcpyHostToDevice));
   return LOAM_OK;
 }
 

@@ -66,6 +66,19 @@ __global__ void __launch_bounds__(VX_THREADS) k_voxel_one(VoxSeg S) {
   voxel_segment(S, lds);
 }
 
+// re-VoxelGrid of fixed-point content + new points (the map update path); *merged = 1 if the
+// merge path ran, 0 if it fell back to the full filter
+__global__ void __launch_bounds__(VX_THREADS) k_voxel_merge(VoxSeg S, int* merged) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
+  if (S.n1 > 0 && (uint32_t)S.n1 <= VX_MERGE_CAP && S.n0 > 0 && vx_merge_fixed_point(S, lds)) {
+    if (threadIdx.x == 0) *merged = 1;
+    return;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *merged = 0;
+  voxel_segment(S, lds);
+}
+
 // standalone cell hash (one point set)
 __global__ void k_hash_insert(const float4* pts, int n, const int* origin, unsigned long long* hk,
                               unsigned long long* hc, uint32_t mask, uint32_t epoch, uint32_t* ps,
@@ -310,6 +323,61 @@ int32_t loam_voxel_grid(int32_t device, const float* in, int32_t n, float leaf, 
   }
   if (cnt) LOAM_HIP(hipMemcpy(out, dout.p, sizeof(float4) * cnt, hipMemcpyDeviceToHost));
   *n_out = (int32_t)cnt;
+  return LOAM_OK;
+}
+
+int32_t loam_voxel_merge(int32_t device, const float* fixed, int32_t n0, const float* added, int32_t n1,
+                         float leaf, float* out, int32_t* n_out, int32_t* merged) {
+  if (n0 < 0 || n1 < 0 || (n0 > 0 && !fixed) || (n1 > 0 && !added) || !out || !n_out || !(leaf > 0.f)) {
+    set_error("loam_voxel_merge: bad arguments");
+    return LOAM_ERR_ARG;
+  }
+  int32_t rc = ensure_device(device);
+  if (rc != LOAM_OK) return rc;
+  LOAM_HIP(hipSetDevice(device));
+  const int32_t n = n0 + n1;
+  DevBuf dc, da, dout, dsp, dsi, doff, dcnt, derr, dm;
+  LOAM_HIP(dmalloc<float4>(dc, n0));
+  LOAM_HIP(dmalloc<float4>(da, n1));
+  LOAM_HIP(dmalloc<float4>(dout, n));
+  LOAM_HIP(dmalloc<float4>(dsp, n));
+  LOAM_HIP(dmalloc<int>(dsi, n));
+  LOAM_HIP(dmalloc<uint32_t>(doff, 1));
+  LOAM_HIP(dmalloc<uint32_t>(dcnt, 1));
+  LOAM_HIP(dmalloc<int>(derr, 1));
+  LOAM_HIP(dmalloc<int>(dm, 1));
+  if (n0) LOAM_HIP(hipMemcpy(dc.p, fixed, sizeof(float4) * n0, hipMemcpyHostToDevice));
+  if (n1) LOAM_HIP(hipMemcpy(da.p, added, sizeof(float4) * n1, hipMemcpyHostToDevice));
+  VoxSeg S{};
+  S.src0 = (const float4*)dc.p;
+  S.n0 = n0;
+  S.src1 = (const float4*)da.p;
+  S.tag1 = nullptr;
+  S.n1 = n1;
+  S.leaf = leaf;
+  S.out = (float4*)dout.p;
+  S.cap = (uint32_t)n;
+  S.res_off = (uint32_t*)doff.p;
+  S.res_cnt = (uint32_t*)dcnt.p;
+  S.scratch_pts = (float4*)dsp.p;
+  S.scratch_idx = (int*)dsi.p;
+  S.scratch_cap = (uint32_t)n;
+  S.err = (int*)derr.p;
+  k_voxel_merge<<<1, VX_THREADS>>>(S, (int*)dm.p);
+  LOAM_HIP(hipGetLastError());
+  uint32_t off = 0, cnt = 0;
+  int err = 0, m = 0;
+  LOAM_HIP(hipMemcpy(&off, doff.p, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  LOAM_HIP(hipMemcpy(&cnt, dcnt.p, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  LOAM_HIP(hipMemcpy(&err, derr.p, sizeof(int), hipMemcpyDeviceToHost));
+  LOAM_HIP(hipMemcpy(&m, dm.p, sizeof(int), hipMemcpyDeviceToHost));
+  if (err) {
+    set_error("loam_voxel_merge: capacity");
+    return LOAM_ERR_CAPACITY;
+  }
+  if (cnt) LOAM_HIP(hipMemcpy(out, (float4*)dout.p + off, sizeof(float4) * cnt, hipMemcpyDeviceToHost));
+  *n_out = (int32_t)cnt;
+  if (merged) *merged = m;
   return LOAM_OK;
 }
 

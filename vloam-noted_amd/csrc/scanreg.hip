@@ -506,7 +506,9 @@ template <typename T>
 int32_t sralloc(loam_scanreg* h, T** p, size_t n) {
   void* q = nullptr;
   LOAM_HIP(hipMalloc(&q, std::max<size_t>(n, 1) * sizeof(T)));
-  LOAM_HIP(hipMemset(q, 0, std::max<size_t>(n, 1) * sizeof(T)));
+  // zero on the handle's own (non-blocking) stream: a null-stream memset is not ordered
+  // before this stream's kernels; create() synchronizes the stream before returning
+  LOAM_HIP(hipMemsetAsync(q, 0, std::max<size_t>(n, 1) * sizeof(T), h->st));
   h->allocs.push_back(q);
   *p = reinterpret_cast<T*>(q);
   return LOAM_OK;
@@ -571,6 +573,7 @@ int32_t loam_scanreg_create(const loam_params* p, int32_t device, loam_scanreg**
 #undef SRA
   D.out[0] = D.cloud;
   D.sort_ind = nullptr;
+  if (hipStreamSynchronize(h->st) != hipSuccess) return fail(LOAM_ERR_HIP);
   *out = h;
   return LOAM_OK;
 }

@@ -36,7 +36,7 @@ constexpr int VX_LDS_WORDS = 40960;  // 160 KiB
 struct VoxSeg {
   const float4* src0;
   int n0;
-  const float4* src1;  // optional secondary source filtered by tag
+  const float4* src1;  // optional secondary source filtered by tag (tag1 == nullptr: all of it)
   const int* tag1;
   int n1;
   int tag;
@@ -47,6 +47,8 @@ struct VoxSeg {
   uint32_t cap;           // capacity of out (absolute index bound)
   uint32_t* res_off;      // result offset (absolute index into out) — optional
   uint32_t* res_cnt;      // result count — optional
+  uint32_t* stable_out = nullptr;  // optional: (result offset + 1) if the output is a VoxelGrid fixed
+                          // point (every centroid inside its own voxel), else 0
   float4* scratch_pts;    // gathered secondary points
   int* scratch_idx;       // member lists
   uint32_t* scratch_tail; // if set, scratch slots are allocated from it (per segment)
@@ -97,6 +99,8 @@ __device__ inline uint32_t vx_key(const VxGeom& g, float4 p) {
 struct VxMisc {
   uint32_t sbase[2];
   int sfail;
+  int moved;
+  uint32_t nbig;
   VxGeom g;
   float bb[VX_WAVES][6];
 };
@@ -117,33 +121,68 @@ constexpr int VX_HIST_WORD = 3 * VX_UCAP;      // LDS words [36864, 38912): buck
 constexpr int VX_GEND_WORD = VX_HIST_WORD + VX_NB;  // [38912, 40704): group ends
 constexpr int VX_MAX_GROUPS = VX_LDS_WORDS - 256 - VX_GEND_WORD;
 
-// Member lists (chunk by chunk: members of earlier chunks precede later ones), then per
-// voxel: members sorted by input index, float sums in that order, centroid -> out[j].
+constexpr int VX_UNROLL = 4;
+
+// voxel keys of points i0 + u * VX_THREADS (u < VX_UNROLL), loads issued together; VX_EMPTY
+// past the end
+__device__ inline void vx_keys4(const VxGeom& g, const VxSrc& P, uint32_t N, uint32_t i0,
+                                uint32_t* kk) {
+  float4 p[VX_UNROLL];
+#pragma unroll
+  for (int u = 0; u < VX_UNROLL; ++u) {
+    const uint32_t i = i0 + u * VX_THREADS;
+    if (i < N) p[u] = P(i);
+  }
+#pragma unroll
+  for (int u = 0; u < VX_UNROLL; ++u) kk[u] = i0 + u * VX_THREADS < N ? vx_key(g, p[u]) : VX_EMPTY;
+}
+
+// Member lists, then per voxel: members sorted by input index, float sums in that order,
+// centroid -> out[j].
+// Returns true if some centroid left its voxel (float rounding): then the output is not a
+// fixed point of the filter.  Phases:
+//   1. member lists, chunk by chunk with a barrier (members of earlier chunks precede later
+//      ones, so each list is nearly sorted); the next chunk's points are loaded before the
+//      barrier so the load latency overlaps it
+//   2. per voxel: insertion sort of the list by input index; voxels with <= VX_BIG members
+//      are summed by their thread (gathers batched 4 at a time)
+//   3. voxels with more members: one wave each, 64 member points gathered at once, summed in
+//      input order by a shuffle chain (the same float additions, in the same order)
+constexpr uint32_t VX_BIG = 128;
+
 template <typename MT>
-__device__ inline void vx_centroids(const VxGeom& g, const VxSrc& P, uint32_t N, MT* members,
+__device__ inline bool vx_centroids(const VxGeom& g, const VxSrc& P, uint32_t N, MT* members,
                                     uint32_t klo, uint32_t khi, uint32_t U, const uint32_t* ukey,
-                                    const uint32_t* uoff, uint32_t* ufill, float4* out) {
-  const int tid = threadIdx.x;
+                                    const uint32_t* uoff, uint32_t* ufill, float4* out,
+                                    uint32_t* big_list, uint32_t big_cap, VxMisc& M) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  bool moved = false;
+  float4 pn = make_float4(0.f, 0.f, 0.f, 0.f);
+  if ((uint32_t)tid < N) pn = P(tid);
   for (uint32_t c = 0; c < N; c += VX_THREADS) {
-    uint32_t i = c + tid;
+    const uint32_t i = c + tid;
+    const float4 p = pn;
+    if (i + VX_THREADS < N) pn = P(i + VX_THREADS);  // next chunk, in flight across the barrier
     if (i < N) {
-      uint32_t k = vx_key(g, P(i));
+      const uint32_t k = vx_key(g, p);
       if (k >= klo && k < khi) {
         uint32_t lo = 0, hi = U;  // lower_bound
         while (lo < hi) {
-          uint32_t mid = (lo + hi) >> 1;
+          const uint32_t mid = (lo + hi) >> 1;
           if (ukey[mid] < k) lo = mid + 1; else hi = mid;
         }
-        uint32_t pos = uoff[lo] + atomicAdd(&ufill[lo], 1u);
+        const uint32_t pos = uoff[lo] + atomicAdd(&ufill[lo], 1u);
         members[pos] = (MT)i;
       }
     }
     __syncthreads();
   }
+  if (tid == 0) M.nbig = 0;
+  __syncthreads();
   for (uint32_t j = tid; j < U; j += VX_THREADS) {
     const uint32_t b = uoff[j];
     const uint32_t n = ufill[j];
-    for (uint32_t a = 1; a < n; ++a) {  // insertion sort (lists are short and nearly ordered)
+    for (uint32_t a = 1; a < n; ++a) {  // insertion sort (nearly ordered lists)
       const MT v = members[b + a];
       uint32_t q = a;
       while (q > 0 && members[b + q - 1] > v) {
@@ -152,21 +191,55 @@ __device__ inline void vx_centroids(const VxGeom& g, const VxSrc& P, uint32_t N,
       }
       members[b + q] = v;
     }
+    if (n > VX_BIG) {
+      const uint32_t e = atomicAdd(&M.nbig, 1u);
+      if (e < big_cap) {
+        big_list[e] = j;
+        continue;
+      }
+    }
     float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
     for (uint32_t a = 0; a < n; a += 4) {  // gathers issued together, summed in order
-      float4 p[4];
+      float4 pp[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (a + u < n) p[u] = P((uint32_t)members[b + a + u]);
+        if (a + u < n) pp[u] = P((uint32_t)members[b + a + u]);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (a + u < n) {
-          sx += p[u].x; sy += p[u].y; sz += p[u].z; si += p[u].w;
+          sx += pp[u].x; sy += pp[u].y; sz += pp[u].z; si += pp[u].w;
         }
     }
     const float fn = (float)n;
-    out[j] = make_float4(sx / fn, sy / fn, sz / fn, si / fn);
+    const float4 cc = make_float4(sx / fn, sy / fn, sz / fn, si / fn);
+    out[j] = cc;
+    moved |= vx_key(g, cc) != ukey[j];
   }
+  __syncthreads();
+  const uint32_t nbig = min(M.nbig, big_cap);
+  for (uint32_t e = wid; e < nbig; e += VX_WAVES) {
+    const uint32_t j = big_list[e];
+    const uint32_t b = uoff[j], n = ufill[j];
+    float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;  // every lane keeps the same running sum
+    for (uint32_t a = 0; a < n; a += 64) {
+      float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (a + lane < n) p = P((uint32_t)members[b + a + lane]);
+      const uint32_t m = min(64u, n - a);
+      for (uint32_t l = 0; l < m; ++l) {
+        sx += __shfl(p.x, l, 64);
+        sy += __shfl(p.y, l, 64);
+        sz += __shfl(p.z, l, 64);
+        si += __shfl(p.w, l, 64);
+      }
+    }
+    if (lane == 0) {
+      const float fn = (float)n;
+      const float4 cc = make_float4(sx / fn, sy / fn, sz / fn, si / fn);
+      out[j] = cc;
+      moved |= vx_key(g, cc) != ukey[j];
+    }
+  }
+  return moved;
 }
 
 // Steps 3-6 for the points whose voxel idx lies in [klo, khi): LDS hash -> sorted unique
@@ -175,7 +248,8 @@ __device__ inline void vx_centroids(const VxGeom& g, const VxSrc& P, uint32_t N,
 // effects on the output) when the unique voxels do not fit the LDS.
 __device__ inline uint32_t vx_group(const VoxSeg& S, const VxGeom& g, const VxSrc& P, uint32_t N,
                                     int* members, uint32_t klo, uint32_t khi, uint32_t out_base,
-                                    uint32_t lds_limit, uint32_t* lds, uint32_t* ws, VxMisc& M) {
+                                    uint32_t lds_limit, uint32_t* lds, uint32_t* ws, VxMisc& M,
+                                    int* moved_out) {
   const int tid = threadIdx.x;
   uint32_t* hkey = lds;
   uint32_t* hcnt = lds + VX_HASH;
@@ -183,23 +257,31 @@ __device__ inline uint32_t vx_group(const VoxSeg& S, const VxGeom& g, const VxSr
     hkey[i] = VX_EMPTY;
     hcnt[i] = 0;
   }
-  if (tid == 0) M.sfail = 0;
+  if (tid == 0) {
+    M.sfail = 0;
+    M.moved = 0;
+  }
   __syncthreads();
-  for (uint32_t i = tid; i < N; i += VX_THREADS) {
-    const uint32_t k = vx_key(g, P(i));
-    if (k < klo || k >= khi) continue;
-    uint32_t h = vx_hash(k);
-    int probes = 0;
-    while (true) {
-      uint32_t old = atomicCAS(&hkey[h], VX_EMPTY, k);
-      if (old == VX_EMPTY || old == k) {
-        atomicAdd(&hcnt[h], 1u);
-        break;
-      }
-      h = (h + 1) & (VX_HASH - 1);
-      if (++probes >= VX_HASH) {
-        M.sfail = 1;
-        break;
+  for (uint32_t i0 = tid; i0 < N; i0 += VX_UNROLL * VX_THREADS) {
+    uint32_t kk4[VX_UNROLL];
+    vx_keys4(g, P, N, i0, kk4);
+#pragma unroll
+    for (int u = 0; u < VX_UNROLL; ++u) {
+      const uint32_t k = kk4[u];
+      if (k < klo || k >= khi) continue;  // also skips i >= N (key VX_EMPTY)
+      uint32_t h = vx_hash(k);
+      int probes = 0;
+      while (true) {
+        uint32_t old = atomicCAS(&hkey[h], VX_EMPTY, k);
+        if (old == VX_EMPTY || old == k) {
+          atomicAdd(&hcnt[h], 1u);
+          break;
+        }
+        h = (h + 1) & (VX_HASH - 1);
+        if (++probes >= VX_HASH) {
+          M.sfail = 1;
+          break;
+        }
       }
     }
   }
@@ -287,14 +369,25 @@ __device__ inline uint32_t vx_group(const VoxSeg& S, const VxGeom& g, const VxSr
     if (ob == 0xFFFFFFFFu) return 0;
   }
   // member lists in LDS as u16 point indices when they fit, else in global scratch
-  if (N <= 65536u && 3 * U + (tot + 1) / 2 <= lds_limit)
-    vx_centroids(g, P, N, reinterpret_cast<uint16_t*>(lds + 3 * U), klo, khi, U, ukey, uoff, ufill,
-                 S.out + ob);
-  else
-    vx_centroids(g, P, N, members, klo, khi, U, ukey, uoff, ufill, S.out + ob);
+  // LDS after the tables: u16 member lists (when they fit), then the big-voxel list
+  bool moved;
+  const uint32_t mem_words = (N <= 65536u) ? (tot + 1) / 2 : 0u;
+  if (N <= 65536u && 3 * U + mem_words + 64 <= lds_limit) {
+    uint32_t* big = lds + 3 * U + mem_words;
+    moved = vx_centroids(g, P, N, reinterpret_cast<uint16_t*>(lds + 3 * U), klo, khi, U, ukey, uoff,
+                         ufill, S.out + ob, big, lds_limit - (3 * U + mem_words), M);
+  } else {
+    uint32_t* big = lds + 3 * U;
+    const uint32_t cap = lds_limit > 3 * U ? lds_limit - 3 * U : 0u;
+    moved = vx_centroids(g, P, N, members, klo, khi, U, ukey, uoff, ufill, S.out + ob, big, cap, M);
+  }
+  if (moved) M.moved = 1;
+  __syncthreads();
+  *moved_out |= M.moved;
   if (out_base == VX_ALLOC && tid == 0) {
     if (S.res_off) *S.res_off = ob;
     if (S.res_cnt) *S.res_cnt = U;
+    if (S.stable_out) *S.stable_out = *moved_out ? 0u : ob + 1;
   }
   __syncthreads();
   return U;
@@ -349,10 +442,11 @@ __device__ inline void vx_grouped(const VoxSeg& S, const VxGeom& g, const VxSrc&
   if (ob == 0xFFFFFFFFu) return;
   uint32_t acc = 0;
   int gstart = 0;
+  int moved = 0;
   for (int gi = 0; gi < ng; ++gi) {
     const int ge = (int)gend[gi];
     const uint32_t U = vx_group(S, g, P, N, members, blo(gstart), ge >= VX_NB ? 0xFFFFFFFFu : blo(ge),
-                                ob + acc, VX_HIST_WORD, lds, ws, M);
+                                ob + acc, VX_HIST_WORD, lds, ws, M, &moved);
     if (U == VX_OVERFLOW) {
       if (tid == 0) atomicOr(S.err, VX_ERR_CAPACITY);
       return;
@@ -363,7 +457,63 @@ __device__ inline void vx_grouped(const VoxSeg& S, const VxGeom& g, const VxSrc&
   if (tid == 0) {
     if (S.res_off) *S.res_off = ob;
     if (S.res_cnt) *S.res_cnt = acc;
+    if (S.stable_out) *S.stable_out = 0;  // slack in the reserved slot: never skipped
   }
+}
+
+// bounding box (pcl::getMinMax3D) of the N points P(i) and the grid geometry of leaf -> M.g
+// (all threads; result valid after the trailing barrier)
+template <typename PF>
+__device__ inline void vx_geometry(const PF& P, uint32_t N, float leaf, VxMisc& M) {
+  const int tid = threadIdx.x;
+  const int wid = tid >> 6, lane = tid & 63;
+  float mnx = 3.402823466e38f, mny = 3.402823466e38f, mnz = 3.402823466e38f;
+  float mxx = -3.402823466e38f, mxy = -3.402823466e38f, mxz = -3.402823466e38f;
+  for (uint32_t i0 = tid; i0 < N; i0 += VX_UNROLL * VX_THREADS) {
+    float4 p[VX_UNROLL];
+#pragma unroll
+    for (int u = 0; u < VX_UNROLL; ++u)
+      if (i0 + u * VX_THREADS < N) p[u] = P(i0 + u * VX_THREADS);
+#pragma unroll
+    for (int u = 0; u < VX_UNROLL; ++u) {
+      if (i0 + u * VX_THREADS >= N) continue;
+      mnx = fminf(mnx, p[u].x); mny = fminf(mny, p[u].y); mnz = fminf(mnz, p[u].z);
+      mxx = fmaxf(mxx, p[u].x); mxy = fmaxf(mxy, p[u].y); mxz = fmaxf(mxz, p[u].z);
+    }
+  }
+  mnx = wave_min_f(mnx); mny = wave_min_f(mny); mnz = wave_min_f(mnz);
+  mxx = wave_max_f(mxx); mxy = wave_max_f(mxy); mxz = wave_max_f(mxz);
+  float (*sbb)[6] = M.bb;
+  if (lane == 0) {
+    sbb[wid][0] = mnx; sbb[wid][1] = mny; sbb[wid][2] = mnz;
+    sbb[wid][3] = mxx; sbb[wid][4] = mxy; sbb[wid][5] = mxz;
+  }
+  __syncthreads();
+  VxGeom& sg = M.g;
+  if (tid == 0) {
+    for (int w = 1; w < VX_WAVES; ++w) {
+      mnx = fminf(mnx, sbb[w][0]); mny = fminf(mny, sbb[w][1]); mnz = fminf(mnz, sbb[w][2]);
+      mxx = fmaxf(mxx, sbb[w][3]); mxy = fmaxf(mxy, sbb[w][4]); mxz = fmaxf(mxz, sbb[w][5]);
+    }
+    VxGeom g;
+    g.inv = 1.0f / leaf;
+    long long dx = (long long)((mxx - mnx) * g.inv) + 1;
+    long long dy = (long long)((mxy - mny) * g.inv) + 1;
+    long long dz = (long long)((mxz - mnz) * g.inv) + 1;
+    g.overflow = (dx * dy * dz > 2147483647LL) ? 1 : 0;
+    g.minbx = (int)floorf(mnx * g.inv);
+    int maxbx = (int)floorf(mxx * g.inv);
+    g.minby = (int)floorf(mny * g.inv);
+    int maxby = (int)floorf(mxy * g.inv);
+    g.minbz = (int)floorf(mnz * g.inv);
+    int divx = maxbx - g.minbx + 1, divy = maxby - g.minby + 1;
+    g.mul1 = divx;
+    g.mul2 = divx * divy;
+    int maxbz = (int)floorf(mxz * g.inv);
+    g.nvox = (unsigned long long)divx * (unsigned long long)divy * (unsigned long long)(maxbz - g.minbz + 1);
+    sg = g;
+  }
+  __syncthreads();
 }
 
 // The workgroup routine.  lds: VX_LDS_WORDS u32 words (the whole 160 KiB; the last 256 words
@@ -376,7 +526,10 @@ __device__ inline void voxel_segment(const VoxSeg& S, uint32_t* lds) {
 
   // ---- 1. count secondary matches, allocate scratch, gather (stable)
   uint32_t m1 = 0;
-  if (S.src1 && S.n1 > 0) {
+  const bool direct = S.src1 && !S.tag1;  // secondary source used whole, no gather
+  if (direct) {
+    m1 = (uint32_t)max(S.n1, 0);
+  } else if (S.src1 && S.n1 > 0) {
     uint32_t local = 0;
     for (int i = tid; i < S.n1; i += VX_THREADS) local += (S.tag1[i] == S.tag) ? 1u : 0u;
     uint32_t tot;
@@ -385,7 +538,8 @@ __device__ inline void voxel_segment(const VoxSeg& S, uint32_t* lds) {
   }
   const int n0 = S.n0;
   const uint32_t N = (uint32_t)n0 + m1;
-  const uint32_t req = S.append_only ? m1 : N;  // append: gathered points only
+  // scratch: gathered secondary points (m1, gather mode) and member lists (N, voxelize mode)
+  const uint32_t req = S.append_only ? (direct ? 0u : m1) : N;
   uint32_t* sbase = M.sbase;
   if (tid == 0) {
     uint32_t b = 0;
@@ -399,9 +553,9 @@ __device__ inline void voxel_segment(const VoxSeg& S, uint32_t* lds) {
   __syncthreads();
   const uint32_t sb = sbase[0];
   if (sb == 0xFFFFFFFFu) return;
-  float4* sec = S.scratch_pts + sb;  // gathered secondary points (m1)
+  float4* sec = direct ? const_cast<float4*>(S.src1) : S.scratch_pts + sb;  // secondary points (m1)
   int* members = S.scratch_idx + sb;  // member lists (N, voxelize mode)
-  if (m1 > 0) {
+  if (m1 > 0 && !direct) {
     uint32_t base = 0;
     for (int c = 0; c < S.n1; c += VX_THREADS) {
       int i = c + tid;
@@ -429,6 +583,7 @@ __device__ inline void voxel_segment(const VoxSeg& S, uint32_t* lds) {
     if (N == 0 && !S.append_only) {
       if (tid == 0) {
         if (S.res_cnt) *S.res_cnt = 0;
+        if (S.stable_out) *S.stable_out = 0;
         if (S.res_off) *S.res_off = 0;
       }
       return;
@@ -448,52 +603,14 @@ __device__ inline void voxel_segment(const VoxSeg& S, uint32_t* lds) {
     if (tid == 0) {
       if (S.res_off) *S.res_off = ob;
       if (S.res_cnt) *S.res_cnt = N;
+      if (S.stable_out) *S.stable_out = 0;
     }
     return;
   }
 
-  // ---- 2. bounding box (pcl::getMinMax3D)
-  float mnx = 3.402823466e38f, mny = 3.402823466e38f, mnz = 3.402823466e38f;
-  float mxx = -3.402823466e38f, mxy = -3.402823466e38f, mxz = -3.402823466e38f;
-  for (uint32_t i = tid; i < N; i += VX_THREADS) {
-    float4 p = P(i);
-    mnx = fminf(mnx, p.x); mny = fminf(mny, p.y); mnz = fminf(mnz, p.z);
-    mxx = fmaxf(mxx, p.x); mxy = fmaxf(mxy, p.y); mxz = fmaxf(mxz, p.z);
-  }
-  mnx = wave_min_f(mnx); mny = wave_min_f(mny); mnz = wave_min_f(mnz);
-  mxx = wave_max_f(mxx); mxy = wave_max_f(mxy); mxz = wave_max_f(mxz);
-  float (*sbb)[6] = M.bb;
-  if (lane == 0) {
-    sbb[wid][0] = mnx; sbb[wid][1] = mny; sbb[wid][2] = mnz;
-    sbb[wid][3] = mxx; sbb[wid][4] = mxy; sbb[wid][5] = mxz;
-  }
-  __syncthreads();
-  VxGeom& sg = M.g;
-  if (tid == 0) {
-    for (int w = 1; w < VX_WAVES; ++w) {
-      mnx = fminf(mnx, sbb[w][0]); mny = fminf(mny, sbb[w][1]); mnz = fminf(mnz, sbb[w][2]);
-      mxx = fmaxf(mxx, sbb[w][3]); mxy = fmaxf(mxy, sbb[w][4]); mxz = fmaxf(mxz, sbb[w][5]);
-    }
-    VxGeom g;
-    g.inv = 1.0f / S.leaf;
-    long long dx = (long long)((mxx - mnx) * g.inv) + 1;
-    long long dy = (long long)((mxy - mny) * g.inv) + 1;
-    long long dz = (long long)((mxz - mnz) * g.inv) + 1;
-    g.overflow = (dx * dy * dz > 2147483647LL) ? 1 : 0;
-    g.minbx = (int)floorf(mnx * g.inv);
-    int maxbx = (int)floorf(mxx * g.inv);
-    g.minby = (int)floorf(mny * g.inv);
-    int maxby = (int)floorf(mxy * g.inv);
-    g.minbz = (int)floorf(mnz * g.inv);
-    int divx = maxbx - g.minbx + 1, divy = maxby - g.minby + 1;
-    g.mul1 = divx;
-    g.mul2 = divx * divy;
-    int maxbz = (int)floorf(mxz * g.inv);
-    g.nvox = (unsigned long long)divx * (unsigned long long)divy * (unsigned long long)(maxbz - g.minbz + 1);
-    sg = g;
-  }
-  __syncthreads();
-  const VxGeom g = sg;
+  // ---- 2. bounding box + geometry
+  vx_geometry(P, N, S.leaf, M);
+  const VxGeom g = M.g;
   if (g.overflow) {  // PCL: "Leaf size is too small" -> output = input
     if (tid == 0) {
       uint32_t b = S.tail ? atomicAdd(S.tail, N) : 0;
@@ -510,16 +627,217 @@ __device__ inline void voxel_segment(const VoxSeg& S, uint32_t* lds) {
     if (tid == 0) {
       if (S.res_off) *S.res_off = ob;
       if (S.res_cnt) *S.res_cnt = N;
+      if (S.stable_out) *S.stable_out = 0;
     }
     return;
   }
 
   // ---- 3-6 in one LDS pass when the unique voxels fit, else in idx-range groups
   const VxSrc src{S.src0, n0, sec};
+  int moved = 0;
   uint32_t U = vx_group(S, g, src, N, members, 0u, 0xFFFFFFFFu, VX_ALLOC, VX_LDS_WORDS - 256, lds, ws,
-                        M);
+                        M, &moved);
   if (U != VX_OVERFLOW) return;
   vx_grouped(S, g, src, N, members, lds, ws, M);
+}
+
+// ---------------------------------------------------------------------------------------
+// VoxelGrid of C ++ A where C (src0, n0 points) is already a fixed point of the filter (at
+// most one point per voxel, in voxel order: a previous output whose centroids all stayed in
+// their voxels) and A (src1 used whole, n1 <= VX_MERGE_CAP) are new points.  Exactly the
+// full filter's result, without hashing C:
+//   voxels holding only a C point      -> that point, unchanged ((0 + c) / 1 == c)
+//   voxels holding C point c and A's   -> (0 + c + a1 + a2 ...) / n, A in input order
+//   voxels holding only A points       -> (0 + a1 + ...) / n, inserted in voxel order
+// A is sorted by (voxel, input index) in LDS; C is streamed twice.  Returns false, with
+// nothing written, when the grid overflows (the caller then runs the full filter).
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t VX_MERGE_CAP = 4096;
+
+__device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
+  const int tid = threadIdx.x;
+  uint32_t* ws = lds + VX_LDS_WORDS - 256;
+  VxMisc& M = *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192);
+  const float4* C = S.src0;
+  const float4* A = S.src1;
+  const uint32_t n0 = (uint32_t)S.n0, n1 = (uint32_t)S.n1;
+  auto P = [&](uint32_t i) -> float4 { return i < n0 ? C[i] : A[i - n0]; };
+  vx_geometry(P, n0 + n1, S.leaf, M);
+  const VxGeom g = M.g;
+  if (g.overflow) return false;
+  uint64_t* sk = reinterpret_cast<uint64_t*>(lds);           // words [0, 8192)
+  uint32_t* cstart = lds + 8192;                             // [8192, 12289)
+  int* chit = reinterpret_cast<int*>(lds + 12352);           // [12352, 16448)
+  uint32_t* nhcell = lds + 16448;                            // [16448, 20544)
+  uint32_t* cbelow = lds + 20544;                            // [20544, 25664)
+  uint32_t npad = 1;
+  while (npad < n1) npad <<= 1;
+  for (uint32_t i = tid; i < npad; i += VX_THREADS)
+    sk[i] = i < n1 ? ((uint64_t)vx_key(g, A[i]) << 32) | i : 0xFFFFFFFFFFFFFFFFull;
+  __syncthreads();
+  for (uint32_t k = 2; k <= npad; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = tid; i < npad; i += VX_THREADS) {
+        const uint32_t ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t a = sk[i], b = sk[ixj];
+          if ((a > b) == ((i & k) == 0)) {
+            sk[i] = b;
+            sk[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // runs of one voxel = the new voxels; their members are in input order
+  constexpr int PT = VX_MERGE_CAP / VX_THREADS;  // 4
+  uint32_t fl[PT + 1], cnt = 0;
+#pragma unroll
+  for (int e = 0; e < PT; ++e) {
+    const uint32_t t = tid * PT + e;
+    fl[e] = (t < n1 && (t == 0 || (sk[t] >> 32) != (sk[t - 1] >> 32))) ? 1u : 0u;
+    cnt += fl[e];
+  }
+  uint32_t D;
+  uint32_t pre = vx_block_scan(cnt, ws, &D);
+#pragma unroll
+  for (int e = 0; e < PT; ++e)
+    if (fl[e]) {
+      cstart[pre] = tid * PT + e;
+      chit[pre] = -1;
+      ++pre;
+    }
+  if (tid == 0) cstart[D] = n1;
+  __syncthreads();
+  auto ckey = [&](uint32_t d) { return (uint32_t)(sk[cstart[d]] >> 32); };
+  auto find = [&](uint32_t key) -> int {
+    uint32_t lo = 0, hi = D;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (ckey(mid) < key) lo = mid + 1; else hi = mid;
+    }
+    return (lo < D && ckey(lo) == key) ? (int)lo : -1;
+  };
+  // pass A: the C point (if any) of every new voxel
+  for (uint32_t k0 = tid; k0 < n0; k0 += VX_UNROLL * VX_THREADS) {
+    float4 c[VX_UNROLL];
+#pragma unroll
+    for (int u = 0; u < VX_UNROLL; ++u)
+      if (k0 + u * VX_THREADS < n0) c[u] = C[k0 + u * VX_THREADS];
+#pragma unroll
+    for (int u = 0; u < VX_UNROLL; ++u) {
+      if (k0 + u * VX_THREADS >= n0) continue;
+      const int d = find(vx_key(g, c[u]));
+      if (d >= 0) chit[d] = (int)(k0 + u * VX_THREADS);
+    }
+  }
+  __syncthreads();
+  // voxels with new points only, in voxel order
+  cnt = 0;
+#pragma unroll
+  for (int e = 0; e < PT; ++e) {
+    const uint32_t d = tid * PT + e;
+    fl[e] = (d < D && chit[d] < 0) ? 1u : 0u;
+    cnt += fl[e];
+  }
+  uint32_t Dn;
+  pre = vx_block_scan(cnt, ws, &Dn);
+#pragma unroll
+  for (int e = 0; e < PT; ++e)
+    if (fl[e]) nhcell[pre++] = tid * PT + e;
+  for (uint32_t r = tid; r <= Dn; r += VX_THREADS) cbelow[r] = 0;
+  if (tid == 0) {
+    M.moved = 0;
+    uint32_t b = S.tail ? atomicAdd(S.tail, n0 + Dn) : 0;
+    if (b + n0 + Dn > S.cap) {
+      atomicOr(S.err, VX_ERR_OUTPUT);
+      b = 0xFFFFFFFFu;
+    }
+    M.sbase[1] = b;
+  }
+  __syncthreads();
+  const uint32_t ob = M.sbase[1];
+  if (ob == 0xFFFFFFFFu) return true;
+  float4* out = S.out + ob;
+  bool moved = false;
+  // sum of voxel d's new points after the optional C point, in input order
+  auto centroid = [&](uint32_t d, float sx, float sy, float sz, float si, uint32_t n) -> float4 {
+    const uint32_t t0 = cstart[d], t1 = cstart[d + 1];
+    for (uint32_t t = t0; t < t1; t += 4) {
+      float4 p[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (t + u < t1) p[u] = A[(uint32_t)sk[t + u]];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (t + u < t1) {
+          sx += p[u].x; sy += p[u].y; sz += p[u].z; si += p[u].w;
+        }
+    }
+    n += t1 - t0;
+    const float fn = (float)n;
+    return make_float4(sx / fn, sy / fn, sz / fn, si / fn);
+  };
+  // pass B: C points at k + (new-only voxels before them); merged voxels re-averaged
+  for (uint32_t k0 = tid; k0 < n0; k0 += VX_UNROLL * VX_THREADS) {
+    float4 c[VX_UNROLL];
+#pragma unroll
+    for (int u = 0; u < VX_UNROLL; ++u)
+      if (k0 + u * VX_THREADS < n0) c[u] = C[k0 + u * VX_THREADS];
+#pragma unroll
+    for (int u = 0; u < VX_UNROLL; ++u) {
+      const uint32_t k = k0 + u * VX_THREADS;
+      if (k >= n0) continue;
+      const uint32_t key = vx_key(g, c[u]);
+      uint32_t lo = 0, hi = Dn;  // new-only voxels below key
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (ckey(nhcell[mid]) < key) lo = mid + 1; else hi = mid;
+      }
+      atomicAdd(&cbelow[lo], 1u);
+      float4 v = c[u];
+      const int d = find(key);
+      if (d >= 0) {
+        v = centroid((uint32_t)d, 0.f + c[u].x, 0.f + c[u].y, 0.f + c[u].z, 0.f + c[u].w, 1u);
+        moved |= vx_key(g, v) != key;
+      }
+      out[k + lo] = v;
+    }
+  }
+  __syncthreads();
+  // C points below new-only voxel r: inclusive prefix of cbelow (Dn + 1 <= 4097 entries)
+  constexpr int PB = 5;
+  uint32_t cv[PB], csum = 0;
+#pragma unroll
+  for (int e = 0; e < PB; ++e) {
+    const uint32_t r = tid * PB + e;
+    cv[e] = r <= Dn ? cbelow[r] : 0u;
+    csum += cv[e];
+  }
+  uint32_t ctot;
+  uint32_t cpre = vx_block_scan(csum, ws, &ctot);
+#pragma unroll
+  for (int e = 0; e < PB; ++e) {
+    const uint32_t r = tid * PB + e;
+    cpre += cv[e];
+    if (r <= Dn) cbelow[r] = cpre;
+  }
+  __syncthreads();
+  for (uint32_t r = tid; r < Dn; r += VX_THREADS) {
+    const uint32_t d = nhcell[r];
+    const float4 v = centroid(d, 0.f, 0.f, 0.f, 0.f, 0u);
+    out[r + cbelow[r]] = v;
+    moved |= vx_key(g, v) != ckey(d);
+  }
+  if (moved) M.moved = 1;
+  __syncthreads();
+  if (tid == 0) {
+    if (S.res_off) *S.res_off = ob;
+    if (S.res_cnt) *S.res_cnt = n0 + Dn;
+    if (S.stable_out) *S.stable_out = M.moved ? 0u : ob + 1;
+  }
+  return true;
 }
 
 }  // namespace loam

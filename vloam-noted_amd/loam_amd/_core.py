@@ -90,6 +90,8 @@ SIGNATURES = {
     "loam_lm_solve": (c_i32, [c_i32, vp, c_i32, vp, c_i32, ctypes.POINTER(LMStats)]),
     "loam_lm_normal_equations": (c_i32, [c_i32, vp, c_i32, vp, vp, vp, vp]),
     "loam_voxel_grid": (c_i32, [c_i32, vp, c_i32, c_f, vp, ctypes.POINTER(c_i32)]),
+    "loam_voxel_merge": (c_i32, [c_i32, vp, c_i32, vp, c_i32, c_f, vp, ctypes.POINTER(c_i32),
+                                 ctypes.POINTER(c_i32)]),
     "loam_knn_radius": (c_i32, [c_i32, vp, c_i32, vp, c_i32, c_i32, c_f, vp, vp]),
 }
 

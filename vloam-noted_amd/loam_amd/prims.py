@@ -23,6 +23,16 @@ def voxel_grid(pts, leaf, device=0):
     return out[: n.value].copy()
 
 
+def voxel_merge(fixed, added, leaf, device=0):
+    """VoxelGrid of fixed ++ added, `fixed` being a VoxelGrid fixed point; returns (out, merged)"""
+    c, a = f32x4(fixed), f32x4(added)
+    out = np.empty((len(c) + len(a), 4), dtype=np.float32)
+    n, m = _core.c_i32(), _core.c_i32()
+    check(lib().loam_voxel_merge(device, ptr(c), len(c), ptr(a), len(a), float(leaf), ptr(out),
+                                 ctypes.byref(n), ctypes.byref(m)))
+    return out[: n.value].copy(), bool(m.value)
+
+
 def knn_radius(pts, queries, k=5, radius2=1.0, device=0):
     pts, q = f32x4(pts), f32x4(queries)
     idx = np.empty((len(q), k), dtype=np.int32)
