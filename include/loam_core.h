@@ -104,6 +104,45 @@ int32_t loam_scanreg_curvature(loam_scanreg* h, float* curv, int32_t* label, int
 double loam_scanreg_ms(loam_scanreg* h);
 
 /* --------------------------------------------------------------------------------------
+ * LaserOdometry (laser_odometry.h:70-84) — scan-to-scan odometry, n_streams independent
+ * instances per handle.  One solve = laserOdometryIO's input + solveLO (laser_odometry.cpp:
+ * 137-584) for every stream that received an input.
+ * ------------------------------------------------------------------------------------ */
+typedef struct loam_odometry loam_odometry;
+
+typedef struct loam_odom_stats {
+  int32_t corner_num[2], surf_num[2];  /* corner / plane correspondences per round */
+  loam_lm_stats lm[2];
+  int32_t n_corner_last, n_surf_last;  /* laserCloudCornerLast / SurfLast sizes after the swap */
+  double ms;                           /* device time of the whole call (all streams) */
+} loam_odom_stats;
+
+/* LaserOdometry::init (laser_odometry.cpp:46-126); mapping_skip_frame from params */
+int32_t loam_odometry_create(const loam_params* p, int32_t device, int32_t n_streams, loam_odometry** out);
+int32_t loam_odometry_destroy(loam_odometry* h);
+int32_t loam_odometry_reset(loam_odometry* h);
+/* LaserOdometry::input (laser_odometry.cpp:137-150): cornerPointsSharp, cornerPointsLessSharp,
+ * surfPointsFlat, surfPointsLessFlat (4 floats / point, host memory, copied) */
+int32_t loam_odometry_input(loam_odometry* h, int32_t stream, const float* sharp, int32_t n_sharp,
+                            const float* less_sharp, int32_t n_less_sharp, const float* flat, int32_t n_flat,
+                            const float* less_flat, int32_t n_less_flat);
+/* same, device pointers read in place during the next solve (e.g. loam_scanreg_device_ptr) */
+int32_t loam_odometry_input_device(loam_odometry* h, int32_t stream, const float* sharp, int32_t n_sharp,
+                                   const float* less_sharp, int32_t n_less_sharp, const float* flat,
+                                   int32_t n_flat, const float* less_flat, int32_t n_less_flat);
+/* LaserOdometry::solveLO (laser_odometry.cpp:199-584) */
+int32_t loam_odometry_solve(loam_odometry* h);
+/* LaserOdometry::output (laser_odometry.cpp:660-679): q_w_curr, t_w_curr, q_last_curr,
+ * t_last_curr (each may be NULL), skip_frame = frameCount % mapping_skip_frame != 0 */
+int32_t loam_odometry_output(loam_odometry* h, int32_t stream, double* q_w, double* t_w, double* q_lc,
+                             double* t_lc, int32_t* skip_frame);
+/* laserCloudCornerLast (which 0) / laserCloudSurfLast (1): device pointer valid until the
+ * next solve (feeds loam_mapper_input_device); returns the count */
+int32_t loam_odometry_last_cloud(loam_odometry* h, int32_t stream, int32_t which, const float** d_ptr);
+int32_t loam_odometry_copy_last(loam_odometry* h, int32_t stream, int32_t which, float* out, int32_t cap);
+int32_t loam_odometry_stats(loam_odometry* h, int32_t stream, loam_odom_stats* st);
+
+/* --------------------------------------------------------------------------------------
  * LaserMapping (laser_mapping.h:85-100) — a handle holds n_streams independent mappers
  * (independent sequences / vehicles) processed together by every launch.  n_streams = 1 is
  * exactly the reference's single LaserMapping object.

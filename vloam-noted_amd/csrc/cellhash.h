@@ -74,6 +74,48 @@ __device__ inline bool hash_claim_rank(unsigned long long* hk, unsigned long lon
   return true;
 }
 
+// claim (or find) the slot of `key` and add `count` points to the cell; *base_out = the
+// cell's count before the addition (the rank of this batch's first point), *fresh_out =
+// whether this call started the cell in this epoch.  False if the table is full.
+__device__ inline bool hash_claim_cell(unsigned long long* hk, unsigned long long* hc, uint32_t mask,
+                                       uint32_t epoch, uint32_t key, uint32_t count, uint32_t* slot_out,
+                                       uint32_t* base_out, bool* fresh_out) {
+  const unsigned long long ep = (unsigned long long)epoch << 32;
+  const unsigned long long want = ep | key;
+  uint32_t h = cell_hash(key, mask);
+  uint32_t slot = 0xFFFFFFFFu;
+  for (uint32_t probe = 0; probe <= mask; ++probe) {
+    unsigned long long cur = __hip_atomic_load(&hk[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == want) {
+      slot = h;
+      break;
+    }
+    if ((cur >> 32) != epoch) {
+      unsigned long long prev = atomicCAS(&hk[h], cur, want);
+      if (prev == cur || prev == want) {
+        slot = h;
+        break;
+      }
+    }
+    h = (h + 1) & mask;
+  }
+  if (slot == 0xFFFFFFFFu) return false;
+  unsigned long long c = __hip_atomic_load(&hc[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  while (true) {
+    const bool fresh = (c >> 32) != epoch;
+    const unsigned long long nc = fresh ? (ep | count) : c + count;
+    const unsigned long long prev = atomicCAS(&hc[slot], c, nc);
+    if (prev == c) {
+      *base_out = fresh ? 0u : (uint32_t)(c & 0xFFFFFFFFu);
+      *fresh_out = fresh;
+      break;
+    }
+    c = prev;
+  }
+  *slot_out = slot;
+  return true;
+}
+
 // Cell start allocation with one atomic per wave, and the packed query entry
 // {key, epoch, start, count} (one 16-byte load per probe on the query side).  Called by
 // whole waves: lanes with first = false (not the cell's rank-0 point, or past the end)

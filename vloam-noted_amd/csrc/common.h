@@ -24,6 +24,12 @@ void set_error(const std::string& msg);
 // one-time check that a gfx950 device is present and usable
 int32_t ensure_device(int32_t device);
 
+#define TRY(x)                      \
+  do {                              \
+    int32_t rc_ = (x);              \
+    if (rc_ != LOAM_OK) return rc_; \
+  } while (0)
+
 // Wave-wide inclusive scan / reductions on 64-lane waves
 __device__ inline int wave_lane() { return threadIdx.x & 63; }
 

@@ -457,4 +457,157 @@ __device__ inline bool lm_step_wave(const double* partials, int nblk, LmState& S
   return done;
 }
 
+// ---------------------------------------------------------------------------------------
+// Persistent LM round: all <= 5 passes of one solve in one launch.  G workgroups evaluate a
+// share of the records each; the leader (g = 0) keeps the trust-region state in its LDS,
+// reduces the workers' partials and runs the step.  Hand-offs follow the agent-scope
+// release/acquire recipe (cdna_hip_programming.md §6 Guideline 16): partials are plain
+// stores + drain + release fence + relaxed ticket; the eval point is published with sc1
+// (atomic) stores + drain + a relaxed flag; consumers poll relaxed and acquire once.  The
+// caller sizes the grid so every workgroup is resident; every spin is bounded (err_code).
+// ---------------------------------------------------------------------------------------
+#define RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+
+constexpr int LM_MAX_PASSES = 8;          // a round needs <= 1 + max_num_iterations = 5
+constexpr uint32_t LM_SPIN_LIMIT = 1u << 21;
+
+__device__ inline bool lm_spin_ge(uint32_t* w, uint32_t target) {
+  for (uint32_t spins = 0;; ++spins) {
+    if (__hip_atomic_load(w, RLX_AGENT) >= target) return true;
+    if (spins >= LM_SPIN_LIMIT) return false;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// one LM solve (one outer round of one stream) spread over G workgroups
+struct LmJob {
+  LmState* S;         // state, initialised by lm_init in an earlier launch
+  LmRecView R;        // factor records
+  int nrec;
+  double* part;       // [G][LM_NACC] worker partials
+  uint32_t* sync;     // [4] zeroed in an earlier launch: arrivals, generation, status
+  double* xpub;       // [8] published evaluation point
+  double* best_out;   // [7] pose written when the solve terminates
+  int* err;
+  int err_code;
+};
+
+template <int kThreads>
+__device__ inline void lm_round_device(const LmJob& J, int g, int G) {
+  __shared__ LmState ls;
+  __shared__ double sx[7];
+  __shared__ double bsum[LM_NACC];
+  __shared__ double sred[LM_NACC];
+  __shared__ int sstat;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  LmState& S = *J.S;
+  const LmRecView& R = J.R;
+  const int nrec = J.nrec;
+  uint32_t* sync = J.sync;
+  double* xpub = J.xpub;
+  double* part = J.part;
+  if (g == 0) {  // state written by an earlier launch: plain loads
+    constexpr int NW = sizeof(LmState) / 8;
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&S);
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(&ls);
+    for (int w = tid; w < NW; w += kThreads) dst[w] = src[w];
+  }
+  __syncthreads();
+  bool aborted = false;
+  for (int pass = 0; pass < LM_MAX_PASSES; ++pass) {
+    // ---- evaluation point of this pass
+    if (g == 0) {
+      if (tid == 0) {
+        sstat = ls.status;
+        for (int i = 0; i < 7; ++i) sx[i] = ls.status == LM_EVAL_X ? ls.x[i] : ls.cand[i];
+      }
+      __syncthreads();
+      if (G > 1 && wid == 0) {  // publish: sc1 stores, drain, relaxed flag
+        if (lane < 7) __hip_atomic_store(&xpub[lane], sx[lane], RLX_AGENT);
+        if (lane == 7) __hip_atomic_store(&sync[2], (uint32_t)sstat, RLX_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(&sync[1], (uint32_t)(pass + 1), RLX_AGENT);
+      }
+    } else {
+      if (tid == 0) {
+        if (lm_spin_ge(&sync[1], (uint32_t)(pass + 1))) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          sstat = (int)__hip_atomic_load(&sync[2], RLX_AGENT);
+          for (int i = 0; i < 7; ++i) sx[i] = __hip_atomic_load(&xpub[i], RLX_AGENT);
+        } else {
+          atomicOr(J.err, J.err_code);
+          sstat = LM_DONE;
+        }
+      }
+      __syncthreads();
+    }
+    if (sstat == LM_DONE) break;
+    double X[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) X[i] = sx[i];
+    // ---- evaluation of this workgroup's share
+    lm_eval_sum<kThreads>(R, nrec, X, g, G, bsum);
+    if (g != 0) {  // publish the partial: plain stores, drain, release, relaxed ticket
+      if (tid < LM_NACC) part[(size_t)g * LM_NACC + tid] = bsum[tid];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(&sync[0], 1u, RLX_AGENT);
+      }
+      continue;
+    }
+    // ---- leader: gather the partials, step
+    if (tid == 0 && G > 1) {
+      if (lm_spin_ge(&sync[0], (uint32_t)(pass + 1) * (uint32_t)(G - 1))) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        atomicOr(J.err, J.err_code);
+        sstat = -1;
+      }
+    }
+    __syncthreads();
+    if (sstat == -1) {
+      aborted = true;
+      break;
+    }
+    if (wid == 0) {
+      double v[LM_NACC];
+#pragma unroll
+      for (int i = 0; i < LM_NACC; ++i) v[i] = lane == 0 ? bsum[i] : 0.0;
+      for (int c = lane; c < G; c += 64) {
+        if (c == 0) continue;
+#pragma unroll
+        for (int i = 0; i < LM_NACC; ++i) v[i] += part[(size_t)c * LM_NACC + i];
+      }
+#pragma unroll
+      for (int i = 0; i < LM_NACC; ++i) {
+        const double t = wave_sum_d(v[i]);
+        if (lane == 0) sred[i] = t;
+      }
+      if (lane == 0) {
+        LmState L = ls;  // registers for the dependent chain
+        lm_step(L, sred);
+        ls = L;
+      }
+    }
+    __syncthreads();
+  }
+  if (g != 0) return;
+  if (aborted && tid == 0) {  // stop this stream's LM where it is (best so far)
+    ls.term = 6;
+    ls.status = LM_DONE;
+  }
+  __syncthreads();
+  if (ls.status == LM_DONE && tid < 7 && J.best_out) J.best_out[tid] = ls.best[tid];
+  constexpr int NW = sizeof(LmState) / 8;
+  const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&ls);
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(&S);
+  for (int w = tid; w < NW; w += kThreads) dst[w] = src[w];
+}
+
+
 }  // namespace loam

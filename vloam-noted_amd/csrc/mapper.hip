@@ -41,8 +41,6 @@ constexpr int LM_THREADS = 256;
 constexpr int LM_EBLK = 32;     // LM evaluation workgroups per stream (grid-stride)
 constexpr int SUBMAP_BLOCKS = 64;
 constexpr int INS_SLOTS = WIN_VALID_MAX + EXTRA_CAP;
-constexpr int LM_MAX_PASSES = 8;          // a round needs <= 1 + max_num_iterations = 5
-constexpr uint32_t LM_SPIN_LIMIT = 1u << 21;
 constexpr int MAP_ERR_SUBMAP = 4, MAP_ERR_EXTRA = 8, MAP_ERR_HASH = 16, MAP_ERR_LM_SYNC = 32;
 
 struct StreamFrame {
@@ -65,6 +63,7 @@ struct StreamFrame {
   uint32_t scratch_tail[2];
   uint32_t cursor[2];
   uint32_t hmask[2];              // this frame's cell-hash size - 1 (>= 2x the submap points)
+  uint32_t ncells[2];             // cells claimed this frame (cell list length)
   int extra_n[2];
   int extra_list[2][EXTRA_CAP];
   int err;
@@ -88,6 +87,7 @@ struct MapperDev {
   unsigned long long* hcnt;
   uint32_t* hstart;
   uint4* qtab;      // [B][2][T] packed query entries {key, epoch, start, count}
+  uint32_t* cells;  // [B][2][T] slots claimed this frame (alloc iterates cells, not points)
   int* knn_id;      // [5][B][2*max_in] neighbour ids (submap index) per query, -1: none
   size_t knn_stride;
   float4* sub_lin;  // [B][2][sub_cap] window-order submap
@@ -198,6 +198,7 @@ __global__ void __launch_bounds__(128) k_submap_prep(MapperDev D) {
     F.sub_n[m] = total;
     F.scratch_tail[m] = 0;
     F.cursor[m] = 0;
+    F.ncells[m] = 0;
     F.extra_n[m] = 0;
     uint32_t T = 1024;
     while (T < 2 * total && T < (uint32_t)D.hash_T) T <<= 1;
@@ -208,59 +209,140 @@ __global__ void __launch_bounds__(128) k_submap_prep(MapperDev D) {
   if (threadIdx.x == 0) F.optimize = (F.sub_n[0] > 10 && F.sub_n[1] > 50) ? 1 : 0;
 }
 
-// gather the window cubes into sub_lin and claim the cell slots; rank within the cell
-__global__ void k_submap_insert(MapperDev D) {
-  const int sm = blockIdx.y;
+// Submap hash build, one workgroup per (stream, map, window cube): the cube's points are
+// copied to sub_lin (window order = laserCloudCornerFromMap order, laser_mapping.cpp:
+// 448-489) and grouped by 1 m cell in an LDS hash; each distinct cell is then claimed in the
+// global table once, adding its whole count (the rank base of this cube's points in it).
+// Points whose cell does not fit the LDS table take the per-point global path.
+constexpr int SUB_THREADS = 512;
+constexpr int SUB_LHASH = 8192;
+constexpr uint32_t SUB_OVERFLOW = 0xFFFFFFFEu, SUB_FAILED = 0xFFFFFFFFu;
+
+__device__ inline void append_cells_wave(bool fresh, uint32_t slot, uint32_t* cells, uint32_t* ncells) {
+  const uint64_t b = __ballot(fresh);
+  if (!b) return;
+  const int lane = threadIdx.x & 63;
+  uint32_t base = 0;
+  if (lane == 0) base = atomicAdd(ncells, (uint32_t)__popcll(b));
+  base = __shfl(base, 0, 64);
+  if (fresh) cells[base + __popcll(b & lanemask_lt())] = slot;
+}
+
+__global__ void __launch_bounds__(SUB_THREADS) k_submap_insert(MapperDev D) {
+  __shared__ uint32_t lkey[SUB_LHASH];
+  __shared__ uint32_t lcnt[SUB_LHASH];
+  const int w = blockIdx.x % WIN_VALID_MAX, sm = blockIdx.x / WIN_VALID_MAX;
   const int s = sm >> 1, m = sm & 1;
-  const StreamFrame& F = D.fr[s];
-  if (!F.active) return;
-  const uint32_t n = F.sub_n[m];
-  const uint2* tab = D.cube_tab + sm_index(s, m) * NCUBE;
-  const float4* ar = arena_base(D, s, m, F.arena_active[m]);
-  float4* lin = D.sub_lin + sm_index(s, m) * D.sub_cap;
+  StreamFrame& F = D.fr[s];
+  if (!F.active || w >= F.valid_num) return;
+  const uint32_t base = (uint32_t)F.sub_off[m][w];
+  const uint32_t n = (uint32_t)F.sub_off[m][w + 1] - base;
+  if (n == 0 || F.sub_n[m] == 0) return;
+  const int tid = threadIdx.x;
+  const uint2 cv = D.cube_tab[sm_index(s, m) * NCUBE + F.window[w]];
+  const float4* src = arena_base(D, s, m, F.arena_active[m]) + cv.x;
+  float4* lin = D.sub_lin + sm_index(s, m) * D.sub_cap + base;
   unsigned long long* hk = D.hkey + sm_index(s, m) * D.hash_T;
   unsigned long long* hc = D.hcnt + sm_index(s, m) * D.hash_T;
-  uint32_t* ps = D.pt_slot + sm_index(s, m) * D.sub_cap;
-  uint32_t* pr = D.pt_rank + sm_index(s, m) * D.sub_cap;
+  uint32_t* ps = D.pt_slot + sm_index(s, m) * D.sub_cap + base;
+  uint32_t* pr = D.pt_rank + sm_index(s, m) * D.sub_cap + base;
+  uint32_t* cells = D.cells + sm_index(s, m) * D.hash_T;
   const uint32_t mask = F.hmask[m];
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    int lo = 0, hi = F.valid_num;  // window slot: largest w with sub_off[w] <= i
-    while (hi - lo > 1) {
-      int mid = (lo + hi) >> 1;
-      if ((uint32_t)F.sub_off[m][mid] <= i) lo = mid; else hi = mid;
-    }
-    const uint2 cv = tab[F.window[lo]];
-    const float4 p = ar[cv.x + (i - F.sub_off[m][lo])];
+  for (int i = tid; i < SUB_LHASH; i += SUB_THREADS) {
+    lkey[i] = VX_EMPTY;
+    lcnt[i] = 0;
+  }
+  __syncthreads();
+  // 1. copy + group by cell in LDS
+  for (uint32_t i = tid; i < n; i += SUB_THREADS) {
+    const float4 p = src[i];
     lin[i] = p;
-    uint32_t slot, rank;
-    if (!hash_claim_rank(hk, hc, mask, D.epoch, cell_key_rel(p.x, p.y, p.z, F.origin), &slot, &rank)) {
-      atomicOr(&D.fr[s].err, MAP_ERR_HASH);
-      ps[i] = 0;
-      pr[i] = 0xFFFFFFFFu;
-      continue;
+    const uint32_t key = cell_key_rel(p.x, p.y, p.z, F.origin);
+    uint32_t h = cell_hash(key, SUB_LHASH - 1);
+    bool ok = false;
+    for (int probe = 0; probe < 64; ++probe) {
+      const uint32_t old = atomicCAS(&lkey[h], VX_EMPTY, key);
+      if (old == VX_EMPTY || old == key) {
+        ok = true;
+        break;
+      }
+      h = (h + 1) & (SUB_LHASH - 1);
     }
-    ps[i] = slot;
-    pr[i] = rank;
+    if (ok) {
+      ps[i] = h;
+      pr[i] = atomicAdd(&lcnt[h], 1u);
+    } else {
+      ps[i] = key;
+      pr[i] = SUB_OVERFLOW;
+    }
+  }
+  __syncthreads();
+  // 2. one global claim per distinct cell; LDS entry becomes (global slot, rank base)
+  for (int s0 = 0; s0 < SUB_LHASH; s0 += SUB_THREADS) {
+    const int sl = s0 + tid;
+    const uint32_t key = lkey[sl];
+    bool fresh = false;
+    uint32_t g = 0;
+    if (key != VX_EMPTY) {
+      uint32_t b0 = 0;
+      if (hash_claim_cell(hk, hc, mask, D.epoch, key, lcnt[sl], &g, &b0, &fresh)) {
+        lkey[sl] = g;
+        lcnt[sl] = b0;
+      } else {
+        atomicOr(&F.err, MAP_ERR_HASH);
+        lkey[sl] = SUB_FAILED;
+      }
+    }
+    append_cells_wave(fresh, g, cells, &F.ncells[m]);
+  }
+  __syncthreads();
+  // 3. global slot and rank of every point (overflow points: per-point claim)
+  for (uint32_t b0 = 0; b0 < n; b0 += SUB_THREADS) {
+    const uint32_t i = b0 + tid;
+    bool fresh = false;
+    uint32_t g = 0;
+    if (i < n) {
+      const uint32_t r = pr[i], v = ps[i];
+      if (r == SUB_OVERFLOW) {
+        uint32_t b1 = 0;
+        if (hash_claim_cell(hk, hc, mask, D.epoch, v, 1u, &g, &b1, &fresh)) {
+          ps[i] = g;
+          pr[i] = b1;
+        } else {
+          atomicOr(&F.err, MAP_ERR_HASH);
+          pr[i] = SUB_FAILED;
+          fresh = false;
+        }
+      } else {
+        const uint32_t gs = lkey[v];
+        if (gs == SUB_FAILED) {
+          pr[i] = SUB_FAILED;
+        } else {
+          ps[i] = gs;
+          pr[i] = lcnt[v] + r;
+        }
+      }
+    }
+    append_cells_wave(fresh, g, cells, &F.ncells[m]);
   }
 }
 
+// cell starts: one pass over the cells claimed this frame (wave-aggregated cursor)
 __global__ void k_submap_alloc(MapperDev D) {
   const int sm = blockIdx.y;
   const int s = sm >> 1, m = sm & 1;
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
-  const uint32_t n = F.sub_n[m];
+  const uint32_t nc = F.ncells[m];
   const unsigned long long* hk = D.hkey + sm_index(s, m) * D.hash_T;
   const unsigned long long* hc = D.hcnt + sm_index(s, m) * D.hash_T;
   uint32_t* hs = D.hstart + sm_index(s, m) * D.hash_T;
   uint4* qt = D.qtab + sm_index(s, m) * D.hash_T;
-  const uint32_t* ps = D.pt_slot + sm_index(s, m) * D.sub_cap;
-  const uint32_t* pr = D.pt_rank + sm_index(s, m) * D.sub_cap;
-  // block-uniform trip count: hash_alloc_cell needs whole waves
-  for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < n; b0 += gridDim.x * blockDim.x) {
+  const uint32_t* cells = D.cells + sm_index(s, m) * D.hash_T;
+  for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < nc; b0 += gridDim.x * blockDim.x) {  // whole waves
     const uint32_t i = b0 + threadIdx.x;
-    const bool first = i < n && pr[i] == 0;
-    hash_alloc_cell(first, first ? ps[i] : 0u, hk, hc, D.epoch, hs, qt, &F.cursor[m]);
+    const bool valid = i < nc;
+    hash_alloc_cell(valid, valid ? cells[i] : 0u, hk, hc, D.epoch, hs, qt, &F.cursor[m]);
   }
 }
 
@@ -421,135 +503,23 @@ __global__ void __launch_bounds__(64) k_lm_step(MapperDev D, int round) {
 // The grid is sized on the host so that every workgroup is resident, and every spin is
 // bounded (MAP_ERR_LM_SYNC, the stream's LM then stops).
 // ---------------------------------------------------------------------------------------
-#define RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
-
-__device__ inline bool lm_spin_ge(uint32_t* w, uint32_t target) {
-  for (uint32_t spins = 0;; ++spins) {
-    if (__hip_atomic_load(w, RLX_AGENT) >= target) return true;
-    if (spins >= LM_SPIN_LIMIT) return false;
-    __builtin_amdgcn_s_sleep(2);
-  }
-}
-
 __global__ void __launch_bounds__(LM_THREADS) k_lm_round(MapperDev D, int round, int G) {
-  __shared__ LmState ls;
-  __shared__ double sx[7];
-  __shared__ double bsum[LM_NACC];
-  __shared__ double sred[LM_NACC];
-  __shared__ int sstat;
   const int s = blockIdx.x / G, g = blockIdx.x % G;
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  LmState& S = F.lm[round];
-  const int nrec = F.nc_stack + F.ns_stack;
   const size_t rb = (size_t)s * 2 * D.max_in;
-  const LmRecView R{D.r_type + rb, D.r_px + rb, D.r_py + rb, D.r_pz + rb, D.r_a[0] + rb, D.r_a[1] + rb,
-                    D.r_a[2] + rb, D.r_b[0] + rb, D.r_b[1] + rb, D.r_b[2] + rb};
-  uint32_t* sync = D.lm_sync + ((size_t)s * 2 + round) * 4;  // [0] arrivals, [1] generation
-  double* xpub = D.lm_xpub + ((size_t)s * 2 + round) * 8;
-  double* part = D.partials + (size_t)s * D.max_chunks * LM_NACC;
-  if (g == 0) {  // state written by k_knn (earlier launch): plain loads
-    constexpr int NW = sizeof(LmState) / 8;
-    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&S);
-    unsigned long long* dst = reinterpret_cast<unsigned long long*>(&ls);
-    for (int w = tid; w < NW; w += LM_THREADS) dst[w] = src[w];
-  }
-  __syncthreads();
-  bool aborted = false;
-  for (int pass = 0; pass < LM_MAX_PASSES; ++pass) {
-    // ---- evaluation point of this pass
-    if (g == 0) {
-      if (tid == 0) {
-        sstat = ls.status;
-        for (int i = 0; i < 7; ++i) sx[i] = ls.status == LM_EVAL_X ? ls.x[i] : ls.cand[i];
-      }
-      __syncthreads();
-      if (G > 1 && wid == 0) {  // publish: sc1 stores, drain, relaxed flag
-        if (lane < 7) __hip_atomic_store(&xpub[lane], sx[lane], RLX_AGENT);
-        if (lane == 7) __hip_atomic_store(&sync[2], (uint32_t)sstat, RLX_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_store(&sync[1], (uint32_t)(pass + 1), RLX_AGENT);
-      }
-    } else {
-      if (tid == 0) {
-        if (lm_spin_ge(&sync[1], (uint32_t)(pass + 1))) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          sstat = (int)__hip_atomic_load(&sync[2], RLX_AGENT);
-          for (int i = 0; i < 7; ++i) sx[i] = __hip_atomic_load(&xpub[i], RLX_AGENT);
-        } else {
-          atomicOr(&F.err, MAP_ERR_LM_SYNC);
-          sstat = LM_DONE;
-        }
-      }
-      __syncthreads();
-    }
-    if (sstat == LM_DONE) break;
-    double X[7];
-#pragma unroll
-    for (int i = 0; i < 7; ++i) X[i] = sx[i];
-    // ---- evaluation of this workgroup's share
-    lm_eval_sum<LM_THREADS>(R, nrec, X, g, G, bsum);
-    if (g != 0) {  // publish the partial: plain stores, drain, release, relaxed ticket
-      if (tid < LM_NACC) part[(size_t)g * LM_NACC + tid] = bsum[tid];
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(&sync[0], 1u, RLX_AGENT);
-      }
-      continue;
-    }
-    // ---- leader: gather the partials, step
-    if (tid == 0 && G > 1) {
-      if (lm_spin_ge(&sync[0], (uint32_t)(pass + 1) * (uint32_t)(G - 1))) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else {
-        atomicOr(&F.err, MAP_ERR_LM_SYNC);
-        sstat = -1;
-      }
-    }
-    __syncthreads();
-    if (sstat == -1) {
-      aborted = true;
-      break;
-    }
-    if (wid == 0) {
-      double v[LM_NACC];
-#pragma unroll
-      for (int i = 0; i < LM_NACC; ++i) v[i] = lane == 0 ? bsum[i] : 0.0;
-      for (int c = lane; c < G; c += 64) {
-        if (c == 0) continue;
-#pragma unroll
-        for (int i = 0; i < LM_NACC; ++i) v[i] += part[(size_t)c * LM_NACC + i];
-      }
-#pragma unroll
-      for (int i = 0; i < LM_NACC; ++i) {
-        const double t = wave_sum_d(v[i]);
-        if (lane == 0) sred[i] = t;
-      }
-      if (lane == 0) {
-        LmState L = ls;  // registers for the dependent chain
-        lm_step(L, sred);
-        ls = L;
-      }
-    }
-    __syncthreads();
-  }
-  if (g != 0) return;
-  if (aborted && tid == 0) {  // stop this stream's LM where it is (best so far)
-    ls.term = 6;
-    ls.status = LM_DONE;
-  }
-  __syncthreads();
-  if (ls.status == LM_DONE && tid < 7) F.pose[tid] = ls.best[tid];
-  constexpr int NW = sizeof(LmState) / 8;
-  const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&ls);
-  unsigned long long* dst = reinterpret_cast<unsigned long long*>(&S);
-  for (int w = tid; w < NW; w += LM_THREADS) dst[w] = src[w];
+  LmJob J;
+  J.S = &F.lm[round];
+  J.R = LmRecView{D.r_type + rb, D.r_px + rb, D.r_py + rb, D.r_pz + rb, D.r_a[0] + rb, D.r_a[1] + rb,
+                  D.r_a[2] + rb, D.r_b[0] + rb, D.r_b[1] + rb, D.r_b[2] + rb};
+  J.nrec = F.nc_stack + F.ns_stack;
+  J.part = D.partials + (size_t)s * D.max_chunks * LM_NACC;
+  J.sync = D.lm_sync + ((size_t)s * 2 + round) * 4;
+  J.xpub = D.lm_xpub + ((size_t)s * 2 + round) * 8;
+  J.best_out = F.pose;
+  J.err = &F.err;
+  J.err_code = MAP_ERR_LM_SYNC;
+  lm_round_device<LM_THREADS>(J, g, G);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -848,12 +818,6 @@ int32_t dalloc(loam_mapper* h, T** p, size_t count) {
   return LOAM_OK;
 }
 
-#define TRY(x)                   \
-  do {                           \
-    int32_t rc_ = (x);           \
-    if (rc_ != LOAM_OK) return rc_; \
-  } while (0)
-
 uint32_t next_pow2(uint32_t v) {
   uint32_t p = 1;
   while (p < v) p <<= 1;
@@ -976,6 +940,7 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
   ALLOC(D.hcnt, B * 2 * (size_t)D.hash_T);
   ALLOC(D.hstart, B * 2 * (size_t)D.hash_T);
   ALLOC(D.qtab, B * 2 * (size_t)D.hash_T);
+  ALLOC(D.cells, B * 2 * (size_t)D.hash_T);
   D.knn_stride = B * 2 * (size_t)D.max_in;
   ALLOC(D.knn_id, 5 * D.knn_stride);
   ALLOC(D.sub_lin, B * 2 * (size_t)D.sub_cap);
@@ -1215,7 +1180,7 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   }
   LAUNCH(FAM_OTHER, k_submap_prep<<<B, 128, 0, st>>>(D));
   LOAM_HIP(hipEventRecord(h->ev[1], st));
-  LAUNCH(FAM_HASH, k_submap_insert<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D));
+  LAUNCH(FAM_HASH, k_submap_insert<<<B * 2 * WIN_VALID_MAX, SUB_THREADS, 0, st>>>(D));
   LAUNCH(FAM_HASH, k_submap_alloc<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D));
   LAUNCH(FAM_HASH, k_submap_scatter<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D));
   LOAM_HIP(hipStreamWaitEvent(st, h->ev_join, 0));

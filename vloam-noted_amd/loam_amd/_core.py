@@ -47,6 +47,11 @@ class MapStats(ctypes.Structure):
                 ("valid_num", c_i32), ("ms_total", c_d), ("ms_opt", c_d)]
 
 
+class OdomStats(ctypes.Structure):
+    _fields_ = [("corner_num", c_i32 * 2), ("surf_num", c_i32 * 2), ("lm", LMStats * 2),
+                ("n_corner_last", c_i32), ("n_surf_last", c_i32), ("ms", c_d)]
+
+
 KFAM = ("stack_voxelgrid", "submap_hash_build", "correspondence", "lm_pass", "insert",
         "cube_revoxel", "other")
 
@@ -69,6 +74,16 @@ SIGNATURES = {
     "loam_scanreg_device_ptr": (c_i32, [vp, c_i32, ctypes.POINTER(vp)]),
     "loam_scanreg_curvature": (c_i32, [vp, vp, vp, c_i32]),
     "loam_scanreg_ms": (c_d, [vp]),
+    "loam_odometry_create": (c_i32, [ctypes.POINTER(Params), c_i32, c_i32, ctypes.POINTER(vp)]),
+    "loam_odometry_destroy": (c_i32, [vp]),
+    "loam_odometry_reset": (c_i32, [vp]),
+    "loam_odometry_input": (c_i32, [vp, c_i32, vp, c_i32, vp, c_i32, vp, c_i32, vp, c_i32]),
+    "loam_odometry_input_device": (c_i32, [vp, c_i32, vp, c_i32, vp, c_i32, vp, c_i32, vp, c_i32]),
+    "loam_odometry_solve": (c_i32, [vp]),
+    "loam_odometry_output": (c_i32, [vp, c_i32, vp, vp, vp, vp, ctypes.POINTER(c_i32)]),
+    "loam_odometry_last_cloud": (c_i32, [vp, c_i32, c_i32, ctypes.POINTER(vp)]),
+    "loam_odometry_copy_last": (c_i32, [vp, c_i32, c_i32, vp, c_i32]),
+    "loam_odometry_stats": (c_i32, [vp, c_i32, ctypes.POINTER(OdomStats)]),
     "loam_mapper_create": (c_i32, [ctypes.POINTER(Params), c_i32, c_i32, ctypes.POINTER(vp)]),
     "loam_mapper_destroy": (c_i32, [vp]),
     "loam_mapper_reset": (c_i32, [vp]),
