@@ -8,8 +8,9 @@ of `--streams` independent mapping streams held by one handle (one launch sequen
 LM iterations are counted like Ceres' summary.iterations.size() - 1 (trust-region steps).
 
 Inputs are produced before the timed region, on the GPU: synthetic raw scans
-(vloam-noted_amd/csrc/synth.cpp) -> HIP ScanRegistration -> lessSharp / lessFlat clouds kept
-in HBM; the odometry pose prior is ground truth plus a seeded random-walk drift.  Stream b
+(vloam-noted_amd/csrc/synth.cpp) -> HIP ScanRegistration -> HIP LaserOdometry -> lessSharp /
+lessFlat clouds kept in HBM + the odometry pose as the mapping prior (--prior drift: ground
+truth plus a seeded random walk instead).  Stream b
 replays the sequence from frame b * --stride.  The W warmup steps build every stream's map
 (the 5x5x3-cube window saturates after ~150 m of travel), so the K timed steps run at the
 steady-state map size of a long stream (BASELINE configs[3], 10k-frame stream).
@@ -53,6 +54,8 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=40, help="cpu_baseline timed frames (after warmup)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-prof", action="store_true", help="no per-launch HIP events")
+    ap.add_argument("--prior", choices=["odometry", "drift"], default="odometry",
+                    help="mapping prior: GPU LaserOdometry output (default) or ground truth + random walk")
     ap.add_argument("--no-single-stream", action="store_true",
                     help="skip the single-stream (latency view) timing")
     return ap.parse_args()
@@ -73,14 +76,17 @@ def drift_priors(seed, n, q_gt, t_gt):
     return q, t
 
 
-def make_frames(seed, n_frames, n_az, device, keep_raw=0):
-    """raw scans (threads) -> HIP ScanRegistration -> features in HBM (torch tensors); the raw
-    scans of the first keep_raw frames are kept for the CPU baseline"""
+def make_frames(seed, n_frames, n_az, device, keep_raw=0, prior="odometry"):
+    """raw scans (threads) -> HIP ScanRegistration -> HIP LaserOdometry -> features in HBM
+    (torch tensors) + the odometry pose (the mapping prior, laser_odometry.cpp:660-679); the
+    raw scans of the first keep_raw frames are kept for the CPU baseline"""
     import torch
     from loam_amd import synth
+    from loam_amd.odometry import BatchOdometry
     from loam_amd.scanreg import ScanRegistration
 
     sr = ScanRegistration(device=device)
+    od = BatchOdometry(1, device=device)
     frames = []
     chunk = 64
     with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4)) as ex:
@@ -88,17 +94,23 @@ def make_frames(seed, n_frames, n_az, device, keep_raw=0):
             raw = list(ex.map(lambda f: synth.frame(seed, f, n_az), range(c0, min(n_frames, c0 + chunk))))
             for k, (xyz, gt) in enumerate(raw):
                 sr.input(xyz)
+                ptrs, counts = zip(*(sr.device_ptr(w) for w in (1, 2, 3, 4)))
+                od.input_device(0, ptrs, counts)
+                od.solve()
+                q, t, _, _, _ = od.output(0)
                 corner = sr.cloud(2)  # cornerPointsLessSharp -> laserCloudCornerLast
                 surf = sr.cloud(4)    # surfPointsLessFlat   -> laserCloudSurfLast
                 frames.append(dict(corner=torch.from_numpy(corner).to(f"cuda:{device}"),
                                    surf=torch.from_numpy(surf).to(f"cuda:{device}"),
-                                   gt=gt, raw=xyz if c0 + k < keep_raw else None))
+                                   gt=gt, q=q, t=t, raw=xyz if c0 + k < keep_raw else None))
     sr.close()
-    q_gt = np.array([f["gt"][:4] for f in frames])
-    t_gt = np.array([f["gt"][4:] for f in frames])
-    q, t = drift_priors(seed, n_frames, q_gt, t_gt)
-    for i, f in enumerate(frames):
-        f["q"], f["t"] = q[i], t[i]
+    od.close()
+    if prior == "drift":
+        q_gt = np.array([f["gt"][:4] for f in frames])
+        t_gt = np.array([f["gt"][4:] for f in frames])
+        q, t = drift_priors(seed, n_frames, q_gt, t_gt)
+        for i, f in enumerate(frames):
+            f["q"], f["t"] = q[i], t[i]
     torch.cuda.synchronize(device)
     return frames
 
@@ -126,8 +138,9 @@ def run_steps(mapper, plan, first, count):
 
 
 def cpu_baseline(frames, warm, n):
-    """oracle pipeline on stream 0's frames: `warm` untimed frames build the map, then n frames
-    timed (solveMapping, the oracle's own steady_clock over the whole call)"""
+    """oracle pipeline on stream 0's frames (same features and priors as the GPU run): `warm`
+    untimed frames build the map, then n frames timed (solveMapping, the oracle's own
+    steady_clock over the whole call)"""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import loam_oracle as O
     sr, mp = O.ScanRegistration(), O.LaserMapping()
@@ -161,7 +174,8 @@ def main():
     B, K, W = args.streams, args.steps, args.warmup
     n_frames = (B - 1) * args.stride + W + K
     cpu_n = 0 if (args.no_cpu or world > 1 or rank != 0) else W + args.cpu_frames
-    frames = make_frames(args.seed + 1000 * rank, max(n_frames, cpu_n), args.n_az, local, keep_raw=cpu_n)
+    frames = make_frames(args.seed + 1000 * rank, max(n_frames, cpu_n), args.n_az, local, keep_raw=cpu_n,
+                         prior=args.prior)
     mapper = BatchMapper(B, device=local)
 
     def barrier():
@@ -233,8 +247,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp64 pose/normal equations, fp32 points",
-            "data": "synthetic HDL-64E street sequence (64 rings x 2000 azimuths), GPU scan registration "
-                    "features, ground-truth + random-walk odometry prior; maps built by the warmup steps",
+            "data": "synthetic HDL-64E street sequence (64 rings x 2000 azimuths); GPU scan registration "
+                    f"features; mapping prior from {'GPU LaserOdometry' if args.prior == 'odometry' else 'ground truth + random walk'}; "
+                    "maps built by the warmup steps",
             "config": {"workload": "laserMapping solveMapping, voxel-hashed map resident in HBM "
                                    "(BASELINE configs[3])",
                        "streams_per_gpu": B, "frames_per_step": B * world, "n_az": args.n_az,

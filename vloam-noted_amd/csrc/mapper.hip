@@ -4,8 +4,10 @@
 // Per frame (all device resident, one host round-trip at the end for the poses):
 //   k_shift_cubes      ring-buffer recentering of the 21x21x11 cube grid (:252-444), rare
 //   k_stack_ds         VoxelGrid of laserCloudCornerLast (0.4 m) / SurfLast (0.8 m) (:492-500)
-//   k_submap_*         gather the 5x5x3 window cubes (:448-489) and build a 1 m-cell hash
-//                      (replaces the KD-tree build, :519-520); exact 5-NN because accepted
+//   k_submap_prep      offsets of the 5x5x3 window cubes in the submap order (:448-489);
+//                      no per-frame index build: every cube keeps a persistent 1 m cell
+//                      index (cubeindex.h, replaces the KD-tree build :519-520), rebuilt
+//                      only when its content changes (k_revox); exact 5-NN because accepted
 //                      matches need all 5 neighbours within 1 m (:557, :642)
 //   2 x { k_knn         exact 5-NN of every query in the cell hash (:554, :633)
 //         k_geom        PCA line / QR plane fit of the neighbours -> factor records (:557-699)
@@ -26,6 +28,7 @@
 #include "common.h"
 #include "device_math.h"
 #include "cellhash.h"
+#include "cubeindex.h"
 #include "lm.h"
 #include "voxel.h"
 
@@ -41,7 +44,8 @@ constexpr int LM_THREADS = 256;
 constexpr int LM_EBLK = 32;     // LM evaluation workgroups per stream (grid-stride)
 constexpr int SUBMAP_BLOCKS = 64;
 constexpr int INS_SLOTS = WIN_VALID_MAX + EXTRA_CAP;
-constexpr int MAP_ERR_SUBMAP = 4, MAP_ERR_EXTRA = 8, MAP_ERR_HASH = 16, MAP_ERR_LM_SYNC = 32;
+constexpr int MAP_ERR_SUBMAP = 4, MAP_ERR_EXTRA = 8, MAP_ERR_HASH = 16, MAP_ERR_LM_SYNC = 32,
+              MAP_ERR_INDEX = 64;
 
 struct StreamFrame {
   double pose[7];  // in: initial guess (transformAssociateToMap); out: optimised pose
@@ -61,39 +65,30 @@ struct StreamFrame {
   uint32_t arena_tail[2];
   int arena_active[2];
   uint32_t scratch_tail[2];
-  uint32_t cursor[2];
-  uint32_t hmask[2];              // this frame's cell-hash size - 1 (>= 2x the submap points)
-  uint32_t ncells[2];             // cells claimed this frame (cell list length)
   int extra_n[2];
   int extra_list[2][EXTRA_CAP];
   int err;
   const float4* in_ptr[2];        // input clouds (mapper staging buffer or caller's HBM)
   unsigned long long cand[2];     // map points examined by the kNN of each round
+  unsigned long long vx_bytes;    // algorithmic bytes of this frame's re-VoxelGrid + cell index
   LmState lm[2];
 };
 
 struct MapperDev {
   int B;
-  int max_in, map_cap, sub_cap, hash_T, scratch_cap, max_chunks;
+  int max_in, map_cap, sub_cap, scratch_cap, max_chunks;
   float leaf[2];
   uint32_t epoch;
   StreamFrame* fr;
   float4* in_pts[2];
   float4* stack[2];
   float4* arena;  // [B][2 maps][2 arenas][map_cap]
+  float4* carena; // same shape: each cube's points sorted by 1 m cell (cubeindex.h)
+  uint2* ctab;    // [B][2 maps][2 arenas][4 * map_cap]: each cube's cell table
   uint2* cube_tab;  // [B][2 maps][NCUBE] (off, cnt) — current parity
   uint32_t* extra_flag;  // [B][2][NCUBE]
-  unsigned long long* hkey;  // [B][2][T]
-  unsigned long long* hcnt;
-  uint32_t* hstart;
-  uint4* qtab;      // [B][2][T] packed query entries {key, epoch, start, count}
-  uint32_t* cells;  // [B][2][T] slots claimed this frame (alloc iterates cells, not points)
   int* knn_id;      // [5][B][2*max_in] neighbour ids (submap index) per query, -1: none
   size_t knn_stride;
-  float4* sub_lin;  // [B][2][sub_cap] window-order submap
-  float4* spts;     // [B][2][sub_cap] cell-sorted submap (w = submap index bits)
-  uint32_t* pt_slot;
-  uint32_t* pt_rank;
   // factor records (SoA) [B][2*max_in]
   int* r_type;
   float* r_px;
@@ -119,6 +114,18 @@ __device__ inline size_t sm_index(int s, int m) { return (size_t)s * 2 + m; }
 
 __device__ inline float4* arena_base(const MapperDev& D, int s, int m, int active) {
   return D.arena + ((sm_index(s, m) * 2 + active) * (size_t)D.map_cap);
+}
+__device__ inline float4* carena_base(const MapperDev& D, int s, int m, int active) {
+  return D.carena + ((sm_index(s, m) * 2 + active) * (size_t)D.map_cap);
+}
+__device__ inline uint2* ctab_base(const MapperDev& D, int s, int m, int active) {
+  return D.ctab + ((sm_index(s, m) * 2 + active) * (size_t)D.map_cap * 4);
+}
+// lower corner of cube c (grid index) given the grid centre
+__device__ inline void cube_corner(int c, const int* cen, int corner[3]) {
+  corner[0] = ci_corner(c % CW, cen[0]);
+  corner[1] = ci_corner((c / CW) % CH, cen[1]);
+  corner[2] = ci_corner(c / (CW * CH), cen[2]);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -196,180 +203,49 @@ __global__ void __launch_bounds__(128) k_submap_prep(MapperDev D) {
     }
     F.sub_off[m][vn] = total;
     F.sub_n[m] = total;
-    F.scratch_tail[m] = 0;
-    F.cursor[m] = 0;
-    F.ncells[m] = 0;
+    F.scratch_tail[m] = 0;  // re-VoxelGrid scratch (bounded by max_submap_points + stacks)
     F.extra_n[m] = 0;
-    uint32_t T = 1024;
-    while (T < 2 * total && T < (uint32_t)D.hash_T) T <<= 1;
-    F.hmask[m] = T - 1;
+    if (m == 0) F.vx_bytes = 0;
   }
   __syncthreads();
   // laser_mapping.cpp:514
   if (threadIdx.x == 0) F.optimize = (F.sub_n[0] > 10 && F.sub_n[1] > 50) ? 1 : 0;
 }
 
-// Submap hash build, one workgroup per (stream, map, window cube): the cube's points are
-// copied to sub_lin (window order = laserCloudCornerFromMap order, laser_mapping.cpp:
-// 448-489) and grouped by 1 m cell in an LDS hash; each distinct cell is then claimed in the
-// global table once, adding its whole count (the rank base of this cube's points in it).
-// Points whose cell does not fit the LDS table take the per-point global path.
-constexpr int SUB_THREADS = 512;
-constexpr int SUB_LHASH = 8192;
-constexpr uint32_t SUB_OVERFLOW = 0xFFFFFFFEu, SUB_FAILED = 0xFFFFFFFFu;
-
-__device__ inline void append_cells_wave(bool fresh, uint32_t slot, uint32_t* cells, uint32_t* ncells) {
-  const uint64_t b = __ballot(fresh);
-  if (!b) return;
-  const int lane = threadIdx.x & 63;
-  uint32_t base = 0;
-  if (lane == 0) base = atomicAdd(ncells, (uint32_t)__popcll(b));
-  base = __shfl(base, 0, 64);
-  if (fresh) cells[base + __popcll(b & lanemask_lt())] = slot;
-}
-
-__global__ void __launch_bounds__(SUB_THREADS) k_submap_insert(MapperDev D) {
-  __shared__ uint32_t lkey[SUB_LHASH];
-  __shared__ uint32_t lcnt[SUB_LHASH];
-  const int w = blockIdx.x % WIN_VALID_MAX, sm = blockIdx.x / WIN_VALID_MAX;
-  const int s = sm >> 1, m = sm & 1;
-  StreamFrame& F = D.fr[s];
-  if (!F.active || w >= F.valid_num) return;
-  const uint32_t base = (uint32_t)F.sub_off[m][w];
-  const uint32_t n = (uint32_t)F.sub_off[m][w + 1] - base;
-  if (n == 0 || F.sub_n[m] == 0) return;
-  const int tid = threadIdx.x;
-  const uint2 cv = D.cube_tab[sm_index(s, m) * NCUBE + F.window[w]];
-  const float4* src = arena_base(D, s, m, F.arena_active[m]) + cv.x;
-  float4* lin = D.sub_lin + sm_index(s, m) * D.sub_cap + base;
-  unsigned long long* hk = D.hkey + sm_index(s, m) * D.hash_T;
-  unsigned long long* hc = D.hcnt + sm_index(s, m) * D.hash_T;
-  uint32_t* ps = D.pt_slot + sm_index(s, m) * D.sub_cap + base;
-  uint32_t* pr = D.pt_rank + sm_index(s, m) * D.sub_cap + base;
-  uint32_t* cells = D.cells + sm_index(s, m) * D.hash_T;
-  const uint32_t mask = F.hmask[m];
-  for (int i = tid; i < SUB_LHASH; i += SUB_THREADS) {
-    lkey[i] = VX_EMPTY;
-    lcnt[i] = 0;
-  }
-  __syncthreads();
-  // 1. copy + group by cell in LDS
-  for (uint32_t i = tid; i < n; i += SUB_THREADS) {
-    const float4 p = src[i];
-    lin[i] = p;
-    const uint32_t key = cell_key_rel(p.x, p.y, p.z, F.origin);
-    uint32_t h = cell_hash(key, SUB_LHASH - 1);
-    bool ok = false;
-    for (int probe = 0; probe < 64; ++probe) {
-      const uint32_t old = atomicCAS(&lkey[h], VX_EMPTY, key);
-      if (old == VX_EMPTY || old == key) {
-        ok = true;
-        break;
-      }
-      h = (h + 1) & (SUB_LHASH - 1);
-    }
-    if (ok) {
-      ps[i] = h;
-      pr[i] = atomicAdd(&lcnt[h], 1u);
-    } else {
-      ps[i] = key;
-      pr[i] = SUB_OVERFLOW;
-    }
-  }
-  __syncthreads();
-  // 2. one global claim per distinct cell; LDS entry becomes (global slot, rank base)
-  for (int s0 = 0; s0 < SUB_LHASH; s0 += SUB_THREADS) {
-    const int sl = s0 + tid;
-    const uint32_t key = lkey[sl];
-    bool fresh = false;
-    uint32_t g = 0;
-    if (key != VX_EMPTY) {
-      uint32_t b0 = 0;
-      if (hash_claim_cell(hk, hc, mask, D.epoch, key, lcnt[sl], &g, &b0, &fresh)) {
-        lkey[sl] = g;
-        lcnt[sl] = b0;
-      } else {
-        atomicOr(&F.err, MAP_ERR_HASH);
-        lkey[sl] = SUB_FAILED;
-      }
-    }
-    append_cells_wave(fresh, g, cells, &F.ncells[m]);
-  }
-  __syncthreads();
-  // 3. global slot and rank of every point (overflow points: per-point claim)
-  for (uint32_t b0 = 0; b0 < n; b0 += SUB_THREADS) {
-    const uint32_t i = b0 + tid;
-    bool fresh = false;
-    uint32_t g = 0;
-    if (i < n) {
-      const uint32_t r = pr[i], v = ps[i];
-      if (r == SUB_OVERFLOW) {
-        uint32_t b1 = 0;
-        if (hash_claim_cell(hk, hc, mask, D.epoch, v, 1u, &g, &b1, &fresh)) {
-          ps[i] = g;
-          pr[i] = b1;
-        } else {
-          atomicOr(&F.err, MAP_ERR_HASH);
-          pr[i] = SUB_FAILED;
-          fresh = false;
-        }
-      } else {
-        const uint32_t gs = lkey[v];
-        if (gs == SUB_FAILED) {
-          pr[i] = SUB_FAILED;
-        } else {
-          ps[i] = gs;
-          pr[i] = lcnt[v] + r;
-        }
-      }
-    }
-    append_cells_wave(fresh, g, cells, &F.ncells[m]);
-  }
-}
-
-// cell starts: one pass over the cells claimed this frame (wave-aggregated cursor)
-__global__ void k_submap_alloc(MapperDev D) {
-  const int sm = blockIdx.y;
-  const int s = sm >> 1, m = sm & 1;
-  StreamFrame& F = D.fr[s];
-  if (!F.active) return;
-  const uint32_t nc = F.ncells[m];
-  const unsigned long long* hk = D.hkey + sm_index(s, m) * D.hash_T;
-  const unsigned long long* hc = D.hcnt + sm_index(s, m) * D.hash_T;
-  uint32_t* hs = D.hstart + sm_index(s, m) * D.hash_T;
-  uint4* qt = D.qtab + sm_index(s, m) * D.hash_T;
-  const uint32_t* cells = D.cells + sm_index(s, m) * D.hash_T;
-  for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < nc; b0 += gridDim.x * blockDim.x) {  // whole waves
-    const uint32_t i = b0 + threadIdx.x;
-    const bool valid = i < nc;
-    hash_alloc_cell(valid, valid ? cells[i] : 0u, hk, hc, D.epoch, hs, qt, &F.cursor[m]);
-  }
-}
-
-__global__ void k_submap_scatter(MapperDev D) {
-  const int sm = blockIdx.y;
-  const int s = sm >> 1, m = sm & 1;
-  const StreamFrame& F = D.fr[s];
-  if (!F.active) return;
-  const uint32_t n = F.sub_n[m];
-  const uint32_t* hs = D.hstart + sm_index(s, m) * D.hash_T;
-  const uint32_t* ps = D.pt_slot + sm_index(s, m) * D.sub_cap;
-  const uint32_t* pr = D.pt_rank + sm_index(s, m) * D.sub_cap;
-  const float4* lin = D.sub_lin + sm_index(s, m) * D.sub_cap;
-  float4* sp = D.spts + sm_index(s, m) * D.sub_cap;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    if (pr[i] == 0xFFFFFFFFu) continue;
-    float4 p = lin[i];
-    sp[hs[ps[i]] + pr[i]] = make_float4(p.x, p.y, p.z, __int_as_float((int)i));
-  }
-}
-
 // ---------------------------------------------------------------------------------------
 // correspondences of one outer round (laser_mapping.cpp:545-699) -> factor records
 // ---------------------------------------------------------------------------------------
-// pass 1: exact 5-NN of every query in the cell hash -> neighbour ids (laser_mapping.cpp:554,
-// :633, accepted only if the 5th is within 1 m: :557, :642)
+// pass 1: exact 5-NN of every query (laser_mapping.cpp:554, :633; accepted only if the 5th is
+// within 1 m: :557, :642) over the window cubes' cell indexes (cubeindex.h).  Distances are
+// FLANN's L2_Simple<float>; ties go to the lower submap index (sub_off[slot] + position in
+// the cube).  Output: positions of the 5 neighbours in the cell-sorted arena, -1: none.
+struct Near5 {
+  float d[5];
+  int id[5];   // submap index (tie-break)
+  int pos[5];  // cell-sorted arena position
+};
+__device__ inline void near5_offer(Near5& T, float d, int id, int pos) {
+  if (!(d < T.d[4] || (d == T.d[4] && id < T.id[4]))) return;
+  T.d[4] = d; T.id[4] = id; T.pos[4] = pos;
+#pragma unroll
+  for (int k = 4; k > 0; --k) {
+    if (T.d[k] < T.d[k - 1] || (T.d[k] == T.d[k - 1] && T.id[k] < T.id[k - 1])) {
+      float td = T.d[k]; T.d[k] = T.d[k - 1]; T.d[k - 1] = td;
+      int ti = T.id[k]; T.id[k] = T.id[k - 1]; T.id[k - 1] = ti;
+      int tp = T.pos[k]; T.pos[k] = T.pos[k - 1]; T.pos[k - 1] = tp;
+    }
+  }
+}
+__device__ inline int floor_div50(int v) { return v >= 0 ? v / 50 : -((-v + 49) / 50); }
+
+struct WinMap {  // per (stream, map) window cubes, in LDS
+  uint32_t off[WIN_MAX], n[WIN_MAX], tsize[WIN_MAX];
+  int sub[WIN_MAX];
+};
+
 __global__ void __launch_bounds__(CORR_THREADS) k_knn(MapperDev D, int round) {
+  __shared__ WinMap W[2];
+  __shared__ int slot_of[75];  // 5 x 5 x 3 window position -> slot (laserCloudValidInd order)
   const int s = blockIdx.x / CORR_BLK, blk = blockIdx.x % CORR_BLK;
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
@@ -379,19 +255,101 @@ __global__ void __launch_bounds__(CORR_THREADS) k_knn(MapperDev D, int round) {
   if (blk == 0 && threadIdx.x < 4) D.lm_sync[((size_t)s * 2 + round) * 4 + threadIdx.x] = 0;
   if (blk == 0 && threadIdx.x == 0) lm_init(F.lm[round], X, 4, F.optimize != 0);
   if (!F.optimize) return;  // k_geom types every record 0
+  const int tid = threadIdx.x;
+  const int c0 = F.center[0] - 2, c1 = F.center[1] - 2, c2 = F.center[2] - 1;
+  if (tid < 75) slot_of[tid] = -1;
+  __syncthreads();
+  if (tid < F.valid_num) {
+    const int cube = F.window[tid];
+    const int ci = cube % CW, cj = (cube / CW) % CH, ck = cube / (CW * CH);
+    slot_of[(ci - c0) * 15 + (cj - c1) * 3 + (ck - c2)] = tid;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const uint2 cv = D.cube_tab[sm_index(s, m) * NCUBE + cube];
+      W[m].off[tid] = cv.x;
+      W[m].n[tid] = cv.y;
+      W[m].tsize[tid] = cv.y ? ci_table_size(cv.y) : 0u;
+      W[m].sub[tid] = F.sub_off[m][tid];
+    }
+  }
+  __syncthreads();
   const int nc = F.nc_stack, ns = F.ns_stack;
   const size_t rb = (size_t)s * 2 * D.max_in;
   uint32_t ncand = 0;
-  for (int ridx = blk * CORR_THREADS + threadIdx.x; ridx < nc + ns; ridx += CORR_BLK * CORR_THREADS) {
+  for (int ridx = blk * CORR_THREADS + tid; ridx < nc + ns; ridx += CORR_BLK * CORR_THREADS) {
     const int m = ridx < nc ? 0 : 1;  // corners [0, nc), surfs [nc, nc + ns)
     const int qi = m == 0 ? ridx : ridx - nc;
-    const float4 sel = to_map(X, D.stack[m][(size_t)s * D.max_in + qi]);
-    Top5 T;
-    knn5_hash(sel, F.origin, D.qtab + sm_index(s, m) * D.hash_T, D.spts + sm_index(s, m) * D.sub_cap,
-              F.hmask[m], D.epoch, 1.0f, T, &ncand);
+    const float4 q = to_map(X, D.stack[m][(size_t)s * D.max_in + qi]);
+    const float4* cp = carena_base(D, s, m, F.arena_active[m]);
+    const uint2* ct = ctab_base(D, s, m, F.arena_active[m]);
+    const WinMap& WM = W[m];
+    Near5 T;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      T.d[k] = INFINITY;
+      T.id[k] = 0x7FFFFFFF;
+      T.pos[k] = -1;
+    }
+    const float fx = floorf(q.x), fy = floorf(q.y), fz = floorf(q.z);
+    const int qx = (int)fx, qy = (int)fy, qz = (int)fz;
+    const float lx = q.x - fx, hx = (fx + 1.0f) - q.x;
+    const float ly = q.y - fy, hy = (fy + 1.0f) - q.y;
+    const float lz = q.z - fz, hz = (fz + 1.0f) - q.z;
+    // points of cell (x, y, z) filed in cube (bi, bj, bk) at local (ax, ay, az)
+    auto scan = [&](int bi, int bj, int bk, int ax, int ay, int az) {
+      const int wx = bi - c0, wy = bj - c1, wz = bk - c2;
+      if (wx < 0 || wx > 4 || wy < 0 || wy > 4 || wz < 0 || wz > 2) return;  // not in the submap
+      const int sl = slot_of[wx * 15 + wy * 3 + wz];
+      if (sl < 0) return;
+      const uint32_t n = WM.n[sl];
+      if (n == 0) return;
+      const uint32_t off = WM.off[sl];
+      const uint2 e = ci_find(ct + 4 * (size_t)off, WM.tsize[sl],
+                              (uint32_t)ax | ((uint32_t)ay << 6) | ((uint32_t)az << 12));
+      ncand += e.y;
+      const int sub = WM.sub[sl];
+      for (uint32_t k = 0; k < e.y; ++k) {
+        const uint32_t pos = off + e.x + k;
+        const float4 p = cp[pos];
+        near5_offer(T, fdist2(q.x, q.y, q.z, p.x, p.y, p.z), sub + __float_as_int(p.w), (int)pos);
+      }
+    };
+    for (int o = 0; o < 27; ++o) {
+      const uint32_t code = cell_order_code(o);
+      const int dx = (int)(code & 3u) - 1, dy = (int)((code >> 2) & 3u) - 1, dz = (int)(code >> 4) - 1;
+      const float gx = dx < 0 ? lx : (dx > 0 ? hx : 0.f);
+      const float gy = dy < 0 ? ly : (dy > 0 ? hy : 0.f);
+      const float gz = dz < 0 ? lz : (dz > 0 ? hz : 0.f);
+      const float bound = fminf(T.d[4], 1.0f) * 1.01f + 1e-6f;  // rounding margin
+      if (gx * gx + gy * gy + gz * gz > bound) continue;
+      const int x = qx + dx, y = qy + dy, z = qz + dz;
+      const int bi = floor_div50(x + 25) + F.cen[0], bj = floor_div50(y + 25) + F.cen[1],
+                bk = floor_div50(z + 25) + F.cen[2];
+      int cx[3] = {bi, bj, bk};
+      int lc[3];
+      const int cv[3] = {x, y, z};
+#pragma unroll
+      for (int a = 0; a < 3; ++a) lc[a] = cv[a] - ci_corner(cx[a], F.cen[a]);
+      scan(bi, bj, bk, lc[0], lc[1], lc[2]);
+      // the reference files points at an exact negative multiple of 50 (v + 25) in the cube
+      // below (laser_mapping.cpp:747-756): local coordinate 50 there
+      int edge = 0;
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+        if (cv[a] + 25 < 0 && (cv[a] + 25) % 50 == 0) edge |= 1 << a;
+      for (int e = edge; e; e = (e - 1) & edge) {
+        int b2[3], l2[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          b2[a] = (e >> a) & 1 ? cx[a] - 1 : cx[a];
+          l2[a] = (e >> a) & 1 ? 50 : lc[a];
+        }
+        scan(b2[0], b2[1], b2[2], l2[0], l2[1], l2[2]);
+      }
+    }
     const bool ok = T.d[4] < 1.0f;
 #pragma unroll
-    for (int k = 0; k < 5; ++k) D.knn_id[k * D.knn_stride + rb + ridx] = ok ? T.id[k] : -1;
+    for (int k = 0; k < 5; ++k) D.knn_id[k * D.knn_stride + rb + ridx] = ok ? T.pos[k] : -1;
   }
   unsigned long long wc = ncand;
 #pragma unroll
@@ -419,7 +377,7 @@ __global__ void __launch_bounds__(CORR_THREADS) k_geom(MapperDev D, int round) {
     int type = 0;
     double a[3] = {0, 0, 0}, b[3] = {0, 0, 0};
     if (D.knn_id[rb + ridx] >= 0) {
-      const float4* lin = D.sub_lin + sm_index(s, m) * D.sub_cap;
+      const float4* lin = carena_base(D, s, m, F.arena_active[m]);
       float nb[5][3];
 #pragma unroll
       for (int j = 0; j < 5; ++j) {
@@ -689,11 +647,52 @@ __global__ void __launch_bounds__(VX_THREADS) k_revox(MapperDev D) {
   S.scratch_tail = &F.scratch_tail[m];
   S.scratch_cap = D.scratch_cap;
   S.err = &F.err;
+  bool done = false;
   if (!append && n_new > 0 && n_new <= VX_MERGE_CAP && cv.y > 0 && *tok == cv.x + 1) {
-    if (vx_merge_fixed_point(S, lds)) return;
-    __syncthreads();  // grid overflow: full filter below
+    done = vx_merge_fixed_point(S, lds);
+    __syncthreads();  // false: grid overflow, full filter below
   }
-  voxel_segment(S, lds);
+  if (!done) voxel_segment(S, lds);
+  // the cube's new content -> its cell index (cubeindex.h)
+  __syncthreads();
+  uint32_t* res = lds + VX_LDS_WORDS - 2;
+  if (threadIdx.x == 0) {
+    const uint2 v = tab[cube];  // written by this thread inside the filter
+    res[0] = v.x;
+    res[1] = v.y;
+  }
+  __syncthreads();
+  const uint32_t off = res[0], n = res[1];
+  int corner[3];
+  cube_corner(cube, F.cen, corner);
+  if (!cube_index_build<VX_THREADS>(ar + off, n, corner, carena_base(D, s, m, F.arena_active[m]) + off,
+                                    ctab_base(D, s, m, F.arena_active[m]) + 4 * (size_t)off, lds) &&
+      threadIdx.x == 0)
+    atomicOr(&F.err, MAP_ERR_INDEX);
+  // read old content + new points, write the filtered cube, then its index (read it, write
+  // the cell-sorted copy and the table)
+  if (threadIdx.x == 0)
+    atomicAdd(&F.vx_bytes, 16ull * (cv.y + n_new) + 16ull * 3 * n + (n ? 8ull * ci_table_size(n) : 0ull));
+}
+
+// cell index of one cube whose content was set through the API (cen: the host's grid centre)
+__global__ void __launch_bounds__(VX_THREADS) k_cube_index(MapperDev D, int s, int m, int c0, int c1,
+                                                           int3 cen) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[CI_LDS_MAX_T + VX_WAVES + 1];
+  const int cube = c0 + blockIdx.x;
+  if (cube >= c1) return;
+  StreamFrame& F = D.fr[s];
+  const uint2 cv = D.cube_tab[sm_index(s, m) * NCUBE + cube];
+  if (cv.y == 0) return;
+  const int cenv[3] = {cen.x, cen.y, cen.z};
+  int corner[3];
+  cube_corner(cube, cenv, corner);
+  const int active = F.arena_active[m];
+  if (!cube_index_build<VX_THREADS>(arena_base(D, s, m, active) + cv.x, cv.y, corner,
+                                    carena_base(D, s, m, active) + cv.x,
+                                    ctab_base(D, s, m, active) + 4 * (size_t)cv.x, lds) &&
+      threadIdx.x == 0)
+    atomicOr(&F.err, MAP_ERR_INDEX);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -734,9 +733,20 @@ __global__ void k_compact_copy(MapperDev D, const int* pairs, const uint32_t* ne
   const uint32_t* no = new_off + (size_t)p * (NCUBE + 1);
   const float4* src = arena_base(D, s, m, F.arena_active[m]);
   float4* dst = arena_base(D, s, m, 1 - F.arena_active[m]);
+  const float4* csrc = carena_base(D, s, m, F.arena_active[m]);
+  float4* cdst = carena_base(D, s, m, 1 - F.arena_active[m]);
+  const uint2* tsrc = ctab_base(D, s, m, F.arena_active[m]);
+  uint2* tdst = ctab_base(D, s, m, 1 - F.arena_active[m]);
   for (int c = blockIdx.x; c < NCUBE; c += gridDim.x) {
     const uint2 cv = tab[c];
-    for (uint32_t i = threadIdx.x; i < cv.y; i += blockDim.x) dst[no[c] + i] = src[cv.x + i];
+    for (uint32_t i = threadIdx.x; i < cv.y; i += blockDim.x) {
+      dst[no[c] + i] = src[cv.x + i];
+      cdst[no[c] + i] = csrc[cv.x + i];  // the cell index moves verbatim (offsets are local)
+    }
+    if (cv.y) {
+      const uint32_t T = ci_table_size(cv.y);
+      for (uint32_t h = threadIdx.x; h < T; h += blockDim.x) tdst[4 * (size_t)no[c] + h] = tsrc[4 * (size_t)cv.x + h];
+    }
   }
 }
 
@@ -894,7 +904,6 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
   D.max_in = h->P.max_input_points;
   D.map_cap = h->P.max_map_points;
   D.sub_cap = h->P.max_submap_points;
-  D.hash_T = (int)next_pow2((uint32_t)D.sub_cap);
   D.scratch_cap = D.sub_cap + D.max_in;
   D.max_chunks = LM_EBLK;
   {
@@ -933,20 +942,13 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
     ALLOC(D.stack[m], B * D.max_in);
   }
   ALLOC(D.arena, B * 2 * 2 * (size_t)D.map_cap);
+  ALLOC(D.carena, B * 2 * 2 * (size_t)D.map_cap);
+  ALLOC(D.ctab, B * 2 * 2 * 4 * (size_t)D.map_cap);
   ALLOC(h->cube_tab[0], B * 2 * NCUBE);
   ALLOC(h->cube_tab[1], B * 2 * NCUBE);
   ALLOC(D.extra_flag, B * 2 * NCUBE);
-  ALLOC(D.hkey, B * 2 * (size_t)D.hash_T);
-  ALLOC(D.hcnt, B * 2 * (size_t)D.hash_T);
-  ALLOC(D.hstart, B * 2 * (size_t)D.hash_T);
-  ALLOC(D.qtab, B * 2 * (size_t)D.hash_T);
-  ALLOC(D.cells, B * 2 * (size_t)D.hash_T);
   D.knn_stride = B * 2 * (size_t)D.max_in;
   ALLOC(D.knn_id, 5 * D.knn_stride);
-  ALLOC(D.sub_lin, B * 2 * (size_t)D.sub_cap);
-  ALLOC(D.spts, B * 2 * (size_t)D.sub_cap);
-  ALLOC(D.pt_slot, B * 2 * (size_t)D.sub_cap);
-  ALLOC(D.pt_rank, B * 2 * (size_t)D.sub_cap);
   ALLOC(D.r_type, B * 2 * (size_t)D.max_in);
   ALLOC(D.r_px, B * 2 * (size_t)D.max_in);
   ALLOC(D.r_py, B * 2 * (size_t)D.max_in);
@@ -1180,9 +1182,6 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   }
   LAUNCH(FAM_OTHER, k_submap_prep<<<B, 128, 0, st>>>(D));
   LOAM_HIP(hipEventRecord(h->ev[1], st));
-  LAUNCH(FAM_HASH, k_submap_insert<<<B * 2 * WIN_VALID_MAX, SUB_THREADS, 0, st>>>(D));
-  LAUNCH(FAM_HASH, k_submap_alloc<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D));
-  LAUNCH(FAM_HASH, k_submap_scatter<<<dim3(SUBMAP_BLOCKS, B * 2), 256, 0, st>>>(D));
   LOAM_HIP(hipStreamWaitEvent(st, h->ev_join, 0));
   for (int round = 0; round < 2; ++round) {
     LAUNCH(FAM_CORR, k_knn<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round));
@@ -1220,7 +1219,6 @@ int32_t loam_mapper_solve(loam_mapper* h) {
       if (!F.active) continue;
       const double nst = (double)F.nc_stack + F.ns_stack;
       h->fam_bytes[FAM_STACK] += 16.0 * ((double)F.nc_in + F.ns_in + nst);
-      h->fam_bytes[FAM_HASH] += 32.0 * ((double)F.sub_n[0] + F.sub_n[1]);
       h->fam_bytes[FAM_INSERT] += 36.0 * nst;
       if (F.optimize) {
         for (int r = 0; r < 2; ++r) {
@@ -1264,10 +1262,7 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     S.valid_num = F.valid_num;
     S.ms_total = ms_total;
     S.ms_opt = ms_opt;
-    if (h->prof) {  // window content read + stacks read + new content written
-      const double written = (double)(F.arena_tail[0] - tail0[2 * s]) + (double)(F.arena_tail[1] - tail0[2 * s + 1]);
-      h->fam_bytes[FAM_REVOX] += 16.0 * ((double)F.sub_n[0] + F.sub_n[1] + F.nc_stack + F.ns_stack + written);
-    }
+    if (h->prof) h->fam_bytes[FAM_REVOX] += (double)F.vx_bytes;  // counted by k_revox
     if (F.err) {
       set_error("loam_mapper_solve: device capacity exceeded (err flags " + std::to_string(F.err) + ")");
       status = LOAM_ERR_CAPACITY;
@@ -1351,12 +1346,32 @@ int32_t loam_mapper_get_state(loam_mapper* h, int32_t s, int32_t* cen, double* q
   return LOAM_OK;
 }
 
+// cell index of cubes [c0, c1) of (stream, map) after host-side changes
+static int32_t build_cube_index(loam_mapper* h, int32_t s, int32_t m, int32_t c0, int32_t c1) {
+  LOAM_HIP(hipSetDevice(h->dev));
+  // the device copy of the stream record supplies arena_active: refresh it first
+  LOAM_HIP(hipMemcpyAsync(h->D.fr + s, &h->hf[s], sizeof(StreamFrame), hipMemcpyHostToDevice, h->st));
+  MapperDev D = h->D;
+  D.cube_tab = h->cube_tab[h->parity];
+  const int3 cen = make_int3(h->hf[s].cen[0], h->hf[s].cen[1], h->hf[s].cen[2]);
+  k_cube_index<<<c1 - c0, VX_THREADS, 0, h->st>>>(D, s, m, c0, c1, cen);
+  LOAM_HIP(hipGetLastError());
+  LOAM_HIP(hipStreamSynchronize(h->st));
+  return LOAM_OK;
+}
+
 int32_t loam_mapper_set_state(loam_mapper* h, int32_t s, const int32_t* cen, const double* q, const double* t) {
   TRY(check_stream(h, s));
   if (!cen || !q || !t) return LOAM_ERR_ARG;
-  for (int a = 0; a < 3; ++a) h->hf[s].cen[a] = cen[a];
+  bool moved = false;
+  for (int a = 0; a < 3; ++a) {
+    moved |= h->hf[s].cen[a] != cen[a];
+    h->hf[s].cen[a] = cen[a];
+  }
   for (int i = 0; i < 4; ++i) h->hs[s].q_wmap_wodom[i] = q[i];
   for (int i = 0; i < 3; ++i) h->hs[s].t_wmap_wodom[i] = t[i];
+  if (moved)  // cube world positions changed: rebuild every cube's cell index
+    for (int m = 0; m < 2; ++m) TRY(build_cube_index(h, s, m, 0, NCUBE));
   return LOAM_OK;
 }
 
@@ -1397,7 +1412,7 @@ int32_t loam_mapper_cube_set(loam_mapper* h, int32_t s, int32_t which, int32_t c
   LOAM_HIP(hipMemcpy(h->cube_tab[h->parity] + ((size_t)s * 2 + which) * NCUBE + cube, &v, sizeof(uint2), hipMemcpyHostToDevice));
   const uint32_t zero = 0;  // caller content: not known to be a VoxelGrid fixed point
   LOAM_HIP(hipMemcpy(h->D.stable_tok + ((size_t)s * 2 + which) * NCUBE + cube, &zero, sizeof(zero), hipMemcpyHostToDevice));
-  return LOAM_OK;
+  return build_cube_index(h, s, which, cube, cube + 1);
 }
 
 }  // extern "C"
