@@ -157,6 +157,36 @@ def cpu_baseline(frames, warm, n):
     return iters, ms
 
 
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
+
+
+def pmc_traffic(family):
+    """HBM bytes per launch of a kernel family measured by the rocprofv3 PMC passes of this
+    bench configuration (tools/pmc_traffic.py -> profiles/r1_pmc_traffic.json), or None"""
+    try:
+        return json.load(open(PMC_TRAFFIC))["families"][family]["bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def aggregate(iters, dt, world, device):
+    """whole-job totals: LM iterations summed over ranks, wall time = max over ranks"""
+    if world <= 1:
+        return float(iters), float(dt)
+    import torch
+    import torch.distributed as dist
+    it_t = torch.tensor([float(iters)], dtype=torch.float64, device=device)
+    dt_t = torch.tensor([float(dt)], dtype=torch.float64, device=device)
+    dist.all_reduce(it_t, op=dist.ReduceOp.SUM)
+    dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+    return float(it_t.item()), float(dt_t.item())
+
+
+def stream_seed(seed, rank):
+    """each rank owns its own independent streams (weak scaling, no data-path collective)"""
+    return seed + 1000 * rank
+
+
 def main():
     args = parse()
     import torch
@@ -174,7 +204,7 @@ def main():
     B, K, W = args.streams, args.steps, args.warmup
     n_frames = (B - 1) * args.stride + W + K
     cpu_n = 0 if (args.no_cpu or world > 1 or rank != 0) else W + args.cpu_frames
-    frames = make_frames(args.seed + 1000 * rank, max(n_frames, cpu_n), args.n_az, local, keep_raw=cpu_n,
+    frames = make_frames(stream_seed(args.seed, rank), max(n_frames, cpu_n), args.n_az, local, keep_raw=cpu_n,
                          prior=args.prior)
     mapper = BatchMapper(B, device=local)
 
@@ -196,15 +226,7 @@ def main():
     kt = mapper.kernel_times()
     mapper.set_profiling(False)
 
-    tot = torch.tensor([float(iters), dt], dtype=torch.float64, device=f"cuda:{local}")
-    if world > 1:
-        it_t = tot[:1].clone()
-        dist.all_reduce(it_t, op=dist.ReduceOp.SUM)
-        dt_t = tot[1:].clone()
-        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
-        iters_all, dt_max = float(it_t.item()), float(dt_t.item())
-    else:
-        iters_all, dt_max = float(iters), dt
+    iters_all, dt_max = aggregate(iters, dt, world, f"cuda:{local}")
 
     single = None
     if not args.no_single_stream and rank == 0 and world == 1:
@@ -223,8 +245,11 @@ def main():
         dom = max(kt, key=lambda k: kt[k]["ms"])
         d = kt[dom]
         achieved = d["bytes"] / (d["ms"] * 1e-3) / 1e9 if d["ms"] > 0 else 0.0
+        traffic = pmc_traffic(dom)
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                    "traffic": round(traffic, 1) if traffic is not None else None,
+                    "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) if traffic is not None else None,
                     "launches": d["launches"], "avg_launch_us": round(1e3 * d["ms"] / max(1, d["launches"]), 3),
                     "algorithmic_bytes_per_launch": round(d["bytes"] / max(1, d["launches"]), 1)}
         cpu = None

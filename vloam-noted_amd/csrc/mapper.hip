@@ -914,6 +914,9 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
     const bool allow = !(env && env[0] == '0');
     if (allow && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_lm_round, LM_THREADS, 0) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess) {
+      // 256 threads x 256 VGPRs: exactly one block per CU; the API can over-report by one
+      // block per CU at some SGPR counts (MI355X_MICROARCH.md, correctness boundaries)
+      occ = std::min(occ, 1);
       const int cap = occ * cus;
       h->lm_G = std::min(LM_EBLK, std::min(16, cap / n_streams));
     }

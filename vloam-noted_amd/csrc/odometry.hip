@@ -470,7 +470,7 @@ int32_t loam_odometry_create(const loam_params* p, int32_t device, int32_t n_str
     if (!(env && env[0] == '0') &&
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_od_lm, OD_LM_THREADS, 0) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess)
-      h->G = std::min(OD_PBLK, std::min(4, occ * cus / n_streams));
+      h->G = std::min(OD_PBLK, std::min(4, std::min(occ, 1) * cus / n_streams));  // 1 block/CU (256 VGPRs)
     if (h->G < 1) {
       set_error("loam_odometry_create: too many streams for one resident LM launch");
       return fail(LOAM_ERR_CAPACITY);
