@@ -225,6 +225,9 @@ def main():
     dt = time.perf_counter() - t0
     kt = mapper.kernel_times()
     mapper.set_profiling(False)
+    if os.environ.get("BENCH_DEBUG_COUNTERS"):
+        dc = mapper.debug_counters()
+        print(json.dumps({"debug_counters": [int(v) for v in dc]}), file=sys.stderr, flush=True)
 
     iters_all, dt_max = aggregate(iters, dt, world, f"cuda:{local}")
 

@@ -100,6 +100,10 @@ struct MapperDev {
   int* ins_tag;
   float4* ins_sorted;    // [B][2][max_in] inserted points grouped by target cube (input order kept)
   uint32_t* ins_off;     // [B][2][INS_SLOTS + 1] group offsets: window slots, then extra cubes
+  unsigned long long* dbg;  // [16] phase cycle counters (loam_mapper_debug_counters)
+  uint32_t* rv_list;     // [B][2][INS_SLOTS] re-VoxelGrid worklist (stream, map, slot)
+  uint32_t* rv_count;    // [2]: worklist length, next item
+  uint32_t* rv_next;
   uint32_t* stable_tok;  // [B][2][NCUBE] arena offset + 1 of content known to be a VoxelGrid
                          // fixed point (re-filtering it is the identity), else 0
   float4* vx_pts;  // [B][2][scratch_cap]
@@ -246,7 +250,7 @@ struct WinMap {  // per (stream, map) window cubes, in LDS
 __global__ void __launch_bounds__(CORR_THREADS) k_knn(MapperDev D, int round) {
   __shared__ WinMap W[2];
   __shared__ int slot_of[75];  // 5 x 5 x 3 window position -> slot (laserCloudValidInd order)
-  const int s = blockIdx.x / CORR_BLK, blk = blockIdx.x % CORR_BLK;
+  const int s = blockIdx.x % D.B, blk = blockIdx.x / D.B;  // a stream's blocks on one XCD
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
   double X[7];
@@ -360,7 +364,7 @@ __global__ void __launch_bounds__(CORR_THREADS) k_knn(MapperDev D, int round) {
 // pass 2: line PCA / plane fit of the 5 neighbours -> factor records (laser_mapping.cpp:557-603,
 // :642-680)
 __global__ void __launch_bounds__(CORR_THREADS) k_geom(MapperDev D, int round) {
-  const int s = blockIdx.x / CORR_BLK, blk = blockIdx.x % CORR_BLK;
+  const int s = blockIdx.x % D.B, blk = blockIdx.x / D.B;  // a stream's blocks on one XCD
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
   const int nc = F.nc_stack, ns = F.ns_stack;
@@ -462,7 +466,9 @@ __global__ void __launch_bounds__(64) k_lm_step(MapperDev D, int round) {
 // bounded (MAP_ERR_LM_SYNC, the stream's LM then stops).
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(LM_THREADS) k_lm_round(MapperDev D, int round, int G) {
-  const int s = blockIdx.x / G, g = blockIdx.x % G;
+  // block b -> stream b % B, member b / B: with B a multiple of 8 all of a stream's blocks
+  // share an XCD (b % 8), so its hand-offs stay in one L2 (placement is speed only)
+  const int s = blockIdx.x % D.B, g = blockIdx.x / D.B;
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
   const size_t rb = (size_t)s * 2 * D.max_in;
@@ -599,16 +605,13 @@ __global__ void __launch_bounds__(VX_THREADS) k_bucket(MapperDev D) {
 // re-VoxelGrid of every window cube (old content ++ inserted points, :795-808); cubes outside
 // the window that received points get them appended raw (:762).  One workgroup per cube.
 // ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(VX_THREADS) k_revox(MapperDev D) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
-  constexpr int SLOTS = WIN_VALID_MAX + EXTRA_CAP;
-  const int slot = blockIdx.x % SLOTS;
-  const int sm = blockIdx.x / SLOTS;
-  const int s = sm >> 1, m = sm & 1;
-  StreamFrame& F = D.fr[s];
-  if (!F.active) return;
-  int cube;
-  int append;
+// which cube (if any) slot `slot` of (s, m) re-filters this frame; false: nothing to do.  A
+// window cube that received nothing and whose content is a VoxelGrid fixed point keeps it:
+// re-filtering it (laser_mapping.cpp:795-808) would reproduce it bit for bit.
+__device__ inline bool revox_target(const MapperDev& D, int s, int m, int slot, int* cube_out, int* append_out) {
+  const StreamFrame& F = D.fr[s];
+  if (!F.active) return false;
+  int cube, append;
   if (slot < F.valid_num) {
     cube = F.window[slot];
     append = 0;
@@ -616,16 +619,40 @@ __global__ void __launch_bounds__(VX_THREADS) k_revox(MapperDev D) {
     cube = F.extra_list[m][slot - WIN_VALID_MAX];
     append = 1;
   } else {
-    return;
+    return false;
   }
+  const uint32_t* ioff = D.ins_off + sm_index(s, m) * (INS_SLOTS + 1);
+  const uint32_t n_new = ioff[slot + 1] - ioff[slot];
+  const uint2 cv = D.cube_tab[sm_index(s, m) * NCUBE + cube];
+  if (!append && n_new == 0 && (cv.y == 0 || D.stable_tok[sm_index(s, m) * NCUBE + cube] == cv.x + 1))
+    return false;
+  *cube_out = cube;
+  *append_out = append;
+  return true;
+}
+
+// worklist of the slots to re-filter (one thread per (stream, map, slot))
+__global__ void k_revox_list(MapperDev D) {
+  const int item = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = item < D.B * 2 * INS_SLOTS;
+  const int slot = in ? item % INS_SLOTS : 0, sm = in ? item / INS_SLOTS : 0;
+  int cube = 0, append = 0;
+  const bool work = in && revox_target(D, sm >> 1, sm & 1, slot, &cube, &append);
+  const uint64_t b = __ballot(work);
+  if (!b) return;
+  uint32_t base = 0;
+  if ((threadIdx.x & 63) == __ffsll((unsigned long long)b) - 1) base = atomicAdd(D.rv_count, (uint32_t)__popcll(b));
+  base = __shfl(base, __ffsll((unsigned long long)b) - 1, 64);
+  if (work) D.rv_list[base + __popcll(b & lanemask_lt())] = item;
+}
+
+__device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube, int append, uint32_t* lds) {
+  StreamFrame& F = D.fr[s];
   const uint32_t* ioff = D.ins_off + sm_index(s, m) * (INS_SLOTS + 1);
   const uint32_t i0 = ioff[slot], n_new = ioff[slot + 1] - i0;
   uint32_t* tok = D.stable_tok + sm_index(s, m) * NCUBE + cube;
   uint2* tab = D.cube_tab + sm_index(s, m) * NCUBE;
   const uint2 cv = tab[cube];
-  // a cube that received nothing and whose content is a VoxelGrid fixed point keeps it:
-  // re-filtering it (laser_mapping.cpp:795-808) would reproduce it bit for bit
-  if (!append && n_new == 0 && (cv.y == 0 || *tok == cv.x + 1)) return;
   float4* ar = arena_base(D, s, m, F.arena_active[m]);
   VoxSeg S;
   S.src0 = ar + cv.x;
@@ -648,11 +675,15 @@ __global__ void __launch_bounds__(VX_THREADS) k_revox(MapperDev D) {
   S.scratch_cap = D.scratch_cap;
   S.err = &F.err;
   bool done = false;
+  const unsigned long long t0 = __builtin_readcyclecounter();
   if (!append && n_new > 0 && n_new <= VX_MERGE_CAP && cv.y > 0 && *tok == cv.x + 1) {
     done = vx_merge_fixed_point(S, lds);
     __syncthreads();  // false: grid overflow, full filter below
   }
+  const bool merged = done;
   if (!done) voxel_segment(S, lds);
+  __syncthreads();
+  const unsigned long long t1 = __builtin_readcyclecounter();
   // the cube's new content -> its cell index (cubeindex.h)
   __syncthreads();
   uint32_t* res = lds + VX_LDS_WORDS - 2;
@@ -671,8 +702,34 @@ __global__ void __launch_bounds__(VX_THREADS) k_revox(MapperDev D) {
     atomicOr(&F.err, MAP_ERR_INDEX);
   // read old content + new points, write the filtered cube, then its index (read it, write
   // the cell-sorted copy and the table)
-  if (threadIdx.x == 0)
+  if (threadIdx.x == 0) {
     atomicAdd(&F.vx_bytes, 16ull * (cv.y + n_new) + 16ull * 3 * n + (n ? 8ull * ci_table_size(n) : 0ull));
+    const unsigned long long t2 = __builtin_readcyclecounter();
+    const int k = merged ? 0 : (append ? 2 : 1);
+    atomicAdd(&D.dbg[k], t1 - t0);       // filter cycles: merge / full / append
+    atomicAdd(&D.dbg[4 + k], 1ull);      // items
+    atomicAdd(&D.dbg[8], t2 - t1);       // index build cycles
+    atomicAdd(&D.dbg[9], (unsigned long long)n);
+    atomicAdd(&D.dbg[10], (unsigned long long)cv.y);
+  }
+}
+
+// one workgroup per CU, pulling slots from the worklist (160 KiB LDS each: one per CU)
+__global__ void __launch_bounds__(VX_THREADS) k_revox(MapperDev D) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
+  uint32_t* cur = lds + VX_LDS_WORDS - 3;  // free word of the VoxelGrid misc area
+  const uint32_t count = *D.rv_count;
+  while (true) {
+    __syncthreads();  // every thread has read `cur` of the previous item
+    if (threadIdx.x == 0) *cur = atomicAdd(D.rv_next, 1u);
+    __syncthreads();
+    const int it = (int)*cur;
+    if ((uint32_t)it >= count) break;
+    const int slot = D.rv_list[it] % INS_SLOTS, sm = D.rv_list[it] / INS_SLOTS;
+    int cube = 0, append = 0;
+    if (!revox_target(D, sm >> 1, sm & 1, slot, &cube, &append)) continue;
+    revox_item(D, sm >> 1, sm & 1, slot, cube, append, lds);
+  }
 }
 
 // cell index of one cube whose content was set through the API (cen: the host's grid centre)
@@ -810,6 +867,7 @@ struct loam_mapper {
   uint32_t* d_new_off = nullptr;
   std::vector<void*> allocs;
   uint32_t frame_counter = 0;
+  int n_cu = 256;  // compute units (grid of the worklist kernels)
   int lm_G = 0;  // workgroups per stream of k_lm_round (0: two-kernel path k_lm_eval / k_lm_step)
 };
 
@@ -912,6 +970,8 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
     int occ = 0, cus = 0;
     const char* env = std::getenv("LOAM_LM_PERSISTENT");
     const bool allow = !(env && env[0] == '0');
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+      h->n_cu = cus;
     if (allow && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_lm_round, LM_THREADS, 0) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess) {
       // 256 threads x 256 VGPRs: exactly one block per CU; the API can over-report by one
@@ -965,6 +1025,10 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
   ALLOC(D.ins_sorted, B * 2 * (size_t)D.max_in);
   ALLOC(D.ins_off, B * 2 * (size_t)(INS_SLOTS + 1));
   ALLOC(D.stable_tok, B * 2 * (size_t)NCUBE);
+  ALLOC(D.rv_list, B * 2 * (size_t)INS_SLOTS);
+  ALLOC(D.dbg, 16);
+  ALLOC(D.rv_count, 4);
+  D.rv_next = D.rv_count + 1;
   ALLOC(D.vx_pts, B * 2 * (size_t)D.scratch_cap);
   ALLOC(D.vx_idx, B * 2 * (size_t)D.scratch_cap);
   ALLOC(D.partials, B * (size_t)D.max_chunks * LM_NACC);
@@ -1201,7 +1265,9 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   LOAM_HIP(hipEventRecord(h->ev[2], st));
   LAUNCH(FAM_INSERT, k_insert<<<dim3(16, B), 256, 0, st>>>(D));
   LAUNCH(FAM_INSERT, k_bucket<<<B * 2, VX_THREADS, 0, st>>>(D));
-  LAUNCH(FAM_REVOX, k_revox<<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D));
+  LOAM_HIP(hipMemsetAsync(D.rv_count, 0, 2 * sizeof(uint32_t), st));
+  LAUNCH(FAM_REVOX, k_revox_list<<<(B * 2 * INS_SLOTS + 255) / 256, 256, 0, st>>>(D));
+  LAUNCH(FAM_REVOX, k_revox<<<h->n_cu, VX_THREADS, 0, st>>>(D));
   LOAM_HIP(hipGetLastError());
   LOAM_HIP(hipEventRecord(h->ev[3], st));
   LOAM_HIP(hipMemcpyAsync(h->hf.data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
@@ -1292,6 +1358,15 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     }
   }
   return status;
+}
+
+int32_t loam_mapper_debug_counters(loam_mapper* h, uint64_t* out, int32_t n, int32_t reset) {
+  if (!h || !out || n < 0 || n > 16) return LOAM_ERR_ARG;
+  LOAM_HIP(hipSetDevice(h->dev));
+  LOAM_HIP(hipStreamSynchronize(h->st));
+  LOAM_HIP(hipMemcpy(out, h->D.dbg, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
+  if (reset) LOAM_HIP(hipMemset(h->D.dbg, 0, sizeof(uint64_t) * 16));
+  return LOAM_OK;
 }
 
 int32_t loam_mapper_set_profiling(loam_mapper* h, int32_t enable) {

@@ -73,6 +73,11 @@ class BatchMapper:
         check(lib().loam_mapper_stats_all(self.h, out, self.n_streams))
         return list(out)
 
+    def debug_counters(self, reset=False):
+        out = np.zeros(16, dtype=np.uint64)
+        check(lib().loam_mapper_debug_counters(self.h, ptr(out), 16, int(reset)))
+        return out
+
     def solve(self):
         check(lib().loam_mapper_solve(self.h))
 
