@@ -132,8 +132,7 @@ def run_steps(mapper, plan, first, count):
     for k in range(first, first + count):
         mapper.input_device_batch(*plan[k])
         mapper.solve()
-        for st in mapper.stats_all():
-            iters += st.lm[0].iterations + st.lm[1].iterations
+        iters += mapper.total_iterations()
     return iters
 
 

@@ -182,6 +182,8 @@ int32_t loam_mapper_stats(loam_mapper* h, int32_t stream, loam_map_stats* st);
 /* device phase counters (diagnostics): [0..2] re-VoxelGrid cycles merge / full / append,
  * [4..6] items of each, [8] cell-index build cycles, [9] points indexed, [10] old points */
 int32_t loam_mapper_debug_counters(loam_mapper* h, uint64_t* out, int32_t n, int32_t reset);
+/* sum over all streams of the LM iterations (both rounds) of the last solve */
+int64_t loam_mapper_total_iterations(loam_mapper* h);
 /* stats of streams 0..n-1 */
 int32_t loam_mapper_stats_all(loam_mapper* h, loam_map_stats* out, int32_t n);
 

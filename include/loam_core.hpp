@@ -1,6 +1,7 @@
 // loam_core.hpp — header-only C++ shim over the C-ABI (loam_core.h) with the reference's
 // class and method names, for the lidar_odometry_mapping nodes:
 //   vloam::ScanRegistration  scan_registration.h:64-81   -> loam_amd::ScanRegistration
+//   vloam::LaserOdometry     laser_odometry.h:70-84      -> loam_amd::LaserOdometry
 //   vloam::LaserMapping      laser_mapping.h:85-100      -> loam_amd::LaserMapping
 // Clouds cross the boundary as packed float4 (x, y, z, intensity) arrays. pcl::PointXYZI
 // is 32 bytes, so the node packs and unpacks it (INTEGRATION.md shows the adapter). Errors
@@ -12,6 +13,7 @@
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "loam_core.h"
@@ -75,6 +77,57 @@ class ScanRegistration {
 
  private:
   loam_scanreg* h_ = nullptr;
+};
+
+// LaserOdometry::init / input / solveLO / output (laser_odometry.cpp:46-679), one stream
+class LaserOdometry {
+ public:
+  explicit LaserOdometry(const loam_params& p = default_params(), int32_t device = 0) {
+    check(loam_odometry_create(&p, device, 1, &h_));
+  }
+  ~LaserOdometry() { loam_odometry_destroy(h_); }
+  LaserOdometry(const LaserOdometry&) = delete;
+  LaserOdometry& operator=(const LaserOdometry&) = delete;
+
+  void init() { check(loam_odometry_reset(h_)); }
+  void reset() {}  // laser_odometry.cpp:128-135 clears per-frame buffers only
+  void input(const Cloud& sharp, const Cloud& less_sharp, const Cloud& flat, const Cloud& less_flat) {
+    check(loam_odometry_input(h_, 0, sharp.data(), n(sharp), less_sharp.data(), n(less_sharp), flat.data(), n(flat),
+                              less_flat.data(), n(less_flat)));
+  }
+  // features already in HBM (ScanRegistration::device_cloud)
+  void input_device(const float* sharp, int32_t ns, const float* less_sharp, int32_t nls, const float* flat,
+                    int32_t nf, const float* less_flat, int32_t nlf) {
+    check(loam_odometry_input_device(h_, 0, sharp, ns, less_sharp, nls, flat, nf, less_flat, nlf));
+  }
+  void solveLO() { check(loam_odometry_solve(h_)); }
+  // q_w_curr, t_w_curr, q_last_curr, t_last_curr, skip_frame (laser_odometry.cpp:660-679)
+  bool output(double q_w[4], double t_w[3], double q_lc[4] = nullptr, double t_lc[3] = nullptr) const {
+    int32_t skip = 0;
+    check(loam_odometry_output(h_, 0, q_w, t_w, q_lc, t_lc, &skip));
+    return skip != 0;
+  }
+  // laserCloudCornerLast (0) / laserCloudSurfLast (1) in HBM, valid until the next solve
+  std::pair<const float*, int32_t> last_cloud(int32_t which) const {
+    const float* p = nullptr;
+    const int32_t c = check(loam_odometry_last_cloud(h_, 0, which, &p));
+    return {p, c};
+  }
+  Cloud copy_last(int32_t which) const {
+    Cloud out(static_cast<size_t>(last_cloud(which).second) * 4);
+    if (!out.empty()) check(loam_odometry_copy_last(h_, 0, which, out.data(), static_cast<int32_t>(out.size() / 4)));
+    return out;
+  }
+  loam_odom_stats stats() const {
+    loam_odom_stats st;
+    check(loam_odometry_stats(h_, 0, &st));
+    return st;
+  }
+  loam_odometry* handle() const { return h_; }
+
+ private:
+  static int32_t n(const Cloud& c) { return static_cast<int32_t>(c.size() / 4); }
+  loam_odometry* h_ = nullptr;
 };
 
 // B independent LaserMapping instances in one handle (one launch sequence per solve)

@@ -16,6 +16,14 @@ int main(int argc, char** argv) {
     if (e.code() != LOAM_ERR_ARG) return 4;
   }
   try {
+    loam_amd::LaserOdometry o(p, 0);
+    double q[4], t[3];
+    o.output(q, t);
+    if (!expect_device) return 7;
+  } catch (const loam_amd::Error& e) {
+    if (expect_device || (e.code() != LOAM_ERR_NODEVICE && e.code() != LOAM_ERR_HIP)) return 8;
+  }
+  try {
     loam_amd::LaserMapping m(p, 0);
     double q[4] = {0, 0, 0, 1}, t[3] = {0, 0, 0};
     m.output(q, t);

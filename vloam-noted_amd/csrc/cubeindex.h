@@ -70,21 +70,21 @@ __device__ inline uint32_t ci_block_scan(uint32_t v, uint32_t* ws, uint32_t* tot
 // CI_LDS_MAX_T + nthreads / 64 + 1 words.  Cubes with 2n > CI_LDS_MAX_T build their
 // table in global memory.  Returns false if a cell holds more points than the entry can
 // count (2^14 - 1).
-template <int nthreads>
+template <int nthreads, int MAXT = CI_LDS_MAX_T>
 __device__ inline bool cube_index_build(const float4* pts, uint32_t n, const int corner[3], float4* cpts,
                                         uint2* ctab, uint32_t* lds) {
   const int tid = threadIdx.x;
   if (n == 0) return true;
   const uint32_t T = ci_table_size(n), mask = T - 1;
-  uint32_t* ws = lds + CI_LDS_MAX_T;
+  uint32_t* ws = lds + MAXT;
   const uint32_t chunk = (T + nthreads - 1) / nthreads;
   bool ok = true;
-  if (T <= (uint32_t)CI_LDS_MAX_T && n < (1u << 14)) {  // counts fit the packed word
+  if (T <= (uint32_t)MAXT && n < (1u << 14)) {  // counts fit the packed word
     uint32_t* lent = lds;  // key | count << 18 (count < n <= 2^14)
     for (uint32_t i = tid; i < T; i += nthreads) lent[i] = CI_EMPTY;
     __syncthreads();
     // 1. cells + per-point rank, kept in registers (n <= CI_LDS_MAX_T / 2 here)
-    constexpr int PER = (CI_LDS_MAX_T / 2 + nthreads - 1) / nthreads;
+    constexpr int PER = (MAXT / 2 + nthreads - 1) / nthreads;
     uint32_t sr[PER];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {

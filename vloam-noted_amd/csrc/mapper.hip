@@ -101,9 +101,6 @@ struct MapperDev {
   float4* ins_sorted;    // [B][2][max_in] inserted points grouped by target cube (input order kept)
   uint32_t* ins_off;     // [B][2][INS_SLOTS + 1] group offsets: window slots, then extra cubes
   unsigned long long* dbg;  // [16] phase cycle counters (loam_mapper_debug_counters)
-  uint32_t* rv_list;     // [B][2][INS_SLOTS] re-VoxelGrid worklist (stream, map, slot)
-  uint32_t* rv_count;    // [2]: worklist length, next item
-  uint32_t* rv_next;
   uint32_t* stable_tok;  // [B][2][NCUBE] arena offset + 1 of content known to be a VoxelGrid
                          // fixed point (re-filtering it is the identity), else 0
   float4* vx_pts;  // [B][2][scratch_cap]
@@ -631,21 +628,6 @@ __device__ inline bool revox_target(const MapperDev& D, int s, int m, int slot, 
   return true;
 }
 
-// worklist of the slots to re-filter (one thread per (stream, map, slot))
-__global__ void k_revox_list(MapperDev D) {
-  const int item = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool in = item < D.B * 2 * INS_SLOTS;
-  const int slot = in ? item % INS_SLOTS : 0, sm = in ? item / INS_SLOTS : 0;
-  int cube = 0, append = 0;
-  const bool work = in && revox_target(D, sm >> 1, sm & 1, slot, &cube, &append);
-  const uint64_t b = __ballot(work);
-  if (!b) return;
-  uint32_t base = 0;
-  if ((threadIdx.x & 63) == __ffsll((unsigned long long)b) - 1) base = atomicAdd(D.rv_count, (uint32_t)__popcll(b));
-  base = __shfl(base, __ffsll((unsigned long long)b) - 1, 64);
-  if (work) D.rv_list[base + __popcll(b & lanemask_lt())] = item;
-}
-
 __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube, int append, uint32_t* lds) {
   StreamFrame& F = D.fr[s];
   const uint32_t* ioff = D.ins_off + sm_index(s, m) * (INS_SLOTS + 1);
@@ -714,22 +696,13 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
   }
 }
 
-// one workgroup per CU, pulling slots from the worklist (160 KiB LDS each: one per CU)
+// one workgroup per (stream, map, slot); slots with nothing to do exit at once
 __global__ void __launch_bounds__(VX_THREADS) k_revox(MapperDev D) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
-  uint32_t* cur = lds + VX_LDS_WORDS - 3;  // free word of the VoxelGrid misc area
-  const uint32_t count = *D.rv_count;
-  while (true) {
-    __syncthreads();  // every thread has read `cur` of the previous item
-    if (threadIdx.x == 0) *cur = atomicAdd(D.rv_next, 1u);
-    __syncthreads();
-    const int it = (int)*cur;
-    if ((uint32_t)it >= count) break;
-    const int slot = D.rv_list[it] % INS_SLOTS, sm = D.rv_list[it] / INS_SLOTS;
-    int cube = 0, append = 0;
-    if (!revox_target(D, sm >> 1, sm & 1, slot, &cube, &append)) continue;
-    revox_item(D, sm >> 1, sm & 1, slot, cube, append, lds);
-  }
+  const int slot = blockIdx.x % INS_SLOTS, sm = blockIdx.x / INS_SLOTS;
+  int cube = 0, append = 0;
+  if (!revox_target(D, sm >> 1, sm & 1, slot, &cube, &append)) return;
+  revox_item(D, sm >> 1, sm & 1, slot, cube, append, lds);
 }
 
 // cell index of one cube whose content was set through the API (cen: the host's grid centre)
@@ -830,6 +803,34 @@ __global__ void k_compact_commit(MapperDev D, const int* pairs, int npairs, cons
 // ---------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------
+// page-locked host array (hipHostMalloc) with the few vector operations used here
+template <typename T>
+struct PinnedArray {
+  T* p = nullptr;
+  size_t n = 0;
+  ~PinnedArray() { release(); }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  bool assign(size_t count, const T& v) {
+    release();
+    if (hipHostMalloc(reinterpret_cast<void**>(&p), sizeof(T) * std::max<size_t>(count, 1), hipHostMallocDefault) !=
+        hipSuccess) {
+      p = nullptr;
+      return false;
+    }
+    n = count;
+    for (size_t i = 0; i < n; ++i) p[i] = v;
+    return true;
+  }
+  T& operator[](size_t i) { return p[i]; }
+  const T& operator[](size_t i) const { return p[i]; }
+  T* data() { return p; }
+  size_t size() const { return n; }
+};
+
 struct HostStream {
   double q_wmap_wodom[4] = {0, 0, 0, 1}, t_wmap_wodom[3] = {0, 0, 0};
   double q_wodom[4] = {0, 0, 0, 1}, t_wodom[3] = {0, 0, 0};
@@ -859,7 +860,7 @@ struct loam_mapper {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   MapperDev D{};
-  std::vector<StreamFrame> hf;
+  PinnedArray<StreamFrame> hf;  // pinned: the per-frame H2D / D2H of the stream records
   std::vector<HostStream> hs;
   uint2* cube_tab[2] = {nullptr, nullptr};
   int parity = 0;
@@ -1025,10 +1026,7 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
   ALLOC(D.ins_sorted, B * 2 * (size_t)D.max_in);
   ALLOC(D.ins_off, B * 2 * (size_t)(INS_SLOTS + 1));
   ALLOC(D.stable_tok, B * 2 * (size_t)NCUBE);
-  ALLOC(D.rv_list, B * 2 * (size_t)INS_SLOTS);
   ALLOC(D.dbg, 16);
-  ALLOC(D.rv_count, 4);
-  D.rv_next = D.rv_count + 1;
   ALLOC(D.vx_pts, B * 2 * (size_t)D.scratch_cap);
   ALLOC(D.vx_idx, B * 2 * (size_t)D.scratch_cap);
   ALLOC(D.partials, B * (size_t)D.max_chunks * LM_NACC);
@@ -1039,7 +1037,7 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
   ALLOC(h->d_new_off, B * 2 * (NCUBE + 1));
 #undef ALLOC
   D.cube_tab = h->cube_tab[0];
-  h->hf.assign(B, StreamFrame{});
+  if (!h->hf.assign(B, StreamFrame{})) return fail(LOAM_ERR_HIP);
   h->hs.assign(B, HostStream{});
   for (size_t s = 0; s < B; ++s) {
     StreamFrame& F = h->hf[s];
@@ -1175,6 +1173,13 @@ int32_t loam_mapper_input_device_batch(loam_mapper* h, int32_t n, const int32_t*
   return LOAM_OK;
 }
 
+int64_t loam_mapper_total_iterations(loam_mapper* h) {
+  if (!h) return LOAM_ERR_ARG;
+  int64_t it = 0;
+  for (int s = 0; s < h->B; ++s) it += h->hs[s].st.lm[0].iterations + h->hs[s].st.lm[1].iterations;
+  return it;
+}
+
 int32_t loam_mapper_stats_all(loam_mapper* h, loam_map_stats* out, int32_t n) {
   if (!h || !out || n < 0 || n > h->B) return LOAM_ERR_ARG;
   for (int s = 0; s < n; ++s) out[s] = h->hs[s].st;
@@ -1265,9 +1270,7 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   LOAM_HIP(hipEventRecord(h->ev[2], st));
   LAUNCH(FAM_INSERT, k_insert<<<dim3(16, B), 256, 0, st>>>(D));
   LAUNCH(FAM_INSERT, k_bucket<<<B * 2, VX_THREADS, 0, st>>>(D));
-  LOAM_HIP(hipMemsetAsync(D.rv_count, 0, 2 * sizeof(uint32_t), st));
-  LAUNCH(FAM_REVOX, k_revox_list<<<(B * 2 * INS_SLOTS + 255) / 256, 256, 0, st>>>(D));
-  LAUNCH(FAM_REVOX, k_revox<<<h->n_cu, VX_THREADS, 0, st>>>(D));
+  LAUNCH(FAM_REVOX, k_revox<<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D));
   LOAM_HIP(hipGetLastError());
   LOAM_HIP(hipEventRecord(h->ev[3], st));
   LOAM_HIP(hipMemcpyAsync(h->hf.data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));

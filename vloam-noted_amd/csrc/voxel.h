@@ -60,25 +60,30 @@ __device__ inline uint32_t vx_hash(uint32_t k) { return (k * 0x9E3779B1u) >> (32
 
 // block-wide exclusive scan of one value per thread (VX_THREADS); returns exclusive prefix,
 // total in *total.  ws: LDS scratch of >= VX_WAVES + 1 words.
-__device__ inline uint32_t vx_block_scan(uint32_t v, uint32_t* ws, uint32_t* total) {
+template <int NT>
+__device__ inline uint32_t vx_block_scan_t(uint32_t v, uint32_t* ws, uint32_t* total) {
+  constexpr int NW = NT / 64;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t inc = wave_incl_scan_u(v);
   if (lane == 63) ws[wid] = inc;
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t acc = 0;
-    for (int w = 0; w < VX_WAVES; ++w) {
+    for (int w = 0; w < NW; ++w) {
       uint32_t t = ws[w];
       ws[w] = acc;
       acc += t;
     }
-    ws[VX_WAVES] = acc;
+    ws[NW] = acc;
   }
   __syncthreads();
   uint32_t r = ws[wid] + inc - v;
-  *total = ws[VX_WAVES];
+  *total = ws[NW];
   __syncthreads();
   return r;
+}
+__device__ inline uint32_t vx_block_scan(uint32_t v, uint32_t* ws, uint32_t* total) {
+  return vx_block_scan_t<VX_THREADS>(v, ws, total);
 }
 
 struct VxGeom {
@@ -463,20 +468,20 @@ __device__ inline void vx_grouped(const VoxSeg& S, const VxGeom& g, const VxSrc&
 
 // bounding box (pcl::getMinMax3D) of the N points P(i) and the grid geometry of leaf -> M.g
 // (all threads; result valid after the trailing barrier)
-template <typename PF>
+template <typename PF, int NT = VX_THREADS>
 __device__ inline void vx_geometry(const PF& P, uint32_t N, float leaf, VxMisc& M) {
   const int tid = threadIdx.x;
   const int wid = tid >> 6, lane = tid & 63;
   float mnx = 3.402823466e38f, mny = 3.402823466e38f, mnz = 3.402823466e38f;
   float mxx = -3.402823466e38f, mxy = -3.402823466e38f, mxz = -3.402823466e38f;
-  for (uint32_t i0 = tid; i0 < N; i0 += VX_UNROLL * VX_THREADS) {
+  for (uint32_t i0 = tid; i0 < N; i0 += VX_UNROLL * NT) {
     float4 p[VX_UNROLL];
 #pragma unroll
     for (int u = 0; u < VX_UNROLL; ++u)
-      if (i0 + u * VX_THREADS < N) p[u] = P(i0 + u * VX_THREADS);
+      if (i0 + u * NT < N) p[u] = P(i0 + u * NT);
 #pragma unroll
     for (int u = 0; u < VX_UNROLL; ++u) {
-      if (i0 + u * VX_THREADS >= N) continue;
+      if (i0 + u * NT >= N) continue;
       mnx = fminf(mnx, p[u].x); mny = fminf(mny, p[u].y); mnz = fminf(mnz, p[u].z);
       mxx = fmaxf(mxx, p[u].x); mxy = fmaxf(mxy, p[u].y); mxz = fmaxf(mxz, p[u].z);
     }
@@ -491,7 +496,7 @@ __device__ inline void vx_geometry(const PF& P, uint32_t N, float leaf, VxMisc& 
   __syncthreads();
   VxGeom& sg = M.g;
   if (tid == 0) {
-    for (int w = 1; w < VX_WAVES; ++w) {
+    for (int w = 1; w < NT / 64; ++w) {
       mnx = fminf(mnx, sbb[w][0]); mny = fminf(mny, sbb[w][1]); mnz = fminf(mnz, sbb[w][2]);
       mxx = fmaxf(mxx, sbb[w][3]); mxy = fmaxf(mxy, sbb[w][4]); mxz = fmaxf(mxz, sbb[w][5]);
     }
@@ -654,30 +659,33 @@ __device__ inline void voxel_segment(const VoxSeg& S, uint32_t* lds) {
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t VX_MERGE_CAP = 4096;
 
+// NT threads, up to CAP new points, LW LDS words (scan scratch and misc in the last 256)
+template <int NT = VX_THREADS, int CAP = (int)VX_MERGE_CAP, int LW = VX_LDS_WORDS>
 __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
+  static_assert(6 * CAP + 64 <= LW - 256, "merge LDS layout");
   const int tid = threadIdx.x;
-  uint32_t* ws = lds + VX_LDS_WORDS - 256;
-  VxMisc& M = *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192);
+  uint32_t* ws = lds + LW - 256;
+  VxMisc& M = *reinterpret_cast<VxMisc*>(lds + LW - 192);
   const float4* C = S.src0;
   const float4* A = S.src1;
   const uint32_t n0 = (uint32_t)S.n0, n1 = (uint32_t)S.n1;
   auto P = [&](uint32_t i) -> float4 { return i < n0 ? C[i] : A[i - n0]; };
-  vx_geometry(P, n0 + n1, S.leaf, M);
+  vx_geometry<decltype(P), NT>(P, n0 + n1, S.leaf, M);
   const VxGeom g = M.g;
   if (g.overflow) return false;
-  uint64_t* sk = reinterpret_cast<uint64_t*>(lds);           // words [0, 8192)
-  uint32_t* cstart = lds + 8192;                             // [8192, 12289)
-  int* chit = reinterpret_cast<int*>(lds + 12352);           // [12352, 16448)
-  uint32_t* nhcell = lds + 16448;                            // [16448, 20544)
-  uint32_t* cbelow = lds + 20544;                            // [20544, 25664)
+  uint64_t* sk = reinterpret_cast<uint64_t*>(lds);           // 2 CAP words
+  uint32_t* cstart = lds + 2 * CAP;                          // CAP + 1
+  int* chit = reinterpret_cast<int*>(lds + 3 * CAP + 16);    // CAP
+  uint32_t* nhcell = lds + 4 * CAP + 16;                     // CAP
+  uint32_t* cbelow = lds + 5 * CAP + 16;                     // CAP + 1
   uint32_t npad = 1;
   while (npad < n1) npad <<= 1;
-  for (uint32_t i = tid; i < npad; i += VX_THREADS)
+  for (uint32_t i = tid; i < npad; i += NT)
     sk[i] = i < n1 ? ((uint64_t)vx_key(g, A[i]) << 32) | i : 0xFFFFFFFFFFFFFFFFull;
   __syncthreads();
   for (uint32_t k = 2; k <= npad; k <<= 1) {
     for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = tid; i < npad; i += VX_THREADS) {
+      for (uint32_t i = tid; i < npad; i += NT) {
         const uint32_t ixj = i ^ j;
         if (ixj > i) {
           const uint64_t a = sk[i], b = sk[ixj];
@@ -691,7 +699,7 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
     }
   }
   // runs of one voxel = the new voxels; their members are in input order
-  constexpr int PT = VX_MERGE_CAP / VX_THREADS;  // 4
+  constexpr int PT = CAP / NT;
   uint32_t fl[PT + 1], cnt = 0;
 #pragma unroll
   for (int e = 0; e < PT; ++e) {
@@ -700,7 +708,7 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
     cnt += fl[e];
   }
   uint32_t D;
-  uint32_t pre = vx_block_scan(cnt, ws, &D);
+  uint32_t pre = vx_block_scan_t<NT>(cnt, ws, &D);
 #pragma unroll
   for (int e = 0; e < PT; ++e)
     if (fl[e]) {
@@ -720,16 +728,16 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
     return (lo < D && ckey(lo) == key) ? (int)lo : -1;
   };
   // pass A: the C point (if any) of every new voxel
-  for (uint32_t k0 = tid; k0 < n0; k0 += VX_UNROLL * VX_THREADS) {
+  for (uint32_t k0 = tid; k0 < n0; k0 += VX_UNROLL * NT) {
     float4 c[VX_UNROLL];
 #pragma unroll
     for (int u = 0; u < VX_UNROLL; ++u)
-      if (k0 + u * VX_THREADS < n0) c[u] = C[k0 + u * VX_THREADS];
+      if (k0 + u * NT < n0) c[u] = C[k0 + u * NT];
 #pragma unroll
     for (int u = 0; u < VX_UNROLL; ++u) {
-      if (k0 + u * VX_THREADS >= n0) continue;
+      if (k0 + u * NT >= n0) continue;
       const int d = find(vx_key(g, c[u]));
-      if (d >= 0) chit[d] = (int)(k0 + u * VX_THREADS);
+      if (d >= 0) chit[d] = (int)(k0 + u * NT);
     }
   }
   __syncthreads();
@@ -742,11 +750,11 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
     cnt += fl[e];
   }
   uint32_t Dn;
-  pre = vx_block_scan(cnt, ws, &Dn);
+  pre = vx_block_scan_t<NT>(cnt, ws, &Dn);
 #pragma unroll
   for (int e = 0; e < PT; ++e)
     if (fl[e]) nhcell[pre++] = tid * PT + e;
-  for (uint32_t r = tid; r <= Dn; r += VX_THREADS) cbelow[r] = 0;
+  for (uint32_t r = tid; r <= Dn; r += NT) cbelow[r] = 0;
   if (tid == 0) {
     M.moved = 0;
     uint32_t b = S.tail ? atomicAdd(S.tail, n0 + Dn) : 0;
@@ -780,14 +788,14 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
     return make_float4(sx / fn, sy / fn, sz / fn, si / fn);
   };
   // pass B: C points at k + (new-only voxels before them); merged voxels re-averaged
-  for (uint32_t k0 = tid; k0 < n0; k0 += VX_UNROLL * VX_THREADS) {
+  for (uint32_t k0 = tid; k0 < n0; k0 += VX_UNROLL * NT) {
     float4 c[VX_UNROLL];
 #pragma unroll
     for (int u = 0; u < VX_UNROLL; ++u)
-      if (k0 + u * VX_THREADS < n0) c[u] = C[k0 + u * VX_THREADS];
+      if (k0 + u * NT < n0) c[u] = C[k0 + u * NT];
 #pragma unroll
     for (int u = 0; u < VX_UNROLL; ++u) {
-      const uint32_t k = k0 + u * VX_THREADS;
+      const uint32_t k = k0 + u * NT;
       if (k >= n0) continue;
       const uint32_t key = vx_key(g, c[u]);
       uint32_t lo = 0, hi = Dn;  // new-only voxels below key
@@ -807,7 +815,7 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
   }
   __syncthreads();
   // C points below new-only voxel r: inclusive prefix of cbelow (Dn + 1 <= 4097 entries)
-  constexpr int PB = 5;
+  constexpr int PB = (CAP + 1 + NT - 1) / NT;
   uint32_t cv[PB], csum = 0;
 #pragma unroll
   for (int e = 0; e < PB; ++e) {
@@ -816,7 +824,7 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
     csum += cv[e];
   }
   uint32_t ctot;
-  uint32_t cpre = vx_block_scan(csum, ws, &ctot);
+  uint32_t cpre = vx_block_scan_t<NT>(csum, ws, &ctot);
 #pragma unroll
   for (int e = 0; e < PB; ++e) {
     const uint32_t r = tid * PB + e;
@@ -824,7 +832,7 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
     if (r <= Dn) cbelow[r] = cpre;
   }
   __syncthreads();
-  for (uint32_t r = tid; r < Dn; r += VX_THREADS) {
+  for (uint32_t r = tid; r < Dn; r += NT) {
     const uint32_t d = nhcell[r];
     const float4 v = centroid(d, 0.f, 0.f, 0.f, 0.f, 0u);
     out[r + cbelow[r]] = v;

@@ -68,6 +68,10 @@ class BatchMapper:
         check(lib().loam_mapper_input_device_batch(self.h, len(st), ptr(st), ptr(cp), ptr(cn), ptr(sp),
                                                    ptr(sn), ptr(q), ptr(t)))
 
+    def total_iterations(self):
+        """sum of the LM iterations of every stream in the last solve"""
+        return check(lib().loam_mapper_total_iterations(self.h))
+
     def stats_all(self):
         out = (_core.MapStats * self.n_streams)()
         check(lib().loam_mapper_stats_all(self.h, out, self.n_streams))
