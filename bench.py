@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=150, help="untimed steps; they build the maps")
     ap.add_argument("--streams", type=int, default=128, help="mapping streams per GPU")
     ap.add_argument("--stride", type=int, default=1, help="frame offset between streams")
+    ap.add_argument("--map-points", type=int, default=4194304,
+                    help="max_map_points per stream and map (arena size; fewer compactions)")
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--n-az", type=int, default=2000)
     ap.add_argument("--cpu-frames", type=int, default=40, help="cpu_baseline timed frames (after warmup)")
@@ -205,7 +207,7 @@ def main():
     cpu_n = 0 if (args.no_cpu or world > 1 or rank != 0) else W + args.cpu_frames
     frames = make_frames(stream_seed(args.seed, rank), max(n_frames, cpu_n), args.n_az, local, keep_raw=cpu_n,
                          prior=args.prior)
-    mapper = BatchMapper(B, device=local)
+    mapper = BatchMapper(B, device=local, max_map_points=args.map_points)
 
     def barrier():
         torch.cuda.synchronize(local)

@@ -179,8 +179,12 @@ int32_t loam_mapper_solve(loam_mapper* h);
 /* pose after solveMapping: q_w_curr (xyzw), t_w_curr (laser_mapping.cpp:826-832) */
 int32_t loam_mapper_pose(loam_mapper* h, int32_t stream, double* q_w, double* t_w);
 int32_t loam_mapper_stats(loam_mapper* h, int32_t stream, loam_map_stats* st);
-/* device phase counters (diagnostics): [0..2] re-VoxelGrid cycles merge / full / append,
- * [4..6] items of each, [8] cell-index build cycles, [9] points indexed, [10] old points */
+/* device phase counters (diagnostics, n <= LOAM_DEBUG_COUNTERS): [0..2] re-VoxelGrid cycles
+ * merge / full / append, [3] new points of merged cubes, [4..6] items of each, [7] merges with
+ * more than 1024 new points, [8] cell-index build cycles, [9] points indexed, [10] old points,
+ * [11..14] merge phases (bounding box, hash + pass A, new-voxel sort, pass B), [16] cell-index
+ * hash phase, [17..21] LM round: leader eval, leader wait, reduce + step, passes, member wait */
+#define LOAM_DEBUG_COUNTERS 32
 int32_t loam_mapper_debug_counters(loam_mapper* h, uint64_t* out, int32_t n, int32_t reset);
 /* sum over all streams of the LM iterations (both rounds) of the last solve */
 int64_t loam_mapper_total_iterations(loam_mapper* h);

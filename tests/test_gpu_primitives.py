@@ -144,7 +144,8 @@ def test_voxel_grid_many_unique_voxels():
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
 
 
-@pytest.mark.parametrize("leaf,n_new", [(0.4, 300), (0.8, 1500), (0.4, 4096), (0.4, 5000)])
+@pytest.mark.parametrize("leaf,n_new", [(0.4, 1), (0.4, 65), (0.4, 300), (0.8, 1024), (0.4, 1025),
+                                        (0.8, 1500), (0.4, 2049), (0.4, 4096), (0.4, 5000)])
 def test_voxel_merge_bit_exact(frame_clouds, leaf, n_new):
     """map update path: VoxelGrid(fixed ++ added) with `fixed` a VoxelGrid fixed point; the merge
     kernel (n_new <= 4096) must equal the full filter bit for bit"""

@@ -72,56 +72,59 @@ __device__ inline uint32_t ci_block_scan(uint32_t v, uint32_t* ws, uint32_t* tot
 // count (2^14 - 1).
 template <int nthreads, int MAXT = CI_LDS_MAX_T>
 __device__ inline bool cube_index_build(const float4* pts, uint32_t n, const int corner[3], float4* cpts,
-                                        uint2* ctab, uint32_t* lds) {
+                                        uint2* ctab, uint32_t* lds, unsigned long long* prof = nullptr) {
   const int tid = threadIdx.x;
   if (n == 0) return true;
   const uint32_t T = ci_table_size(n), mask = T - 1;
   uint32_t* ws = lds + MAXT;
-  const uint32_t chunk = (T + nthreads - 1) / nthreads;
   bool ok = true;
+  if (prof && tid == 0 && T <= (uint32_t)MAXT && n < (1u << 14)) atomicAdd(prof, 0ull - __builtin_readcyclecounter());
   if (T <= (uint32_t)MAXT && n < (1u << 14)) {  // counts fit the packed word
     uint32_t* lent = lds;  // key | count << 18 (count < n <= 2^14)
     for (uint32_t i = tid; i < T; i += nthreads) lent[i] = CI_EMPTY;
     __syncthreads();
-    // 1. cells + per-point rank, kept in registers (n <= CI_LDS_MAX_T / 2 here)
+    // 1. cells + per-point rank, kept in registers (n <= MAXT / 2 here); the keys first, so
+    //    every load is in flight before the first LDS atomic
     constexpr int PER = (MAXT / 2 + nthreads - 1) / nthreads;
     uint32_t sr[PER];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const uint32_t i = tid + k * nthreads;
-      sr[k] = 0;
-      if (i < n) {
-        const uint32_t key = ci_local_key(pts[i], corner);
-        uint32_t h = ci_hash(key, mask);
-        uint32_t rank;
-        while (true) {
-          const uint32_t old = atomicCAS(&lent[h], CI_EMPTY, key | (1u << 18));
-          if (old == CI_EMPTY) {
-            rank = 0;
-            break;
-          }
-          if ((old & CI_KEY_MASK) == key) {
-            rank = atomicAdd(&lent[h], 1u << 18) >> 18;
-            break;
-          }
-          h = (h + 1) & mask;
+      sr[k] = i < n ? ci_local_key(pts[i], corner) : CI_EMPTY;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (sr[k] == CI_EMPTY) continue;
+      const uint32_t key = sr[k];
+      uint32_t h = ci_hash(key, mask);
+      uint32_t rank;
+      while (true) {
+        const uint32_t old = atomicCAS(&lent[h], CI_EMPTY, key | (1u << 18));
+        if (old == CI_EMPTY) {
+          rank = 0;
+          break;
         }
-        sr[k] = (h << 15) | rank;  // slot < 2^15, rank < n <= 2^14
+        if ((old & CI_KEY_MASK) == key) {
+          rank = atomicAdd(&lent[h], 1u << 18) >> 18;
+          break;
+        }
+        h = (h + 1) & mask;
       }
+      sr[k] = (h << 15) | rank;  // slot < 2^15, rank < n <= 2^14
     }
     __syncthreads();
-    // 2. starts: exclusive scan of the counts, chunk of consecutive slots per thread; the LDS
-    //    word becomes the start
+    if (prof && tid == 0) atomicAdd(prof, __builtin_readcyclecounter());  // minus the start below
+    // 2. starts: exclusive scan of the counts over the slots a thread owns (tid, tid + nthreads,
+    //    ...: the cells' order in cpts is free, and the table writes coalesce); the LDS word
+    //    becomes the start
     uint32_t sum = 0;
-    for (uint32_t k = 0; k < chunk; ++k) {
-      const uint32_t h = tid * chunk + k;
-      if (h < T && lent[h] != CI_EMPTY) sum += lent[h] >> 18;
+    for (uint32_t h = tid; h < T; h += nthreads) {
+      const uint32_t e = lent[h];
+      if (e != CI_EMPTY) sum += e >> 18;
     }
     uint32_t tot;
     uint32_t pre = ci_block_scan<nthreads>(sum, ws, &tot);
-    for (uint32_t k = 0; k < chunk; ++k) {
-      const uint32_t h = tid * chunk + k;
-      if (h >= T) break;
+    for (uint32_t h = tid; h < T; h += nthreads) {
       const uint32_t e = lent[h];
       ctab[h] = make_uint2(e, pre);
       lent[h] = pre;
@@ -155,15 +158,13 @@ __device__ inline bool cube_index_build(const float4* pts, uint32_t n, const int
   }
   __syncthreads();
   uint32_t sum = 0;
-  for (uint32_t k = 0; k < chunk; ++k) {
-    const uint32_t h = tid * chunk + k;
-    if (h < T && ctab[h].x != CI_EMPTY) sum += ctab[h].y;
+  for (uint32_t h = tid; h < T; h += nthreads) {
+    const uint2 e = ctab[h];
+    if (e.x != CI_EMPTY) sum += e.y;
   }
   uint32_t tot;
   uint32_t pre = ci_block_scan<nthreads>(sum, ws, &tot);
-  for (uint32_t k = 0; k < chunk; ++k) {
-    const uint32_t h = tid * chunk + k;
-    if (h >= T) break;
+  for (uint32_t h = tid; h < T; h += nthreads) {
     const uint2 e = ctab[h];
     if (e.x == CI_EMPTY) continue;
     ok &= e.y < (1u << 14);

@@ -73,10 +73,14 @@ __host__ __device__ inline void lm_init(LmState& S, const double* x7, int max_it
   S.passes = 0;
 }
 
-// one residual block at X: accumulates rho' J^T J, rho' J^T r, 1/2 rho, rows
+// one residual block at X: accumulates rho' J^T J, rho' J^T r, 1/2 rho, rows.  The library
+// is built with -ffp-contract=off (bit-exact VoxelGrid / kNN); here FMA contraction is allowed:
+// the LM sums are matched to a tolerance (their order already differs from the reference's),
+// and contraction halves the fp64 instructions of the accumulation, the bound of this loop.
 __device__ inline void lm_accum(int type, float px, float py, float pz, double a0, double a1,
                                 double a2, double b0, double b1, double b2, const double* X,
                                 double* acc) {
+#pragma clang fp contract(fast)
   dq q{X[0], X[1], X[2], X[3]};
   d3 Rp = qrot(q, d3{(double)px, (double)py, (double)pz});
   d3 lp{Rp.x + X[4], Rp.y + X[5], Rp.z + X[6]};
@@ -369,24 +373,37 @@ __device__ inline void lm_eval_sum(const LmRecView& R, int nrec, const double* X
 #pragma unroll
   for (int i = 0; i < LM_NACC; ++i) acc[i] = 0.0;
   const int stride = nblk * kThreads;
-  for (int r = blk * kThreads + tid; r < nrec; r += 2 * stride) {
-    int t[2];
-    float px[2], py[2], pz[2];
-    double a0[2], a1[2], a2[2], b0[2], b1[2], b2[2];
+  // software pipeline: the next two records are loaded while the current two are evaluated
+  struct Rec {
+    int t;
+    float px, py, pz;
+    double a0, a1, a2, b0, b1, b2;
+  };
+  auto load = [&](Rec* q, int r) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int rr = r + u * stride;
-      t[u] = 0;
+      q[u].t = 0;
       if (rr < nrec) {
-        t[u] = R.type[rr];
-        px[u] = R.px[rr]; py[u] = R.py[rr]; pz[u] = R.pz[rr];
-        a0[u] = R.a0[rr]; a1[u] = R.a1[rr]; a2[u] = R.a2[rr];
-        b0[u] = R.b0[rr]; b1[u] = R.b1[rr]; b2[u] = R.b2[rr];
+        q[u].t = R.type[rr];
+        q[u].px = R.px[rr]; q[u].py = R.py[rr]; q[u].pz = R.pz[rr];
+        q[u].a0 = R.a0[rr]; q[u].a1 = R.a1[rr]; q[u].a2 = R.a2[rr];
+        q[u].b0 = R.b0[rr]; q[u].b1 = R.b1[rr]; q[u].b2 = R.b2[rr];
       }
     }
+  };
+  Rec cur[2], nxt[2];
+  const int r0 = blk * kThreads + tid;
+  load(cur, r0);
+  for (int r = r0; r < nrec; r += 2 * stride) {
+    load(nxt, r + 2 * stride);
 #pragma unroll
     for (int u = 0; u < 2; ++u)
-      if (t[u] != 0) lm_accum(t[u], px[u], py[u], pz[u], a0[u], a1[u], a2[u], b0[u], b1[u], b2[u], X, acc);
+      if (cur[u].t != 0)
+        lm_accum(cur[u].t, cur[u].px, cur[u].py, cur[u].pz, cur[u].a0, cur[u].a1, cur[u].a2, cur[u].b0, cur[u].b1,
+                 cur[u].b2, X, acc);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) cur[u] = nxt[u];
   }
 #pragma unroll
   for (int i = 0; i < LM_NACC; ++i) {
@@ -490,6 +507,8 @@ struct LmJob {
   double* best_out;   // [7] pose written when the solve terminates
   int* err;
   int err_code;
+  unsigned long long* prof = nullptr;  // optional cycles: [0] leader eval, [1] leader wait,
+                                       // [2] reduce + step, [3] passes, [4] member wait for x
 };
 
 template <int kThreads>
@@ -514,6 +533,7 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
   }
   __syncthreads();
   bool aborted = false;
+  unsigned long long t0 = 0;
   for (int pass = 0; pass < LM_MAX_PASSES; ++pass) {
     // ---- evaluation point of this pass
     if (g == 0) {
@@ -530,6 +550,7 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
       }
     } else {
       if (tid == 0) {
+        t0 = __builtin_readcyclecounter();
         if (lm_spin_ge(&sync[1], (uint32_t)(pass + 1))) {
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -539,10 +560,12 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
           atomicOr(J.err, J.err_code);
           sstat = LM_DONE;
         }
+        if (J.prof) atomicAdd(&J.prof[4], __builtin_readcyclecounter() - t0);
       }
       __syncthreads();
     }
     if (sstat == LM_DONE) break;
+    if (g == 0 && tid == 0) t0 = __builtin_readcyclecounter();
     double X[7];
 #pragma unroll
     for (int i = 0; i < 7; ++i) X[i] = sx[i];
@@ -560,6 +583,12 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
       continue;
     }
     // ---- leader: gather the partials, step
+    if (tid == 0 && J.prof) {
+      const unsigned long long t1 = __builtin_readcyclecounter();
+      atomicAdd(&J.prof[0], t1 - t0);
+      atomicAdd(&J.prof[3], 1ull);
+      t0 = t1;
+    }
     if (tid == 0 && G > 1) {
       if (lm_spin_ge(&sync[0], (uint32_t)(pass + 1) * (uint32_t)(G - 1))) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -569,25 +598,27 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
         sstat = -1;
       }
     }
+    if (tid == 0 && J.prof) {
+      const unsigned long long t1 = __builtin_readcyclecounter();
+      atomicAdd(&J.prof[1], t1 - t0);
+      t0 = t1;
+    }
     __syncthreads();
     if (sstat == -1) {
       aborted = true;
       break;
     }
     if (wid == 0) {
-      double v[LM_NACC];
-#pragma unroll
-      for (int i = 0; i < LM_NACC; ++i) v[i] = lane == 0 ? bsum[i] : 0.0;
-      for (int c = lane; c < G; c += 64) {
-        if (c == 0) continue;
-#pragma unroll
-        for (int i = 0; i < LM_NACC; ++i) v[i] += part[(size_t)c * LM_NACC + i];
+      // lane i sums accumulator i over the workgroups in order (G <= 16: one lane per
+      // accumulator beats a shuffle tree per accumulator)
+      if (lane < LM_NACC) {
+        double v = bsum[lane];
+        for (int c = 1; c < G; ++c) v += part[(size_t)c * LM_NACC + lane];
+        sred[lane] = v;
       }
-#pragma unroll
-      for (int i = 0; i < LM_NACC; ++i) {
-        const double t = wave_sum_d(v[i]);
-        if (lane == 0) sred[i] = t;
-      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       if (lane == 0) {
         LmState L = ls;  // registers for the dependent chain
         lm_step(L, sred);
@@ -595,6 +626,7 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
       }
     }
     __syncthreads();
+    if (tid == 0 && J.prof) atomicAdd(&J.prof[2], __builtin_readcyclecounter() - t0);
   }
   if (g != 0) return;
   if (aborted && tid == 0) {  // stop this stream's LM where it is (best so far)

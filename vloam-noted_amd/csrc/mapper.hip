@@ -100,7 +100,7 @@ struct MapperDev {
   int* ins_tag;
   float4* ins_sorted;    // [B][2][max_in] inserted points grouped by target cube (input order kept)
   uint32_t* ins_off;     // [B][2][INS_SLOTS + 1] group offsets: window slots, then extra cubes
-  unsigned long long* dbg;  // [16] phase cycle counters (loam_mapper_debug_counters)
+  unsigned long long* dbg;  // [LOAM_DEBUG_COUNTERS] phase cycle counters (loam_mapper_debug_counters)
   uint32_t* stable_tok;  // [B][2][NCUBE] arena offset + 1 of content known to be a VoxelGrid
                          // fixed point (re-filtering it is the identity), else 0
   float4* vx_pts;  // [B][2][scratch_cap]
@@ -480,6 +480,7 @@ __global__ void __launch_bounds__(LM_THREADS) k_lm_round(MapperDev D, int round,
   J.best_out = F.pose;
   J.err = &F.err;
   J.err_code = MAP_ERR_LM_SYNC;
+  J.prof = D.dbg + 17;
   lm_round_device<LM_THREADS>(J, g, G);
 }
 
@@ -656,6 +657,7 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
   S.scratch_tail = &F.scratch_tail[m];
   S.scratch_cap = D.scratch_cap;
   S.err = &F.err;
+  S.prof = D.dbg + 11;  // merge phases: dbg[11..15]
   bool done = false;
   const unsigned long long t0 = __builtin_readcyclecounter();
   if (!append && n_new > 0 && n_new <= VX_MERGE_CAP && cv.y > 0 && *tok == cv.x + 1) {
@@ -679,7 +681,8 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
   int corner[3];
   cube_corner(cube, F.cen, corner);
   if (!cube_index_build<VX_THREADS>(ar + off, n, corner, carena_base(D, s, m, F.arena_active[m]) + off,
-                                    ctab_base(D, s, m, F.arena_active[m]) + 4 * (size_t)off, lds) &&
+                                    ctab_base(D, s, m, F.arena_active[m]) + 4 * (size_t)off, lds,
+                                    D.dbg + 16) &&
       threadIdx.x == 0)
     atomicOr(&F.err, MAP_ERR_INDEX);
   // read old content + new points, write the filtered cube, then its index (read it, write
@@ -693,6 +696,10 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
     atomicAdd(&D.dbg[8], t2 - t1);       // index build cycles
     atomicAdd(&D.dbg[9], (unsigned long long)n);
     atomicAdd(&D.dbg[10], (unsigned long long)cv.y);
+    if (merged) {
+      atomicAdd(&D.dbg[3], (unsigned long long)n_new);           // new points of merged cubes
+      if (n_new > VX_THREADS) atomicAdd(&D.dbg[7], 1ull);        // merges past the rank sort
+    }
   }
 }
 
@@ -869,6 +876,10 @@ struct loam_mapper {
   std::vector<void*> allocs;
   uint32_t frame_counter = 0;
   int n_cu = 256;  // compute units (grid of the worklist kernels)
+  // compact an arena once its tail passes this: one frame writes at most the window content
+  // (<= max_submap_points) plus the stack (<= max_input_points) plus the few cubes outside
+  // the window that receive points; a write past the capacity is reported (err flags)
+  uint32_t compact_at = 0;
   int lm_G = 0;  // workgroups per stream of k_lm_round (0: two-kernel path k_lm_eval / k_lm_step)
 };
 
@@ -964,6 +975,10 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
   D.map_cap = h->P.max_map_points;
   D.sub_cap = h->P.max_submap_points;
   D.scratch_cap = D.sub_cap + D.max_in;
+  {
+    const uint64_t cap = (uint64_t)D.map_cap, margin = (uint64_t)D.sub_cap + 2ull * D.max_in;
+    h->compact_at = (uint32_t)std::max<uint64_t>(cap / 2, cap > margin ? cap - margin : 0);
+  }
   D.max_chunks = LM_EBLK;
   {
     // k_lm_round needs every workgroup resident: G per stream with B * G <= CUs x blocks/CU.
@@ -980,6 +995,8 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
       occ = std::min(occ, 1);
       const int cap = occ * cus;
       h->lm_G = std::min(LM_EBLK, std::min(16, cap / n_streams));
+      const char* genv = std::getenv("LOAM_LM_G");  // measurement override (clamped to the cap)
+      if (genv && std::atoi(genv) > 0) h->lm_G = std::min(h->lm_G, std::atoi(genv));
     }
   }
   D.leaf[0] = (float)h->P.mapping_line_resolution;
@@ -1026,7 +1043,7 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
   ALLOC(D.ins_sorted, B * 2 * (size_t)D.max_in);
   ALLOC(D.ins_off, B * 2 * (size_t)(INS_SLOTS + 1));
   ALLOC(D.stable_tok, B * 2 * (size_t)NCUBE);
-  ALLOC(D.dbg, 16);
+  ALLOC(D.dbg, LOAM_DEBUG_COUNTERS);
   ALLOC(D.vx_pts, B * 2 * (size_t)D.scratch_cap);
   ALLOC(D.vx_idx, B * 2 * (size_t)D.scratch_cap);
   ALLOC(D.partials, B * (size_t)D.max_chunks * LM_NACC);
@@ -1340,7 +1357,7 @@ int32_t loam_mapper_solve(loam_mapper* h) {
       status = LOAM_ERR_CAPACITY;
     }
     for (int m = 0; m < 2; ++m)
-      if (F.arena_tail[m] > (uint32_t)D.map_cap / 2) pairs.push_back(s * 2 + m);
+      if (F.arena_tail[m] > h->compact_at) pairs.push_back(s * 2 + m);
   }
   if (!pairs.empty()) {
     const int np = (int)pairs.size();
@@ -1354,8 +1371,8 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     LOAM_HIP(hipStreamSynchronize(st));
     for (int p : pairs) {
       const StreamFrame& F = h->hf[p >> 1];
-      if (F.arena_tail[p & 1] > (uint32_t)D.map_cap / 2) {
-        set_error("loam_mapper_solve: live map exceeds half of max_map_points");
+      if (F.arena_tail[p & 1] > h->compact_at) {
+        set_error("loam_mapper_solve: live map exceeds the compaction threshold of max_map_points");
         status = LOAM_ERR_CAPACITY;
       }
     }
@@ -1364,11 +1381,11 @@ int32_t loam_mapper_solve(loam_mapper* h) {
 }
 
 int32_t loam_mapper_debug_counters(loam_mapper* h, uint64_t* out, int32_t n, int32_t reset) {
-  if (!h || !out || n < 0 || n > 16) return LOAM_ERR_ARG;
+  if (!h || !out || n < 0 || n > LOAM_DEBUG_COUNTERS) return LOAM_ERR_ARG;
   LOAM_HIP(hipSetDevice(h->dev));
   LOAM_HIP(hipStreamSynchronize(h->st));
   LOAM_HIP(hipMemcpy(out, h->D.dbg, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
-  if (reset) LOAM_HIP(hipMemset(h->D.dbg, 0, sizeof(uint64_t) * 16));
+  if (reset) LOAM_HIP(hipMemset(h->D.dbg, 0, sizeof(uint64_t) * LOAM_DEBUG_COUNTERS));
   return LOAM_OK;
 }
 

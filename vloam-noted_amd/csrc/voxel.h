@@ -54,9 +54,24 @@ struct VoxSeg {
   uint32_t* scratch_tail; // if set, scratch slots are allocated from it (per segment)
   uint32_t scratch_cap;
   int* err;
+  unsigned long long* prof = nullptr;  // optional: merge phase cycles [bbox, sort, runs, pass A, pass B]
 };
 
+// thread 0 adds the cycles since *t to prof[k] and restarts *t (phase counters; call after a barrier)
+__device__ inline void vx_phase(unsigned long long* prof, int k, unsigned long long* t) {
+  if (!prof || threadIdx.x != 0) return;
+  const unsigned long long now = __builtin_readcyclecounter();
+  atomicAdd(&prof[k], now - *t);
+  *t = now;
+}
+
 __device__ inline uint32_t vx_hash(uint32_t k) { return (k * 0x9E3779B1u) >> (32 - 14); }
+// slot of key k in a power-of-two table (mask = size - 1)
+__device__ inline uint32_t vx_slot(uint32_t k, uint32_t mask) {
+  uint32_t h = k * 0x9E3779B1u;
+  h ^= h >> 15;
+  return h & mask;
+}
 
 // block-wide exclusive scan of one value per thread (VX_THREADS); returns exclusive prefix,
 // total in *total.  ws: LDS scratch of >= VX_WAVES + 1 words.
@@ -466,26 +481,13 @@ __device__ inline void vx_grouped(const VoxSeg& S, const VxGeom& g, const VxSrc&
   }
 }
 
-// bounding box (pcl::getMinMax3D) of the N points P(i) and the grid geometry of leaf -> M.g
-// (all threads; result valid after the trailing barrier)
-template <typename PF, int NT = VX_THREADS>
-__device__ inline void vx_geometry(const PF& P, uint32_t N, float leaf, VxMisc& M) {
+// block min/max of the per-thread bounds and the grid geometry of leaf -> M.g (all threads;
+// result valid after the trailing barrier)
+template <int NT = VX_THREADS>
+__device__ inline void vx_geometry_finish(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
+                                          float leaf, VxMisc& M) {
   const int tid = threadIdx.x;
   const int wid = tid >> 6, lane = tid & 63;
-  float mnx = 3.402823466e38f, mny = 3.402823466e38f, mnz = 3.402823466e38f;
-  float mxx = -3.402823466e38f, mxy = -3.402823466e38f, mxz = -3.402823466e38f;
-  for (uint32_t i0 = tid; i0 < N; i0 += VX_UNROLL * NT) {
-    float4 p[VX_UNROLL];
-#pragma unroll
-    for (int u = 0; u < VX_UNROLL; ++u)
-      if (i0 + u * NT < N) p[u] = P(i0 + u * NT);
-#pragma unroll
-    for (int u = 0; u < VX_UNROLL; ++u) {
-      if (i0 + u * NT >= N) continue;
-      mnx = fminf(mnx, p[u].x); mny = fminf(mny, p[u].y); mnz = fminf(mnz, p[u].z);
-      mxx = fmaxf(mxx, p[u].x); mxy = fmaxf(mxy, p[u].y); mxz = fmaxf(mxz, p[u].z);
-    }
-  }
   mnx = wave_min_f(mnx); mny = wave_min_f(mny); mnz = wave_min_f(mnz);
   mxx = wave_max_f(mxx); mxy = wave_max_f(mxy); mxz = wave_max_f(mxz);
   float (*sbb)[6] = M.bb;
@@ -519,6 +521,27 @@ __device__ inline void vx_geometry(const PF& P, uint32_t N, float leaf, VxMisc& 
     sg = g;
   }
   __syncthreads();
+}
+
+// bounding box (pcl::getMinMax3D) of the N points P(i) and the grid geometry of leaf -> M.g
+template <typename PF, int NT = VX_THREADS>
+__device__ inline void vx_geometry(const PF& P, uint32_t N, float leaf, VxMisc& M) {
+  const int tid = threadIdx.x;
+  float mnx = 3.402823466e38f, mny = 3.402823466e38f, mnz = 3.402823466e38f;
+  float mxx = -3.402823466e38f, mxy = -3.402823466e38f, mxz = -3.402823466e38f;
+  for (uint32_t i0 = tid; i0 < N; i0 += VX_UNROLL * NT) {
+    float4 p[VX_UNROLL];
+#pragma unroll
+    for (int u = 0; u < VX_UNROLL; ++u)
+      if (i0 + u * NT < N) p[u] = P(i0 + u * NT);
+#pragma unroll
+    for (int u = 0; u < VX_UNROLL; ++u) {
+      if (i0 + u * NT >= N) continue;
+      mnx = fminf(mnx, p[u].x); mny = fminf(mny, p[u].y); mnz = fminf(mnz, p[u].z);
+      mxx = fmaxf(mxx, p[u].x); mxy = fmaxf(mxy, p[u].y); mxz = fmaxf(mxz, p[u].z);
+    }
+  }
+  vx_geometry_finish<NT>(mnx, mny, mnz, mxx, mxy, mxz, leaf, M);
 }
 
 // The workgroup routine.  lds: VX_LDS_WORDS u32 words (the whole 160 KiB; the last 256 words
@@ -646,6 +669,72 @@ __device__ inline void voxel_segment(const VoxSeg& S, uint32_t* lds) {
   vx_grouped(S, g, src, N, members, lds, ws, M);
 }
 
+// Block bitonic sort of npad (a power of two, 64 <= npad <= E NT) 64-bit keys held in registers:
+// element i = (wave * E + e) * 64 + lane.  Partners closer than 64 are exchanged by lane
+// shuffles, partners within a lane's E registers directly; only partners in another wave go
+// through LDS (xb0 / xb1: npad u64 each, alternating, one barrier per such stage).  Waves past
+// npad / (64 E) take part in the barriers only.  key(i) gives the key of element i (~0 for
+// padding; it may read LDS that sk / xb0 / xb1 alias); the sorted keys end in sk[0 .. npad).
+template <int NT, int E, typename KF>
+__device__ inline void vx_bitonic_regs(uint64_t* sk, uint64_t* xb0, uint64_t* xb1, uint32_t npad, const KF& key) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const bool active = (uint32_t)(w * E * 64) < npad;
+  uint64_t v[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) v[e] = active ? key((uint32_t)((w * E + e) * 64 + lane)) : ~0ull;
+  __syncthreads();  // the key source may alias sk / xb0 / xb1
+  int buf = 0;
+  for (uint32_t k = 2; k <= npad; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      if (j >= 64u * E) {  // partner in another wave
+        uint64_t* xb = buf ? xb1 : xb0;
+        buf ^= 1;
+        if (active) {
+#pragma unroll
+          for (int e = 0; e < E; ++e) xb[(w * E + e) * 64 + lane] = v[e];
+        }
+        __syncthreads();
+        if (active) {
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const uint32_t i = (uint32_t)((w * E + e) * 64 + lane);
+            const uint64_t p = xb[i ^ j];
+            const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+            v[e] = keep_min ? (v[e] < p ? v[e] : p) : (v[e] < p ? p : v[e]);
+          }
+        }
+      } else if (j >= 64) {  // partner in this lane's registers
+        const int ej = (int)(j >> 6);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int f = e ^ ej;
+          if (f > e) {
+            const uint32_t i = (uint32_t)((w * E + e) * 64 + lane);
+            const uint64_t a = v[e], b = v[f];
+            const bool asc = (i & k) == 0;  // i < partner here
+            v[e] = asc ? (a < b ? a : b) : (a < b ? b : a);
+            v[f] = asc ? (a < b ? b : a) : (a < b ? a : b);
+          }
+        }
+      } else if (active) {  // partner in this wave
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const uint32_t i = (uint32_t)((w * E + e) * 64 + lane);
+          const uint64_t p = __shfl_xor(v[e], (int)j, 64);
+          const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+          v[e] = keep_min ? (v[e] < p ? v[e] : p) : (v[e] < p ? p : v[e]);
+        }
+      }
+    }
+  }
+  __syncthreads();  // the last cross-wave buffer may alias sk
+  if (active) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) sk[(w * E + e) * 64 + lane] = v[e];
+  }
+  __syncthreads();
+}
+
 // ---------------------------------------------------------------------------------------
 // VoxelGrid of C ++ A where C (src0, n0 points) is already a fixed point of the filter (at
 // most one point per voxel, in voxel order: a previous output whose centroids all stayed in
@@ -654,106 +743,162 @@ __device__ inline void voxel_segment(const VoxSeg& S, uint32_t* lds) {
 //   voxels holding only a C point      -> that point, unchanged ((0 + c) / 1 == c)
 //   voxels holding C point c and A's   -> (0 + c + a1 + a2 ...) / n, A in input order
 //   voxels holding only A points       -> (0 + a1 + ...) / n, inserted in voxel order
-// A is sorted by (voxel, input index) in LDS; C is streamed twice.  Returns false, with
-// nothing written, when the grid overflows (the caller then runs the full filter).
+// A's voxels go into an LDS hash (with member lists); C points look themselves up in it.  Only
+// the voxels holding A points alone need sorting, and there are few: the map is dense where
+// new points land.  Returns false, with nothing written, when the grid overflows (the caller
+// then runs the full filter).
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t VX_MERGE_CAP = 4096;
 
 // NT threads, up to CAP new points, LW LDS words (scan scratch and misc in the last 256)
 template <int NT = VX_THREADS, int CAP = (int)VX_MERGE_CAP, int LW = VX_LDS_WORDS>
 __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
-  static_assert(6 * CAP + 64 <= LW - 256, "merge LDS layout");
+  constexpr int TMAX = 2 * CAP;       // hash slots (load factor <= 1/2)
+  constexpr int RX = 2 * TMAX + CAP;  // start of the shared region: C hits, then the sort
+  static_assert(RX + 4 * CAP <= LW - 256, "merge LDS layout");
+  static_assert(CAP <= 4 * NT && (CAP & (CAP - 1)) == 0, "merge: at most 4 new points per thread");
+  constexpr int U = VX_UNROLL;       // C points per thread kept in registers
+  constexpr int UA = CAP / NT;       // A points per thread
+  constexpr int SPT = TMAX / NT;     // hash slots per thread
+  static_assert(SPT <= 32, "new-only flags in one word");
+  constexpr uint32_t NONE = 0xFFFFFFFFu;
   const int tid = threadIdx.x;
   uint32_t* ws = lds + LW - 256;
   VxMisc& M = *reinterpret_cast<VxMisc*>(lds + LW - 192);
   const float4* C = S.src0;
   const float4* A = S.src1;
   const uint32_t n0 = (uint32_t)S.n0, n1 = (uint32_t)S.n1;
-  auto P = [&](uint32_t i) -> float4 { return i < n0 ? C[i] : A[i - n0]; };
-  vx_geometry<decltype(P), NT>(P, n0 + n1, S.leaf, M);
+  unsigned long long tp = __builtin_readcyclecounter();
+  // C points tid + u NT (u < U) and A points tid + u NT (u < UA) stay in registers
+  float4 cc[U], aa[UA];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (tid + u * NT < n0) cc[u] = C[tid + u * NT];
+#pragma unroll
+  for (int u = 0; u < UA; ++u)
+    if (tid + u * NT < n1) aa[u] = A[tid + u * NT];
+  {
+    float mnx = 3.402823466e38f, mny = 3.402823466e38f, mnz = 3.402823466e38f;
+    float mxx = -3.402823466e38f, mxy = -3.402823466e38f, mxz = -3.402823466e38f;
+    auto acc = [&](const float4& p) {
+      mnx = fminf(mnx, p.x); mny = fminf(mny, p.y); mnz = fminf(mnz, p.z);
+      mxx = fmaxf(mxx, p.x); mxy = fmaxf(mxy, p.y); mxz = fmaxf(mxz, p.z);
+    };
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (tid + u * NT < n0) acc(cc[u]);
+    for (uint32_t k = tid + U * NT; k < n0; k += NT) acc(C[k]);
+#pragma unroll
+    for (int u = 0; u < UA; ++u)
+      if (tid + u * NT < n1) acc(aa[u]);
+    vx_geometry_finish<NT>(mnx, mny, mnz, mxx, mxy, mxz, S.leaf, M);
+  }
   const VxGeom g = M.g;
+  vx_phase(S.prof, 0, &tp);
   if (g.overflow) return false;
-  uint64_t* sk = reinterpret_cast<uint64_t*>(lds);           // 2 CAP words
-  uint32_t* cstart = lds + 2 * CAP;                          // CAP + 1
-  int* chit = reinterpret_cast<int*>(lds + 3 * CAP + 16);    // CAP
-  uint32_t* nhcell = lds + 4 * CAP + 16;                     // CAP
-  uint32_t* cbelow = lds + 5 * CAP + 16;                     // CAP + 1
-  uint32_t npad = 1;
-  while (npad < n1) npad <<= 1;
-  for (uint32_t i = tid; i < npad; i += NT)
-    sk[i] = i < n1 ? ((uint64_t)vx_key(g, A[i]) << 32) | i : 0xFFFFFFFFFFFFFFFFull;
+  uint32_t T = 64;
+  while (T < 2 * n1) T <<= 1;
+  const uint32_t mask = T - 1;
+  uint32_t* hkey = lds;                                   // T: voxel key
+  uint32_t* hcnt = lds + TMAX;                            // T: member count, then start << 13 | count
+  uint32_t* mem = lds + 2 * TMAX;                         // n1: members, grouped by voxel
+  int* hit = reinterpret_cast<int*>(lds + RX);            // T: the C point of the voxel, or -1
+  uint64_t* srt = reinterpret_cast<uint64_t*>(lds + RX);  // later: the new-only voxels (key, slot)
+  for (uint32_t h = tid; h < T; h += NT) {
+    hkey[h] = NONE;
+    hcnt[h] = 0;
+    hit[h] = -1;
+  }
   __syncthreads();
-  for (uint32_t k = 2; k <= npad; k <<= 1) {
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = tid; i < npad; i += NT) {
-        const uint32_t ixj = i ^ j;
-        if (ixj > i) {
-          const uint64_t a = sk[i], b = sk[ixj];
-          if ((a > b) == ((i & k) == 0)) {
-            sk[i] = b;
-            sk[ixj] = a;
-          }
-        }
-      }
-      __syncthreads();
+  // 1. A's voxels: slot and rank of every new point
+  uint32_t ar[UA];
+#pragma unroll
+  for (int u = 0; u < UA; ++u) {
+    ar[u] = NONE;
+    if (tid + u * NT >= n1) continue;
+    const uint32_t key = vx_key(g, aa[u]);
+    uint32_t h = vx_slot(key, mask);
+    while (true) {
+      const uint32_t old = atomicCAS(&hkey[h], NONE, key);
+      if (old == NONE || old == key) break;
+      h = (h + 1) & mask;
+    }
+    ar[u] = (h << 13) | atomicAdd(&hcnt[h], 1u);  // h < 2^14, rank < 2^13
+  }
+  __syncthreads();
+  // 2. member ranges (slots tid, tid + NT, ...) and the members
+  {
+    uint32_t sum = 0;
+    for (uint32_t h = tid; h < T; h += NT) sum += hcnt[h];
+    uint32_t tot;
+    uint32_t pre = vx_block_scan_t<NT>(sum, ws, &tot);
+    for (uint32_t h = tid; h < T; h += NT) {
+      const uint32_t c = hcnt[h];
+      hcnt[h] = (pre << 13) | c;
+      pre += c;
     }
   }
-  // runs of one voxel = the new voxels; their members are in input order
-  constexpr int PT = CAP / NT;
-  uint32_t fl[PT + 1], cnt = 0;
-#pragma unroll
-  for (int e = 0; e < PT; ++e) {
-    const uint32_t t = tid * PT + e;
-    fl[e] = (t < n1 && (t == 0 || (sk[t] >> 32) != (sk[t - 1] >> 32))) ? 1u : 0u;
-    cnt += fl[e];
-  }
-  uint32_t D;
-  uint32_t pre = vx_block_scan_t<NT>(cnt, ws, &D);
-#pragma unroll
-  for (int e = 0; e < PT; ++e)
-    if (fl[e]) {
-      cstart[pre] = tid * PT + e;
-      chit[pre] = -1;
-      ++pre;
-    }
-  if (tid == 0) cstart[D] = n1;
   __syncthreads();
-  auto ckey = [&](uint32_t d) { return (uint32_t)(sk[cstart[d]] >> 32); };
-  auto find = [&](uint32_t key) -> int {
-    uint32_t lo = 0, hi = D;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (ckey(mid) < key) lo = mid + 1; else hi = mid;
+#pragma unroll
+  for (int u = 0; u < UA; ++u)
+    if (ar[u] != NONE) mem[(hcnt[ar[u] >> 13] >> 13) + (ar[u] & 0x1FFFu)] = tid + u * NT;
+  // 3. pass A: every C point looks its voxel up; hit voxels remember it
+  auto lookup = [&](uint32_t key) -> uint32_t {
+    uint32_t h = vx_slot(key, mask);
+    while (true) {
+      const uint32_t k2 = hkey[h];
+      if (k2 == key) return h;
+      if (k2 == NONE) return NONE;
+      h = (h + 1) & mask;
     }
-    return (lo < D && ckey(lo) == key) ? (int)lo : -1;
   };
-  // pass A: the C point (if any) of every new voxel
-  for (uint32_t k0 = tid; k0 < n0; k0 += VX_UNROLL * NT) {
-    float4 c[VX_UNROLL];
+  uint32_t cl[U], ck[U];
 #pragma unroll
-    for (int u = 0; u < VX_UNROLL; ++u)
-      if (k0 + u * NT < n0) c[u] = C[k0 + u * NT];
-#pragma unroll
-    for (int u = 0; u < VX_UNROLL; ++u) {
-      if (k0 + u * NT >= n0) continue;
-      const int d = find(vx_key(g, c[u]));
-      if (d >= 0) chit[d] = (int)(k0 + u * NT);
+  for (int u = 0; u < U; ++u) {
+    const uint32_t k = tid + u * NT;
+    cl[u] = NONE;
+    ck[u] = 0;
+    if (k < n0) {
+      ck[u] = vx_key(g, cc[u]);
+      cl[u] = lookup(ck[u]);
+      if (cl[u] != NONE) hit[cl[u]] = (int)k;
     }
   }
+  for (uint32_t k = tid + U * NT; k < n0; k += NT) {
+    const uint32_t h = lookup(vx_key(g, C[k]));
+    if (h != NONE) hit[h] = (int)k;
+  }
   __syncthreads();
-  // voxels with new points only, in voxel order
-  cnt = 0;
+  vx_phase(S.prof, 1, &tp);
+  // 4. the voxels holding A points only, listed then sorted by key
+  uint32_t fmask = 0, cnt = 0;
 #pragma unroll
-  for (int e = 0; e < PT; ++e) {
-    const uint32_t d = tid * PT + e;
-    fl[e] = (d < D && chit[d] < 0) ? 1u : 0u;
-    cnt += fl[e];
+  for (int q = 0; q < SPT; ++q) {
+    const uint32_t h = tid + q * NT;
+    if (h < T && hkey[h] != NONE && hit[h] < 0) {
+      fmask |= 1u << q;
+      ++cnt;
+    }
   }
   uint32_t Dn;
-  pre = vx_block_scan_t<NT>(cnt, ws, &Dn);
+  uint32_t pre = vx_block_scan_t<NT>(cnt, ws, &Dn);  // its barriers end every read of hit
 #pragma unroll
-  for (int e = 0; e < PT; ++e)
-    if (fl[e]) nhcell[pre++] = tid * PT + e;
+  for (int q = 0; q < SPT; ++q)
+    if (fmask & (1u << q)) {
+      const uint32_t h = tid + q * NT;
+      srt[pre++] = ((uint64_t)hkey[h] << 32) | h;
+    }
+  __syncthreads();
+  uint32_t npad = 64;
+  while (npad < Dn) npad <<= 1;
+  if (Dn > 1) {
+    auto key = [&](uint32_t i) -> uint64_t { return i < Dn ? srt[i] : ~0ull; };
+    uint64_t* xb1 = srt + npad;
+    if (npad <= (uint32_t)NT) vx_bitonic_regs<NT, 1>(srt, srt, xb1, npad, key);
+    else if (npad <= 2u * NT) vx_bitonic_regs<NT, 2>(srt, srt, xb1, npad, key);
+    else vx_bitonic_regs<NT, 4>(srt, srt, xb1, npad, key);
+  }
+  uint32_t* cbelow = reinterpret_cast<uint32_t*>(srt + npad);  // Dn + 1 <= 2 npad words
   for (uint32_t r = tid; r <= Dn; r += NT) cbelow[r] = 0;
   if (tid == 0) {
     M.moved = 0;
@@ -765,81 +910,86 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
     M.sbase[1] = b;
   }
   __syncthreads();
+  vx_phase(S.prof, 2, &tp);
   const uint32_t ob = M.sbase[1];
   if (ob == 0xFFFFFFFFu) return true;
   float4* out = S.out + ob;
   bool moved = false;
-  // sum of voxel d's new points after the optional C point, in input order
-  auto centroid = [&](uint32_t d, float sx, float sy, float sz, float si, uint32_t n) -> float4 {
-    const uint32_t t0 = cstart[d], t1 = cstart[d + 1];
-    for (uint32_t t = t0; t < t1; t += 4) {
+  // sum of slot h's members after the optional C point, in input order (the owner sorts the
+  // member range in place first: atomics ranked them in arbitrary order)
+  auto centroid = [&](uint32_t h, float sx, float sy, float sz, float si, uint32_t n) -> float4 {
+    const uint32_t e = hcnt[h], m0 = e >> 13, mc = e & 0x1FFFu;
+    for (uint32_t a = 1; a < mc; ++a) {
+      const uint32_t x = mem[m0 + a];
+      uint32_t b = a;
+      while (b > 0 && mem[m0 + b - 1] > x) {
+        mem[m0 + b] = mem[m0 + b - 1];
+        --b;
+      }
+      mem[m0 + b] = x;
+    }
+    for (uint32_t t = 0; t < mc; t += 4) {
       float4 p[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (t + u < t1) p[u] = A[(uint32_t)sk[t + u]];
+        if (t + u < mc) p[u] = A[mem[m0 + t + u]];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (t + u < t1) {
+        if (t + u < mc) {
           sx += p[u].x; sy += p[u].y; sz += p[u].z; si += p[u].w;
         }
     }
-    n += t1 - t0;
+    n += mc;
     const float fn = (float)n;
     return make_float4(sx / fn, sy / fn, sz / fn, si / fn);
   };
-  // pass B: C points at k + (new-only voxels before them); merged voxels re-averaged
-  for (uint32_t k0 = tid; k0 < n0; k0 += VX_UNROLL * NT) {
-    float4 c[VX_UNROLL];
-#pragma unroll
-    for (int u = 0; u < VX_UNROLL; ++u)
-      if (k0 + u * NT < n0) c[u] = C[k0 + u * NT];
-#pragma unroll
-    for (int u = 0; u < VX_UNROLL; ++u) {
-      const uint32_t k = k0 + u * NT;
-      if (k >= n0) continue;
-      const uint32_t key = vx_key(g, c[u]);
-      uint32_t lo = 0, hi = Dn;  // new-only voxels below key
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (ckey(nhcell[mid]) < key) lo = mid + 1; else hi = mid;
-      }
-      atomicAdd(&cbelow[lo], 1u);
-      float4 v = c[u];
-      const int d = find(key);
-      if (d >= 0) {
-        v = centroid((uint32_t)d, 0.f + c[u].x, 0.f + c[u].y, 0.f + c[u].z, 0.f + c[u].w, 1u);
-        moved |= vx_key(g, v) != key;
-      }
-      out[k + lo] = v;
+  // new-only voxels with key below `key`
+  auto below = [&](uint32_t key) -> uint32_t {
+    uint32_t lo = 0, hi = Dn;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if ((uint32_t)(srt[mid] >> 32) < key) lo = mid + 1; else hi = mid;
     }
+    return lo;
+  };
+  // 5. pass B: C point k goes to k + (new-only voxels before it); merged voxels re-averaged
+  auto emit = [&](uint32_t k, const float4& c, uint32_t key, uint32_t h) {
+    const uint32_t b = below(key);
+    atomicAdd(&cbelow[b], 1u);
+    float4 v = c;
+    if (h != NONE) {
+      v = centroid(h, 0.f + c.x, 0.f + c.y, 0.f + c.z, 0.f + c.w, 1u);
+      moved |= vx_key(g, v) != key;
+    }
+    out[k + b] = v;
+  };
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (tid + u * NT < n0) emit(tid + u * NT, cc[u], ck[u], cl[u]);
+  for (uint32_t k = tid + U * NT; k < n0; k += NT) {
+    const float4 c = C[k];
+    const uint32_t key = vx_key(g, c);
+    emit(k, c, key, lookup(key));
   }
   __syncthreads();
-  // C points below new-only voxel r: inclusive prefix of cbelow (Dn + 1 <= 4097 entries)
-  constexpr int PB = (CAP + 1 + NT - 1) / NT;
-  uint32_t cv[PB], csum = 0;
-#pragma unroll
-  for (int e = 0; e < PB; ++e) {
-    const uint32_t r = tid * PB + e;
-    cv[e] = r <= Dn ? cbelow[r] : 0u;
-    csum += cv[e];
+  // C points below new-only voxel r: inclusive prefix of cbelow (Dn + 1 entries)
+  for (uint32_t r0 = 0; r0 <= Dn; r0 += NT) {
+    const uint32_t r = r0 + tid;
+    const uint32_t v = r <= Dn ? cbelow[r] : 0u;
+    uint32_t tot;
+    const uint32_t ex = vx_block_scan_t<NT>(v, ws, &tot);
+    if (r <= Dn) cbelow[r] = ex + v + (r0 ? cbelow[r0 - 1] : 0u);
+    __syncthreads();
   }
-  uint32_t ctot;
-  uint32_t cpre = vx_block_scan_t<NT>(csum, ws, &ctot);
-#pragma unroll
-  for (int e = 0; e < PB; ++e) {
-    const uint32_t r = tid * PB + e;
-    cpre += cv[e];
-    if (r <= Dn) cbelow[r] = cpre;
-  }
-  __syncthreads();
   for (uint32_t r = tid; r < Dn; r += NT) {
-    const uint32_t d = nhcell[r];
-    const float4 v = centroid(d, 0.f, 0.f, 0.f, 0.f, 0u);
+    const uint32_t h = (uint32_t)srt[r];
+    const float4 v = centroid(h, 0.f, 0.f, 0.f, 0.f, 0u);
     out[r + cbelow[r]] = v;
-    moved |= vx_key(g, v) != ckey(d);
+    moved |= vx_key(g, v) != (uint32_t)(srt[r] >> 32);
   }
   if (moved) M.moved = 1;
   __syncthreads();
+  vx_phase(S.prof, 3, &tp);
   if (tid == 0) {
     if (S.res_off) *S.res_off = ob;
     if (S.res_cnt) *S.res_cnt = n0 + Dn;
