@@ -183,8 +183,10 @@ int32_t loam_mapper_stats(loam_mapper* h, int32_t stream, loam_map_stats* st);
  * merge / full / append, [3] new points of merged cubes, [4..6] items of each, [7] merges with
  * more than 1024 new points, [8] cell-index build cycles, [9] points indexed, [10] old points,
  * [11..14] merge phases (bounding box, hash + pass A, new-voxel sort, pass B), [16] cell-index
- * hash phase, [17..21] LM round: leader eval, leader wait, reduce + step, passes, member wait */
-#define LOAM_DEBUG_COUNTERS 32
+ * hash phase, [17..21] LM round: leader eval, leader wait, reduce + step, passes, member wait,
+ * [24..31] re-VoxelGrid items by output size (< 1k, 2k, 4k, 8k, 16k, 32k, 64k, more),
+ * [32..39] their cycles (filter + index) */
+#define LOAM_DEBUG_COUNTERS 48
 int32_t loam_mapper_debug_counters(loam_mapper* h, uint64_t* out, int32_t n, int32_t reset);
 /* sum over all streams of the LM iterations (both rounds) of the last solve */
 int64_t loam_mapper_total_iterations(loam_mapper* h);

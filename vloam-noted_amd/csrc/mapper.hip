@@ -44,6 +44,7 @@ constexpr int LM_THREADS = 256;
 constexpr int LM_EBLK = 32;     // LM evaluation workgroups per stream (grid-stride)
 constexpr int SUBMAP_BLOCKS = 64;
 constexpr int INS_SLOTS = WIN_VALID_MAX + EXTRA_CAP;
+constexpr int MAX_GROUPS = 4;  // stream groups launched on separate HIP streams
 constexpr int MAP_ERR_SUBMAP = 4, MAP_ERR_EXTRA = 8, MAP_ERR_HASH = 16, MAP_ERR_LM_SYNC = 32,
               MAP_ERR_INDEX = 64;
 
@@ -75,7 +76,8 @@ struct StreamFrame {
 };
 
 struct MapperDev {
-  int B;
+  int B;       // streams of this launch (a group of the handle's streams)
+  int s0 = 0;  // first stream of the launch
   int max_in, map_cap, sub_cap, scratch_cap, max_chunks;
   float leaf[2];
   uint32_t epoch;
@@ -101,6 +103,11 @@ struct MapperDev {
   float4* ins_sorted;    // [B][2][max_in] inserted points grouped by target cube (input order kept)
   uint32_t* ins_off;     // [B][2][INS_SLOTS + 1] group offsets: window slots, then extra cubes
   unsigned long long* dbg;  // [LOAM_DEBUG_COUNTERS] phase cycle counters (loam_mapper_debug_counters)
+  uint32_t* rv_list[2];  // [B][2][INS_SLOTS] re-VoxelGrid slots for k_revox_merge (0) / k_revox (1),
+                         // a group's entries from 2 s0 INS_SLOTS
+  uint32_t* rv_count;    // [MAX_GROUPS][2] entries of the lists
+  int rv_split;          // 1: k_bucket lists the slots for k_revox_merge + k_revox; 0: k_revox
+                         // takes every slot (one workgroup per slot)
   uint32_t* stable_tok;  // [B][2][NCUBE] arena offset + 1 of content known to be a VoxelGrid
                          // fixed point (re-filtering it is the identity), else 0
   float4* vx_pts;  // [B][2][scratch_cap]
@@ -134,7 +141,7 @@ __device__ inline void cube_corner(int c, const int* cen, int corner[3]) {
 // indices, the slabs that wrap around are cleared.
 // ---------------------------------------------------------------------------------------
 __global__ void k_shift_cubes(MapperDev D, const uint2* __restrict__ old_tab, uint2* new_tab) {
-  int s = blockIdx.y;
+  int s = D.s0 + blockIdx.y;
   const StreamFrame& F = D.fr[s];
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < 2 * NCUBE; t += gridDim.x * blockDim.x) {
     int m = t / NCUBE, c = t % NCUBE;
@@ -152,7 +159,7 @@ __global__ void k_shift_cubes(MapperDev D, const uint2* __restrict__ old_tab, ui
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
-  const int s = blockIdx.x >> 1, m = blockIdx.x & 1;
+  const int s = D.s0 + (blockIdx.x >> 1), m = blockIdx.x & 1;
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
   VoxSeg S;
@@ -182,7 +189,7 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(128) k_submap_prep(MapperDev D) {
   // one wave per map; window slots 2*lane, 2*lane+1 (valid_num <= 75 <= 128)
-  const int s = blockIdx.x;
+  const int s = D.s0 + blockIdx.x;
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
   const int m = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -247,7 +254,7 @@ struct WinMap {  // per (stream, map) window cubes, in LDS
 __global__ void __launch_bounds__(CORR_THREADS) k_knn(MapperDev D, int round) {
   __shared__ WinMap W[2];
   __shared__ int slot_of[75];  // 5 x 5 x 3 window position -> slot (laserCloudValidInd order)
-  const int s = blockIdx.x % D.B, blk = blockIdx.x / D.B;  // a stream's blocks on one XCD
+  const int s = D.s0 + blockIdx.x % D.B, blk = blockIdx.x / D.B;  // a stream's blocks on one XCD
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
   double X[7];
@@ -361,7 +368,7 @@ __global__ void __launch_bounds__(CORR_THREADS) k_knn(MapperDev D, int round) {
 // pass 2: line PCA / plane fit of the 5 neighbours -> factor records (laser_mapping.cpp:557-603,
 // :642-680)
 __global__ void __launch_bounds__(CORR_THREADS) k_geom(MapperDev D, int round) {
-  const int s = blockIdx.x % D.B, blk = blockIdx.x / D.B;  // a stream's blocks on one XCD
+  const int s = D.s0 + blockIdx.x % D.B, blk = blockIdx.x / D.B;  // a stream's blocks on one XCD
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
   const int nc = F.nc_stack, ns = F.ns_stack;
@@ -432,7 +439,7 @@ __global__ void __launch_bounds__(CORR_THREADS) k_geom(MapperDev D, int round) {
 
 // LM evaluation pass at the state's evaluation point (lm.h)
 __global__ void __launch_bounds__(LM_THREADS) k_lm_eval(MapperDev D, int round) {
-  const int s = blockIdx.x / LM_EBLK, blk = blockIdx.x % LM_EBLK;
+  const int s = D.s0 + blockIdx.x / LM_EBLK, blk = blockIdx.x % LM_EBLK;
   const StreamFrame& F = D.fr[s];
   if (!F.active) return;
   const size_t rb = (size_t)s * 2 * D.max_in;
@@ -445,7 +452,7 @@ __global__ void __launch_bounds__(LM_THREADS) k_lm_eval(MapperDev D, int round) 
 // LM step: one wave per stream; on termination the best point becomes the stream pose
 // (Ceres writes it back into the parameter blocks, laser_mapping.cpp:535-536)
 __global__ void __launch_bounds__(64) k_lm_step(MapperDev D, int round) {
-  const int s = blockIdx.x;
+  const int s = D.s0 + blockIdx.x;
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
   LmState& S = F.lm[round];
@@ -465,7 +472,7 @@ __global__ void __launch_bounds__(64) k_lm_step(MapperDev D, int round) {
 __global__ void __launch_bounds__(LM_THREADS) k_lm_round(MapperDev D, int round, int G) {
   // block b -> stream b % B, member b / B: with B a multiple of 8 all of a stream's blocks
   // share an XCD (b % 8), so its hand-offs stay in one L2 (placement is speed only)
-  const int s = blockIdx.x % D.B, g = blockIdx.x / D.B;
+  const int s = D.s0 + blockIdx.x % D.B, g = blockIdx.x / D.B;
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
   const size_t rb = (size_t)s * 2 * D.max_in;
@@ -488,7 +495,8 @@ __global__ void __launch_bounds__(LM_THREADS) k_lm_round(MapperDev D, int round,
 // insertion of the stacks into the cube grid with the final pose (laser_mapping.cpp:741-788)
 // ---------------------------------------------------------------------------------------
 __global__ void k_insert(MapperDev D) {
-  const int s = blockIdx.y;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2) D.rv_count[2 * (D.s0 / D.B) + threadIdx.x] = 0;  // k_bucket's lists
+  const int s = D.s0 + blockIdx.y;
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
   const int nc = F.nc_stack, ns = F.ns_stack;
@@ -520,6 +528,51 @@ __global__ void k_insert(MapperDev D) {
   }
 }
 
+// which cube (if any) slot `slot` of (s, m) re-filters this frame; false: nothing to do.  A
+// window cube that received nothing and whose content is a VoxelGrid fixed point keeps it:
+// re-filtering it (laser_mapping.cpp:795-808) would reproduce it bit for bit.
+__device__ inline bool revox_target(const MapperDev& D, int s, int m, int slot, int* cube_out, int* append_out) {
+  const StreamFrame& F = D.fr[s];
+  if (!F.active) return false;
+  int cube, append;
+  if (slot < F.valid_num) {
+    cube = F.window[slot];
+    append = 0;
+  } else if (slot >= WIN_VALID_MAX && slot - WIN_VALID_MAX < min(F.extra_n[m], EXTRA_CAP)) {
+    cube = F.extra_list[m][slot - WIN_VALID_MAX];
+    append = 1;
+  } else {
+    return false;
+  }
+  const uint32_t* ioff = D.ins_off + sm_index(s, m) * (INS_SLOTS + 1);
+  const uint32_t n_new = ioff[slot + 1] - ioff[slot];
+  const uint2 cv = D.cube_tab[sm_index(s, m) * NCUBE + cube];
+  if (!append && n_new == 0 && (cv.y == 0 || D.stable_tok[sm_index(s, m) * NCUBE + cube] == cv.x + 1))
+    return false;
+  *cube_out = cube;
+  *append_out = append;
+  return true;
+}
+
+// Re-VoxelGrid of one slot's cube, then its cell index.  MERGE: the merge path only, in a
+// workgroup of NT threads with LW LDS words (merge capacity CAP); returns false, with nothing
+// written, when the merge cannot run (grid overflow).  Otherwise: merge or full filter in a
+// VX_THREADS workgroup with the whole LDS.
+constexpr int RV_NT = 512;                    // k_revox_merge workgroup
+constexpr int RV_CAP = 2048;                  // its merge capacity (new points)
+constexpr int RV_LW = 9 * RV_CAP + 256;       // its LDS words: 74 KiB, two workgroups per CU
+constexpr int RV_MAXT = 16384;                // its LDS cell-index tables
+constexpr int RV_SMALL_N = RV_MAXT / 2;       // k_revox_merge cubes: old + new points below this
+static_assert(RV_MAXT + RV_NT / 64 + 1 <= RV_LW - 256, "k_revox_merge LDS");
+
+__device__ inline bool revox_merge_ok(const MapperDev& D, int s, int m, int slot, int cube, int append) {
+  if (append) return false;
+  const uint32_t* ioff = D.ins_off + sm_index(s, m) * (INS_SLOTS + 1);
+  const uint32_t n_new = ioff[slot + 1] - ioff[slot];
+  const uint2 cv = D.cube_tab[sm_index(s, m) * NCUBE + cube];
+  return n_new > 0 && n_new <= (uint32_t)RV_CAP && cv.y > 0 && D.stable_tok[sm_index(s, m) * NCUBE + cube] == cv.x + 1;
+}
+
 // ---------------------------------------------------------------------------------------
 // group the inserted points by target cube (stable counting sort, one workgroup per (stream,
 // map)): each re-VoxelGrid workgroup then reads one contiguous run, in input order
@@ -528,7 +581,7 @@ __global__ void __launch_bounds__(VX_THREADS) k_bucket(MapperDev D) {
   __shared__ int cslot[NCUBE];
   __shared__ uint32_t base[INS_SLOTS];
   __shared__ uint32_t wcnt[VX_WAVES][INS_SLOTS];
-  const int sm = blockIdx.x, s = sm >> 1, m = sm & 1;
+  const int sm = 2 * D.s0 + blockIdx.x, s = sm >> 1, m = sm & 1;
   const StreamFrame& F = D.fr[s];
   if (!F.active) return;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
@@ -597,38 +650,26 @@ __global__ void __launch_bounds__(VX_THREADS) k_bucket(MapperDev D) {
     if (sl >= 0) out[wcnt[wid][sl] + rank] = pts[i];
     __syncthreads();
   }
+  // the re-VoxelGrid work of each slot: merges of cubes small enough for k_revox_merge's LDS,
+  // everything else for k_revox
+  if (D.rv_split && tid < INS_SLOTS) {
+    int cube = 0, append = 0;
+    if (revox_target(D, s, m, tid, &cube, &append)) {
+      const uint32_t n_new = off[tid + 1] - off[tid];
+      const uint32_t n0 = D.cube_tab[sm_index(s, m) * NCUBE + cube].y;
+      const int k = revox_merge_ok(D, s, m, tid, cube, append) && n0 + n_new < (uint32_t)RV_SMALL_N ? 0 : 1;
+      const int g = D.s0 / D.B;
+      D.rv_list[k][2 * (size_t)D.s0 * INS_SLOTS + atomicAdd(&D.rv_count[2 * g + k], 1u)] =
+          (uint32_t)(sm * INS_SLOTS + tid);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------
 // re-VoxelGrid of every window cube (old content ++ inserted points, :795-808); cubes outside
 // the window that received points get them appended raw (:762).  One workgroup per cube.
 // ---------------------------------------------------------------------------------------
-// which cube (if any) slot `slot` of (s, m) re-filters this frame; false: nothing to do.  A
-// window cube that received nothing and whose content is a VoxelGrid fixed point keeps it:
-// re-filtering it (laser_mapping.cpp:795-808) would reproduce it bit for bit.
-__device__ inline bool revox_target(const MapperDev& D, int s, int m, int slot, int* cube_out, int* append_out) {
-  const StreamFrame& F = D.fr[s];
-  if (!F.active) return false;
-  int cube, append;
-  if (slot < F.valid_num) {
-    cube = F.window[slot];
-    append = 0;
-  } else if (slot >= WIN_VALID_MAX && slot - WIN_VALID_MAX < min(F.extra_n[m], EXTRA_CAP)) {
-    cube = F.extra_list[m][slot - WIN_VALID_MAX];
-    append = 1;
-  } else {
-    return false;
-  }
-  const uint32_t* ioff = D.ins_off + sm_index(s, m) * (INS_SLOTS + 1);
-  const uint32_t n_new = ioff[slot + 1] - ioff[slot];
-  const uint2 cv = D.cube_tab[sm_index(s, m) * NCUBE + cube];
-  if (!append && n_new == 0 && (cv.y == 0 || D.stable_tok[sm_index(s, m) * NCUBE + cube] == cv.x + 1))
-    return false;
-  *cube_out = cube;
-  *append_out = append;
-  return true;
-}
-
+template <int NT, int CAP, int LW, int MAXT, bool MERGE>
 __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube, int append, uint32_t* lds) {
   StreamFrame& F = D.fr[s];
   const uint32_t* ioff = D.ins_off + sm_index(s, m) * (INS_SLOTS + 1);
@@ -657,20 +698,24 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
   S.scratch_tail = &F.scratch_tail[m];
   S.scratch_cap = D.scratch_cap;
   S.err = &F.err;
-  S.prof = D.dbg + 11;  // merge phases: dbg[11..15]
-  bool done = false;
+  S.prof = D.dbg + 11;  // merge phases: dbg[11..14]
+  bool merged = false;
   const unsigned long long t0 = __builtin_readcyclecounter();
-  if (!append && n_new > 0 && n_new <= VX_MERGE_CAP && cv.y > 0 && *tok == cv.x + 1) {
-    done = vx_merge_fixed_point(S, lds);
-    __syncthreads();  // false: grid overflow, full filter below
+  if (MERGE) {
+    merged = vx_merge_fixed_point<NT, CAP, LW>(S, lds);
+    __syncthreads();
+    if (!merged) vx_copy_through<NT>(S, lds + LW - 3);  // grid overflow: output = input (PCL)
+  } else {
+    if (!append && n_new > 0 && n_new <= VX_MERGE_CAP && cv.y > 0 && *tok == cv.x + 1) {
+      merged = vx_merge_fixed_point(S, lds);
+      __syncthreads();  // false: grid overflow, full filter below
+    }
+    if (!merged) voxel_segment(S, lds);
+    __syncthreads();
   }
-  const bool merged = done;
-  if (!done) voxel_segment(S, lds);
-  __syncthreads();
   const unsigned long long t1 = __builtin_readcyclecounter();
   // the cube's new content -> its cell index (cubeindex.h)
-  __syncthreads();
-  uint32_t* res = lds + VX_LDS_WORDS - 2;
+  uint32_t* res = lds + LW - 2;
   if (threadIdx.x == 0) {
     const uint2 v = tab[cube];  // written by this thread inside the filter
     res[0] = v.x;
@@ -678,11 +723,11 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
   }
   __syncthreads();
   const uint32_t off = res[0], n = res[1];
+  __syncthreads();  // res may lie in the index build's LDS
   int corner[3];
   cube_corner(cube, F.cen, corner);
-  if (!cube_index_build<VX_THREADS>(ar + off, n, corner, carena_base(D, s, m, F.arena_active[m]) + off,
-                                    ctab_base(D, s, m, F.arena_active[m]) + 4 * (size_t)off, lds,
-                                    D.dbg + 16) &&
+  if (!cube_index_build<NT, MAXT>(ar + off, n, corner, carena_base(D, s, m, F.arena_active[m]) + off,
+                                  ctab_base(D, s, m, F.arena_active[m]) + 4 * (size_t)off, lds, D.dbg + 16) &&
       threadIdx.x == 0)
     atomicOr(&F.err, MAP_ERR_INDEX);
   // read old content + new points, write the filtered cube, then its index (read it, write
@@ -696,20 +741,45 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
     atomicAdd(&D.dbg[8], t2 - t1);       // index build cycles
     atomicAdd(&D.dbg[9], (unsigned long long)n);
     atomicAdd(&D.dbg[10], (unsigned long long)cv.y);
+    int hb = 0;
+    while (hb < 7 && n >= (1024u << hb)) ++hb;
+    atomicAdd(&D.dbg[24 + hb], 1ull);
+    atomicAdd(&D.dbg[32 + hb], t2 - t0);
     if (merged) {
-      atomicAdd(&D.dbg[3], (unsigned long long)n_new);           // new points of merged cubes
-      if (n_new > VX_THREADS) atomicAdd(&D.dbg[7], 1ull);        // merges past the rank sort
+      atomicAdd(&D.dbg[3], (unsigned long long)n_new);  // new points of merged cubes
+      if (!MERGE) atomicAdd(&D.dbg[7], 1ull);          // merges run by the full-size kernel
     }
   }
 }
 
-// one workgroup per (stream, map, slot); slots with nothing to do exit at once
+// The slots listed by k_bucket: merges of small cubes in 512-thread workgroups, two per CU
+// (k_revox_merge), the rest in VX_THREADS workgroups with the whole LDS (k_revox).  The two
+// run side by side on a group's two HIP streams.  Blocks past a list's end exit at once (a
+// grid-stride loop over the list spills k_revox's registers).
+__global__ void __launch_bounds__(RV_NT, 2) k_revox_merge(MapperDev D) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[RV_LW];
+  const uint32_t e = blockIdx.x;
+  if (e >= D.rv_count[2 * (D.s0 / D.B)]) return;
+  const uint32_t item = D.rv_list[0][2 * (size_t)D.s0 * INS_SLOTS + e];
+  const int slot = (int)(item % INS_SLOTS), sm = (int)(item / INS_SLOTS);
+  int cube = 0, append = 0;
+  revox_target(D, sm >> 1, sm & 1, slot, &cube, &append);
+  revox_item<RV_NT, RV_CAP, RV_LW, RV_MAXT, true>(D, sm >> 1, sm & 1, slot, cube, append, lds);
+}
+
 __global__ void __launch_bounds__(VX_THREADS) k_revox(MapperDev D) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
-  const int slot = blockIdx.x % INS_SLOTS, sm = blockIdx.x / INS_SLOTS;
+  const uint32_t e = blockIdx.x;
+  uint32_t item = 2 * (uint32_t)D.s0 * INS_SLOTS + e;  // rv_split 0: block = slot
+  if (D.rv_split) {
+    if (e >= D.rv_count[2 * (D.s0 / D.B) + 1]) return;
+    item = D.rv_list[1][2 * (size_t)D.s0 * INS_SLOTS + e];
+  }
+  const int slot = (int)(item % INS_SLOTS), sm = (int)(item / INS_SLOTS);
   int cube = 0, append = 0;
   if (!revox_target(D, sm >> 1, sm & 1, slot, &cube, &append)) return;
-  revox_item(D, sm >> 1, sm & 1, slot, cube, append, lds);
+  revox_item<VX_THREADS, (int)VX_MERGE_CAP, VX_LDS_WORDS, CI_LDS_MAX_T, false>(D, sm >> 1, sm & 1, slot, cube, append,
+                                                                              lds);
 }
 
 // cell index of one cube whose content was set through the API (cen: the host's grid centre)
@@ -865,6 +935,16 @@ struct loam_mapper {
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;  // stack VoxelGrid, concurrent with the submap / hash build
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // stream groups: group g > 0 runs its launch sequence on its own HIP streams, so the
+  // groups' phases (memory-bound kNN, fp64 LM, LDS-bound re-VoxelGrid) overlap on the CUs
+  int groups = 1;
+  hipStream_t gst[MAX_GROUPS] = {}, gst2[MAX_GROUPS] = {};
+  hipEvent_t gfork[MAX_GROUPS] = {}, gjoin[MAX_GROUPS] = {}, gdone[MAX_GROUPS] = {};
+  // stagger: phase p of group g waits for phase p of group g - 1, keeping the groups one
+  // kernel apart (LOAM_MAPPER_STAGGER=1)
+  int stagger = 0;
+  static constexpr int NPHASE = 10;
+  hipEvent_t gph[MAX_GROUPS][NPHASE] = {};
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   MapperDev D{};
   PinnedArray<StreamFrame> hf;  // pinned: the per-frame H2D / D2H of the stream records
@@ -915,6 +995,17 @@ void free_all(loam_mapper* h) {
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->st) (void)hipStreamDestroy(h->st);
   if (h->st2) (void)hipStreamDestroy(h->st2);
+  for (int g = 1; g < MAX_GROUPS; ++g) {  // group 0 uses st / st2 / ev_fork / ev_join
+    if (h->gst[g]) (void)hipStreamDestroy(h->gst[g]);
+    if (h->gst2[g]) (void)hipStreamDestroy(h->gst2[g]);
+    if (h->gfork[g]) (void)hipEventDestroy(h->gfork[g]);
+    if (h->gjoin[g]) (void)hipEventDestroy(h->gjoin[g]);
+  }
+  for (int g = 0; g < MAX_GROUPS; ++g) {
+    if (h->gdone[g]) (void)hipEventDestroy(h->gdone[g]);
+    for (auto& e : h->gph[g])
+      if (e) (void)hipEventDestroy(e);
+  }
 }
 
 void host_initial_guess(HostStream& H, double* pose) {
@@ -1017,6 +1108,32 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
     return fail(LOAM_ERR_HIP);
   for (auto& e : h->ev)
     if (hipEventCreate(&e) != hipSuccess) return fail(LOAM_ERR_HIP);
+  {
+    // LOAM_MAPPER_GROUPS: stream groups on separate HIP streams (B divisible by the count)
+    const char* genv = std::getenv("LOAM_MAPPER_GROUPS");
+    int ng = genv ? std::atoi(genv) : 1;
+    ng = std::max(1, std::min(ng, MAX_GROUPS));
+    while (ng > 1 && B % ng != 0) --ng;
+    h->groups = ng;
+    h->gst[0] = h->st;
+    h->gst2[0] = h->st2;
+    h->gfork[0] = h->ev_fork;
+    h->gjoin[0] = h->ev_join;
+    for (int g = 0; g < ng; ++g) {
+      if (g > 0 && (hipStreamCreateWithFlags(&h->gst[g], hipStreamNonBlocking) != hipSuccess ||
+                    hipStreamCreateWithFlags(&h->gst2[g], hipStreamNonBlocking) != hipSuccess ||
+                    hipEventCreateWithFlags(&h->gfork[g], hipEventDisableTiming) != hipSuccess ||
+                    hipEventCreateWithFlags(&h->gjoin[g], hipEventDisableTiming) != hipSuccess))
+        return fail(LOAM_ERR_HIP);
+      if (hipEventCreateWithFlags(&h->gdone[g], hipEventDisableTiming) != hipSuccess) return fail(LOAM_ERR_HIP);
+      for (auto& e : h->gph[g])
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(LOAM_ERR_HIP);
+    }
+    const char* senv = std::getenv("LOAM_MAPPER_STAGGER");
+    h->stagger = (senv && senv[0] == '1') ? 1 : 0;
+    const char* renv = std::getenv("LOAM_REVOX_SPLIT");  // 1: k_revox_merge + k_revox
+    D.rv_split = (renv && renv[0] == '1') ? 1 : 0;
+  }
   ALLOC(D.fr, B);
   for (int m = 0; m < 2; ++m) {
     ALLOC(D.in_pts[m], B * D.max_in);
@@ -1043,6 +1160,9 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
   ALLOC(D.ins_sorted, B * 2 * (size_t)D.max_in);
   ALLOC(D.ins_off, B * 2 * (size_t)(INS_SLOTS + 1));
   ALLOC(D.stable_tok, B * 2 * (size_t)NCUBE);
+  ALLOC(D.rv_list[0], B * 2 * (size_t)INS_SLOTS);
+  ALLOC(D.rv_list[1], B * 2 * (size_t)INS_SLOTS);
+  ALLOC(D.rv_count, 2 * MAX_GROUPS);
   ALLOC(D.dbg, LOAM_DEBUG_COUNTERS);
   ALLOC(D.vx_pts, B * 2 * (size_t)D.scratch_cap);
   ALLOC(D.vx_idx, B * 2 * (size_t)D.scratch_cap);
@@ -1258,36 +1378,103 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   hipStream_t st = h->st;
   LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(StreamFrame) * B, hipMemcpyHostToDevice, st));
   LOAM_HIP(hipEventRecord(h->ev[0], st));
-  // stack VoxelGrid (reads only this frame's inputs) on the second stream, overlapping the
-  // cube shift, submap gather and hash build; joined before the correspondences
-  LOAM_HIP(hipEventRecord(h->ev_fork, st));
-  LOAM_HIP(hipStreamWaitEvent(h->st2, h->ev_fork, 0));
-  LAUNCH_ON(h->st2, FAM_STACK, k_stack_ds<<<B * 2, VX_THREADS, 0, h->st2>>>(D));
-  LOAM_HIP(hipEventRecord(h->ev_join, h->st2));
+  // The streams run in h->groups groups, each on its own HIP streams (gst[g], and gst2[g] for
+  // the stack VoxelGrid); the launch sequences are issued phase by phase so the groups start
+  // together and drift apart as their kernels finish.
+  const int NG = h->groups, Bg = B / NG;
+  MapperDev Dg[MAX_GROUPS];
+  for (int g = 0; g < NG; ++g) {
+    Dg[g] = D;
+    Dg[g].B = Bg;
+    Dg[g].s0 = g * Bg;
+  }
+  // phase bracketing for the stagger: before(g, p) / after(g, p) around group g's phase p
+  auto before = [&](int g, int p, hipStream_t q) -> hipError_t {
+    return (h->stagger && g > 0) ? hipStreamWaitEvent(q, h->gph[g - 1][p], 0) : hipSuccess;
+  };
+  auto after = [&](int g, int p, hipStream_t q) -> hipError_t {
+    return (h->stagger && g + 1 < NG) ? hipEventRecord(h->gph[g][p], q) : hipSuccess;
+  };
+  LOAM_HIP(hipEventRecord(h->gdone[0], st));  // the frame records are on the device
+  for (int g = 0; g < NG; ++g) {
+    hipStream_t sg = h->gst[g], s2 = h->gst2[g];
+    if (g > 0) LOAM_HIP(hipStreamWaitEvent(sg, h->gdone[0], 0));
+    // stack VoxelGrid (reads only this frame's inputs) on the second stream, overlapping the
+    // cube shift and submap gather; joined before the correspondences
+    LOAM_HIP(hipEventRecord(h->gfork[g], sg));
+    LOAM_HIP(hipStreamWaitEvent(s2, h->gfork[g], 0));
+    LOAM_HIP(before(g, 0, s2));
+    LAUNCH_ON(s2, FAM_STACK, k_stack_ds<<<Bg * 2, VX_THREADS, 0, s2>>>(Dg[g]));
+    LOAM_HIP(after(g, 0, s2));
+    LOAM_HIP(hipEventRecord(h->gjoin[g], s2));
+  }
   if (any_shift) {
-    LAUNCH(FAM_OTHER, k_shift_cubes<<<dim3(16, B), 256, 0, st>>>(D, h->cube_tab[h->parity], h->cube_tab[1 - h->parity]));
+    for (int g = 0; g < NG; ++g)
+      LAUNCH_ON(h->gst[g], FAM_OTHER, k_shift_cubes<<<dim3(16, Bg), 256, 0, h->gst[g]>>>(
+                                          Dg[g], h->cube_tab[h->parity], h->cube_tab[1 - h->parity]));
     h->parity ^= 1;
     D.cube_tab = h->cube_tab[h->parity];
+    for (int g = 0; g < NG; ++g) Dg[g].cube_tab = D.cube_tab;
   }
-  LAUNCH(FAM_OTHER, k_submap_prep<<<B, 128, 0, st>>>(D));
+  for (int g = 0; g < NG; ++g) LAUNCH_ON(h->gst[g], FAM_OTHER, k_submap_prep<<<Bg, 128, 0, h->gst[g]>>>(Dg[g]));
   LOAM_HIP(hipEventRecord(h->ev[1], st));
-  LOAM_HIP(hipStreamWaitEvent(st, h->ev_join, 0));
+  for (int g = 0; g < NG; ++g) LOAM_HIP(hipStreamWaitEvent(h->gst[g], h->gjoin[g], 0));
   for (int round = 0; round < 2; ++round) {
-    LAUNCH(FAM_CORR, k_knn<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round));
-    LAUNCH(FAM_CORR, k_geom<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round));
-    if (h->lm_G > 0) {
-      LAUNCH(FAM_LM, k_lm_round<<<B * h->lm_G, LM_THREADS, 0, st>>>(D, round, h->lm_G));
-    } else {
-      for (int it = 0; it < 5; ++it) {  // iteration 0 + max_num_iterations = 4 candidates
-        LAUNCH(FAM_LM, k_lm_eval<<<B * LM_EBLK, LM_THREADS, 0, st>>>(D, round));
-        LAUNCH(FAM_LM, k_lm_step<<<B, 64, 0, st>>>(D, round));
+    for (int g = 0; g < NG; ++g) {
+      hipStream_t sg = h->gst[g];
+      LOAM_HIP(before(g, 2 + 3 * round, sg));
+      LAUNCH_ON(sg, FAM_CORR, k_knn<<<Bg * CORR_BLK, CORR_THREADS, 0, sg>>>(Dg[g], round));
+      LOAM_HIP(after(g, 2 + 3 * round, sg));
+    }
+    for (int g = 0; g < NG; ++g) {
+      hipStream_t sg = h->gst[g];
+      LOAM_HIP(before(g, 3 + 3 * round, sg));
+      LAUNCH_ON(sg, FAM_CORR, k_geom<<<Bg * CORR_BLK, CORR_THREADS, 0, sg>>>(Dg[g], round));
+      LOAM_HIP(after(g, 3 + 3 * round, sg));
+    }
+    for (int g = 0; g < NG; ++g) {
+      hipStream_t sg = h->gst[g];
+      LOAM_HIP(before(g, 4 + 3 * round, sg));
+      if (h->lm_G > 0) {
+        LAUNCH_ON(sg, FAM_LM, k_lm_round<<<Bg * h->lm_G, LM_THREADS, 0, sg>>>(Dg[g], round, h->lm_G));
+      } else {
+        for (int it = 0; it < 5; ++it) {  // iteration 0 + max_num_iterations = 4 candidates
+          LAUNCH_ON(sg, FAM_LM, k_lm_eval<<<Bg * LM_EBLK, LM_THREADS, 0, sg>>>(Dg[g], round));
+          LAUNCH_ON(sg, FAM_LM, k_lm_step<<<Bg, 64, 0, sg>>>(Dg[g], round));
+        }
       }
+      LOAM_HIP(after(g, 4 + 3 * round, sg));
     }
   }
   LOAM_HIP(hipEventRecord(h->ev[2], st));
-  LAUNCH(FAM_INSERT, k_insert<<<dim3(16, B), 256, 0, st>>>(D));
-  LAUNCH(FAM_INSERT, k_bucket<<<B * 2, VX_THREADS, 0, st>>>(D));
-  LAUNCH(FAM_REVOX, k_revox<<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D));
+  for (int g = 0; g < NG; ++g) {
+    hipStream_t sg = h->gst[g];
+    LOAM_HIP(before(g, 8, sg));
+    LAUNCH_ON(sg, FAM_INSERT, k_insert<<<dim3(16, Bg), 256, 0, sg>>>(Dg[g]));
+    LAUNCH_ON(sg, FAM_INSERT, k_bucket<<<Bg * 2, VX_THREADS, 0, sg>>>(Dg[g]));
+    LOAM_HIP(after(g, 8, sg));
+  }
+  for (int g = 0; g < NG; ++g) {
+    hipStream_t sg = h->gst[g];
+    LOAM_HIP(before(g, 9, sg));
+    // the long items (k_revox, whole-CU workgroups) start first on the second stream; the
+    // merges fill the other CUs beside them
+    if (D.rv_split) {
+      hipStream_t s2 = h->gst2[g];
+      LOAM_HIP(hipEventRecord(h->gfork[g], sg));
+      LOAM_HIP(hipStreamWaitEvent(s2, h->gfork[g], 0));
+      LAUNCH_ON(s2, FAM_REVOX, k_revox<<<Bg * 2 * INS_SLOTS, VX_THREADS, 0, s2>>>(Dg[g]));
+      LOAM_HIP(hipEventRecord(h->gjoin[g], s2));
+      LAUNCH_ON(sg, FAM_REVOX, k_revox_merge<<<Bg * 2 * INS_SLOTS, RV_NT, 0, sg>>>(Dg[g]));
+      LOAM_HIP(hipStreamWaitEvent(sg, h->gjoin[g], 0));
+    } else {
+      LAUNCH_ON(sg, FAM_REVOX, k_revox<<<Bg * 2 * INS_SLOTS, VX_THREADS, 0, sg>>>(Dg[g]));
+    }
+    if (g > 0) {
+      LOAM_HIP(hipEventRecord(h->gdone[g], sg));
+      LOAM_HIP(hipStreamWaitEvent(st, h->gdone[g], 0));
+    }
+  }
   LOAM_HIP(hipGetLastError());
   LOAM_HIP(hipEventRecord(h->ev[3], st));
   LOAM_HIP(hipMemcpyAsync(h->hf.data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));

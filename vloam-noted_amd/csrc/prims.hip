@@ -37,8 +37,9 @@ __global__ void __launch_bounds__(P_LM_THREADS)
     k_lm_eval(LmRecDev R, int nrec, const double* x, double* partials) {
   __shared__ double red[P_LM_THREADS / 64][LM_NACC];
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  double X[7];
+  double X[7], Rm[9];
   for (int i = 0; i < 7; ++i) X[i] = x[i];
+  lm_rotmat(X, Rm);
   double acc[LM_NACC];
 #pragma unroll
   for (int i = 0; i < LM_NACC; ++i) acc[i] = 0.0;
@@ -46,7 +47,7 @@ __global__ void __launch_bounds__(P_LM_THREADS)
     const int r = blockIdx.x * P_LM_CHUNK + it * P_LM_THREADS + tid;
     if (r < nrec && R.type[r] != 0)
       lm_accum(R.type[r], R.px[r], R.py[r], R.pz[r], R.a0[r], R.a1[r], R.a2[r], R.b0[r], R.b1[r],
-               R.b2[r], X, acc);
+               R.b2[r], Rm, X, acc);
   }
 #pragma unroll
   for (int i = 0; i < LM_NACC; ++i) {

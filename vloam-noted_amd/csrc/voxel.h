@@ -735,6 +735,30 @@ __device__ inline void vx_bitonic_regs(uint64_t* sk, uint64_t* xb0, uint64_t* xb
   __syncthreads();
 }
 
+// PCL's "leaf size too small" result (output = input): C ++ A copied to the tail (NT threads)
+template <int NT>
+__device__ inline void vx_copy_through(const VoxSeg& S, uint32_t* sbase) {
+  const uint32_t n0 = (uint32_t)S.n0, N = n0 + (uint32_t)S.n1;
+  if (threadIdx.x == 0) {
+    uint32_t b = S.tail ? atomicAdd(S.tail, N) : 0;
+    if (b + N > S.cap) {
+      atomicOr(S.err, VX_ERR_OUTPUT);
+      b = 0xFFFFFFFFu;
+    }
+    *sbase = b;
+  }
+  __syncthreads();
+  const uint32_t ob = *sbase;
+  if (ob == 0xFFFFFFFFu) return;
+  for (uint32_t i = threadIdx.x; i < N; i += NT) S.out[ob + i] = i < n0 ? S.src0[i] : S.src1[i - n0];
+  if (threadIdx.x == 0) {
+    if (S.res_off) *S.res_off = ob;
+    if (S.res_cnt) *S.res_cnt = N;
+    if (S.stable_out) *S.stable_out = 0;
+  }
+  __syncthreads();
+}
+
 // ---------------------------------------------------------------------------------------
 // VoxelGrid of C ++ A where C (src0, n0 points) is already a fixed point of the filter (at
 // most one point per voxel, in voxel order: a previous output whose centroids all stayed in
