@@ -215,6 +215,9 @@ int32_t loam_mapper_get_state(loam_mapper* h, int32_t stream, int32_t* cen,
 int32_t loam_mapper_set_state(loam_mapper* h, int32_t stream, const int32_t* cen,
                               const double* q_wmap_wodom, const double* t_wmap_wodom);
 int32_t loam_mapper_cube_count(loam_mapper* h, int32_t stream, int32_t which, int32_t cube);
+/* laserCloudCornerStack (which 0) / laserCloudSurfStack (1) of the last solve
+ * (laser_mapping.cpp:492-500): copies when cap >= the count; returns the count */
+int32_t loam_mapper_stack_copy(loam_mapper* h, int32_t stream, int32_t which, float* out, int32_t cap);
 int32_t loam_mapper_cube_copy(loam_mapper* h, int32_t stream, int32_t which, int32_t cube,
                               float* out);
 int32_t loam_mapper_cube_set(loam_mapper* h, int32_t stream, int32_t which, int32_t cube,

@@ -111,3 +111,27 @@ def test_lm_paths_many_streams(seq, monkeypatch, persistent):
     for s in range(24):
         _check_frame(m, s, seq[SNAP[s % len(SNAP)]])
     m.close()
+
+
+@pytest.mark.parametrize("n_corner,n_surf", [(3000, 9000), (20000, 70000)])
+def test_stack_voxelgrid_bit_exact(n_corner, n_surf):
+    """CornerStack / SurfStack (laser_mapping.cpp:492-500) bit for bit against the oracle
+    VoxelGrid, for stacks on the single-pass and the grouped (> VX_UCAP voxels) paths"""
+    import loam_oracle as O
+    rng = np.random.default_rng(n_surf)
+
+    def cloud(n):  # street-like: a dense ground band plus walls, sensor frame
+        g = np.c_[rng.uniform(-60, 60, (n // 2, 2)), rng.normal(-1.7, 0.05, n // 2)]
+        w = np.c_[rng.uniform(-60, 60, n - n // 2), rng.choice([-8.0, 8.0], n - n // 2)
+                  + rng.normal(0, 0.05, n - n // 2), rng.uniform(-1.7, 12, n - n // 2)]
+        xyz = np.concatenate([g, w])[rng.permutation(n)]
+        return np.c_[xyz, rng.uniform(0, 64, n)].astype(np.float32)
+
+    corner, surf = cloud(n_corner), cloud(n_surf)
+    m = BatchMapper(1)
+    m.input(0, corner, surf, np.array([0, 0, 0, 1.0]), np.zeros(3))
+    m.solve()
+    for which, (c, leaf) in enumerate([(corner, 0.4), (surf, 0.8)]):
+        got, ref = m.stack(0, which), O.voxel_grid(c, leaf)
+        assert got.shape == ref.shape
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))

@@ -1680,6 +1680,18 @@ int32_t loam_mapper_cube_copy(loam_mapper* h, int32_t s, int32_t which, int32_t 
   return (int32_t)v.y;
 }
 
+int32_t loam_mapper_stack_copy(loam_mapper* h, int32_t s, int32_t which, float* out, int32_t cap) {
+  TRY(check_stream(h, s));
+  if (which < 0 || which > 1 || (cap > 0 && !out)) return LOAM_ERR_ARG;
+  LOAM_HIP(hipSetDevice(h->dev));
+  const int32_t n = which == 0 ? h->hf[s].nc_stack : h->hf[s].ns_stack;
+  if (n > cap) return n;  // the count only
+  if (n) {
+    LOAM_HIP(hipMemcpy(out, h->D.stack[which] + (size_t)s * h->D.max_in, sizeof(float4) * n, hipMemcpyDeviceToHost));
+  }
+  return n;
+}
+
 int32_t loam_mapper_cube_set(loam_mapper* h, int32_t s, int32_t which, int32_t cube, const float* pts, int32_t n) {
   TRY(check_stream(h, s));
   if (which < 0 || which > 1 || cube < 0 || cube >= NCUBE || n < 0 || (n > 0 && !pts)) return LOAM_ERR_ARG;

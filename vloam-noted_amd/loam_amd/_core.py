@@ -103,6 +103,7 @@ SIGNATURES = {
     "loam_mapper_set_state": (c_i32, [vp, c_i32, vp, vp, vp]),
     "loam_mapper_cube_count": (c_i32, [vp, c_i32, c_i32, c_i32]),
     "loam_mapper_cube_copy": (c_i32, [vp, c_i32, c_i32, c_i32, vp]),
+    "loam_mapper_stack_copy": (c_i32, [vp, c_i32, c_i32, vp, c_i32]),
     "loam_mapper_cube_set": (c_i32, [vp, c_i32, c_i32, c_i32, vp, c_i32]),
     "loam_lm_solve": (c_i32, [c_i32, vp, c_i32, vp, c_i32, ctypes.POINTER(LMStats)]),
     "loam_lm_normal_equations": (c_i32, [c_i32, vp, c_i32, vp, vp, vp, vp]),

@@ -68,6 +68,14 @@ class BatchMapper:
         check(lib().loam_mapper_input_device_batch(self.h, len(st), ptr(st), ptr(cp), ptr(cn), ptr(sp),
                                                    ptr(sn), ptr(q), ptr(t)))
 
+    def stack(self, stream, which):
+        """laserCloudCornerStack (0) / laserCloudSurfStack (1) of the last solve, (n, 4) float32"""
+        n = check(lib().loam_mapper_stack_copy(self.h, stream, which, None, 0))
+        out = np.empty((n, 4), dtype=np.float32)
+        if n:
+            check(lib().loam_mapper_stack_copy(self.h, stream, which, ptr(out), n))
+        return out
+
     def total_iterations(self):
         """sum of the LM iterations of every stream in the last solve"""
         return check(lib().loam_mapper_total_iterations(self.h))
