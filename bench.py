@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=150, help="untimed steps; they build the maps")
     ap.add_argument("--streams", type=int, default=128, help="mapping streams per GPU")
     ap.add_argument("--stride", type=int, default=1, help="frame offset between streams")
+    ap.add_argument("--handles", type=int, default=2,
+                    help="mapper handles, each driven by its own host thread (B / handles streams each)")
     ap.add_argument("--map-points", type=int, default=4194304,
                     help="max_map_points per stream and map (arena size; fewer compactions)")
     ap.add_argument("--seed", type=int, default=7)
@@ -117,9 +119,10 @@ def make_frames(seed, n_frames, n_az, device, keep_raw=0, prior="odometry"):
     return frames
 
 
-def step_inputs(frames, streams, stride, k):
-    """batched input arrays for step k (stream b consumes frame b*stride + k)"""
-    fs = [frames[b * stride + k] for b in range(streams)]
+def step_inputs(frames, streams, stride, k, first=0):
+    """batched input arrays for step k (stream b consumes frame b*stride + k); streams
+    first .. first + streams - 1 of the run, numbered from 0 in their handle"""
+    fs = [frames[(first + b) * stride + k] for b in range(streams)]
     return (np.arange(streams, dtype=np.int32),
             np.array([f["corner"].data_ptr() for f in fs], dtype=np.uint64),
             np.array([len(f["corner"]) for f in fs], dtype=np.int32),
@@ -136,6 +139,31 @@ def run_steps(mapper, plan, first, count):
         mapper.solve()
         iters += mapper.total_iterations()
     return iters
+
+
+def run_handles(mappers, plans, first, count):
+    """run_steps on every handle, one host thread each (ctypes releases the GIL in the
+    library calls): one handle's host work overlaps the others' kernels"""
+    if len(mappers) == 1:
+        return run_steps(mappers[0], plans[0], first, count)
+    import threading
+    out = [0] * len(mappers)
+    errs = []
+
+    def work(h):
+        try:
+            out[h] = run_steps(mappers[h], plans[h], first, count)
+        except Exception as e:  # surfaced after the join
+            errs.append(e)
+
+    ts = [threading.Thread(target=work, args=(h,)) for h in range(len(mappers))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    if errs:
+        raise errs[0]
+    return sum(out)
 
 
 def cpu_baseline(frames, warm, n):
@@ -207,25 +235,41 @@ def main():
     cpu_n = 0 if (args.no_cpu or world > 1 or rank != 0) else W + args.cpu_frames
     frames = make_frames(stream_seed(args.seed, rank), max(n_frames, cpu_n), args.n_az, local, keep_raw=cpu_n,
                          prior=args.prior)
-    mapper = BatchMapper(B, device=local, max_map_points=args.map_points)
+    H = max(1, args.handles)
+    if B % H:
+        raise SystemExit("--streams must be divisible by --handles")
+    Bh = B // H
+    if H > 1:
+        # every handle's persistent LM grid must be resident at once: G <= CUs / all streams
+        cus = torch.cuda.get_device_properties(local).multi_processor_count
+        os.environ["LOAM_LM_G"] = str(max(1, cus // B))
+    mappers = [BatchMapper(Bh, device=local, max_map_points=args.map_points) for _ in range(H)]
+    os.environ.pop("LOAM_LM_G", None) if H > 1 else None  # read at create; not for later handles
+    mapper = mappers[0]
 
     def barrier():
         torch.cuda.synchronize(local)
         if world > 1:
             dist.barrier()
 
-    plan = [step_inputs(frames, B, args.stride, k) for k in range(W + K)]
-    run_steps(mapper, plan, 0, W)
-    if not args.no_prof:
-        mapper.set_profiling(True)
-    mapper.reset_kernel_times()
+    plans = [[step_inputs(frames, Bh, args.stride, k, first=h * Bh) for k in range(W + K)] for h in range(H)]
+    run_handles(mappers, plans, 0, W)
+    for m in mappers:
+        if not args.no_prof:
+            m.set_profiling(True)
+        m.reset_kernel_times()
     barrier()
     t0 = time.perf_counter()
-    iters = run_steps(mapper, plan, W, K)
+    iters = run_handles(mappers, plans, W, K)
     barrier()
     dt = time.perf_counter() - t0
-    kt = mapper.kernel_times()
-    mapper.set_profiling(False)
+    kt = {}
+    for m in mappers:
+        for fam, v in m.kernel_times().items():
+            acc = kt.setdefault(fam, {"ms": 0.0, "bytes": 0.0, "launches": 0})
+            for key in acc:
+                acc[key] += v[key]
+        m.set_profiling(False)
     if os.environ.get("BENCH_DEBUG_COUNTERS"):
         dc = mapper.debug_counters()
         print(json.dumps({"debug_counters": [int(v) for v in dc]}), file=sys.stderr, flush=True)
@@ -283,7 +327,8 @@ def main():
                                    "(BASELINE configs[3])",
                        "streams_per_gpu": B, "frames_per_step": B * world, "n_az": args.n_az,
                        "map_frames_before_timing": W,
-                       "parallelism": f"{world} GPU x {B} independent streams"},
+                       "parallelism": f"{world} GPU x {B} independent streams"
+                                      + (f" ({H} handles x {Bh}, one host thread each)" if H > 1 else "")},
             "lm_iterations": int(iters_all),
             "kernel_ms_per_step": {k: round(v["ms"] / K, 4) for k, v in kt.items()},
             "roofline": roofline,
@@ -294,7 +339,8 @@ def main():
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(out["value"] / cpu["value"], 2)
         print(json.dumps(out), flush=True)
-    mapper.close()
+    for m in mappers:
+        m.close()
     if world > 1:
         dist.destroy_process_group()
 
