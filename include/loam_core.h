@@ -224,6 +224,61 @@ int32_t loam_mapper_cube_set(loam_mapper* h, int32_t stream, int32_t which, int3
                              const float* pts, int32_t n);
 
 /* --------------------------------------------------------------------------------------
+ * Sharded LaserMapping: one mapping stream split over `size` GPUs (ranks).
+ * The reference is a single CPU thread and has no counterpart; the semantics are those of
+ * LaserMapping::solveMapping (laser_mapping.cpp:212-814) unchanged.  Each rank stores the map
+ * points of the 4 m voxel-aligned blocks it owns (owner = hash(block) mod size), so the
+ * insertion (:741-788) and the per-cube VoxelGrid (:795-808) are rank-local and exact.  Per
+ * outer round every rank runs the 5-NN (:554, :633) of every query over its own points; one
+ * all-gather merges the per-rank candidate lists into the exact 5-NN.  Every LM pass (Ceres
+ * iteration, :709-729) evaluates a 1/size share of the factors and all-reduces the 29 fp64
+ * normal-equation sums (J^T J upper, J^T r, cost, rows); all ranks then take the identical
+ * trust-region step.  Per frame: one all-reduce of the window cube counts (the submap
+ * sizes of :475-489 and the skip test of :514).
+ *
+ * Transport: a loam_comm is either RCCL (built in, loaded at run time from librccl.so.1; the
+ * collectives are enqueued on the mapper's HIP stream, no host synchronisation) or caller
+ * callbacks.  All ranks call loam_mapper_solve with identical inputs (the feature clouds are
+ * broadcast by the caller, like the reference's single input() call).
+ * ------------------------------------------------------------------------------------ */
+typedef struct loam_comm loam_comm;
+
+#define LOAM_DT_F64 0
+#define LOAM_DT_I32 1
+#define LOAM_RCCL_ID_BYTES 128
+
+typedef struct loam_comm_ops {
+  void* user;
+  /* 1: the library synchronises its stream and passes host (pinned) copies of the buffers;
+     0: device pointers, and hip_stream is the mapper's HIP stream handle to order the work on */
+  int32_t host_buffers;
+  /* in-place sum over all ranks of count elements of dtype (LOAM_DT_*); returns 0 on success */
+  int32_t (*allreduce_sum)(void* user, void* buf, int64_t count, int32_t dtype, void* hip_stream);
+  /* recv[r * bytes .. (r + 1) * bytes) = rank r's send, for every rank r; returns 0 on success */
+  int32_t (*allgather)(void* user, const void* send, void* recv, int64_t bytes, void* hip_stream);
+} loam_comm_ops;
+
+int32_t loam_comm_create(int32_t rank, int32_t size, const loam_comm_ops* ops, loam_comm** out);
+/* RCCL: rank 0 makes the id (ncclGetUniqueId), the caller distributes it to every rank */
+int32_t loam_comm_rccl_unique_id(uint8_t* id);
+int32_t loam_comm_create_rccl(int32_t rank, int32_t size, const uint8_t* id, int32_t device,
+                              loam_comm** out);
+int32_t loam_comm_destroy(loam_comm* c);
+/* collectives through a comm on a device buffer (for tests and callers' own exchanges) */
+int32_t loam_comm_allreduce_sum(loam_comm* c, void* d_buf, int64_t count, int32_t dtype,
+                                void* hip_stream);
+int32_t loam_comm_allgather(loam_comm* c, const void* d_send, void* d_recv, int64_t bytes,
+                            void* hip_stream);
+
+/* a mapper whose streams are each sharded over the comm's ranks (one handle per rank, every
+ * rank with the same n_streams and params); the comm must outlive the mapper */
+int32_t loam_mapper_create_sharded(const loam_params* p, int32_t device, int32_t n_streams,
+                                   loam_comm* comm, loam_mapper** out);
+/* the rank (of nrank) that stores map point xyz of a map with VoxelGrid leaf `leaf`
+ * (mapping_line_resolution for corners, mapping_plane_resolution for surfs); host only */
+int32_t loam_shard_owner(const float* xyz, float leaf, int32_t nrank);
+
+/* --------------------------------------------------------------------------------------
  * Device LM engine on an explicit factor list (lidarFactor.hpp + Ceres TR-LM).  Factor
  * record = 10 doubles: type (1 LidarEdgeFactor, 2 LidarPlaneFactor, 3 LidarPlaneNormFactor),
  * curr_point[3], a[3], b[3] (edge: last_point_a/b; plane: j, unit normal ljm; plane-norm:

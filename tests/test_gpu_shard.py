@@ -1,0 +1,168 @@
+"""GPU: the sharded LaserMapping (include/loam_core.h "Sharded LaserMapping").
+
+One mapping stream split over R ranks (threads of this process on the one GPU of the box,
+meeting in loam_amd.comm.ThreadGroup collectives; RCCL with one rank for the transport):
+  - every rank ends every frame with the bit-identical pose (same all-reduced sums, same step);
+  - poses, submap sizes, correspondence and LM iteration counts equal the unsharded mapper's;
+  - the union of the ranks' cubes is the unsharded map, point for point (bit-exact), and every
+    rank stores only points of the 4 m blocks it owns;
+  - teacher-forced from the oracle's map state: the oracle's pose within 1e-4 m / 1e-4 rad and
+    its correspondence counts.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from helpers import load_state, quat_angle, run_sequence
+from loam_amd.comm import Comm, ThreadGroup
+from loam_amd.mapping import BatchMapper, shard_owner
+
+pytestmark = pytest.mark.gpu
+
+N_FRAMES = 12
+
+
+@pytest.fixture(scope="module")
+def seq():
+    return run_sequence(seed=11, n_frames=N_FRAMES, snapshot_frames=(7,))
+
+
+@pytest.fixture(scope="module")
+def unsharded(seq):
+    m = BatchMapper(1)
+    out = []
+    for rec in seq:
+        m.input(0, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+        m.solve()
+        out.append((m.pose(0), _stat_tuple(m.stats(0))))
+    maps = [m.cubes(0, 0), m.cubes(0, 1)]
+    m.close()
+    return out, maps
+
+
+def _stat_tuple(st):
+    return (st.optimized, st.corner_stack, st.surf_stack, st.corner_map, st.surf_map, tuple(st.corner_num),
+            tuple(st.surf_num), st.lm[0].iterations, st.lm[1].iterations, tuple(st.center), st.valid_num)
+
+
+def _run_ranks(size, body):
+    """body(rank, comm) on `size` threads; returns the per-rank results, re-raises failures"""
+    group = ThreadGroup(size)
+    comms = [group.comm(r) for r in range(size)]
+    res, errs = [None] * size, []
+
+    def run(r):
+        try:
+            res[r] = body(r, comms[r])
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            group.barrier.abort()  # release the other ranks' collectives
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(size)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    if errs:
+        raise errs[0]
+    assert all(not t.is_alive() for t in th)
+    return res
+
+
+def _sequence_body(seq):
+    def body(rank, comm):
+        m = BatchMapper(1, comm=comm)
+        poses, stats = [], []
+        for rec in seq:
+            m.input(0, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+            m.solve()
+            poses.append(m.pose(0))
+            stats.append(_stat_tuple(m.stats(0)))
+        maps = [m.cubes(0, 0), m.cubes(0, 1)]
+        m.close()
+        return poses, stats, maps
+    return body
+
+
+def _rows(a):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    return a[np.lexsort(a.T[::-1])] if len(a) else a
+
+
+def test_single_rank_comm_matches_unsharded(seq, unsharded):
+    """the sharded code path at one rank (trivial collectives) is the unsharded mapper"""
+    ref, ref_maps = unsharded
+    c = Comm.single()
+    poses, stats, maps = _sequence_body(seq)(0, c)
+    for (q, t), ((qr, tr), sr), st in zip(poses, ref, stats):
+        assert st == sr
+        assert np.linalg.norm(t - tr) < 1e-7 and quat_angle(q, qr) < 1e-7
+    for which in range(2):
+        assert sorted(maps[which]) == sorted(ref_maps[which])
+        for cube, pts in ref_maps[which].items():
+            assert np.array_equal(_rows(maps[which][cube]), _rows(pts))
+
+
+@pytest.mark.parametrize("size", [2, 3])
+def test_ranks_match_unsharded(seq, unsharded, size):
+    ref, ref_maps = unsharded
+    res = _run_ranks(size, _sequence_body(seq))
+    for f in range(N_FRAMES):
+        q0, t0 = res[0][0][f]
+        for r in range(1, size):  # identical step on every rank
+            q, t = res[r][0][f]
+            assert np.array_equal(q, q0) and np.array_equal(t, t0), (f, r)
+            assert res[r][1][f] == res[0][1][f]
+        (qr, tr), sr = ref[f]
+        st = res[0][1][f]
+        assert st == sr, (f, st, sr)
+        assert np.linalg.norm(t0 - tr) < 1e-6 and quat_angle(q0, qr) < 1e-6, f
+    leaf = (0.4, 0.8)
+    for which in range(2):
+        cubes = set()
+        for r in range(size):
+            cubes |= set(res[r][2][which])
+            for pts in res[r][2][which].values():  # each rank stores only its blocks
+                for p in pts[:: max(1, len(pts) // 50)]:
+                    assert shard_owner(p, leaf[which], size) == r
+        assert cubes == set(ref_maps[which])
+        for cube, pts in ref_maps[which].items():
+            parts = [res[r][2][which][cube] for r in range(size) if cube in res[r][2][which]]
+            assert np.array_equal(_rows(np.concatenate(parts)), _rows(pts)), (which, cube)
+
+
+def test_teacher_forced_two_ranks(seq):
+    rec = seq[7]
+
+    def body(rank, comm):
+        m = BatchMapper(1, comm=comm)
+        load_state(m, 0, rec["before"])  # cube_set keeps this rank's blocks
+        m.input(0, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+        m.solve()
+        out = m.pose(0), m.stats(0)
+        m.close()
+        return out
+
+    for (q, t), st in _run_ranks(2, body):
+        qr, tr = rec["pose"]
+        sr = rec["stats"]
+        assert np.linalg.norm(t - tr) < 1e-4 and quat_angle(q, qr) < 1e-4
+        assert (st.corner_map, st.surf_map) == (sr.corner_map, sr.surf_map)
+        assert list(st.corner_num) == list(sr.corner_num) and list(st.surf_num) == list(sr.surf_num)
+        assert [st.lm[r].iterations for r in range(2)] == [sr.lm[r].iterations for r in range(2)]
+
+
+def test_rccl_one_rank(seq, unsharded):
+    """RCCL transport (run-time loaded librccl): one rank, collectives on the mapper's stream"""
+    ref, _ = unsharded
+    c = Comm.rccl(0, 1, Comm.rccl_unique_id(), 0)
+    m = BatchMapper(1, comm=c)
+    for rec, ((qr, tr), sr) in zip(seq[:6], ref[:6]):
+        m.input(0, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+        m.solve()
+        q, t = m.pose(0)
+        assert _stat_tuple(m.stats(0)) == sr
+        assert np.linalg.norm(t - tr) < 1e-7 and quat_angle(q, qr) < 1e-7
+    m.close()
+    c.close()

@@ -1,0 +1,52 @@
+// comm.h — the collectives of a sharded mapper (include/loam_core.h, "Sharded LaserMapping").
+//
+// A loam_comm is RCCL (librccl.so.1 loaded at run time; collectives enqueued on the caller's
+// HIP stream, nothing waits on the host) or caller callbacks (device pointers + stream, or
+// host buffers: the library drains its stream into pinned staging, calls back, copies back).
+#pragma once
+#include "common.h"
+
+struct loam_comm {
+  int rank = 0, size = 1;
+  int kind = 0;  // 0 callbacks, 1 RCCL
+  loam_comm_ops ops{};
+  void* nccl = nullptr;  // ncclComm_t
+  int device = 0;
+  // pinned staging of the host-buffer callbacks
+  void* h_send = nullptr;
+  void* h_recv = nullptr;
+  size_t h_cap = 0;
+};
+
+namespace loam {
+
+int32_t comm_allreduce(loam_comm* c, void* d_buf, int64_t count, int32_t dtype, hipStream_t st);
+int32_t comm_allgather(loam_comm* c, const void* d_send, void* d_recv, int64_t bytes, hipStream_t st);
+
+// 4 m voxel-aligned ownership blocks: voxel v = floor(p / leaf) as PCL computes it
+// (floorf(p * (1/leaf)), voxel.h); block = floor(v / bv) with bv voxels per block edge, so a
+// voxel never straddles two owners and every rank's per-cube VoxelGrid is exact.
+__host__ __device__ inline int shard_floor_div(int v, int d) { return v >= 0 ? v / d : -((-v + d - 1) / d); }
+__host__ __device__ inline uint32_t shard_mix(uint32_t h) {  // murmur3 finaliser
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+__host__ __device__ inline int shard_owner(float x, float y, float z, float inv, int bv, int nrank) {
+  if (nrank <= 1) return 0;
+  const int bx = shard_floor_div((int)floorf(x * inv), bv);
+  const int by = shard_floor_div((int)floorf(y * inv), bv);
+  const int bz = shard_floor_div((int)floorf(z * inv), bv);
+  const uint32_t h = shard_mix((uint32_t)bx * 73856093u ^ (uint32_t)by * 19349663u ^ (uint32_t)bz * 83492791u);
+  return (int)(h % (uint32_t)nrank);
+}
+// voxels per block edge for a leaf (4 m blocks: 10 voxels of 0.4 m, 5 of 0.8 m)
+inline int shard_block_voxels(float leaf) {
+  const int bv = (int)lroundf(4.0f / leaf);
+  return bv < 1 ? 1 : bv;
+}
+
+}  // namespace loam

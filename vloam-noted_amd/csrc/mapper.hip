@@ -28,6 +28,7 @@
 #include "common.h"
 #include "device_math.h"
 #include "cellhash.h"
+#include "comm.h"
 #include "cubeindex.h"
 #include "lm.h"
 #include "voxel.h"
@@ -116,6 +117,24 @@ struct MapperDev {
   uint32_t* lm_sync;   // [B][2 rounds][4]: worker arrivals, eval-point generation, status
   double* lm_xpub;     // [B][2 rounds][8]: eval point published to the workers
   uint32_t* tickets;  // [B]
+  // sharded mode (loam_mapper_create_sharded): this rank of nrank; map points are stored by
+  // the rank owning their 4 m block (comm.h, shard_owner); blk_v: voxels per block edge
+  int rank = 0, nrank = 1, sharded = 0;
+  int blk_v[2] = {1, 1};
+  uint32_t* wcnt;        // [B][2][WIN_MAX] window cube counts (all-reduced over the ranks)
+  struct NnRec* nn_send; // [queries of all streams] this rank's 5 nearest candidates per query
+  const struct NnRec* nn_recv;  // [nrank][same]: every rank's candidates (all-gather)
+  const int* q_off;      // [B] first query of stream s in nn_send
+  float4* nn_xyz;        // [5][B][2*max_in] merged neighbours (k_geom input in sharded mode)
+  double* lm_red;        // [B][LM_NACC] this rank's normal-equation sums, then the all-reduced
+};
+
+// one query's 5 nearest candidates on one rank (d: FLANN L2_Simple float distance, id: global
+// tie-break key, xyz: the point) — the all-gathered record of the sharded kNN
+struct NnRec {
+  float d[5];
+  int id[5];
+  float x[5], y[5], z[5];
 };
 
 __device__ inline size_t sm_index(int s, int m) { return (size_t)s * 2 + m; }
@@ -196,8 +215,9 @@ __global__ void __launch_bounds__(128) k_submap_prep(MapperDev D) {
   const uint2* tab = D.cube_tab + sm_index(s, m) * NCUBE;
   const int vn = F.valid_num;
   const int w0 = 2 * lane, w1 = 2 * lane + 1;
-  const uint32_t c0 = w0 < vn ? tab[F.window[w0]].y : 0u;
-  const uint32_t c1 = w1 < vn ? tab[F.window[w1]].y : 0u;
+  const uint32_t* wc = D.wcnt + sm_index(s, m) * WIN_MAX;  // sharded: summed over the ranks
+  const uint32_t c0 = w0 < vn ? (D.sharded ? wc[w0] : tab[F.window[w0]].y) : 0u;
+  const uint32_t c1 = w1 < vn ? (D.sharded ? wc[w1] : tab[F.window[w1]].y) : 0u;
   const uint32_t inc = wave_incl_scan_u(c0 + c1);
   uint32_t total = __shfl(inc, 63, 64);
   const bool over = total > (uint32_t)D.sub_cap;
@@ -218,6 +238,19 @@ __global__ void __launch_bounds__(128) k_submap_prep(MapperDev D) {
   __syncthreads();
   // laser_mapping.cpp:514
   if (threadIdx.x == 0) F.optimize = (F.sub_n[0] > 10 && F.sub_n[1] > 50) ? 1 : 0;
+}
+
+// sharded: this rank's point count of every window cube, all-reduced before k_submap_prep so
+// that every rank sees the whole submap's sizes and concatenation offsets (:475-489, :514)
+__global__ void __launch_bounds__(256) k_submap_count(MapperDev D) {
+  const int s = D.s0 + blockIdx.x;
+  const StreamFrame& F = D.fr[s];
+  for (int t = threadIdx.x; t < 2 * WIN_MAX; t += blockDim.x) {
+    const int m = t / WIN_MAX, w = t % WIN_MAX;
+    uint32_t c = 0;
+    if (F.active && w < F.valid_num) c = D.cube_tab[sm_index(s, m) * NCUBE + F.window[w]].y;
+    D.wcnt[sm_index(s, m) * WIN_MAX + w] = c;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -319,7 +352,10 @@ __global__ void __launch_bounds__(CORR_THREADS) k_knn(MapperDev D, int round) {
       for (uint32_t k = 0; k < e.y; ++k) {
         const uint32_t pos = off + e.x + k;
         const float4 p = cp[pos];
-        near5_offer(T, fdist2(q.x, q.y, q.z, p.x, p.y, p.z), sub + __float_as_int(p.w), (int)pos);
+        // sharded: submap position x ranks + rank keeps the key unique (and equal to the
+        // unsharded key at one rank)
+        const int key = (sub + __float_as_int(p.w)) * D.nrank + D.rank;
+        near5_offer(T, fdist2(q.x, q.y, q.z, p.x, p.y, p.z), key, (int)pos);
       }
     };
     for (int o = 0; o < 27; ++o) {
@@ -355,6 +391,19 @@ __global__ void __launch_bounds__(CORR_THREADS) k_knn(MapperDev D, int round) {
         scan(b2[0], b2[1], b2[2], l2[0], l2[1], l2[2]);
       }
     }
+    if (D.sharded) {  // this rank's candidates; the 1 m test follows the merge (k_nn_merge)
+      NnRec& o = D.nn_send[D.q_off[s] + ridx];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        o.d[k] = T.d[k];
+        o.id[k] = T.id[k];
+        const float4 p = T.pos[k] >= 0 ? cp[T.pos[k]] : make_float4(0.f, 0.f, 0.f, 0.f);
+        o.x[k] = p.x;
+        o.y[k] = p.y;
+        o.z[k] = p.z;
+      }
+      continue;
+    }
     const bool ok = T.d[4] < 1.0f;
 #pragma unroll
     for (int k = 0; k < 5; ++k) D.knn_id[k * D.knn_stride + rb + ridx] = ok ? T.pos[k] : -1;
@@ -363,6 +412,59 @@ __global__ void __launch_bounds__(CORR_THREADS) k_knn(MapperDev D, int round) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wc += __shfl_xor(wc, o, 64);
   if ((threadIdx.x & 63) == 0 && wc) atomicAdd(&F.cand[round], wc);
+}
+
+// sharded: merge every rank's 5 candidates into the exact 5-NN of the whole submap (each
+// rank's list is exact over its own points, so the union's 5 smallest (d, key) are the
+// unsharded result), then the 1 m acceptance (:557, :642).  Neighbours go to nn_xyz.
+__global__ void __launch_bounds__(CORR_THREADS) k_nn_merge(MapperDev D) {
+  const int s = D.s0 + blockIdx.x % D.B, blk = blockIdx.x / D.B;
+  const StreamFrame& F = D.fr[s];
+  if (!F.active || !F.optimize) return;
+  const int nq = F.nc_stack + F.ns_stack;
+  const size_t rb = (size_t)s * 2 * D.max_in;
+  const size_t qtot = (size_t)D.q_off[D.s0 + D.B];  // records per rank
+  for (int ridx = blk * CORR_THREADS + threadIdx.x; ridx < nq; ridx += CORR_BLK * CORR_THREADS) {
+    Near5 T;
+    float px[5], py[5], pz[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      T.d[k] = INFINITY;
+      T.id[k] = 0x7FFFFFFF;
+      T.pos[k] = -1;
+      px[k] = py[k] = pz[k] = 0.f;
+    }
+    for (int r = 0; r < D.nrank; ++r) {
+      const NnRec& c = D.nn_recv[(size_t)r * qtot + D.q_off[s] + ridx];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const float d = c.d[k];
+        const int id = c.id[k];
+        if (!(d < T.d[4] || (d == T.d[4] && id < T.id[4]))) break;  // c is sorted
+        // insert at the tail, bubble up; pos carries the candidate's slot in (px, py, pz)
+        int j = 4;
+        while (j > 0 && (d < T.d[j - 1] || (d == T.d[j - 1] && id < T.id[j - 1]))) {
+          T.d[j] = T.d[j - 1];
+          T.id[j] = T.id[j - 1];
+          px[j] = px[j - 1];
+          py[j] = py[j - 1];
+          pz[j] = pz[j - 1];
+          --j;
+        }
+        T.d[j] = d;
+        T.id[j] = id;
+        px[j] = c.x[k];
+        py[j] = c.y[k];
+        pz[j] = c.z[k];
+      }
+    }
+    const bool ok = T.d[4] < 1.0f;
+    D.knn_id[rb + ridx] = ok ? 0 : -1;
+    if (ok) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) D.nn_xyz[k * D.knn_stride + rb + ridx] = make_float4(px[k], py[k], pz[k], 0.f);
+    }
+  }
 }
 
 // pass 2: line PCA / plane fit of the 5 neighbours -> factor records (laser_mapping.cpp:557-603,
@@ -389,7 +491,7 @@ __global__ void __launch_bounds__(CORR_THREADS) k_geom(MapperDev D, int round) {
       float nb[5][3];
 #pragma unroll
       for (int j = 0; j < 5; ++j) {
-        const float4 p = lin[D.knn_id[j * D.knn_stride + rb + ridx]];
+        const float4 p = D.sharded ? D.nn_xyz[j * D.knn_stride + rb + ridx] : lin[D.knn_id[j * D.knn_stride + rb + ridx]];
         nb[j][0] = p.x;
         nb[j][1] = p.y;
         nb[j][2] = p.z;
@@ -445,8 +547,23 @@ __global__ void __launch_bounds__(LM_THREADS) k_lm_eval(MapperDev D, int round) 
   const size_t rb = (size_t)s * 2 * D.max_in;
   const LmRecView R{D.r_type + rb, D.r_px + rb, D.r_py + rb, D.r_pz + rb, D.r_a[0] + rb,
                     D.r_a[1] + rb, D.r_a[2] + rb, D.r_b[0] + rb, D.r_b[1] + rb, D.r_b[2] + rb};
-  lm_eval_block<LM_THREADS>(R, F.nc_stack + F.ns_stack, F.lm[round], blk, LM_EBLK,
+  // sharded: this rank's workgroups are blocks rank * LM_EBLK + blk of nrank * LM_EBLK
+  lm_eval_block<LM_THREADS>(R, F.nc_stack + F.ns_stack, F.lm[round], D.rank * LM_EBLK + blk, D.nrank * LM_EBLK,
                             D.partials + ((size_t)s * LM_EBLK + blk) * LM_NACC);
+}
+
+// sharded: this rank's partials -> lm_red[s] (fixed order), then all-reduced over the ranks
+__global__ void __launch_bounds__(64) k_lm_reduce(MapperDev D, int round) {
+  const int s = D.s0 + blockIdx.x;
+  const StreamFrame& F = D.fr[s];
+  if (!F.active || F.lm[round].status == LM_DONE) return;
+  const int lane = threadIdx.x;
+  if (lane < LM_NACC) {
+    const double* p = D.partials + (size_t)s * LM_EBLK * LM_NACC;
+    double v = 0.0;
+    for (int c = 0; c < LM_EBLK; ++c) v += p[(size_t)c * LM_NACC + lane];
+    D.lm_red[(size_t)s * LM_NACC + lane] = v;
+  }
 }
 
 // LM step: one wave per stream; on termination the best point becomes the stream pose
@@ -456,7 +573,10 @@ __global__ void __launch_bounds__(64) k_lm_step(MapperDev D, int round) {
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
   LmState& S = F.lm[round];
-  lm_step_wave(D.partials + (size_t)s * LM_EBLK * LM_NACC, LM_EBLK, S, F.pose);  // pose = best when done
+  if (D.sharded)  // the all-reduced sums: every rank takes the identical step
+    lm_step_wave(D.lm_red + (size_t)s * LM_NACC, 1, S, F.pose);
+  else
+    lm_step_wave(D.partials + (size_t)s * LM_EBLK * LM_NACC, LM_EBLK, S, F.pose);  // pose = best when done
 }
 
 // ---------------------------------------------------------------------------------------
@@ -508,7 +628,9 @@ __global__ void k_insert(MapperDev D) {
     const float4 sel = to_map(X, D.stack[m][(size_t)s * D.max_in + i]);
     const int ci = cube_of(sel.x, F.cen[0]), cj = cube_of(sel.y, F.cen[1]), ck = cube_of(sel.z, F.cen[2]);
     int tag = -1;
-    if (ci >= 0 && ci < CW && cj >= 0 && cj < CH && ck >= 0 && ck < CD) {
+    // sharded: only the owner of the point's 4 m block stores it (comm.h)
+    const bool mine = !D.sharded || shard_owner(sel.x, sel.y, sel.z, 1.0f / D.leaf[m], D.blk_v[m], D.nrank) == D.rank;
+    if (mine && ci >= 0 && ci < CW && cj >= 0 && cj < CH && ck >= 0 && ck < CD) {
       tag = ci + CW * cj + CW * CH * ck;
       const bool in_window = ci >= F.center[0] - 2 && ci <= F.center[0] + 2 &&
                              cj >= F.center[1] - 2 && cj <= F.center[1] + 2 &&
@@ -961,6 +1083,9 @@ struct loam_mapper {
   // the window that receive points; a write past the capacity is reported (err flags)
   uint32_t compact_at = 0;
   int lm_G = 0;  // workgroups per stream of k_lm_round (0: two-kernel path k_lm_eval / k_lm_step)
+  loam_comm* comm = nullptr;  // sharded mode (loam_mapper_create_sharded)
+  PinnedArray<int> q_off;     // [B + 1] query offsets of the sharded kNN exchange
+  int* d_q_off = nullptr;
 };
 
 namespace {
@@ -1048,7 +1173,8 @@ int32_t check_stream(loam_mapper* h, int32_t s) {
 
 extern "C" {
 
-int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_streams, loam_mapper** out) {
+static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_streams, loam_comm* comm,
+                             loam_mapper** out) {
   if (!out || n_streams <= 0) {
     set_error("loam_mapper_create: bad arguments");
     return LOAM_ERR_ARG;
@@ -1060,8 +1186,14 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
   if (p) h->P = *p; else loam_params_default(&h->P);
   h->dev = device;
   h->B = n_streams;
+  h->comm = comm;
   MapperDev& D = h->D;
   D.B = n_streams;
+  if (comm) {
+    D.sharded = 1;
+    D.rank = comm->rank;
+    D.nrank = comm->size;
+  }
   D.max_in = h->P.max_input_points;
   D.map_cap = h->P.max_map_points;
   D.sub_cap = h->P.max_submap_points;
@@ -1079,7 +1211,7 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
     const bool allow = !(env && env[0] == '0');
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
       h->n_cu = cus;
-    if (allow && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_lm_round, LM_THREADS, 0) == hipSuccess &&
+    if (allow && !comm && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_lm_round, LM_THREADS, 0) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess) {
       // 256 threads x 256 VGPRs: exactly one block per CU; the API can over-report by one
       // block per CU at some SGPR counts (MI355X_MICROARCH.md, correctness boundaries)
@@ -1111,7 +1243,7 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
   {
     // LOAM_MAPPER_GROUPS: stream groups on separate HIP streams (B divisible by the count)
     const char* genv = std::getenv("LOAM_MAPPER_GROUPS");
-    int ng = genv ? std::atoi(genv) : 1;
+    int ng = (genv && !comm) ? std::atoi(genv) : 1;  // sharded: one group (collectives on st)
     ng = std::max(1, std::min(ng, MAX_GROUPS));
     while (ng > 1 && B % ng != 0) --ng;
     h->groups = ng;
@@ -1172,6 +1304,20 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
   ALLOC(D.tickets, B);
   ALLOC(h->d_pairs, B * 2);
   ALLOC(h->d_new_off, B * 2 * (NCUBE + 1));
+  if (D.sharded) {
+    for (int m = 0; m < 2; ++m) D.blk_v[m] = shard_block_voxels(D.leaf[m]);
+    const size_t nq = B * 2 * (size_t)D.max_in;
+    NnRec* recv = nullptr;
+    ALLOC(D.wcnt, B * 2 * (size_t)WIN_MAX);
+    ALLOC(D.nn_send, nq);
+    ALLOC(recv, nq * D.nrank);
+    D.nn_recv = recv;
+    ALLOC(D.nn_xyz, 5 * nq);
+    ALLOC(D.lm_red, B * (size_t)LM_NACC);
+    ALLOC(h->d_q_off, B + 1);
+    D.q_off = h->d_q_off;
+    if (!h->q_off.assign(B + 1, 0)) return fail(LOAM_ERR_HIP);
+  }
 #undef ALLOC
   D.cube_tab = h->cube_tab[0];
   if (!h->hf.assign(B, StreamFrame{})) return fail(LOAM_ERR_HIP);
@@ -1184,6 +1330,24 @@ int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_strea
   if (hipStreamSynchronize(h->st) != hipSuccess) return fail(LOAM_ERR_HIP);  // zero-fills done
   *out = h;
   return LOAM_OK;
+}
+
+int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_streams, loam_mapper** out) {
+  return mapper_create(p, device, n_streams, nullptr, out);
+}
+
+int32_t loam_mapper_create_sharded(const loam_params* p, int32_t device, int32_t n_streams, loam_comm* comm,
+                                   loam_mapper** out) {
+  if (!comm) {
+    set_error("loam_mapper_create_sharded: null comm");
+    return LOAM_ERR_ARG;
+  }
+  return mapper_create(p, device, n_streams, comm, out);
+}
+
+int32_t loam_shard_owner(const float* xyz, float leaf, int32_t nrank) {
+  if (!xyz || !(leaf > 0.f) || nrank < 1) return LOAM_ERR_ARG;
+  return shard_owner(xyz[0], xyz[1], xyz[2], 1.0f / leaf, shard_block_voxels(leaf), nrank);
 }
 
 int32_t loam_mapper_destroy(loam_mapper* h) {
@@ -1416,15 +1580,36 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     D.cube_tab = h->cube_tab[h->parity];
     for (int g = 0; g < NG; ++g) Dg[g].cube_tab = D.cube_tab;
   }
+  if (D.sharded) {  // the submap sizes over all ranks (NG = 1)
+    LAUNCH(FAM_OTHER, k_submap_count<<<B, 256, 0, st>>>(D));
+    TRY(comm_allreduce(h->comm, D.wcnt, (int64_t)B * 2 * WIN_MAX, LOAM_DT_I32, st));
+  }
   for (int g = 0; g < NG; ++g) LAUNCH_ON(h->gst[g], FAM_OTHER, k_submap_prep<<<Bg, 128, 0, h->gst[g]>>>(Dg[g]));
   LOAM_HIP(hipEventRecord(h->ev[1], st));
   for (int g = 0; g < NG; ++g) LOAM_HIP(hipStreamWaitEvent(h->gst[g], h->gjoin[g], 0));
+  size_t q_tot = 0;
+  if (D.sharded) {
+    // the stack sizes (identical on every rank) place each stream's queries in the exchange
+    LOAM_HIP(hipMemcpyAsync(h->hf.data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
+    LOAM_HIP(hipStreamSynchronize(st));
+    for (int s = 0; s < B; ++s) {
+      const StreamFrame& F = h->hf[s];
+      h->q_off[s] = (int)q_tot;
+      if (F.active) q_tot += (size_t)F.nc_stack + F.ns_stack;
+    }
+    h->q_off[B] = (int)q_tot;
+    LOAM_HIP(hipMemcpyAsync(h->d_q_off, h->q_off.data(), sizeof(int) * (B + 1), hipMemcpyHostToDevice, st));
+  }
   for (int round = 0; round < 2; ++round) {
     for (int g = 0; g < NG; ++g) {
       hipStream_t sg = h->gst[g];
       LOAM_HIP(before(g, 2 + 3 * round, sg));
       LAUNCH_ON(sg, FAM_CORR, k_knn<<<Bg * CORR_BLK, CORR_THREADS, 0, sg>>>(Dg[g], round));
       LOAM_HIP(after(g, 2 + 3 * round, sg));
+    }
+    if (D.sharded) {  // every rank's candidates -> the exact 5-NN on every rank
+      TRY(comm_allgather(h->comm, D.nn_send, const_cast<NnRec*>(D.nn_recv), (int64_t)(q_tot * sizeof(NnRec)), st));
+      LAUNCH(FAM_CORR, k_nn_merge<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D));
     }
     for (int g = 0; g < NG; ++g) {
       hipStream_t sg = h->gst[g];
@@ -1440,6 +1625,10 @@ int32_t loam_mapper_solve(loam_mapper* h) {
       } else {
         for (int it = 0; it < 5; ++it) {  // iteration 0 + max_num_iterations = 4 candidates
           LAUNCH_ON(sg, FAM_LM, k_lm_eval<<<Bg * LM_EBLK, LM_THREADS, 0, sg>>>(Dg[g], round));
+          if (D.sharded) {  // per Ceres iteration: all-reduce of the 6x6 normal equations
+            LAUNCH_ON(sg, FAM_LM, k_lm_reduce<<<Bg, 64, 0, sg>>>(Dg[g], round));
+            TRY(comm_allreduce(h->comm, D.lm_red, (int64_t)B * LM_NACC, LOAM_DT_F64, sg));
+          }
           LAUNCH_ON(sg, FAM_LM, k_lm_step<<<Bg, 64, 0, sg>>>(Dg[g], round));
         }
       }
@@ -1696,6 +1885,13 @@ int32_t loam_mapper_cube_set(loam_mapper* h, int32_t s, int32_t which, int32_t c
   TRY(check_stream(h, s));
   if (which < 0 || which > 1 || cube < 0 || cube >= NCUBE || n < 0 || (n > 0 && !pts)) return LOAM_ERR_ARG;
   LOAM_HIP(hipSetDevice(h->dev));
+  std::vector<float> mine;
+  if (h->D.sharded) {  // a sharded handle stores the points of the blocks its rank owns
+    for (int i = 0; i < n; ++i)
+      if (loam_shard_owner(pts + 4 * (size_t)i, h->D.leaf[which], h->D.nrank) == h->D.rank) mine.insert(mine.end(), pts + 4 * (size_t)i, pts + 4 * (size_t)i + 4);
+    pts = mine.data();
+    n = (int32_t)(mine.size() / 4);
+  }
   StreamFrame& F = h->hf[s];
   uint32_t& tail = F.arena_tail[which];
   if (tail + (uint32_t)n > (uint32_t)h->D.map_cap) {

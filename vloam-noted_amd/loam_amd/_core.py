@@ -105,6 +105,14 @@ SIGNATURES = {
     "loam_mapper_cube_copy": (c_i32, [vp, c_i32, c_i32, c_i32, vp]),
     "loam_mapper_stack_copy": (c_i32, [vp, c_i32, c_i32, vp, c_i32]),
     "loam_mapper_cube_set": (c_i32, [vp, c_i32, c_i32, c_i32, vp, c_i32]),
+    "loam_comm_create": (c_i32, [c_i32, c_i32, vp, ctypes.POINTER(vp)]),
+    "loam_comm_rccl_unique_id": (c_i32, [vp]),
+    "loam_comm_create_rccl": (c_i32, [c_i32, c_i32, vp, c_i32, ctypes.POINTER(vp)]),
+    "loam_comm_destroy": (c_i32, [vp]),
+    "loam_comm_allreduce_sum": (c_i32, [vp, vp, ctypes.c_int64, c_i32, vp]),
+    "loam_comm_allgather": (c_i32, [vp, vp, vp, ctypes.c_int64, vp]),
+    "loam_mapper_create_sharded": (c_i32, [ctypes.POINTER(Params), c_i32, c_i32, vp, ctypes.POINTER(vp)]),
+    "loam_shard_owner": (c_i32, [vp, c_f, c_i32]),
     "loam_lm_solve": (c_i32, [c_i32, vp, c_i32, vp, c_i32, ctypes.POINTER(LMStats)]),
     "loam_lm_normal_equations": (c_i32, [c_i32, vp, c_i32, vp, vp, vp, vp]),
     "loam_voxel_grid": (c_i32, [c_i32, vp, c_i32, c_f, vp, ctypes.POINTER(c_i32)]),

@@ -1,0 +1,187 @@
+"""Communicators of the sharded LaserMapping (include/loam_core.h, "Sharded LaserMapping").
+
+A sharded mapper (``BatchMapper(..., comm=c)``) splits every mapping stream over ``c.size``
+ranks: each rank stores the map points of the 4 m blocks it owns, the 5-NN candidate lists are
+all-gathered once per outer round and every Ceres iteration all-reduces the 29 normal-equation
+sums.  Transports:
+
+- ``Comm.rccl(rank, size, uid, device)`` — RCCL over xGMI, collectives enqueued on the
+  mapper's HIP stream (no host synchronisation).  ``Comm.rccl_unique_id()`` on rank 0, shared
+  by the caller (``bench.py`` uses torch.distributed's object broadcast).
+- ``ThreadGroup(size).comm(rank)`` — ranks as threads of one process (one GPU or several):
+  host-buffer callbacks meeting at a barrier, summed in rank order.
+- ``TorchDistComm.create()`` — host-buffer callbacks over an initialised torch.distributed group
+  (gloo), all-gather + ordered sum so every rank gets bit-identical sums.
+
+Every allreduce must give bit-identical results on all ranks (every rank then takes the same
+trust-region step and stores points with the same pose); RCCL's ring / tree algorithms reduce
+each element once and broadcast it, the Python transports sum in rank order.
+"""
+import ctypes
+import threading
+
+import numpy as np
+
+from ._core import check, lib
+
+DT_F64, DT_I32 = 0, 1
+RCCL_ID_BYTES = 128
+
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                ctypes.c_int32, ctypes.c_void_p)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_int64, ctypes.c_void_p)
+
+
+class CommOps(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("host_buffers", ctypes.c_int32),
+                ("allreduce_sum", ALLREDUCE_FN), ("allgather", ALLGATHER_FN)]
+
+
+def _view(buf, count, dtype):
+    ct = ctypes.c_double if dtype == DT_F64 else ctypes.c_int32
+    return np.ctypeslib.as_array(ctypes.cast(buf, ctypes.POINTER(ct)), shape=(count,))
+
+
+def _bytes_view(buf, n):
+    return np.ctypeslib.as_array(ctypes.cast(buf, ctypes.POINTER(ctypes.c_uint8)), shape=(n,))
+
+
+class Comm:
+    """A loam_comm handle (must outlive the mappers that use it)."""
+
+    def __init__(self, handle, rank, size, keep=()):
+        self.h = handle
+        self.rank = rank
+        self.size = size
+        self._keep = keep  # ctypes callbacks referenced by the C side
+
+    @staticmethod
+    def rccl_unique_id():
+        buf = (ctypes.c_uint8 * RCCL_ID_BYTES)()
+        check(lib().loam_comm_rccl_unique_id(buf))
+        return bytes(buf)
+
+    @classmethod
+    def rccl(cls, rank, size, uid, device=0):
+        if len(uid) != RCCL_ID_BYTES:
+            raise ValueError("RCCL unique id must be 128 bytes")
+        buf = (ctypes.c_uint8 * RCCL_ID_BYTES).from_buffer_copy(uid)
+        h = ctypes.c_void_p()
+        check(lib().loam_comm_create_rccl(rank, size, buf, device, ctypes.byref(h)))
+        return cls(h, rank, size)
+
+    @classmethod
+    def from_host_callbacks(cls, rank, size, allreduce, allgather):
+        """allreduce(np_array) sums in place over the ranks; allgather(np_uint8_send) -> bytes of
+        every rank's send in rank order (written into the returned buffer)."""
+
+        def ar(user, buf, count, dtype, stream):
+            try:
+                allreduce(_view(buf, count, dtype))
+                return 0
+            except Exception:  # noqa: BLE001 — reported to the C side as a failed collective
+                return 1
+
+        def ag(user, send, recv, nbytes, stream):
+            try:
+                out = allgather(_bytes_view(send, nbytes))
+                _bytes_view(recv, nbytes * size)[:] = out
+                return 0
+            except Exception:  # noqa: BLE001
+                return 1
+
+        ops = CommOps()
+        ops.user = None
+        ops.host_buffers = 1
+        ops.allreduce_sum = ALLREDUCE_FN(ar)
+        ops.allgather = ALLGATHER_FN(ag)
+        h = ctypes.c_void_p()
+        check(lib().loam_comm_create(rank, size, ctypes.byref(ops), ctypes.byref(h)))
+        return cls(h, rank, size, keep=(ops, ops.allreduce_sum, ops.allgather, ar, ag))
+
+    @classmethod
+    def single(cls):
+        """a one-rank comm: the sharded code path with trivial collectives"""
+        h = ctypes.c_void_p()
+        check(lib().loam_comm_create(0, 1, None, ctypes.byref(h)))
+        return cls(h, 0, 1)
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().loam_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ThreadGroup:
+    """Ranks as threads of one process: collectives meet at a barrier (timeout: a rank that
+    fails makes the others' collectives fail instead of hanging)."""
+
+    def __init__(self, size, timeout=120.0):
+        self.size = size
+        self.barrier = threading.Barrier(size, timeout=timeout)
+        self.slots = [None] * size
+
+    def _allreduce(self, rank, arr):
+        self.slots[rank] = arr.copy()
+        self.barrier.wait()
+        total = self.slots[0].copy()
+        for r in range(1, self.size):
+            total += self.slots[r]
+        self.barrier.wait()
+        arr[:] = total
+
+    def _allgather(self, rank, send):
+        self.slots[rank] = send.copy()
+        self.barrier.wait()
+        out = np.concatenate(self.slots)
+        self.barrier.wait()
+        return out
+
+    def comm(self, rank):
+        return Comm.from_host_callbacks(rank, self.size, lambda a: self._allreduce(rank, a),
+                                        lambda s: self._allgather(rank, s))
+
+
+def dist_allreduce_ordered(arr):
+    """in-place sum of a numpy array over the default torch.distributed group, as an
+    all-gather + rank-ordered sum: bit-identical on every rank whatever the backend"""
+    import torch
+    import torch.distributed as dist
+
+    t = torch.from_numpy(np.array(arr, copy=True))
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    total = parts[0].clone()
+    for p in parts[1:]:
+        total += p
+    arr[:] = total.numpy()
+
+
+def dist_allgather_bytes(send):
+    """every rank's uint8 buffer (same size everywhere), concatenated in rank order"""
+    import torch
+    import torch.distributed as dist
+
+    t = torch.from_numpy(np.array(send, copy=True))
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return torch.cat(parts).numpy()
+
+
+class TorchDistComm:
+    """Host-buffer comm over the default torch.distributed group (e.g. gloo, one process per
+    rank), through dist_allreduce_ordered / dist_allgather_bytes."""
+
+    @staticmethod
+    def create():
+        import torch.distributed as dist
+
+        return Comm.from_host_callbacks(dist.get_rank(), dist.get_world_size(), dist_allreduce_ordered,
+                                        dist_allgather_bytes)

@@ -20,13 +20,28 @@ N_CUBES = 21 * 21 * 11
 
 
 class BatchMapper:
-    def __init__(self, n_streams=1, device=0, params=None, **param_overrides):
+    """n_streams independent LaserMapping streams.  With ``comm`` (loam_amd.comm.Comm) every
+    stream is sharded over the comm's ranks: this object is one rank's share, every rank
+    feeds identical inputs and calls ``solve`` together (include/loam_core.h)."""
+
+    def __init__(self, n_streams=1, device=0, params=None, comm=None, **param_overrides):
         self.params = params if params is not None else _core.default_params(**param_overrides)
         self.n_streams = n_streams
         self.device = device
+        self.comm = comm  # kept alive as long as the mapper
         h = ctypes.c_void_p()
-        check(lib().loam_mapper_create(ctypes.byref(self.params), device, n_streams, ctypes.byref(h)))
+        if comm is None:
+            check(lib().loam_mapper_create(ctypes.byref(self.params), device, n_streams, ctypes.byref(h)))
+        else:
+            check(lib().loam_mapper_create_sharded(ctypes.byref(self.params), device, n_streams, comm.h,
+                                                   ctypes.byref(h)))
         self.h = h
+
+    def point_owner(self, which, xyz):
+        """rank storing map point xyz of map `which` (0 corner, 1 surf) under this sharding"""
+        leaf = self.params.mapping_line_resolution if which == 0 else self.params.mapping_plane_resolution
+        return shard_owner(xyz, leaf, self.comm.size if self.comm is not None else 1)
+
 
     def close(self):
         if getattr(self, "h", None) and self.h.value:
@@ -179,3 +194,9 @@ class LaserMapping:
     @property
     def batch(self):
         return self._m
+
+
+def shard_owner(xyz, leaf, nrank):
+    """owner rank of a map point (4 m voxel-aligned blocks, include/loam_core.h)"""
+    p = np.ascontiguousarray(np.asarray(xyz, dtype=np.float32)[:3])
+    return check(lib().loam_shard_owner(ptr(p), float(leaf), int(nrank)))
