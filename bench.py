@@ -62,6 +62,10 @@ def parse():
                     help="mapping prior: GPU LaserOdometry output (default) or ground truth + random walk")
     ap.add_argument("--no-single-stream", action="store_true",
                     help="skip the single-stream (latency view) timing")
+    ap.add_argument("--shard", action="store_true",
+                    help="sharded mapping (SURVEY.md §8e): every stream split over all N ranks, map "
+                         "blocks owned per rank, RCCL all-gather of 5-NN candidates per round and "
+                         "all-reduce of the normal equations per LM iteration (strong scaling)")
     return ap.parse_args()
 
 
@@ -233,17 +237,33 @@ def main():
     B, K, W = args.streams, args.steps, args.warmup
     n_frames = (B - 1) * args.stride + W + K
     cpu_n = 0 if (args.no_cpu or world > 1 or rank != 0) else W + args.cpu_frames
-    frames = make_frames(stream_seed(args.seed, rank), max(n_frames, cpu_n), args.n_az, local, keep_raw=cpu_n,
-                         prior=args.prior)
-    H = max(1, args.handles)
+    # sharded: every rank runs the same streams (identical inputs, one share of each map)
+    frames = make_frames(stream_seed(args.seed, 0 if args.shard else rank), max(n_frames, cpu_n), args.n_az, local,
+                         keep_raw=cpu_n, prior=args.prior)
+    H = 1 if args.shard else max(1, args.handles)
     if B % H:
         raise SystemExit("--streams must be divisible by --handles")
     Bh = B // H
+    comm = None
+    if args.shard:
+        from loam_amd.comm import Comm
+        uid = [Comm.rccl_unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        # RCCL prints its banner on stdout at init: keep stdout for the one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            comm = Comm.rccl(rank, world, uid[0], local)
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
     if H > 1:
         # every handle's persistent LM grid must be resident at once: G <= CUs / all streams
         cus = torch.cuda.get_device_properties(local).multi_processor_count
         os.environ["LOAM_LM_G"] = str(max(1, cus // B))
-    mappers = [BatchMapper(Bh, device=local, max_map_points=args.map_points) for _ in range(H)]
+    mappers = [BatchMapper(Bh, device=local, max_map_points=args.map_points, comm=comm) for _ in range(H)]
     os.environ.pop("LOAM_LM_G", None) if H > 1 else None  # read at create; not for later handles
     mapper = mappers[0]
 
@@ -275,9 +295,11 @@ def main():
         print(json.dumps({"debug_counters": [int(v) for v in dc]}), file=sys.stderr, flush=True)
 
     iters_all, dt_max = aggregate(iters, dt, world, f"cuda:{local}")
+    if args.shard:  # every rank counted the same iterations of the same streams
+        iters_all = iters_all / world
 
     single = None
-    if not args.no_single_stream and rank == 0 and world == 1:
+    if not args.no_single_stream and rank == 0 and world == 1 and not args.shard:
         m1 = BatchMapper(1, device=local)
         plan1 = [step_inputs(frames, 1, args.stride, k) for k in range(W + K)]
         run_steps(m1, plan1, 0, W)
@@ -293,7 +315,7 @@ def main():
         dom = max(kt, key=lambda k: kt[k]["ms"])
         d = kt[dom]
         achieved = d["bytes"] / (d["ms"] * 1e-3) / 1e9 if d["ms"] > 0 else 0.0
-        traffic = pmc_traffic(dom)
+        traffic = None if args.shard else pmc_traffic(dom)  # PMC passes are of the default mode
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                     "traffic": round(traffic, 1) if traffic is not None else None,
@@ -317,7 +339,7 @@ def main():
             "warmup": W,
             "ms_per_step": round(1e3 * dt_max / K, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.shard else "weak",
             "vs_baseline": None,
             "dtype": "fp64 pose/normal equations, fp32 points",
             "data": "synthetic HDL-64E street sequence (64 rings x 2000 azimuths); GPU scan registration "
@@ -325,10 +347,13 @@ def main():
                     "maps built by the warmup steps",
             "config": {"workload": "laserMapping solveMapping, voxel-hashed map resident in HBM "
                                    "(BASELINE configs[3])",
-                       "streams_per_gpu": B, "frames_per_step": B * world, "n_az": args.n_az,
-                       "map_frames_before_timing": W,
-                       "parallelism": f"{world} GPU x {B} independent streams"
-                                      + (f" ({H} handles x {Bh}, one host thread each)" if H > 1 else "")},
+                       "streams_per_gpu": B, "frames_per_step": B if args.shard else B * world,
+                       "n_az": args.n_az, "map_frames_before_timing": W,
+                       "parallelism": (f"{B} streams, each sharded over {world} GPU(s): RCCL all-gather of the "
+                                       f"5-NN candidates per round, all-reduce of the normal equations per LM "
+                                       f"iteration" if args.shard else
+                                       f"{world} GPU x {B} independent streams"
+                                       + (f" ({H} handles x {Bh}, one host thread each)" if H > 1 else ""))},
             "lm_iterations": int(iters_all),
             "kernel_ms_per_step": {k: round(v["ms"] / K, 4) for k, v in kt.items()},
             "roofline": roofline,
@@ -341,6 +366,8 @@ def main():
         print(json.dumps(out), flush=True)
     for m in mappers:
         m.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # default bench (with cpu_baseline) + kernel-trace profile of the same command; time-limited, chained
-cd "$(dirname "$0")"
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 R="$(pwd)"
 timeout -k 10 900 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err && \

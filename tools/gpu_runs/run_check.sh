@@ -1,0 +1,6 @@
+#!/bin/bash
+# GPU tests then the default bench; each step time-limited, chained with &&
+cd "$(dirname "$0")/../.."
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1 && \
+timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err

@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU tests + bench with the device phase counters + LM G=1 variant + kernel trace
-cd "$(dirname "$0")"
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 R="$(pwd)"
 timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1 && \

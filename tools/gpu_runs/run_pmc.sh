@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes over the default bench (each counter group in its own run, kernel trace only)
-cd "$(dirname "$0")"
+cd "$(dirname "$0")/../.."
 R="$(pwd)"
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp

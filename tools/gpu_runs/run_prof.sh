@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 kernel-trace summary of the bench (PMC collection is a separate pass)
-cd "$(dirname "$0")"
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 ROOTD=$PWD
 export TMPDIR=/tmp

@@ -82,11 +82,12 @@ int32_t comm_allreduce(loam_comm* c, void* d_buf, int64_t count, int32_t dtype, 
     set_error("comm allreduce: bad arguments");
     return LOAM_ERR_ARG;
   }
-  if (count == 0 || c->size == 1) return LOAM_OK;
-  if (c->kind == 1)
+  if (count == 0) return LOAM_OK;
+  if (c->kind == 1)  // RCCL runs even at one rank (the transport is then exercised by tests)
     return rccl_check(rccl().all_reduce(d_buf, d_buf, (size_t)count, dtype == LOAM_DT_F64 ? ncclFloat64 : ncclInt32,
                                         ncclSum, static_cast<ncclComm_t>(c->nccl), st),
                       "ncclAllReduce");
+  if (c->size == 1) return LOAM_OK;
   if (!c->ops.host_buffers) {
     if (c->ops.allreduce_sum(c->ops.user, d_buf, count, dtype, st) != 0) {
       set_error("comm allreduce callback failed");
@@ -112,13 +113,13 @@ int32_t comm_allgather(loam_comm* c, const void* d_send, void* d_recv, int64_t b
     return LOAM_ERR_ARG;
   }
   if (bytes == 0) return LOAM_OK;
+  if (c->kind == 1)
+    return rccl_check(rccl().all_gather(d_send, d_recv, (size_t)bytes, ncclUint8, static_cast<ncclComm_t>(c->nccl), st),
+                      "ncclAllGather");
   if (c->size == 1) {
     if (d_recv != d_send) LOAM_HIP(hipMemcpyAsync(d_recv, d_send, (size_t)bytes, hipMemcpyDeviceToDevice, st));
     return LOAM_OK;
   }
-  if (c->kind == 1)
-    return rccl_check(rccl().all_gather(d_send, d_recv, (size_t)bytes, ncclUint8, static_cast<ncclComm_t>(c->nccl), st),
-                      "ncclAllGather");
   if (!c->ops.host_buffers) {
     if (c->ops.allgather(c->ops.user, d_send, d_recv, bytes, st) != 0) {
       set_error("comm allgather callback failed");
