@@ -96,6 +96,7 @@ def make_frames(seed, n_frames, n_az, device, keep_raw=0, prior="odometry"):
     sr = ScanRegistration(device=device)
     od = BatchOdometry(1, device=device)
     frames = []
+    stage_ms = {"scan_registration": [], "odometry": [], "odometry_iters": []}
     chunk = 64
     with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4)) as ex:
         for c0 in range(0, n_frames, chunk):
@@ -106,6 +107,10 @@ def make_frames(seed, n_frames, n_az, device, keep_raw=0, prior="odometry"):
                 od.input_device(0, ptrs, counts)
                 od.solve()
                 q, t, _, _, _ = od.output(0)
+                ost = od.stats(0)
+                stage_ms["scan_registration"].append(sr.ms)
+                stage_ms["odometry"].append(ost.ms)
+                stage_ms["odometry_iters"].append(ost.lm[0].iterations + ost.lm[1].iterations)
                 corner = sr.cloud(2)  # cornerPointsLessSharp -> laserCloudCornerLast
                 surf = sr.cloud(4)    # surfPointsLessFlat   -> laserCloudSurfLast
                 frames.append(dict(corner=torch.from_numpy(corner).to(f"cuda:{device}"),
@@ -120,7 +125,7 @@ def make_frames(seed, n_frames, n_az, device, keep_raw=0, prior="odometry"):
         for i, f in enumerate(frames):
             f["q"], f["t"] = q[i], t[i]
     torch.cuda.synchronize(device)
-    return frames
+    return frames, stage_ms
 
 
 def step_inputs(frames, streams, stride, k, first=0):
@@ -173,13 +178,17 @@ def run_handles(mappers, plans, first, count):
 def cpu_baseline(frames, warm, n):
     """oracle pipeline on stream 0's frames (same features and priors as the GPU run): `warm`
     untimed frames build the map, then n frames timed (solveMapping, the oracle's own
-    steady_clock over the whole call)"""
+    steady_clock over the whole call).  The oracle ScanRegistration and LaserOdometry run on
+    every frame too; their own timers over the same n frames give the stage baselines."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import loam_oracle as O
-    sr, mp = O.ScanRegistration(), O.LaserMapping()
+    sr, od, mp = O.ScanRegistration(), O.LaserOdometry(), O.LaserMapping()
     iters, ms = 0, 0.0
+    st_ms = {"scan_registration": 0.0, "odometry": 0.0, "odometry_iters": 0}
     for k, f in enumerate(frames[:warm + n]):
         sr.input(f["raw"])
+        od.input(*sr.output())
+        od.solve()
         mp.input(sr.cloud(2), sr.cloud(4), None, f["q"], f["t"])
         mp.solve()
         if k < warm:
@@ -187,7 +196,11 @@ def cpu_baseline(frames, warm, n):
         st = mp.stats()
         iters += st.lm[0].iterations + st.lm[1].iterations
         ms += st.ms_total
-    return iters, ms
+        st_ms["scan_registration"] += sr.ms
+        st_ms["odometry"] += od.ms
+        _, lm = od.stats()
+        st_ms["odometry_iters"] += lm[0].iterations + lm[1].iterations
+    return iters, ms, st_ms
 
 
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
@@ -238,7 +251,7 @@ def main():
     n_frames = (B - 1) * args.stride + W + K
     cpu_n = 0 if (args.no_cpu or world > 1 or rank != 0) else W + args.cpu_frames
     # sharded: every rank runs the same streams (identical inputs, one share of each map)
-    frames = make_frames(stream_seed(args.seed, 0 if args.shard else rank), max(n_frames, cpu_n), args.n_az, local,
+    frames, stage_ms = make_frames(stream_seed(args.seed, 0 if args.shard else rank), max(n_frames, cpu_n), args.n_az, local,
                          keep_raw=cpu_n, prior=args.prior)
     H = 1 if args.shard else max(1, args.handles)
     if B % H:
@@ -323,8 +336,9 @@ def main():
                     "launches": d["launches"], "avg_launch_us": round(1e3 * d["ms"] / max(1, d["launches"]), 3),
                     "algorithmic_bytes_per_launch": round(d["bytes"] / max(1, d["launches"]), 1)}
         cpu = None
+        cpu_st = None
         if not args.no_cpu and world == 1:
-            ci, cms = cpu_baseline(frames, W, args.cpu_frames)
+            ci, cms, cpu_st = cpu_baseline(frames, W, args.cpu_frames)
             cpu = {"value": round(ci / (cms * 1e-3), 3), "unit": "LM iters/s", "cores": 1, "kind": "port",
                    "sample": f"stream 0, frames {W}..{W + args.cpu_frames - 1} after {W} untimed map-building "
                              f"frames: oracle solveMapping (KD-tree, VoxelGrid, Ceres-LM/DENSE_QR restatement), "
@@ -361,6 +375,27 @@ def main():
         }
         if single is not None:
             out["single_stream"] = {k: round(v, 4) for k, v in single.items()}
+        # the stages before the mapper (BASELINE configs[1], configs[2]): one stream, device time
+        # per frame (HIP events around each call) over the frames after the first 10, and the
+        # oracle's own timers over the cpu_baseline frames
+        stages = {}
+        for name in ("scan_registration", "odometry"):
+            g = np.array(stage_ms[name][10:], dtype=np.float64)
+            if not len(g):
+                continue
+            e = {"gpu_ms_per_frame": round(float(g.mean()), 4), "gpu_frames": int(len(g)),
+                 "gpu_frames_per_s": round(1e3 / float(g.mean()), 1)}
+            if name == "odometry":
+                it = float(np.sum(stage_ms["odometry_iters"][10:]))
+                e["gpu_lm_iters_per_s"] = round(it / (float(g.sum()) * 1e-3), 1)
+            if cpu_st is not None:
+                c = cpu_st[name] / args.cpu_frames
+                e.update(cpu_ms_per_frame=round(c, 4), cpu_cores=1, cpu_kind="port",
+                         speedup=round(c / float(g.mean()), 2))
+                if name == "odometry":
+                    e["cpu_lm_iters_per_s"] = round(cpu_st["odometry_iters"] / (cpu_st[name] * 1e-3), 1)
+            stages[name] = e
+        out["stages"] = stages
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(out["value"] / cpu["value"], 2)
         print(json.dumps(out), flush=True)

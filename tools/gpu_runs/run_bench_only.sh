@@ -1,0 +1,5 @@
+#!/bin/bash
+# the default bench alone (with cpu_baseline)
+cd "$(dirname "$0")/../.."
+mkdir -p gpurun_out
+timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err

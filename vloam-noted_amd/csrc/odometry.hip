@@ -1,7 +1,7 @@
 // odometry.hip — LaserOdometry::solveLO (laser_odometry.cpp:199-584) on MI355X.
 //
 // One handle = B independent odometry streams; every launch covers all of them.  Per frame:
-//   2 x { k_od_corr   per query (cornerPointsSharp, surfPointsFlat): TransformToStart
+//   2 x { k_od_corr   one wave per query (cornerPointsSharp, surfPointsFlat): TransformToStart
 //                     (:152-173, s = 1), exact 1-NN in the last cloud (KdTreeFLANN, d2 < 25,
 //                     :292/:398) and the second / third point of the reference's ring scans
 //                     (:303-349 corner, :407-468 surf) as a ring-filtered nearest search over
@@ -33,7 +33,7 @@ constexpr float OD_INV_CELL = 0.5f;  // 2 m cells
 constexpr float OD_CELL = 2.0f;
 constexpr int OD_ORIGIN = 256;       // cell coordinates offset: +-512 m around the sensor
 constexpr float OD_THR = 25.0f;      // DISTANCE_SQ_THRESHOLD (laser_odometry.h:90)
-constexpr int OD_QBLK = 16;          // query workgroups per stream
+constexpr int OD_QBLK_MAX = 1024;   // query workgroups per stream (at most; one wave per query)
 constexpr int OD_QTHREADS = 256;
 constexpr int OD_LM_THREADS = 256;
 constexpr int OD_BUILD_THREADS = 1024;
@@ -209,29 +209,50 @@ __device__ inline void od_offer(OdNear& b, float d, uint32_t ord, int j) {
   }
 }
 
-// visit the cells around q nearest-shell first; f(cell entry) evaluates its points.  Stops
-// once the next shell is farther than bound() (squared, with a rounding margin).
-template <typename F, typename B>
-__device__ inline void od_visit(const uint4* tab, float qx, float qy, float qz, F&& f, B&& bound) {
+// wave-wide minimum of (d2, order): every lane ends with the same candidate
+__device__ inline OdNear od_wave_min(OdNear b) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float d = __shfl_xor(b.d, o, 64);
+    const uint32_t ord = __shfl_xor(b.ord, o, 64);
+    const int j = __shfl_xor(b.j, o, 64);
+    if (d < b.d || (d == b.d && ord < b.ord)) {
+      b.d = d;
+      b.ord = ord;
+      b.j = j;
+    }
+  }
+  return b;
+}
+
+// One wave per query: visit the cells around q nearest-shell first (every lane the same
+// cell), the lanes split each cell's points, f(entry) evaluates them and returns the new
+// (wave-uniform) bound.  Stops once the next shell is farther than the bound (squared, with
+// a rounding margin); cells farther than the bound are skipped.  The minimum of (d2, order)
+// does not depend on the visiting order, so the result is the sequential search's.
+template <typename F>
+__device__ inline void od_visit(const uint4* tab, float qx, float qy, float qz, float bound, F&& f) {
   const int cx = od_cell(qx), cy = od_cell(qy), cz = od_cell(qz);
   for (int k = 0; k <= 3; ++k) {
     const float shell_gap = (float)(k > 0 ? k - 1 : 0) * OD_CELL;  // cells of shell k are >= this far
-    if (k > 0 && shell_gap * shell_gap > bound()) break;
+    if (k > 0 && shell_gap * shell_gap > bound) break;
     for (int dz = -k; dz <= k; ++dz)
       for (int dy = -k; dy <= k; ++dy)
         for (int dx = -k; dx <= k; ++dx) {
           if (max(abs(dx), max(abs(dy), abs(dz))) != k) continue;
           const int x = cx + dx, y = cy + dy, z = cz + dz;
           if (x < 0 || y < 0 || z < 0 || x > 511 || y > 511 || z > 511) continue;
-          if (od_gap2(qx, qy, qz, x, y, z) > bound()) continue;
+          if (od_gap2(qx, qy, qz, x, y, z) > bound) continue;
           const uint4 e = od_find(tab, od_key(x, y, z));
-          if (e.x != OD_EMPTY) f(e);
+          if (e.x != OD_EMPTY && e.z > 0) bound = f(e);
         }
   }
 }
 
-__global__ void __launch_bounds__(OD_QTHREADS) k_od_corr(OdomDev D, int round) {
-  const int s = blockIdx.x / OD_QBLK, blk = blockIdx.x % OD_QBLK;
+constexpr int OD_QWAVES = OD_QTHREADS / 64;  // queries in flight per workgroup (one per wave)
+
+__global__ void __launch_bounds__(OD_QTHREADS) k_od_corr(OdomDev D, int round, int qblk) {
+  const int s = blockIdx.x / qblk, blk = blockIdx.x % qblk;
   OdomFrame& F = D.fr[s];
   if (!F.active || !F.inited) return;
   double X[7];
@@ -242,8 +263,9 @@ __global__ void __launch_bounds__(OD_QTHREADS) k_od_corr(OdomDev D, int round) {
   const int ns = F.n_in[0], nf = F.n_in[2];
   const size_t rb = (size_t)s * OD_MAXQ;
   const size_t cb = (size_t)s * D.cap;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t n_edge = 0, n_plane = 0;
-  for (int q = blk * OD_QTHREADS + threadIdx.x; q < ns + nf; q += OD_QBLK * OD_QTHREADS) {
+  for (int q = blk * OD_QWAVES + wid; q < ns + nf; q += qblk * OD_QWAVES) {
     const int c = q < ns ? 0 : 1;  // 0: sharp vs cornerLast, 1: flat vs surfLast
     const float4 cp = c == 0 ? F.in_ptr[0][q] : F.in_ptr[2][q - ns];
     const float4 sel = to_map(X, cp);  // TransformToStart, s = 1: same double transform
@@ -255,41 +277,40 @@ __global__ void __launch_bounds__(OD_QTHREADS) k_od_corr(OdomDev D, int round) {
     double a[3] = {0, 0, 0}, b[3] = {0, 0, 0};
     // 1-NN (FLANN L2_Simple<float>, ties by index)
     OdNear n1{INFINITY, 0xFFFFFFFFu, -1};
-    od_visit(
-        tab, sel.x, sel.y, sel.z,
-        [&](const uint4& e) {
-          for (uint32_t k = 0; k < e.z; ++k) {
-            const float4 p = srt[e.y + k];
-            const int j = sidx[e.y + k];
-            od_offer(n1, fdist2(sel.x, sel.y, sel.z, p.x, p.y, p.z), (uint32_t)j, j);
-          }
-        },
-        [&]() { return fminf(n1.d, OD_THR) * 1.01f + 1e-5f; });
+    od_visit(tab, sel.x, sel.y, sel.z, OD_THR * 1.01f + 1e-5f, [&](const uint4& e) {
+      for (uint32_t k = lane; k < e.z; k += 64) {
+        const float4 p = srt[e.y + k];
+        const int j = sidx[e.y + k];
+        od_offer(n1, fdist2(sel.x, sel.y, sel.z, p.x, p.y, p.z), (uint32_t)j, j);
+      }
+      n1 = od_wave_min(n1);
+      return fminf(n1.d, OD_THR) * 1.01f + 1e-5f;
+    });
     if (n1.j >= 0 && n1.d < OD_THR) {
       const int cl = n1.j;
       const int cid = (int)last[cl].w;
       OdNear b2{OD_THR, 0xFFFFFFFFu, -1}, b3{OD_THR, 0xFFFFFFFFu, -1};
-      od_visit(
-          tab, sel.x, sel.y, sel.z,
-          [&](const uint4& e) {
-            for (uint32_t k = 0; k < e.z; ++k) {
-              const float4 p = srt[e.y + k];
-              const int j = sidx[e.y + k];
-              if (j == cl) continue;
-              const int r = (int)p.w;
-              if (r > cid + 2 || r < cid - 2) continue;  // NEARBY_SCAN = 2.5
-              const float d = fdist2(sel.x, sel.y, sel.z, p.x, p.y, p.z);
-              const uint32_t ord = j > cl ? (uint32_t)(j - cl) : (uint32_t)(cl - j) + (1u << 30);
-              if (c == 0) {
-                if (r != cid) od_offer(b2, d, ord, j);  // corner: rings cid +- 1, 2
-              } else if (r == cid) {
-                od_offer(b2, d, ord, j);                // surf ind2: same ring
-              } else {
-                od_offer(b3, d, ord, j);                // surf ind3: rings cid +- 1, 2
-              }
-            }
-          },
-          [&]() { return fmaxf(b2.d, c == 0 ? 0.0f : b3.d) * 1.01f + 1e-5f; });
+      od_visit(tab, sel.x, sel.y, sel.z, OD_THR * 1.01f + 1e-5f, [&](const uint4& e) {
+        for (uint32_t k = lane; k < e.z; k += 64) {
+          const float4 p = srt[e.y + k];
+          const int j = sidx[e.y + k];
+          if (j == cl) continue;
+          const int r = (int)p.w;
+          if (r > cid + 2 || r < cid - 2) continue;  // NEARBY_SCAN = 2.5
+          const float d = fdist2(sel.x, sel.y, sel.z, p.x, p.y, p.z);
+          const uint32_t ord = j > cl ? (uint32_t)(j - cl) : (uint32_t)(cl - j) + (1u << 30);
+          if (c == 0) {
+            if (r != cid) od_offer(b2, d, ord, j);  // corner: rings cid +- 1, 2
+          } else if (r == cid) {
+            od_offer(b2, d, ord, j);                // surf ind2: same ring
+          } else {
+            od_offer(b3, d, ord, j);                // surf ind3: rings cid +- 1, 2
+          }
+        }
+        b2 = od_wave_min(b2);
+        if (c == 1) b3 = od_wave_min(b3);
+        return fmaxf(b2.d, c == 0 ? 0.0f : b3.d) * 1.01f + 1e-5f;
+      });
       const float4 pa = last[cl];
       if (c == 0 && b2.j >= 0) {
         // LidarEdgeFactor(curr, a = last[cl], b = last[ind2]): r = (lp - a) x e, e = (a - b)/|a - b|
@@ -299,7 +320,7 @@ __global__ void __launch_bounds__(OD_QTHREADS) k_od_corr(OdomDev D, int round) {
         type = 1;
         a[0] = pa.x; a[1] = pa.y; a[2] = pa.z;
         b[0] = de.x / dn; b[1] = de.y / dn; b[2] = de.z / dn;
-        ++n_edge;
+        n_edge += lane == 0;
       } else if (c == 1 && b2.j >= 0 && b3.j >= 0) {
         // LidarPlaneFactor ctor (lidarFactor.hpp:73-74): ljm = normalize((j - l) x (j - m))
         const float4 pl = last[b2.j], pm = last[b3.j];
@@ -310,17 +331,19 @@ __global__ void __launch_bounds__(OD_QTHREADS) k_od_corr(OdomDev D, int round) {
         type = 2;
         a[0] = jv.x; a[1] = jv.y; a[2] = jv.z;
         b[0] = nv.x; b[1] = nv.y; b[2] = nv.z;
-        ++n_plane;
+        n_plane += lane == 0;
       }
     }
-    D.r_type[rb + q] = type;
-    D.r_px[rb + q] = cp.x;
-    D.r_py[rb + q] = cp.y;
-    D.r_pz[rb + q] = cp.z;
+    if (lane == 0) {
+      D.r_type[rb + q] = type;
+      D.r_px[rb + q] = cp.x;
+      D.r_py[rb + q] = cp.y;
+      D.r_pz[rb + q] = cp.z;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      D.r_a[k][rb + q] = a[k];
-      D.r_b[k][rb + q] = b[k];
+      for (int k = 0; k < 3; ++k) {
+        D.r_a[k][rb + q] = a[k];
+        D.r_b[k][rb + q] = b[k];
+      }
     }
   }
   uint32_t we = n_edge, wp = n_plane;
@@ -571,8 +594,13 @@ int32_t loam_odometry_solve(loam_odometry* h) {
   LOAM_HIP(hipEventRecord(h->ev[0], st));
   LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(OdomFrame) * B, hipMemcpyHostToDevice, st));
   if (any_inited) {
+    // one wave per query: enough workgroups per stream for the largest query count
+    int maxq = 1;
+    for (int s = 0; s < B; ++s)
+      if (h->hf[s].active) maxq = std::max(maxq, h->hf[s].n_in[0] + h->hf[s].n_in[2]);
+    const int qblk = std::min(OD_QBLK_MAX, (maxq + OD_QWAVES - 1) / OD_QWAVES);
     for (int round = 0; round < 2; ++round) {
-      k_od_corr<<<B * OD_QBLK, OD_QTHREADS, 0, st>>>(D, round);
+      k_od_corr<<<B * qblk, OD_QTHREADS, 0, st>>>(D, round, qblk);
       k_od_lm<<<B * h->G, OD_LM_THREADS, 0, st>>>(D, round, h->G);
     }
   }
