@@ -11,9 +11,10 @@
 //                   offsets = laserCloudScans concatenation (:308-315)
 //   k_sr_scatter    stable scatter into the ring-major cloud, intensity = scanID + 0.1*relTime
 //   k_sr_curv       11-tap curvature over the concatenated cloud (:323-346), crossing rings
-//   k_sr_select     one workgroup per ring: 6 sectors, LDS bitonic sort by curvature, greedy
-//                   sharp / lessSharp / flat picks with +-5 neighbour suppression (:352-493);
-//                   one wave runs the (inherently sequential) greedy scan with 64-wide ballots
+//   k_sr_select     one workgroup per ring: the 6 sectors sorted by curvature at once (one wave
+//                   per sector, register bitonic), then the greedy sharp / lessSharp / flat
+//                   picks with +-5 neighbour suppression (:352-493): one wave runs the
+//                   (inherently sequential) greedy scan with 64-wide ballots, all in LDS
 //   k_sr_ringvox    VoxelGrid 0.2 m of each ring's lessFlat candidates (:497-503)
 //   k_sr_gather     concatenation of the per-ring outputs in ring order
 // The reference sorts each sector with std::sort (unstable); the kernel sorts by
@@ -250,28 +251,162 @@ __global__ void k_sr_curv(SrDev D) {
 }
 
 // +-5 neighbour suppression while consecutive squared gaps stay <= 0.05 (:406-429)
-__device__ inline void sr_suppress(const float4* L, uint8_t* picked, int base, int ind) {
+// +-5 neighbour suppression of a pick (scan_registration.cpp:402-429): the reference walks
+// outwards while consecutive points are within sqrt(0.05); gapok[k] holds that test for the
+// pair (k, k + 1) of the ring (ring-local indices), precomputed in parallel.
+__device__ inline void sr_suppress(const uint8_t* gapok, uint8_t* picked, int ind) {
   for (int l = 1; l <= 5; l++) {
-    float dX = L[ind + l].x - L[ind + l - 1].x;
-    float dY = L[ind + l].y - L[ind + l - 1].y;
-    float dZ = L[ind + l].z - L[ind + l - 1].z;
-    if (dX * dX + dY * dY + dZ * dZ > 0.05) break;
-    picked[ind + l - base] = 1;
+    if (!gapok[ind + l - 1]) break;
+    picked[ind + l] = 1;
   }
   for (int l = -1; l >= -5; l--) {
-    float dX = L[ind + l].x - L[ind + l + 1].x;
-    float dY = L[ind + l].y - L[ind + l + 1].y;
-    float dZ = L[ind + l].z - L[ind + l + 1].z;
-    if (dX * dX + dY * dY + dZ * dZ > 0.05) break;
-    picked[ind + l - base] = 1;
+    if (!gapok[ind + l]) break;
+    picked[ind + l] = 1;
   }
 }
 
-__global__ void __launch_bounds__(SR_BLOCK) k_sr_select(SrDev D) {
-  __shared__ uint64_t keys[SR_SECT_CAP];
+// One wave sorts one sector in registers: E * 64 keys (curvature bits << 32 | index), bitonic,
+// partners within a lane's registers swapped directly and partners in other lanes by
+// shuffles (no barriers); padding keys are ~0 and end last.
+template <int E>
+__device__ inline void sr_wave_sort(const float* curv, int sp, int len, uint64_t* out) {
+  const int lane = threadIdx.x & 63;
+  uint64_t v[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = e * 64 + lane;
+    v[e] = i < len ? (((uint64_t)__float_as_uint(curv[sp + i]) << 32) | (uint32_t)(sp + i)) : ~0ull;
+  }
+#pragma unroll
+  for (int k = 2; k <= E * 64; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j >= 64) {
+        const int ej = j >> 6;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int f = e ^ ej;
+          if (f > e) {
+            const int i = e * 64 + lane;
+            const uint64_t a = v[e], b = v[f];
+            const bool asc = (i & k) == 0;
+            v[e] = asc ? (a < b ? a : b) : (a < b ? b : a);
+            v[f] = asc ? (a < b ? b : a) : (a < b ? a : b);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int i = e * 64 + lane;
+          const uint64_t p = __shfl_xor(v[e], j, 64);
+          const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+          v[e] = keep_min ? (v[e] < p ? v[e] : p) : (v[e] < p ? p : v[e]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) out[e * 64 + lane] = v[e];
+}
+
+constexpr int SR_SEL_THREADS = 512;
+constexpr int SR_WSORT_MAX = 1024;  // register sort (one wave per sector) up to this length
+
+// sharp / lessSharp (descending curvature, :371-431) and flat (ascending, :439-483) picks of
+// one sector from its sorted keys K[0, len): one wave, 64 candidates tested per ballot
+__device__ inline void sr_greedy(SrDev& D, int r, int base, const uint64_t* K, int len, uint8_t* picked,
+                                 int8_t* lab, const uint8_t* gapok, int& nsh, int& nls, int& nfl) {
+  const int lane = threadIdx.x & 63;
+  int largest = 0;
+  int pos = len - 1;
+  while (pos >= 0) {
+    const int k = pos - lane;
+    bool cond = false, low = false;
+    int ind = 0;
+    if (k >= 0) {
+      const uint64_t key = K[k];
+      ind = (int)(key & 0xFFFFFFFFu);
+      const float c = __uint_as_float((uint32_t)(key >> 32));
+      cond = picked[ind - base] == 0 && c > 0.1f;
+      low = !(c > 0.1f);
+    }
+    const uint64_t bc = __ballot(cond);
+    const uint64_t bl = __ballot(low);
+    const int fc = bc ? __ffsll((long long)bc) - 1 : 64;
+    const int fl = bl ? __ffsll((long long)bl) - 1 : 64;
+    if (fc < fl) {
+      const int pind = __shfl(ind, fc, 64);
+      largest++;
+      if (largest > SR_LESS_SHARP) break;
+      if (lane == 0) {
+        if (largest <= SR_SHARP) {
+          lab[pind - base] = 2;
+          D.ring_sharp[r * 6 * SR_SHARP + nsh++] = pind;
+          D.ring_less_sharp[r * 6 * SR_LESS_SHARP + nls++] = pind;
+        } else {
+          lab[pind - base] = 1;
+          D.ring_less_sharp[r * 6 * SR_LESS_SHARP + nls++] = pind;
+        }
+        picked[pind - base] = 1;
+        sr_suppress(gapok, picked, pind - base);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      pos = pos - fc - 1;
+    } else if (fl < 64) {
+      break;  // every remaining curvature <= 0.1
+    } else {
+      pos -= 64;
+    }
+  }
+  int smallest = 0;
+  pos = 0;
+  while (pos < len) {
+    const int k = pos + lane;
+    bool cond = false, high = false;
+    int ind = 0;
+    if (k < len) {
+      const uint64_t key = K[k];
+      ind = (int)(key & 0xFFFFFFFFu);
+      const float c = __uint_as_float((uint32_t)(key >> 32));
+      cond = picked[ind - base] == 0 && c < 0.1f;
+      high = !(c < 0.1f);
+    }
+    const uint64_t bc = __ballot(cond);
+    const uint64_t bh = __ballot(high);
+    const int fc = bc ? __ffsll((long long)bc) - 1 : 64;
+    const int fh = bh ? __ffsll((long long)bh) - 1 : 64;
+    if (fc < fh) {
+      const int pind = __shfl(ind, fc, 64);
+      if (lane == 0) {
+        lab[pind - base] = -1;
+        D.ring_flat[r * 6 * SR_FLAT + nfl++] = pind;
+      }
+      smallest++;
+      if (smallest >= SR_FLAT) break;
+      if (lane == 0) {
+        picked[pind - base] = 1;
+        sr_suppress(gapok, picked, pind - base);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      pos = pos + fc + 1;
+    } else if (fh < 64) {
+      break;
+    } else {
+      pos += 64;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(SrDev D) {
+  __shared__ uint64_t keys[6 * SR_WSORT_MAX];  // 48 KiB: the 6 sorted sectors
   __shared__ uint8_t picked[SR_RING_CAP];
   __shared__ int8_t lab[SR_RING_CAP];
-  __shared__ uint32_t ws[8];
+  __shared__ uint8_t gapok[SR_RING_CAP];
+  __shared__ uint32_t ws[SR_SEL_THREADS / 64];
   const int r = blockIdx.x;
   SrFrame& F = *D.fr;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
@@ -286,144 +421,87 @@ __global__ void __launch_bounds__(SR_BLOCK) k_sr_select(SrDev D) {
     return;
   }
   const float4* L = D.cloud;
-  for (int k = tid; k < n; k += SR_BLOCK) {
+  for (int k = tid; k < n; k += SR_SEL_THREADS) {
     picked[k] = 0;
     lab[k] = 0;
+    uint8_t ok = 0;
+    if (k + 1 < n) {  // the reference's float test, (dX^2 + dY^2 + dZ^2) > 0.05 in double
+      const float4 a = L[base + k], b = L[base + k + 1];
+      const float dX = b.x - a.x, dY = b.y - a.y, dZ = b.z - a.z;
+      ok = (dX * dX + dY * dY + dZ * dZ > 0.05) ? 0 : 1;
+    }
+    gapok[k] = ok;
   }
-  int nsh = 0, nls = 0, nfl = 0, nlf = 0;  // valid in thread 0 / wave 0
-  __syncthreads();
+  // sectors (:361-365); with all 6 short enough, wave j sorts sector j in registers
+  int sp[6], len[6], maxlen = 0;
+#pragma unroll
   for (int j = 0; j < 6; j++) {
-    const int sp = s + (e - s) * j / 6;
-    const int ep = s + (e - s) * (j + 1) / 6 - 1;
-    const int len = ep - sp + 1;
-    if (len > SR_SECT_CAP) {
-      if (tid == 0) atomicOr(&F.err, SR_ERR_RING);
-      return;
-    }
-    int pad = 1;
-    while (pad < len) pad <<= 1;
-    for (int k = tid; k < pad; k += SR_BLOCK)
-      keys[k] = k < len ? (((uint64_t)__float_as_uint(D.curv[sp + k]) << 32) | (uint32_t)(sp + k))
-                        : 0xFFFFFFFFFFFFFFFFull;
-    __syncthreads();
-    for (int kk = 2; kk <= pad; kk <<= 1) {
-      for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-        for (int i = tid; i < pad; i += SR_BLOCK) {
-          int ixj = i ^ jj;
-          if (ixj > i) {
-            uint64_t a = keys[i], b = keys[ixj];
-            bool asc = (i & kk) == 0;
-            if ((a > b) == asc) {
-              keys[i] = b;
-              keys[ixj] = a;
-            }
-          }
-        }
-        __syncthreads();
-      }
-    }
-    if (wid == 0) {
-      // sharp / lessSharp: descending curvature (:371-431)
-      int largest = 0;
-      int pos = len - 1;
-      while (pos >= 0) {
-        const int k = pos - lane;
-        bool cond = false, low = false;
-        int ind = 0;
-        if (k >= 0) {
-          const uint64_t key = keys[k];
-          ind = (int)(key & 0xFFFFFFFFu);
-          const float c = __uint_as_float((uint32_t)(key >> 32));
-          cond = picked[ind - base] == 0 && c > 0.1f;
-          low = !(c > 0.1f);
-        }
-        const uint64_t bc = __ballot(cond);
-        const uint64_t bl = __ballot(low);
-        const int fc = bc ? __ffsll((long long)bc) - 1 : 64;
-        const int fl = bl ? __ffsll((long long)bl) - 1 : 64;
-        if (fc < fl) {
-          const int pind = __shfl(ind, fc, 64);
-          largest++;
-          if (largest > SR_LESS_SHARP) break;
-          if (lane == 0) {
-            if (largest <= SR_SHARP) {
-              lab[pind - base] = 2;
-              D.ring_sharp[r * 6 * SR_SHARP + nsh++] = pind;
-              D.ring_less_sharp[r * 6 * SR_LESS_SHARP + nls++] = pind;
-            } else {
-              lab[pind - base] = 1;
-              D.ring_less_sharp[r * 6 * SR_LESS_SHARP + nls++] = pind;
-            }
-            picked[pind - base] = 1;
-            sr_suppress(L, picked, base, pind);
-          }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          pos = pos - fc - 1;
-        } else if (fl < 64) {
-          break;  // every remaining curvature <= 0.1
-        } else {
-          pos -= 64;
-        }
-      }
-      // flat: ascending curvature (:439-483)
-      int smallest = 0;
-      pos = 0;
-      while (pos < len) {
-        const int k = pos + lane;
-        bool cond = false, high = false;
-        int ind = 0;
-        if (k < len) {
-          const uint64_t key = keys[k];
-          ind = (int)(key & 0xFFFFFFFFu);
-          const float c = __uint_as_float((uint32_t)(key >> 32));
-          cond = picked[ind - base] == 0 && c < 0.1f;
-          high = !(c < 0.1f);
-        }
-        const uint64_t bc = __ballot(cond);
-        const uint64_t bh = __ballot(high);
-        const int fc = bc ? __ffsll((long long)bc) - 1 : 64;
-        const int fh = bh ? __ffsll((long long)bh) - 1 : 64;
-        if (fc < fh) {
-          const int pind = __shfl(ind, fc, 64);
-          if (lane == 0) {
-            lab[pind - base] = -1;
-            D.ring_flat[r * 6 * SR_FLAT + nfl++] = pind;
-          }
-          smallest++;
-          if (smallest >= SR_FLAT) break;
-          if (lane == 0) {
-            picked[pind - base] = 1;
-            sr_suppress(L, picked, base, pind);
-          }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          pos = pos + fc + 1;
-        } else if (fh < 64) {
-          break;
-        } else {
-          pos += 64;
-        }
-      }
-    }
-    __syncthreads();
-    // lessFlat candidates: label <= 0 in index order (:486-493), stable block compaction
-    for (int c = sp; c <= ep; c += SR_BLOCK) {
-      const int k = c + tid;
-      const bool pred = k <= ep && lab[k - base] <= 0;
-      const uint64_t bal = __ballot(pred);
-      const uint32_t pre = __popcll(bal & lanemask_lt());
-      if (lane == 0) ws[wid] = __popcll(bal);
-      __syncthreads();
-      uint32_t off = 0, tot = 0;
-      for (int w = 0; w < SR_BLOCK / 64; ++w) {
-        if (w < wid) off += ws[w];
-        tot += ws[w];
-      }
-      if (pred) D.less_flat_scan[base + nlf + off + pre] = L[k];
-      nlf += tot;
-      __syncthreads();
-    }
+    sp[j] = s + (e - s) * j / 6;
+    len[j] = (s + (e - s) * (j + 1) / 6 - 1) - sp[j] + 1;
+    maxlen = max(maxlen, len[j]);
   }
-  for (int k = tid; k < n; k += SR_BLOCK) D.label[base + k] = lab[k];
+  const bool fast = maxlen <= SR_WSORT_MAX;
+  if (!fast && maxlen > 6 * SR_WSORT_MAX) {
+    if (tid == 0) atomicOr(&F.err, SR_ERR_RING);
+    return;
+  }
+  if (fast && wid < 6) {
+    if (maxlen <= 512) sr_wave_sort<8>(D.curv, sp[wid], len[wid], keys + wid * SR_WSORT_MAX);
+    else sr_wave_sort<16>(D.curv, sp[wid], len[wid], keys + wid * SR_WSORT_MAX);
+  }
+  __syncthreads();
+  int nsh = 0, nls = 0, nfl = 0;  // valid in wave 0
+  for (int j = 0; j < 6; j++) {
+    const uint64_t* K = keys + j * SR_WSORT_MAX;
+    if (!fast) {  // long sectors: block bitonic in LDS, one sector at a time
+      K = keys;
+      int pad = 1;
+      while (pad < len[j]) pad <<= 1;
+      for (int k = tid; k < pad; k += SR_SEL_THREADS)
+        keys[k] = k < len[j] ? (((uint64_t)__float_as_uint(D.curv[sp[j] + k]) << 32) | (uint32_t)(sp[j] + k))
+                             : 0xFFFFFFFFFFFFFFFFull;
+      __syncthreads();
+      for (int kk = 2; kk <= pad; kk <<= 1) {
+        for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+          for (int i = tid; i < pad; i += SR_SEL_THREADS) {
+            const int ixj = i ^ jj;
+            if (ixj > i) {
+              const uint64_t a = keys[i], b = keys[ixj];
+              const bool asc = (i & kk) == 0;
+              if ((a > b) == asc) {
+                keys[i] = b;
+                keys[ixj] = a;
+              }
+            }
+          }
+          __syncthreads();
+        }
+      }
+    }
+    if (wid == 0) sr_greedy(D, r, base, K, len[j], picked, lab, gapok, nsh, nls, nfl);
+    if (!fast) __syncthreads();
+  }
+  __syncthreads();
+  // lessFlat candidates: label <= 0 in index order (:486-493) over [s, e), the 6 sectors
+  // back to back; stable block compaction
+  int nlf = 0;
+  for (int c = s; c < e; c += SR_SEL_THREADS) {
+    const int k = c + tid;
+    const bool pred = k < e && lab[k - base] <= 0;
+    const uint64_t bal = __ballot(pred);
+    const uint32_t pre = __popcll(bal & lanemask_lt());
+    if (lane == 0) ws[wid] = __popcll(bal);
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (int w = 0; w < SR_SEL_THREADS / 64; ++w) {
+      if (w < wid) off += ws[w];
+      tot += ws[w];
+    }
+    if (pred) D.less_flat_scan[base + nlf + off + pre] = L[k];
+    nlf += tot;
+    __syncthreads();
+  }
+  for (int k = tid; k < n; k += SR_SEL_THREADS) D.label[base + k] = lab[k];
   if (tid == 0) {
     F.n_sharp[r] = nsh;
     F.n_less_sharp[r] = nls;
@@ -624,7 +702,7 @@ static int32_t sr_run(loam_scanreg* h, const float* xyz, int32_t n, int32_t stri
     k_sr_ring_scan<<<1, 1024, 0, st>>>(D, nblocks);
     k_sr_scatter<<<nblocks, SR_BLOCK, 0, st>>>(D, nblocks);
     k_sr_curv<<<std::min(nblocks, 1024), SR_BLOCK, 0, st>>>(D);
-    k_sr_select<<<SR_MAX_RINGS, SR_BLOCK, 0, st>>>(D);
+    k_sr_select<<<SR_MAX_RINGS, SR_SEL_THREADS, 0, st>>>(D);
     k_sr_ringvox<<<SR_MAX_RINGS, VX_THREADS, 0, st>>>(D);
     k_sr_gather<<<SR_MAX_RINGS, 256, 0, st>>>(D);
     LOAM_HIP(hipGetLastError());
