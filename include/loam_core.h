@@ -279,6 +279,50 @@ int32_t loam_mapper_create_sharded(const loam_params* p, int32_t device, int32_t
 int32_t loam_shard_owner(const float* xyz, float leaf, int32_t nrank);
 
 /* --------------------------------------------------------------------------------------
+ * Visual-odometry depth association — vloam::PointCloudUtil
+ * (src/visual_odometry/include/visual_odometry/point_cloud_util.h:25-75), n_streams
+ * independent instances per handle (the reference keeps two, point_cloud_utils[0/1]).
+ * ------------------------------------------------------------------------------------ */
+typedef struct loam_depth loam_depth;
+
+typedef struct loam_depth_params {
+  float cam_T_velo[16];   /* 4x4 row-major (visual_odometry.cpp:162-163) */
+  float rect0_T_cam[16];  /* 4x4 row-major, R_rect_00 (point_cloud_util.cpp:113-125) */
+  float P_rect0[12];      /* 3x4 row-major (visual_odometry.cpp:178-181) */
+  int32_t grid;           /* downsample_grid_size, 5 */
+  int32_t img_width;      /* IMG_WIDTH 1242 (point_cloud_util.h:50) */
+  int32_t img_height;     /* IMG_HEIGHT 375 (point_cloud_util.h:49) */
+  int32_t max_points;     /* per input cloud (default 262144) */
+} loam_depth_params;
+
+/* matrices zero (set them from the calibration), KITTI image, grid 5 */
+void loam_depth_params_default(loam_depth_params* p);
+int32_t loam_depth_create(const loam_depth_params* p, int32_t device, int32_t n_streams, loam_depth** out);
+int32_t loam_depth_destroy(loam_depth* h);
+/* point_cloud_3d_tilde of stream s (visual_odometry.cpp:201-208): n points, `stride` floats
+ * each (x, y, z first); host memory (copied) or device memory (read in place) */
+int32_t loam_depth_input(loam_depth* h, int32_t stream, const float* xyz, int32_t n, int32_t stride);
+int32_t loam_depth_input_device(loam_depth* h, int32_t stream, const float* d_xyz, int32_t n, int32_t stride);
+/* projectPointCloud + downsamplePointCloud (point_cloud_util.cpp:183-324) of every stream
+ * with an input */
+int32_t loam_depth_process(loam_depth* h);
+/* sizes of point_cloud_2d (points in front) and point_cloud_2d_dnsp */
+int32_t loam_depth_counts(loam_depth* h, int32_t stream, int32_t* n_front, int32_t* n_dnsp);
+/* which 0: point_cloud_2d, 1: point_cloud_2d_dnsp, 3 floats (u, v, depth) per row; copies
+ * when cap >= the count; returns the count */
+int32_t loam_depth_copy(loam_depth* h, int32_t stream, int32_t which, float* out, int32_t cap);
+/* bucket_x / bucket_y / bucket_depth / bucket_count, [i * new_height + j] */
+int32_t loam_depth_buckets(loam_depth* h, int32_t stream, float* bx, float* by, float* bd, int32_t* bc);
+/* queryDepth (point_cloud_util.cpp:381-487): depth of n image points xy (2 floats each) in
+ * streams[i]'s buckets; -1 where fewer than 10 buckets are occupied (searching_radius 2) */
+int32_t loam_depth_query(loam_depth* h, int32_t n, const int32_t* streams, const float* xy, int32_t radius,
+                         float* depth);
+int32_t loam_depth_query_device(loam_depth* h, int32_t n, const int32_t* d_streams, const float* d_xy,
+                                int32_t radius, float* d_depth);
+/* device time of the last loam_depth_process (ms) */
+double loam_depth_ms(loam_depth* h);
+
+/* --------------------------------------------------------------------------------------
  * Device LM engine on an explicit factor list (lidarFactor.hpp + Ceres TR-LM).  Factor
  * record = 10 doubles: type (1 LidarEdgeFactor, 2 LidarPlaneFactor, 3 LidarPlaneNormFactor),
  * curr_point[3], a[3], b[3] (edge: last_point_a/b; plane: j, unit normal ljm; plane-norm:

@@ -126,6 +126,22 @@ int32_t oracle_map_factors(oracle_map* h, int32_t round, double* out);
 /* pose at the start of round r (0/1) */
 int32_t oracle_map_round_pose(oracle_map* h, int32_t round, double* x7);
 
+/* ---- visual-odometry depth association (depth_oracle.cpp; point_cloud_util.cpp:183-487) ----
+ * matrices row-major: cam_T_velo 4x4, rect0_T_cam 4x4, P_rect0 3x4 */
+void* oracle_depth_create(const float* cam_T_velo, const float* rect0_T_cam, const float* P_rect0, int32_t grid,
+                          int32_t img_w, int32_t img_h);
+void oracle_depth_destroy(void* h);
+/* projectPointCloud + downsamplePointCloud; returns the point_cloud_2d_dnsp count */
+int32_t oracle_depth_process(void* h, const float* xyz, int32_t n, int32_t stride);
+/* which 0: point_cloud_2d (n x 3), 1: point_cloud_2d_dnsp */
+int32_t oracle_depth_count(void* h, int32_t which);
+void oracle_depth_copy(void* h, int32_t which, float* out);
+/* bucket_x / _y / _depth / _count, [i * new_height + j] */
+void oracle_depth_buckets(void* h, float* bx, float* by, float* bd, int32_t* bc);
+/* queryDepth of n image points (x, y); returns the milliseconds taken */
+double oracle_depth_query(void* h, const float* xy, int32_t n, int32_t radius, float* depth);
+double oracle_depth_ms(void* h);
+
 #ifdef __cplusplus
 }
 #endif

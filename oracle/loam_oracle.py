@@ -73,6 +73,14 @@ def lib():
             "oracle_map_factor_count": (c_i32, [vp, c_i32]),
             "oracle_map_factors": (c_i32, [vp, c_i32, vp]),
             "oracle_map_round_pose": (c_i32, [vp, c_i32, vp]),
+            "oracle_depth_create": (vp, [vp, vp, vp, c_i32, c_i32, c_i32]),
+            "oracle_depth_destroy": (None, [vp]),
+            "oracle_depth_process": (c_i32, [vp, vp, c_i32, c_i32]),
+            "oracle_depth_count": (c_i32, [vp, c_i32]),
+            "oracle_depth_copy": (None, [vp, c_i32, vp]),
+            "oracle_depth_buckets": (None, [vp, vp, vp, vp, vp]),
+            "oracle_depth_query": (c_d, [vp, vp, c_i32, c_i32, vp]),
+            "oracle_depth_ms": (c_d, [vp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -299,3 +307,52 @@ class LaserMapping:
         x = np.empty(7)
         lib().oracle_map_round_pose(self.h, rnd, _ptr(x))
         return x
+
+
+class PointCloudUtil:
+    """Oracle depth association (visual_odometry point_cloud_util.cpp:183-487)."""
+
+    def __init__(self, cam_T_velo, rect0_T_cam, P_rect0, grid=5, img_w=1242, img_h=375):
+        self._m = [np.ascontiguousarray(cam_T_velo, dtype=np.float32).reshape(16),
+                   np.ascontiguousarray(rect0_T_cam, dtype=np.float32).reshape(16),
+                   np.ascontiguousarray(P_rect0, dtype=np.float32).reshape(12)]
+        self.h = lib().oracle_depth_create(_ptr(self._m[0]), _ptr(self._m[1]), _ptr(self._m[2]), grid, img_w, img_h)
+        self.grid = grid
+        self.new_w = int(np.ceil(np.float32(img_w) / np.float32(grid)))
+        self.new_h = int(np.ceil(np.float32(img_h) / np.float32(grid)))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_depth_destroy(self.h)
+            self.h = None
+
+    def process(self, xyz):
+        """projectPointCloud + downsamplePointCloud (visual_odometry.cpp:201-214)"""
+        xyz = np.ascontiguousarray(xyz, dtype=np.float32)
+        return lib().oracle_depth_process(self.h, _ptr(xyz), len(xyz), xyz.shape[1])
+
+    def cloud(self, which):
+        """0: point_cloud_2d, 1: point_cloud_2d_dnsp, (n, 3) float32"""
+        n = lib().oracle_depth_count(self.h, which)
+        out = np.empty((n, 3), dtype=np.float32)
+        if n:
+            lib().oracle_depth_copy(self.h, which, _ptr(out))
+        return out
+
+    def buckets(self):
+        n = self.new_w * self.new_h
+        bx, by, bd = (np.empty(n, dtype=np.float32) for _ in range(3))
+        bc = np.empty(n, dtype=np.int32)
+        lib().oracle_depth_buckets(self.h, _ptr(bx), _ptr(by), _ptr(bd), _ptr(bc))
+        return bx, by, bd, bc
+
+    def query(self, xy, radius=2):
+        xy = np.ascontiguousarray(xy, dtype=np.float32).reshape(-1, 2)
+        out = np.empty(len(xy), dtype=np.float32)
+        ms = lib().oracle_depth_query(self.h, _ptr(xy), len(xy), radius, _ptr(out)) if len(xy) else 0.0
+        self.query_ms = ms
+        return out
+
+    @property
+    def ms(self):
+        return lib().oracle_depth_ms(self.h)

@@ -6,7 +6,7 @@ against independent implementations (cKDTree, numpy eigh/lstsq, finite differenc
 Ceres-LM restatement).  CPU tests check the oracle still reproduces them; GPU tests check the
 HIP path against them.
 
-    python tests/golden/make_golden.py     # rewrites tests/golden/*.npz
+    python tests/golden/make_golden.py [case ...]    # rewrites tests/golden/<case>.npz
 """
 import hashlib
 import os
@@ -86,11 +86,32 @@ def mapping_case():
                 stats=np.array(stats))
 
 
-CASES = dict(knn=knn_case, voxel=voxel_case, lm=lm_case, scanreg=scanreg_case, mapping=mapping_case)
+DEPTH = dict(seed=21, frame=4, n_az=800, n_query=600)
+
+
+def depth_case():
+    """visual-odometry depth association (point_cloud_util.cpp:183-487) of a synthetic scan with
+    the KITTI calibration of loam_amd.depth"""
+    from loam_amd.depth import KITTI_CAM_T_VELO, KITTI_P_RECT0, KITTI_RECT0_T_CAM
+    xyz, _ = synth.frame(DEPTH["seed"], DEPTH["frame"], DEPTH["n_az"])
+    u = O.PointCloudUtil(KITTI_CAM_T_VELO, KITTI_RECT0_T_CAM, KITTI_P_RECT0)
+    u.process(xyz)
+    rng = np.random.default_rng(4)
+    q = np.stack([rng.uniform(-10, 1252, DEPTH["n_query"]), rng.uniform(-10, 385, DEPTH["n_query"])],
+                 axis=1).astype(np.float32)
+    bx, by, bd, bc = u.buckets()
+    return dict(params=np.array([DEPTH["seed"], DEPTH["frame"], DEPTH["n_az"]]), p2d_sha=np.array(cloud_digest(u.cloud(0))),
+                n_front=np.int32(len(u.cloud(0))), dnsp=u.cloud(1), bucket_count=bc, queries=q, depth=u.query(q))
+
+
+CASES = dict(knn=knn_case, voxel=voxel_case, lm=lm_case, scanreg=scanreg_case, mapping=mapping_case,
+             depth=depth_case)
 
 
 def main():
-    for name, fn in CASES.items():
+    names = sys.argv[1:] or list(CASES)
+    for name in names:
+        fn = CASES[name]
         path = os.path.join(HERE, f"{name}.npz")
         np.savez_compressed(path, **fn())
         print(f"{path}: {os.path.getsize(path)} bytes")

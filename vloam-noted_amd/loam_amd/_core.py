@@ -52,6 +52,11 @@ class OdomStats(ctypes.Structure):
                 ("n_corner_last", c_i32), ("n_surf_last", c_i32), ("ms", c_d)]
 
 
+class DepthParams(ctypes.Structure):
+    _fields_ = [("cam_T_velo", c_f * 16), ("rect0_T_cam", c_f * 16), ("P_rect0", c_f * 12),
+                ("grid", c_i32), ("img_width", c_i32), ("img_height", c_i32), ("max_points", c_i32)]
+
+
 KFAM = ("stack_voxelgrid", "submap_hash_build", "correspondence", "lm_pass", "insert",
         "cube_revoxel", "other")
 
@@ -113,6 +118,18 @@ SIGNATURES = {
     "loam_comm_allgather": (c_i32, [vp, vp, vp, ctypes.c_int64, vp]),
     "loam_mapper_create_sharded": (c_i32, [ctypes.POINTER(Params), c_i32, c_i32, vp, ctypes.POINTER(vp)]),
     "loam_shard_owner": (c_i32, [vp, c_f, c_i32]),
+    "loam_depth_params_default": (None, [ctypes.POINTER(DepthParams)]),
+    "loam_depth_create": (c_i32, [ctypes.POINTER(DepthParams), c_i32, c_i32, ctypes.POINTER(vp)]),
+    "loam_depth_destroy": (c_i32, [vp]),
+    "loam_depth_input": (c_i32, [vp, c_i32, vp, c_i32, c_i32]),
+    "loam_depth_input_device": (c_i32, [vp, c_i32, vp, c_i32, c_i32]),
+    "loam_depth_process": (c_i32, [vp]),
+    "loam_depth_counts": (c_i32, [vp, c_i32, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)]),
+    "loam_depth_copy": (c_i32, [vp, c_i32, c_i32, vp, c_i32]),
+    "loam_depth_buckets": (c_i32, [vp, c_i32, vp, vp, vp, vp]),
+    "loam_depth_query": (c_i32, [vp, c_i32, vp, vp, c_i32, vp]),
+    "loam_depth_query_device": (c_i32, [vp, c_i32, vp, vp, c_i32, vp]),
+    "loam_depth_ms": (c_d, [vp]),
     "loam_lm_solve": (c_i32, [c_i32, vp, c_i32, vp, c_i32, ctypes.POINTER(LMStats)]),
     "loam_lm_normal_equations": (c_i32, [c_i32, vp, c_i32, vp, vp, vp, vp]),
     "loam_voxel_grid": (c_i32, [c_i32, vp, c_i32, c_f, vp, ctypes.POINTER(c_i32)]),
