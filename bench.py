@@ -62,6 +62,7 @@ def parse():
                     help="mapping prior: GPU LaserOdometry output (default) or ground truth + random walk")
     ap.add_argument("--no-single-stream", action="store_true",
                     help="skip the single-stream (latency view) timing")
+    ap.add_argument("--no-depth", action="store_true", help="skip the VO depth-association stage")
     ap.add_argument("--shard", action="store_true",
                     help="sharded mapping (SURVEY.md §8e): every stream split over all N ranks, map "
                          "blocks owned per rank, RCCL all-gather of 5-NN candidates per round and "
@@ -201,6 +202,75 @@ def cpu_baseline(frames, warm, n):
         _, lm = od.stats()
         st_ms["odometry_iters"] += lm[0].iterations + lm[1].iterations
     return iters, ms, st_ms
+
+
+def depth_stage(seed, device, n_frames=64, n_queries=2800, n_az=2000, with_cpu=True):
+    """VO depth association (point_cloud_util.cpp:183-487): one stream
+    per frame (device time of projectPointCloud + downsamplePointCloud) and n_frames streams in
+    one launch sequence (wall time, clouds resident in HBM), plus queryDepth of n_queries image
+    points per frame (the reference queries ~1400 matches x 2 clouds, visual_odometry.cpp:371-372);
+    the oracle's own timers on the same frames as the CPU baseline."""
+    import torch
+    from loam_amd import synth
+    from loam_amd.depth import KITTI_CAM_T_VELO, KITTI_P_RECT0, KITTI_RECT0_T_CAM, BatchDepth
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4)) as ex:
+        clouds = list(ex.map(lambda f: synth.frame(seed + 77, f, n_az)[0], range(n_frames)))
+    rng = np.random.default_rng(seed)
+    qs = [np.stack([rng.uniform(0, 1242, n_queries), rng.uniform(0, 375, n_queries)], 1).astype(np.float32)
+          for _ in range(n_frames)]
+    one = BatchDepth(1, device=device)
+    ms1, qms1, pts, front, dnsp = [], [], 0, 0, 0
+    for f in range(n_frames):
+        one.input(0, clouds[f])
+        one.process()
+        ms1.append(one.ms)
+        t0 = time.perf_counter()
+        one.query(0, qs[f])
+        qms1.append(1e3 * (time.perf_counter() - t0))
+        nf, nd = one.counts(0)
+        pts, front, dnsp = pts + len(clouds[f]), front + nf, dnsp + nd
+    one.close()
+    many = BatchDepth(n_frames, device=device)
+    dev = [torch.from_numpy(c).to(f"cuda:{device}") for c in clouds]
+    dq = torch.from_numpy(np.concatenate(qs)).to(f"cuda:{device}")
+    dqs = torch.repeat_interleave(torch.arange(n_frames, dtype=torch.int32), n_queries).to(f"cuda:{device}")
+    dd = torch.empty(n_frames * n_queries, dtype=torch.float32, device=f"cuda:{device}")
+    torch.cuda.synchronize(device)
+    reps, t_all = 10, 0.0
+    for r in range(reps + 2):
+        t0 = time.perf_counter()
+        for f in range(n_frames):
+            many.input_device(f, dev[f].data_ptr(), len(clouds[f]), 3)
+        many.process()
+        many.query_device(n_frames * n_queries, dqs.data_ptr(), dq.data_ptr(), dd.data_ptr())
+        if r >= 2:
+            t_all += time.perf_counter() - t0
+    many.close()
+    g1 = float(np.mean(ms1[4:]))
+    alg = (12.0 * pts + 12.0 * front + 12.0 * dnsp) / n_frames  # points in, point_cloud_2d, dnsp out
+    e = {"gpu_ms_per_frame": round(g1, 4), "gpu_query_ms_per_frame": round(float(np.mean(qms1[4:])), 4),
+         "queries_per_frame": n_queries,
+         "batched_frames_per_s": round(n_frames * reps / t_all, 1),
+         "batched": f"{n_frames} streams per launch sequence + {n_frames * n_queries} queries, wall time",
+         "algorithmic_bytes_per_frame": round(alg, 1),
+         "achieved_gbs_one_stream": round(alg / (g1 * 1e-3) / 1e9, 2),
+         "points_per_frame": pts // n_frames, "front_per_frame": front // n_frames, "dnsp_per_frame": dnsp // n_frames}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import loam_oracle as O
+        u = O.PointCloudUtil(KITTI_CAM_T_VELO, KITTI_RECT0_T_CAM, KITTI_P_RECT0)
+        cms, cq = [], []
+        for f in range(min(n_frames, 32)):
+            u.process(clouds[f])
+            cms.append(u.ms)
+            u.query(qs[f])
+            cq.append(u.query_ms)
+        c = float(np.mean(cms)) + float(np.mean(cq))
+        e.update(cpu_ms_per_frame=round(float(np.mean(cms)), 4), cpu_query_ms_per_frame=round(float(np.mean(cq)), 4),
+                 cpu_cores=1, cpu_kind="port",
+                 speedup_one_stream=round(c / (g1 + e["gpu_query_ms_per_frame"]), 2),
+                 speedup_batched=round((n_frames * reps / t_all) * c * 1e-3, 2))
+    return e
 
 
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
@@ -395,6 +465,8 @@ def main():
                 if name == "odometry":
                     e["cpu_lm_iters_per_s"] = round(cpu_st["odometry_iters"] / (cpu_st[name] * 1e-3), 1)
             stages[name] = e
+        if not args.no_depth and world == 1:
+            stages["depth_association"] = depth_stage(args.seed, local, with_cpu=not args.no_cpu)
         out["stages"] = stages
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(out["value"] / cpu["value"], 2)
