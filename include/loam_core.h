@@ -222,6 +222,16 @@ int32_t loam_mapper_cube_copy(loam_mapper* h, int32_t stream, int32_t which, int
                               float* out);
 int32_t loam_mapper_cube_set(loam_mapper* h, int32_t stream, int32_t which, int32_t cube,
                              const float* pts, int32_t n);
+/* /laser_cloud_map (laser_mapping.cpp:884-899): corner cube 0, surf cube 0, corner cube 1, ...
+ * gathered on the device; copies when cap >= the count (4 floats / point); returns the count.
+ * On a sharded handle: this rank's points. */
+int32_t loam_mapper_map_copy(loam_mapper* h, int32_t stream, float* out, int64_t cap);
+/* /velodyne_cloud_registered (:901-911): laserCloudFullRes transformed with the pose that
+ * loam_mapper_pose returns (pointAssociateToMap, :154-164); n points of 4 floats; host
+ * buffers, or device buffers (in place allowed) for the _device form; returns n */
+int32_t loam_mapper_register_cloud(loam_mapper* h, int32_t stream, const float* in, int32_t n, float* out);
+int32_t loam_mapper_register_cloud_device(loam_mapper* h, int32_t stream, const float* d_in, int32_t n,
+                                          float* d_out);
 
 /* --------------------------------------------------------------------------------------
  * Sharded LaserMapping: one mapping stream split over `size` GPUs (ranks).

@@ -152,6 +152,20 @@ class BatchMapper {
   }
   void solve() { check(loam_mapper_solve(h_)); }
   void pose(int32_t stream, double q_w[4], double t_w[3]) const { check(loam_mapper_pose(h_, stream, q_w, t_w)); }
+  // /laser_cloud_map (laser_mapping.cpp:884-899)
+  Cloud map(int32_t stream) const {
+    const int32_t n = check(loam_mapper_map_copy(h_, stream, nullptr, 0));
+    Cloud out(static_cast<size_t>(n) * 4);
+    if (n) check(loam_mapper_map_copy(h_, stream, out.data(), n));
+    return out;
+  }
+  // /velodyne_cloud_registered (:901-911)
+  Cloud registered(int32_t stream, const Cloud& full_res) const {
+    Cloud out(full_res.size());
+    check(loam_mapper_register_cloud(h_, stream, full_res.data(), static_cast<int32_t>(full_res.size() / 4),
+                                     out.data()));
+    return out;
+  }
   loam_map_stats stats(int32_t stream) const {
     loam_map_stats st;
     check(loam_mapper_stats(h_, stream, &st));
@@ -186,6 +200,9 @@ class LaserMapping {
   // q_w_curr / t_w_curr: what publish() sends on /aft_mapped_to_init (laser_mapping.cpp:816-874)
   void output(double q_w_curr[4], double t_w_curr[3]) const { m_.pose(0, q_w_curr, t_w_curr); }
   loam_map_stats stats() const { return m_.stats(0); }
+  // publish() payloads: laserCloudMap and laserCloudFullRes in the map frame
+  Cloud laserCloudMap() const { return m_.map(0); }
+  Cloud laserCloudFullResRegistered(const Cloud& full_res) const { return m_.registered(0, full_res); }
   BatchMapper& batch() { return m_; }
 
  private:

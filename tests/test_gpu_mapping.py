@@ -135,3 +135,49 @@ def test_stack_voxelgrid_bit_exact(n_corner, n_surf):
         got, ref = m.stack(0, which), O.voxel_grid(c, leaf)
         assert got.shape == ref.shape
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def _to_map_np(pose, pts):
+    """pointAssociateToMap (laser_mapping.cpp:154-164) with Eigen's _transformVector order"""
+    x, y, z, w = (float(v) for v in pose[0])
+    t = pose[1]
+    out = np.empty_like(pts)
+    for i, p in enumerate(pts.astype(np.float64)):
+        vx, vy, vz = p[0], p[1], p[2]
+        ux, uy, uz = y * vz - z * vy, z * vx - x * vz, x * vy - y * vx
+        ux, uy, uz = ux + ux, uy + uy, uz + uz
+        cx, cy, cz = y * uz - z * uy, z * ux - x * uz, x * uy - y * ux
+        r = ((vx + w * ux) + cx, (vy + w * uy) + cy, (vz + w * uz) + cz)
+        out[i, :3] = [np.float32(r[k] + t[k]) for k in range(3)]
+        out[i, 3] = pts[i, 3]
+    return out
+
+
+def test_publish_outputs(seq):
+    """/laser_cloud_map gather (laser_mapping.cpp:884-899) and the registered full-res cloud
+    (:901-911) after a teacher-forced frame"""
+    rec = seq[7]
+    m = BatchMapper(1)
+    load_state(m, 0, rec["before"])
+    m.input(0, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+    m.solve()
+    got = m.map_cloud(0)
+    corner, surf = m.cubes(0, 0), m.cubes(0, 1)
+    parts = []
+    for c in range(21 * 21 * 11):
+        for cubes in (corner, surf):
+            if c in cubes:
+                parts.append(cubes[c])
+    ref = np.concatenate(parts)
+    assert np.array_equal(got, ref)
+    oref = []
+    for c in range(21 * 21 * 11):
+        for key in ("corner", "surf"):
+            if c in rec["after"][key]:
+                oref.append(rec["after"][key][c])
+    oref = np.concatenate(oref)
+    assert got.shape == oref.shape and np.max(np.abs(got[:, :3] - oref[:, :3])) < 1e-5
+    cloud = np.concatenate([rec["corner"], rec["surf"]])[:3000]
+    reg = m.register_cloud(0, cloud)
+    assert np.array_equal(reg, _to_map_np(m.pose(0), cloud))
+    assert len(m.register_cloud(0, np.zeros((0, 4), np.float32))) == 0

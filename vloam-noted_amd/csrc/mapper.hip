@@ -76,6 +76,10 @@ struct StreamFrame {
   LmState lm[2];
 };
 
+struct MapPose {  // by-value kernel argument: q (xyzw) + t
+  double x[7];
+};
+
 struct MapperDev {
   int B;       // streams of this launch (a group of the handle's streams)
   int s0 = 0;  // first stream of the launch
@@ -1000,6 +1004,50 @@ __global__ void k_compact_commit(MapperDev D, const int* pairs, int npairs, cons
 }
 
 // ---------------------------------------------------------------------------------------
+// publish-side outputs (laser_mapping.cpp:884-911)
+// ---------------------------------------------------------------------------------------
+// laserCloudMap = corner cube 0, surf cube 0, corner cube 1, ... (:886-891): offsets of every
+// (cube, map) run, one workgroup
+__global__ void __launch_bounds__(VX_THREADS) k_map_scan(MapperDev D, int s, uint32_t* off) {
+  __shared__ uint32_t ws[VX_WAVES + 1];
+  const uint2* tc = D.cube_tab + sm_index(s, 0) * NCUBE;
+  const uint2* ts = D.cube_tab + sm_index(s, 1) * NCUBE;
+  constexpr int PER = (NCUBE + VX_THREADS - 1) / VX_THREADS;
+  uint32_t v[2 * PER], sum = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int c = threadIdx.x * PER + k;
+    v[2 * k] = c < NCUBE ? tc[c].y : 0u;
+    v[2 * k + 1] = c < NCUBE ? ts[c].y : 0u;
+    sum += v[2 * k] + v[2 * k + 1];
+  }
+  uint32_t total;
+  uint32_t pre = vx_block_scan(sum, ws, &total);
+#pragma unroll
+  for (int k = 0; k < 2 * PER; ++k) {
+    const int c = threadIdx.x * PER + k / 2;
+    if (c < NCUBE) off[2 * c + (k & 1)] = pre;
+    pre += v[k];
+  }
+  if (threadIdx.x == 0) off[2 * NCUBE] = total;
+}
+
+__global__ void k_map_gather(MapperDev D, int s, const uint32_t* off, float4* out) {
+  const StreamFrame& F = D.fr[s];
+  for (int e = blockIdx.x; e < 2 * NCUBE; e += gridDim.x) {
+    const int c = e >> 1, m = e & 1;
+    const uint2 cv = D.cube_tab[sm_index(s, m) * NCUBE + c];
+    const float4* src = arena_base(D, s, m, F.arena_active[m]) + cv.x;
+    for (uint32_t i = threadIdx.x; i < cv.y; i += blockDim.x) out[off[e] + i] = src[i];
+  }
+}
+
+// laserCloudFullRes registered with the mapped pose: pointAssociateToMap (:154-164, :901-905)
+__global__ void k_register(const float4* in, float4* out, int n, MapPose P) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) out[i] = to_map(P.x, in[i]);
+}
+
+// ---------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------
 // page-locked host array (hipHostMalloc) with the few vector operations used here
@@ -1086,6 +1134,10 @@ struct loam_mapper {
   loam_comm* comm = nullptr;  // sharded mode (loam_mapper_create_sharded)
   PinnedArray<int> q_off;     // [B + 1] query offsets of the sharded kNN exchange
   int* d_q_off = nullptr;
+  // publish-side buffers (grown on demand)
+  uint32_t* d_map_off = nullptr;  // [2 * NCUBE + 1]
+  float4* d_pub = nullptr;
+  size_t pub_cap = 0;
 };
 
 namespace {
@@ -1112,6 +1164,9 @@ uint32_t next_pow2(uint32_t v) {
 void free_all(loam_mapper* h) {
   for (void* p : h->allocs) (void)hipFree(p);
   h->allocs.clear();
+  if (h->d_pub) (void)hipFree(h->d_pub);
+  h->d_pub = nullptr;
+  h->pub_cap = 0;
   for (auto& e : h->ev_pool) (void)hipEventDestroy(e);
   h->ev_pool.clear();
   for (auto& e : h->ev)
@@ -1302,6 +1357,7 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   ALLOC(D.lm_sync, B * 2 * 4);
   ALLOC(D.lm_xpub, B * 2 * 8);
   ALLOC(D.tickets, B);
+  ALLOC(h->d_map_off, 2 * NCUBE + 1);
   ALLOC(h->d_pairs, B * 2);
   ALLOC(h->d_new_off, B * 2 * (NCUBE + 1));
   if (D.sharded) {
@@ -1906,6 +1962,68 @@ int32_t loam_mapper_cube_set(loam_mapper* h, int32_t s, int32_t which, int32_t c
   const uint32_t zero = 0;  // caller content: not known to be a VoxelGrid fixed point
   LOAM_HIP(hipMemcpy(h->D.stable_tok + ((size_t)s * 2 + which) * NCUBE + cube, &zero, sizeof(zero), hipMemcpyHostToDevice));
   return build_cube_index(h, s, which, cube, cube + 1);
+}
+
+static int32_t pub_reserve(loam_mapper* h, size_t n) {
+  if (n <= h->pub_cap) return LOAM_OK;
+  if (h->d_pub) (void)hipFree(h->d_pub);
+  h->d_pub = nullptr;
+  h->pub_cap = 0;
+  LOAM_HIP(hipMalloc(&h->d_pub, sizeof(float4) * std::max<size_t>(n, 1)));
+  h->pub_cap = n;
+  return LOAM_OK;
+}
+
+int32_t loam_mapper_map_copy(loam_mapper* h, int32_t s, float* out, int64_t cap) {
+  TRY(check_stream(h, s));
+  if (cap < 0 || (cap > 0 && !out)) return LOAM_ERR_ARG;
+  LOAM_HIP(hipSetDevice(h->dev));
+  MapperDev D = h->D;
+  D.cube_tab = h->cube_tab[h->parity];
+  // the device stream record supplies arena_active (current after every solve / set)
+  LOAM_HIP(hipMemcpyAsync(h->D.fr + s, &h->hf[s], sizeof(StreamFrame), hipMemcpyHostToDevice, h->st));
+  k_map_scan<<<1, VX_THREADS, 0, h->st>>>(D, s, h->d_map_off);
+  uint32_t total = 0;
+  LOAM_HIP(hipMemcpyAsync(&total, h->d_map_off + 2 * NCUBE, sizeof(uint32_t), hipMemcpyDeviceToHost, h->st));
+  LOAM_HIP(hipStreamSynchronize(h->st));
+  if ((int64_t)total > cap) return (int32_t)total;  // the count only
+  if (total) {
+    TRY(pub_reserve(h, total));
+    k_map_gather<<<512, 256, 0, h->st>>>(D, s, h->d_map_off, h->d_pub);
+    LOAM_HIP(hipGetLastError());
+    LOAM_HIP(hipMemcpyAsync(out, h->d_pub, sizeof(float4) * total, hipMemcpyDeviceToHost, h->st));
+    LOAM_HIP(hipStreamSynchronize(h->st));
+  }
+  return (int32_t)total;
+}
+
+static int32_t register_common(loam_mapper* h, int32_t s, const float* in, int32_t n, float* out, bool device) {
+  TRY(check_stream(h, s));
+  if (n < 0 || (n > 0 && (!in || !out))) return LOAM_ERR_ARG;
+  if (n == 0) return 0;
+  LOAM_HIP(hipSetDevice(h->dev));
+  MapPose P;
+  TRY(loam_mapper_pose(h, s, P.x, P.x + 4));
+  const float4* src = reinterpret_cast<const float4*>(in);
+  float4* dst = reinterpret_cast<float4*>(out);
+  if (!device) {
+    TRY(pub_reserve(h, n));
+    LOAM_HIP(hipMemcpyAsync(h->d_pub, in, sizeof(float4) * n, hipMemcpyHostToDevice, h->st));
+    src = dst = h->d_pub;
+  }
+  k_register<<<std::min(1024, (n + 255) / 256), 256, 0, h->st>>>(src, dst, n, P);
+  LOAM_HIP(hipGetLastError());
+  if (!device) LOAM_HIP(hipMemcpyAsync(out, h->d_pub, sizeof(float4) * n, hipMemcpyDeviceToHost, h->st));
+  LOAM_HIP(hipStreamSynchronize(h->st));
+  return n;
+}
+
+int32_t loam_mapper_register_cloud(loam_mapper* h, int32_t s, const float* in, int32_t n, float* out) {
+  return register_common(h, s, in, n, out, false);
+}
+
+int32_t loam_mapper_register_cloud_device(loam_mapper* h, int32_t s, const float* d_in, int32_t n, float* d_out) {
+  return register_common(h, s, d_in, n, d_out, true);
 }
 
 }  // extern "C"

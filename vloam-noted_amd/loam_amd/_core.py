@@ -110,6 +110,9 @@ SIGNATURES = {
     "loam_mapper_cube_copy": (c_i32, [vp, c_i32, c_i32, c_i32, vp]),
     "loam_mapper_stack_copy": (c_i32, [vp, c_i32, c_i32, vp, c_i32]),
     "loam_mapper_cube_set": (c_i32, [vp, c_i32, c_i32, c_i32, vp, c_i32]),
+    "loam_mapper_map_copy": (c_i32, [vp, c_i32, vp, ctypes.c_int64]),
+    "loam_mapper_register_cloud": (c_i32, [vp, c_i32, vp, c_i32, vp]),
+    "loam_mapper_register_cloud_device": (c_i32, [vp, c_i32, vp, c_i32, vp]),
     "loam_comm_create": (c_i32, [c_i32, c_i32, vp, ctypes.POINTER(vp)]),
     "loam_comm_rccl_unique_id": (c_i32, [vp]),
     "loam_comm_create_rccl": (c_i32, [c_i32, c_i32, vp, c_i32, ctypes.POINTER(vp)]),

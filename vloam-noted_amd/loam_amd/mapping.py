@@ -155,6 +155,21 @@ class BatchMapper:
         pts = f32x4(pts)
         check(lib().loam_mapper_cube_set(self.h, stream, which, cube, ptr(pts), len(pts)))
 
+    def map_cloud(self, stream=0):
+        """laserCloudMap of the /laser_cloud_map publisher (laser_mapping.cpp:884-899)"""
+        n = check(lib().loam_mapper_map_copy(self.h, stream, None, 0))
+        out = np.empty((n, 4), dtype=np.float32)
+        if n:
+            check(lib().loam_mapper_map_copy(self.h, stream, ptr(out), n))
+        return out
+
+    def register_cloud(self, stream, cloud):
+        """laserCloudFullRes in the map frame with the current pose (laser_mapping.cpp:901-905)"""
+        c = f32x4(cloud)
+        out = np.empty_like(c)
+        check(lib().loam_mapper_register_cloud(self.h, stream, ptr(c), len(c), ptr(out)))
+        return out
+
     def cubes(self, stream, which):
         out = {}
         for c in range(N_CUBES):
