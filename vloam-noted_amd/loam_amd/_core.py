@@ -9,7 +9,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libloam_core.so")
+# LOAM_CORE_LIB: an alternative build of the same library (A/B measurements of kernel variants)
+LIB_PATH = os.environ.get("LOAM_CORE_LIB") or os.path.join(_HERE, "_lib", "libloam_core.so")
 
 c_i32 = ctypes.c_int32
 c_f = ctypes.c_float
