@@ -123,6 +123,7 @@ struct MapperDev {
   uint32_t* tickets;  // [B]
   // sharded mode (loam_mapper_create_sharded): this rank of nrank; map points are stored by
   // the rank owning their 4 m block (comm.h, shard_owner); blk_v: voxels per block edge
+  int knn_order = 0;  // corr_block ordering (LOAM_KNN_ORDER)
   int rank = 0, nrank = 1, sharded = 0;
   int blk_v[2] = {1, 1};
   uint32_t* wcnt;        // [B][2][WIN_MAX] window cube counts (all-reduced over the ranks)
@@ -288,10 +289,32 @@ struct WinMap {  // per (stream, map) window cubes, in LDS
   int sub[WIN_MAX];
 };
 
+// L lanes per query (L | 64): the lanes of a group visit the same cells and split each cell's
+// points; the pruning bound is the group minimum of the lanes' 5th distances (each bounds the
+// union's 5th from above, so it is safe), and a butterfly merge leaves the union's 5 nearest in
+// every lane.  The result is the L = 1 result (the minimum over (d, key) of the same
+// candidates); L > 1 shortens each query's chain of dependent loads.
+// block -> (stream, member).  Default: stream b % B, member b / B (a stream's blocks on one XCD,
+// b % 8, when B is a multiple of 8).  knn_order 1: the same XCD per stream, but each XCD runs
+// its streams one after another (b = 8 k + xcd, stream xcd + 8 (k / CORR_BLK)), so fewer
+// streams' cell indexes share an XCD's L2 at a time.
+__device__ inline void corr_block(const MapperDev& D, int* s, int* blk) {
+  if (D.knn_order && (D.B & 7) == 0) {
+    const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
+    *s = D.s0 + x + 8 * (k / CORR_BLK);
+    *blk = k % CORR_BLK;
+  } else {
+    *s = D.s0 + blockIdx.x % D.B;
+    *blk = blockIdx.x / D.B;
+  }
+}
+
+template <int L>
 __global__ void __launch_bounds__(CORR_THREADS) k_knn(MapperDev D, int round) {
   __shared__ WinMap W[2];
   __shared__ int slot_of[75];  // 5 x 5 x 3 window position -> slot (laserCloudValidInd order)
-  const int s = D.s0 + blockIdx.x % D.B, blk = blockIdx.x / D.B;  // a stream's blocks on one XCD
+  int s, blk;
+  corr_block(D, &s, &blk);
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
   double X[7];
@@ -321,7 +344,8 @@ __global__ void __launch_bounds__(CORR_THREADS) k_knn(MapperDev D, int round) {
   const int nc = F.nc_stack, ns = F.ns_stack;
   const size_t rb = (size_t)s * 2 * D.max_in;
   uint32_t ncand = 0;
-  for (int ridx = blk * CORR_THREADS + tid; ridx < nc + ns; ridx += CORR_BLK * CORR_THREADS) {
+  const int gsub = tid % L;
+  for (int ridx = blk * (CORR_THREADS / L) + tid / L; ridx < nc + ns; ridx += CORR_BLK * (CORR_THREADS / L)) {
     const int m = ridx < nc ? 0 : 1;  // corners [0, nc), surfs [nc, nc + ns)
     const int qi = m == 0 ? ridx : ridx - nc;
     const float4 q = to_map(X, D.stack[m][(size_t)s * D.max_in + qi]);
@@ -353,7 +377,7 @@ __global__ void __launch_bounds__(CORR_THREADS) k_knn(MapperDev D, int round) {
                               (uint32_t)ax | ((uint32_t)ay << 6) | ((uint32_t)az << 12));
       ncand += e.y;
       const int sub = WM.sub[sl];
-      for (uint32_t k = 0; k < e.y; ++k) {
+      for (uint32_t k = gsub; k < e.y; k += L) {
         const uint32_t pos = off + e.x + k;
         const float4 p = cp[pos];
         // sharded: submap position x ranks + rank keeps the key unique (and equal to the
@@ -368,7 +392,9 @@ __global__ void __launch_bounds__(CORR_THREADS) k_knn(MapperDev D, int round) {
       const float gx = dx < 0 ? lx : (dx > 0 ? hx : 0.f);
       const float gy = dy < 0 ? ly : (dy > 0 ? hy : 0.f);
       const float gz = dz < 0 ? lz : (dz > 0 ? hz : 0.f);
-      const float bound = fminf(T.d[4], 1.0f) * 1.01f + 1e-6f;  // rounding margin
+      float bound = fminf(T.d[4], 1.0f) * 1.01f + 1e-6f;  // rounding margin
+#pragma unroll
+      for (int o = 1; o < L; o <<= 1) bound = fminf(bound, __shfl_xor(bound, o, 64));
       if (gx * gx + gy * gy + gz * gz > bound) continue;
       const int x = qx + dx, y = qy + dy, z = qz + dz;
       const int bi = floor_div50(x + 25) + F.cen[0], bj = floor_div50(y + 25) + F.cen[1],
@@ -395,6 +421,21 @@ __global__ void __launch_bounds__(CORR_THREADS) k_knn(MapperDev D, int round) {
         scan(b2[0], b2[1], b2[2], l2[0], l2[1], l2[2]);
       }
     }
+#pragma unroll
+    for (int o = 1; o < L; o <<= 1) {  // butterfly: disjoint candidate sets at every step
+      float pd[5];
+      int pid[5], ppos[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        pd[k] = __shfl_xor(T.d[k], o, 64);
+        pid[k] = __shfl_xor(T.id[k], o, 64);
+        ppos[k] = __shfl_xor(T.pos[k], o, 64);
+      }
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        if (ppos[k] >= 0) near5_offer(T, pd[k], pid[k], ppos[k]);
+    }
+    if (gsub != 0) continue;
     if (D.sharded) {  // this rank's candidates; the 1 m test follows the merge (k_nn_merge)
       NnRec& o = D.nn_send[D.q_off[s] + ridx];
 #pragma unroll
@@ -474,7 +515,8 @@ __global__ void __launch_bounds__(CORR_THREADS) k_nn_merge(MapperDev D) {
 // pass 2: line PCA / plane fit of the 5 neighbours -> factor records (laser_mapping.cpp:557-603,
 // :642-680)
 __global__ void __launch_bounds__(CORR_THREADS) k_geom(MapperDev D, int round) {
-  const int s = D.s0 + blockIdx.x % D.B, blk = blockIdx.x / D.B;  // a stream's blocks on one XCD
+  int s, blk;
+  corr_block(D, &s, &blk);
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
   const int nc = F.nc_stack, ns = F.ns_stack;
@@ -1131,6 +1173,7 @@ struct loam_mapper {
   // the window that receive points; a write past the capacity is reported (err flags)
   uint32_t compact_at = 0;
   int lm_G = 0;  // workgroups per stream of k_lm_round (0: two-kernel path k_lm_eval / k_lm_step)
+  int knn_lanes = 1;  // lanes per query of k_knn (LOAM_KNN_LANES: 1, 2, 4, 8)
   loam_comm* comm = nullptr;  // sharded mode (loam_mapper_create_sharded)
   PinnedArray<int> q_off;     // [B + 1] query offsets of the sharded kNN exchange
   int* d_q_off = nullptr;
@@ -1318,6 +1361,13 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     }
     const char* senv = std::getenv("LOAM_MAPPER_STAGGER");
     h->stagger = (senv && senv[0] == '1') ? 1 : 0;
+    const char* oenv = std::getenv("LOAM_KNN_ORDER");
+    D.knn_order = (oenv && oenv[0] == '1') ? 1 : 0;
+    const char* kenv = std::getenv("LOAM_KNN_LANES");
+    if (kenv) {
+      const int l = std::atoi(kenv);
+      h->knn_lanes = (l == 2 || l == 4 || l == 8) ? l : 1;
+    }
     const char* renv = std::getenv("LOAM_REVOX_SPLIT");  // 1: k_revox_merge + k_revox
     D.rv_split = (renv && renv[0] == '1') ? 1 : 0;
   }
@@ -1660,7 +1710,12 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     for (int g = 0; g < NG; ++g) {
       hipStream_t sg = h->gst[g];
       LOAM_HIP(before(g, 2 + 3 * round, sg));
-      LAUNCH_ON(sg, FAM_CORR, k_knn<<<Bg * CORR_BLK, CORR_THREADS, 0, sg>>>(Dg[g], round));
+      switch (h->knn_lanes) {
+        case 1: LAUNCH_ON(sg, FAM_CORR, k_knn<1><<<Bg * CORR_BLK, CORR_THREADS, 0, sg>>>(Dg[g], round)); break;
+        case 2: LAUNCH_ON(sg, FAM_CORR, k_knn<2><<<Bg * CORR_BLK, CORR_THREADS, 0, sg>>>(Dg[g], round)); break;
+        case 4: LAUNCH_ON(sg, FAM_CORR, k_knn<4><<<Bg * CORR_BLK, CORR_THREADS, 0, sg>>>(Dg[g], round)); break;
+        default: LAUNCH_ON(sg, FAM_CORR, k_knn<8><<<Bg * CORR_BLK, CORR_THREADS, 0, sg>>>(Dg[g], round)); break;
+      }
       LOAM_HIP(after(g, 2 + 3 * round, sg));
     }
     if (D.sharded) {  // every rank's candidates -> the exact 5-NN on every rank
