@@ -333,6 +333,20 @@ int32_t loam_depth_query_device(loam_depth* h, int32_t n, const int32_t* d_strea
 double loam_depth_ms(loam_depth* h);
 
 /* --------------------------------------------------------------------------------------
+ * Visual-odometry pose solve — VisualOdometry::solveNlsAll
+ * (src/visual_odometry/src/visual_odometry.cpp:304-509): n_problems independent problems,
+ * factor records of 10 doubles, problem p = records offsets[p] .. offsets[p + 1]:
+ *   type 4 CostFunctor32 (ceres_cost_function.h:58-102): p = X0 (point_3d_rect0_0),
+ *          a[0..1] = (x1_bar, y1_bar)
+ *   type 5 CostFunctor22 (:151-189): a[0..1] = (x0_bar, y0_bar), b[0..1] = (x1_bar, y1_bar)
+ * x: n_problems x 6 = angles_0to1 (angle-axis), t_0to1; in: initial values (zeros, or the
+ * LiDAR-odometry prior, :311-331), out: the solution.  HuberLoss(0.1), Ceres TR-LM, DENSE_QR,
+ * max_iterations (the reference: 100).  st: n_problems stats (may be NULL).
+ * ------------------------------------------------------------------------------------ */
+int32_t loam_vo_solve(int32_t device, int32_t n_problems, const int32_t* offsets, const double* factors,
+                      double* x, int32_t max_iterations, loam_lm_stats* st);
+
+/* --------------------------------------------------------------------------------------
  * Device LM engine on an explicit factor list (lidarFactor.hpp + Ceres TR-LM).  Factor
  * record = 10 doubles: type (1 LidarEdgeFactor, 2 LidarPlaneFactor, 3 LidarPlaneNormFactor),
  * curr_point[3], a[3], b[3] (edge: last_point_a/b; plane: j, unit normal ljm; plane-norm:

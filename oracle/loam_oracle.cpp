@@ -472,6 +472,120 @@ static inline int eval_block(const Factor& F, const Quat& q, const V3& t, double
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Visual-odometry residual blocks (src/visual_odometry/include/visual_odometry/
+// ceres_cost_function.h), parameters angles_0to1 (angle-axis) and t_0to1, evaluated the way
+// Ceres' AutoDiffCostFunction<.., 3, 3> does: forward-mode Jets through the functor, with
+// ceres::AngleAxisRotatePoint / CrossProduct / DotProduct (ceres/rotation.h) and the Jet
+// rules of ceres/jet.h.
+//   type 4 CostFunctor32 (:58-102): p = X0, a[0..1] = (x1_bar, y1_bar), 2 rows
+//   type 5 CostFunctor22 (:151-189): a[0..1] = (x0_bar, y0_bar), b[0..1] = (x1_bar, y1_bar), 1 row
+// ---------------------------------------------------------------------------------------
+struct Jet {
+  double a;
+  double v[6];
+};
+static inline Jet jconst(double c) {
+  Jet j{c, {0, 0, 0, 0, 0, 0}};
+  return j;
+}
+static inline Jet operator+(const Jet& f, const Jet& g) {
+  Jet r{f.a + g.a, {}};
+  for (int k = 0; k < 6; ++k) r.v[k] = f.v[k] + g.v[k];
+  return r;
+}
+static inline Jet operator-(const Jet& f, const Jet& g) {
+  Jet r{f.a - g.a, {}};
+  for (int k = 0; k < 6; ++k) r.v[k] = f.v[k] - g.v[k];
+  return r;
+}
+static inline Jet operator-(const Jet& f) {
+  Jet r{-f.a, {}};
+  for (int k = 0; k < 6; ++k) r.v[k] = -f.v[k];
+  return r;
+}
+static inline Jet operator*(const Jet& f, const Jet& g) {  // jet.h: (f.a g.a, f.a g.v + f.v g.a)
+  Jet r{f.a * g.a, {}};
+  for (int k = 0; k < 6; ++k) r.v[k] = f.a * g.v[k] + f.v[k] * g.a;
+  return r;
+}
+static inline Jet operator/(const Jet& f, const Jet& g) {  // jet.h: a = f.a / g.a, v = (f.v - a g.v) / g.a
+  const double gi = 1.0 / g.a, fa = f.a * gi;
+  Jet r{fa, {}};
+  for (int k = 0; k < 6; ++k) r.v[k] = (f.v[k] - fa * g.v[k]) * gi;
+  return r;
+}
+static inline Jet jsqrt(const Jet& f) {
+  const double t = std::sqrt(f.a), ti = 1.0 / (2.0 * t);
+  Jet r{t, {}};
+  for (int k = 0; k < 6; ++k) r.v[k] = f.v[k] * ti;
+  return r;
+}
+static inline Jet jcos(const Jet& f) {
+  const double sn = -std::sin(f.a);
+  Jet r{std::cos(f.a), {}};
+  for (int k = 0; k < 6; ++k) r.v[k] = sn * f.v[k];
+  return r;
+}
+static inline Jet jsin(const Jet& f) {
+  const double cs = std::cos(f.a);
+  Jet r{std::sin(f.a), {}};
+  for (int k = 0; k < 6; ++k) r.v[k] = cs * f.v[k];
+  return r;
+}
+
+// ceres::AngleAxisRotatePoint (rotation.h)
+static void aa_rotate(const Jet aa[3], const Jet pt[3], Jet out[3]) {
+  const Jet theta2 = (aa[0] * aa[0] + aa[1] * aa[1]) + aa[2] * aa[2];
+  if (theta2.a > std::numeric_limits<double>::epsilon()) {
+    const Jet theta = jsqrt(theta2);
+    const Jet costheta = jcos(theta), sintheta = jsin(theta);
+    const Jet theta_inverse = jconst(1.0) / theta;
+    const Jet w[3] = {aa[0] * theta_inverse, aa[1] * theta_inverse, aa[2] * theta_inverse};
+    const Jet wc[3] = {w[1] * pt[2] - w[2] * pt[1], w[2] * pt[0] - w[0] * pt[2], w[0] * pt[1] - w[1] * pt[0]};
+    const Jet tmp = ((w[0] * pt[0] + w[1] * pt[1]) + w[2] * pt[2]) * (jconst(1.0) - costheta);
+    for (int i = 0; i < 3; ++i) out[i] = (pt[i] * costheta + wc[i] * sintheta) + w[i] * tmp;
+  } else {
+    const Jet wc[3] = {aa[1] * pt[2] - aa[2] * pt[1], aa[2] * pt[0] - aa[0] * pt[2], aa[0] * pt[1] - aa[1] * pt[0]};
+    for (int i = 0; i < 3; ++i) out[i] = pt[i] + wc[i];
+  }
+}
+
+// residual rows r[m] and Jacobian rows J[m][6] of a VO block at x = (angles, t)
+static int eval_vo_block(const Factor& F, const double* x, double r[3], double J[3][6]) {
+  Jet aa[3], t[3];
+  for (int i = 0; i < 3; ++i) {
+    aa[i] = jconst(x[i]);
+    aa[i].v[i] = 1.0;
+    t[i] = jconst(x[3 + i]);
+    t[i].v[3 + i] = 1.0;
+  }
+  Jet res[2];
+  int m;
+  if (F.type == 4) {  // CostFunctor32::operator()
+    const Jet X0[3] = {jconst(F.p[0]), jconst(F.p[1]), jconst(F.p[2])};
+    Jet R[3];
+    aa_rotate(aa, X0, R);
+    for (int i = 0; i < 3; ++i) R[i] = R[i] + t[i];
+    res[0] = R[0] - R[2] * jconst(F.a[0]);
+    res[1] = R[1] - R[2] * jconst(F.a[1]);
+    m = 2;
+  } else {  // CostFunctor22::operator()
+    const Jet X0[3] = {jconst(F.a[0]), jconst(F.a[1]), jconst(1.0)};
+    const Jet X1[3] = {jconst(F.b[0]), jconst(F.b[1]), jconst(1.0)};
+    Jet q[3];
+    aa_rotate(aa, X0, q);
+    const Jet c[3] = {t[1] * q[2] - t[2] * q[1], t[2] * q[0] - t[0] * q[2], t[0] * q[1] - t[1] * q[0]};
+    res[0] = (X1[0] * c[0] + X1[1] * c[1]) + X1[2] * c[2];
+    m = 1;
+  }
+  for (int i = 0; i < m; ++i) {
+    r[i] = res[i].a;
+    for (int k = 0; k < 6; ++k) J[i][k] = res[i].v[k];
+  }
+  return m;
+}
+
 // HuberLoss(a=0.1): rho(s) and Corrector scale sqrt(rho') (ceres/loss_function.cc,
 // ceres/corrector.cc; rho'' <= 0 branch => r, J scaled by sqrt(rho'))
 static inline void huber(double s, double& rho0, double& rho1) {
@@ -498,6 +612,27 @@ static double evaluate(const std::vector<Factor>& fs, const double* x, Eval* ev)
   for (const Factor& F : fs) {
     double r[3], drdp[3][3];
     V3 Rp;
+    if (F.type >= 4) {  // VO block: full Jacobian rows from the Jets
+      double Jv[3][6];
+      const int mv = eval_vo_block(F, x, r, Jv);
+      double sq = 0.0;
+      for (int i = 0; i < mv; ++i) sq += r[i] * r[i];
+      double rho0, rho1;
+      huber(sq, rho0, rho1);
+      cost += 0.5 * rho0;
+      if (!ev) continue;
+      const double sc = std::sqrt(rho1);
+      for (int i = 0; i < mv; ++i) {
+        const double ri = r[i] * sc;
+        for (int c = 0; c < 6; ++c) {
+          const double v = Jv[i][c] * sc;
+          ev->J.push_back(v);
+          ev->g[c] += v * ri;
+        }
+        ev->f.push_back(ri);
+      }
+      continue;
+    }
     int m = eval_block(F, q, t, r, drdp, Rp);
     double sq = 0.0;
     for (int i = 0; i < m; ++i) sq += r[i] * r[i];
@@ -527,8 +662,15 @@ static double evaluate(const std::vector<Factor>& fs, const double* x, Eval* ev)
   return cost;
 }
 
-// EigenQuaternionParameterization::Plus + Euclidean t
+// EigenQuaternionParameterization::Plus + Euclidean t; euclid: plain x + d on 6 parameters
+// (the VO problem's angle-axis + t blocks have no parameterization), x[6] = 0 kept
+static bool g_plus_euclid = false;
 static void plus(const double* x, const double* d, double* out) {
+  if (g_plus_euclid) {
+    for (int i = 0; i < 6; ++i) out[i] = x[i] + d[i];
+    out[6] = x[6];
+    return;
+  }
   double nd = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
   if (nd > 0.0) {
     double s = std::sin(nd) / nd;
@@ -1306,6 +1448,33 @@ int32_t oracle_plane_from_nbrs(const float* nbr, double* n, double* d) {
 int32_t oracle_lm_solve(const double* factors, int32_t nf, double* x, int32_t max_iter,
                         oracle_lm_stats* st) {
   return lm_solve(to_factors(factors, nf), x, max_iter, st);
+}
+
+int32_t oracle_vo_solve(const double* factors, int32_t nf, double* x6, int32_t max_iter, oracle_lm_stats* st) {
+  double x[7] = {x6[0], x6[1], x6[2], x6[3], x6[4], x6[5], 0.0};
+  g_plus_euclid = true;
+  const int32_t rc = lm_solve(to_factors(factors, nf), x, max_iter, st);
+  g_plus_euclid = false;
+  for (int i = 0; i < 6; ++i) x6[i] = x[i];
+  return rc;
+}
+
+int32_t oracle_vo_normal_eq(const double* factors, int32_t nf, const double* x6, double* cost, double* jtj,
+                            double* jtr) {
+  const double x[7] = {x6[0], x6[1], x6[2], x6[3], x6[4], x6[5], 0.0};
+  Eval ev;
+  evaluate(to_factors(factors, nf), x, &ev);
+  const int M = static_cast<int>(ev.f.size());
+  *cost = ev.cost;
+  for (int a = 0; a < 6; ++a) {
+    jtr[a] = ev.g[a];
+    for (int b = 0; b < 6; ++b) {
+      double v = 0.0;
+      for (int i = 0; i < M; ++i) v += ev.J[i * 6 + a] * ev.J[i * 6 + b];
+      jtj[a * 6 + b] = v;
+    }
+  }
+  return M;
 }
 
 int32_t oracle_lm_normal_eq(const double* factors, int32_t nf, const double* x, double* cost,

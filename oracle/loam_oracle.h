@@ -142,6 +142,15 @@ void oracle_depth_buckets(void* h, float* bx, float* by, float* bd, int32_t* bc)
 double oracle_depth_query(void* h, const float* xy, int32_t n, int32_t radius, float* depth);
 double oracle_depth_ms(void* h);
 
+/* ---- visual-odometry LM (visual_odometry.cpp:304-509): factor records of 10 doubles,
+ * type 4 CostFunctor32 (p = X0, a[0..1] = x1_bar, y1_bar), type 5 CostFunctor22
+ * (a[0..1] = x0_bar, y0_bar, b[0..1] = x1_bar, y1_bar); x6 = angles_0to1 (angle-axis), t_0to1.
+ * Jet autodiff of the functors, HuberLoss(0.1), Ceres TR-LM / DENSE_QR on Euclidean params. */
+int32_t oracle_vo_solve(const double* factors, int32_t nf, double* x6, int32_t max_iter, oracle_lm_stats* st);
+/* cost, J^T J (6x6 row-major), J^T r (Huber-corrected); returns the residual rows */
+int32_t oracle_vo_normal_eq(const double* factors, int32_t nf, const double* x6, double* cost, double* jtj,
+                            double* jtr);
+
 #ifdef __cplusplus
 }
 #endif

@@ -73,6 +73,8 @@ def lib():
             "oracle_map_factor_count": (c_i32, [vp, c_i32]),
             "oracle_map_factors": (c_i32, [vp, c_i32, vp]),
             "oracle_map_round_pose": (c_i32, [vp, c_i32, vp]),
+            "oracle_vo_solve": (c_i32, [vp, c_i32, vp, c_i32, ctypes.POINTER(LMStats)]),
+            "oracle_vo_normal_eq": (c_i32, [vp, c_i32, vp, vp, vp, vp]),
             "oracle_depth_create": (vp, [vp, vp, vp, c_i32, c_i32, c_i32]),
             "oracle_depth_destroy": (None, [vp]),
             "oracle_depth_process": (c_i32, [vp, vp, c_i32, c_i32]),
@@ -140,6 +142,25 @@ def lm_solve(factors, x, max_iter=4):
     st = LMStats()
     lib().oracle_lm_solve(_ptr(f), len(f), _ptr(x), max_iter, ctypes.byref(st))
     return x, st
+
+
+def vo_solve(factors, x6, max_iter=100):
+    """visual-odometry LM (angles_0to1, t_0to1); factors: (n, 10) type 4 / 5 records"""
+    f = np.ascontiguousarray(factors, dtype=np.float64).reshape(-1, 10)
+    x = np.array(x6, dtype=np.float64).copy()
+    st = LMStats()
+    lib().oracle_vo_solve(_ptr(f), len(f), _ptr(x), max_iter, ctypes.byref(st))
+    return x, st
+
+
+def vo_normal_eq(factors, x6):
+    f = np.ascontiguousarray(factors, dtype=np.float64).reshape(-1, 10)
+    x = np.ascontiguousarray(x6, dtype=np.float64)
+    cost = np.empty(1)
+    jtj = np.empty(36)
+    jtr = np.empty(6)
+    m = lib().oracle_vo_normal_eq(_ptr(f), len(f), _ptr(x), _ptr(cost), _ptr(jtj), _ptr(jtr))
+    return float(cost[0]), jtj.reshape(6, 6), jtr, m
 
 
 def lm_normal_eq(factors, x):

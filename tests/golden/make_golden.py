@@ -104,8 +104,19 @@ def depth_case():
                 n_front=np.int32(len(u.cloud(0))), dnsp=u.cloud(1), bucket_count=bc, queries=q, depth=u.query(q))
 
 
+def vo_case():
+    """visual-odometry LM (visual_odometry.cpp:304-509) on a synthetic frame pair"""
+    from vo_problems import make_problem
+    F, xt = make_problem(np.random.default_rng(5))
+    x0 = np.zeros(6)
+    x, st = O.vo_solve(F, x0, 100)
+    return dict(factors=F, x0=x0, x_true=xt, x=x, max_iter=np.int32(100),
+                stats=np.array([st.iterations, st.successful, st.invalid, st.termination]),
+                costs=np.array([st.initial_cost, st.final_cost]))
+
+
 CASES = dict(knn=knn_case, voxel=voxel_case, lm=lm_case, scanreg=scanreg_case, mapping=mapping_case,
-             depth=depth_case)
+             depth=depth_case, vo=vo_case)
 
 
 def main():

@@ -39,6 +39,7 @@ struct LmState {
   int status, iteration, reuse_diag, consec_invalid;
   int term, successful, invalid, max_iter;
   int passes;  // evaluation passes consumed (iteration 0 + candidates)
+  int euclid;  // 1: x[0..5] = (angle-axis, t) with plain x + delta (the VO problem), x[6] = 0
 };
 
 __host__ __device__ inline int ut_index(int r, int c) {  // r <= c, upper triangle of 6x6
@@ -71,6 +72,7 @@ __host__ __device__ inline void lm_init(LmState& S, const double* x7, int max_it
   S.invalid = 0;
   S.max_iter = max_iter;
   S.passes = 0;
+  S.euclid = 0;
 }
 
 // one residual block at X: accumulates rho' J^T J, rho' J^T r, 1/2 rho, rows.  The library
@@ -158,8 +160,13 @@ __device__ inline void lm_accum(int type, float px, float py, float pz, double a
   }
 }
 
-// EigenQuaternionParameterization::Plus + Euclidean t
-__host__ __device__ inline void lm_plus(const double* x, const double* d, double* out) {
+// EigenQuaternionParameterization::Plus + Euclidean t; euclid: x + d on all 6 parameters
+__host__ __device__ inline void lm_plus(const double* x, const double* d, double* out, int euclid = 0) {
+  if (euclid) {
+    for (int i = 0; i < 6; ++i) out[i] = x[i] + d[i];
+    out[6] = x[6];
+    return;
+  }
   double nd = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
   if (nd > 0.0) {
     double sn, cs;
@@ -186,7 +193,12 @@ __host__ __device__ inline void lm_plus(const double* x, const double* d, double
 // gmax <= gradient_tolerance (1e-10): the translation terms are computed exactly as in the
 // full expression, so when one of them already exceeds the tolerance the rotation terms
 // (two transcendentals) cannot change the outcome and are skipped.
-__host__ __device__ inline double lm_gradmax(const double* x, const double* g) {
+__host__ __device__ inline double lm_gradmax(const double* x, const double* g, int euclid = 0) {
+  if (euclid) {
+    double m = 0.0;
+    for (int c = 0; c < 6; ++c) m = fmax(m, fabs(x[c] - (x[c] + -g[c])));
+    return m;
+  }
   double mt = 0.0;
   for (int c = 0; c < 3; ++c) mt = fmax(mt, fabs(x[4 + c] - (x[4 + c] + -g[3 + c])));
   if (mt > 1e-10) return mt;
@@ -275,7 +287,7 @@ __host__ __device__ inline void lm_step(LmState& S, const double* red) {
       return;
     }
     for (int i = 0; i < 6; ++i) S.scaling[i] = 1.0 / (1.0 + sqrt(S.jtj[ut_index(i, i)]));
-    S.gmax = lm_gradmax(S.x, S.g);
+    S.gmax = lm_gradmax(S.x, S.g, S.euclid);
     S.x_norm = lm_norm7(S.x);
     step_ok = true;
   } else {
@@ -293,7 +305,7 @@ __host__ __device__ inline void lm_step(LmState& S, const double* red) {
       for (int i = 0; i < 6; ++i) S.g[i] = red[21 + i];
       S.cost = cand_cost;
       S.x_norm = lm_norm7(S.x);
-      S.gmax = lm_gradmax(S.x, S.g);
+      S.gmax = lm_gradmax(S.x, S.g, S.euclid);
       S.successful++;
       double f = 2.0 * rel - 1.0;
       S.radius = S.radius / fmax(1.0 / 3.0, 1.0 - f * f * f);
@@ -344,7 +356,7 @@ __host__ __device__ inline void lm_step(LmState& S, const double* red) {
     S.consec_invalid = 0;
     double delta[6];
     for (int i = 0; i < 6; ++i) delta[i] = step[i] * S.scaling[i];
-    lm_plus(S.x, delta, S.cand);
+    lm_plus(S.x, delta, S.cand, S.euclid);
     double sn = 0;
     for (int i = 0; i < 7; ++i) sn += (S.x[i] - S.cand[i]) * (S.x[i] - S.cand[i]);
     sn = sqrt(sn);

@@ -134,6 +134,7 @@ SIGNATURES = {
     "loam_depth_query": (c_i32, [vp, c_i32, vp, vp, c_i32, vp]),
     "loam_depth_query_device": (c_i32, [vp, c_i32, vp, vp, c_i32, vp]),
     "loam_depth_ms": (c_d, [vp]),
+    "loam_vo_solve": (c_i32, [c_i32, c_i32, vp, vp, vp, c_i32, vp]),
     "loam_lm_solve": (c_i32, [c_i32, vp, c_i32, vp, c_i32, ctypes.POINTER(LMStats)]),
     "loam_lm_normal_equations": (c_i32, [c_i32, vp, c_i32, vp, vp, vp, vp]),
     "loam_voxel_grid": (c_i32, [c_i32, vp, c_i32, c_f, vp, ctypes.POINTER(c_i32)]),
