@@ -273,6 +273,48 @@ def depth_stage(seed, device, n_frames=64, n_queries=2800, n_az=2000, with_cpu=T
     return e
 
 
+def vo_stage(seed, device, n_problems=256, with_cpu=True):
+    """VO pose solve (VisualOdometry::solveNlsAll, visual_odometry.cpp:304-509; SURVEY.md §8f
+    rank 4): synthetic frame pairs of ~1400 matches (the reference's count, :339), 60% with a
+    LiDAR depth (CostFunctor32) and 40% without (CostFunctor22), HuberLoss, max 100 iterations.
+    One problem alone and n_problems in one launch (wall time incl. the host copies); the oracle
+    (Jet autodiff + Ceres TR-LM restatement) on the same problems as the CPU baseline."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from vo_problems import make_problem
+    from loam_amd import vo
+    rng = np.random.default_rng(seed + 5)
+    probs = [make_problem(rng, n32=840, n22=560, w=rng.normal(0, 0.02, 3), t=(0.02, -0.01, -1.0))[0]
+             for _ in range(n_problems)]
+    vo.solve(probs[:2])  # warm the kernel
+    t0 = time.perf_counter()
+    for k in range(16):
+        _, st1 = vo.solve([probs[k]])
+    one = (time.perf_counter() - t0) / 16
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        _, st = vo.solve(probs)
+    dt = (time.perf_counter() - t0) / reps
+    iters = sum(x.iterations for x in st)
+    e = {"gpu_ms_one_problem": round(1e3 * one, 4), "batched_problems": n_problems,
+         "batched_ms": round(1e3 * dt, 4), "batched_problems_per_s": round(n_problems / dt, 1),
+         "batched_lm_iters_per_s": round(iters / dt, 1), "mean_iterations": round(iters / n_problems, 2),
+         "residual_blocks_per_problem": 1400}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import loam_oracle as O
+        n = min(32, n_problems)
+        ci = 0
+        t0 = time.perf_counter()
+        for F in probs[:n]:
+            _, ost = O.vo_solve(F, np.zeros(6), 100)
+            ci += ost.iterations
+        cdt = time.perf_counter() - t0
+        e.update(cpu_ms_per_problem=round(1e3 * cdt / n, 4), cpu_lm_iters_per_s=round(ci / cdt, 1), cpu_cores=1,
+                 cpu_kind="port", speedup_batched=round((n_problems / dt) / (n / cdt), 2))
+    return e
+
+
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
 
 
@@ -467,6 +509,7 @@ def main():
             stages[name] = e
         if not args.no_depth and world == 1:
             stages["depth_association"] = depth_stage(args.seed, local, with_cpu=not args.no_cpu)
+            stages["vo_solve"] = vo_stage(args.seed, local, with_cpu=not args.no_cpu)
         out["stages"] = stages
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(out["value"] / cpu["value"], 2)
