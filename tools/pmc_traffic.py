@@ -25,7 +25,7 @@ def load(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        name = r["Kernel_Name"].split("(")[0].replace("loam::", "")
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("loam::", "").split("<")[0]
         per[name].append(float(r["Counter_Value"]) * 1024.0)
     return per
 
