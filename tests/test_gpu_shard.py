@@ -80,6 +80,7 @@ def _sequence_body(seq):
             poses.append(m.pose(0))
             stats.append(_stat_tuple(m.stats(0)))
         maps = [m.cubes(0, 0), m.cubes(0, 1)]
+        assert m.debug_counters()[40] == 0  # every rank's LM ended on rank 0's pose bits
         m.close()
         return poses, stats, maps
     return body

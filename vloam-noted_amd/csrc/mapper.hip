@@ -131,6 +131,7 @@ struct MapperDev {
   const struct NnRec* nn_recv;  // [nrank][same]: every rank's candidates (all-gather)
   const int* q_off;      // [B] first query of stream s in nn_send
   float4* nn_xyz;        // [5][B][2*max_in] merged neighbours (k_geom input in sharded mode)
+  double* pose_x;        // [nrank][B][8] every rank's optimised pose (agreement check)
   double* lm_red;        // [B][LM_NACC] this rank's normal-equation sums, then the all-reduced
 };
 
@@ -655,6 +656,23 @@ __global__ void __launch_bounds__(LM_THREADS) k_lm_round(MapperDev D, int round,
   J.err_code = MAP_ERR_LM_SYNC;
   J.prof = D.dbg + 17;
   lm_round_device<LM_THREADS>(J, g, G);
+}
+
+// sharded: every rank stores points with the same pose, so after the LM every rank adopts
+// rank 0's (they are equal when the all-reduce is bit-identical on every rank, as RCCL's and
+// the Python transports are); a rank that differed counts it in debug counter 40
+__global__ void k_pose_publish(MapperDev D) {
+  const int s = D.s0 + blockIdx.x, i = threadIdx.x;
+  if (i < 7) D.pose_x[((size_t)D.rank * D.B + s) * 8 + i] = D.fr[s].pose[i];
+}
+__global__ void k_pose_adopt(MapperDev D) {
+  const int s = D.s0 + blockIdx.x, i = threadIdx.x;
+  StreamFrame& F = D.fr[s];
+  if (i < 7) {
+    const double v = D.pose_x[(size_t)s * 8 + i];  // rank 0's slot
+    if (__double_as_longlong(v) != __double_as_longlong(F.pose[i])) atomicAdd(&D.dbg[40], 1ull);
+    F.pose[i] = v;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1424,6 +1442,7 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     D.nn_recv = recv;
     ALLOC(D.nn_xyz, 5 * nq);
     ALLOC(D.lm_red, B * (size_t)LM_NACC);
+    ALLOC(D.pose_x, (size_t)D.nrank * B * 8);
     ALLOC(h->d_q_off, B + 1);
     D.q_off = h->d_q_off;
     if (!h->q_off.assign(B + 1, 0)) return fail(LOAM_ERR_HIP);
@@ -1749,6 +1768,11 @@ int32_t loam_mapper_solve(loam_mapper* h) {
       }
       LOAM_HIP(after(g, 4 + 3 * round, sg));
     }
+  }
+  if (D.sharded) {  // pose agreement across ranks before anything is stored (k_pose_adopt)
+    LAUNCH(FAM_OTHER, k_pose_publish<<<B, 64, 0, st>>>(D));
+    TRY(comm_allgather(h->comm, D.pose_x + (size_t)D.rank * B * 8, D.pose_x, (int64_t)B * 8 * sizeof(double), st));
+    LAUNCH(FAM_OTHER, k_pose_adopt<<<B, 64, 0, st>>>(D));
   }
   LOAM_HIP(hipEventRecord(h->ev[2], st));
   for (int g = 0; g < NG; ++g) {
