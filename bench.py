@@ -315,6 +315,51 @@ def vo_stage(seed, device, n_problems=256, with_cpu=True):
     return e
 
 
+def pipeline_stage(seed, device, n_frames=160, timed=80, n_az=2000):
+    """the whole LOAM chain on one stream, frame after frame (scanRegistrationIO ->
+    laserOdometryIO -> laserMappingIO, lidar_odometry_mapping.cpp:40-176): raw scan in host
+    memory -> features -> odometry -> mapping, all device-resident between stages.  'sequential'
+    copies each scan from pageable memory when its frame starts; 'overlapped' queues the next
+    scan's copy + scan registration (pinned ingest buffer, loam_scanreg_input_async) before the
+    current frame's mapping solve.  Wall time over the last `timed` frames."""
+    from loam_amd import synth
+    from loam_amd.mapping import BatchMapper
+    from loam_amd.odometry import BatchOdometry
+    from loam_amd.scanreg import ScanRegistration
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4)) as ex:
+        scans = list(ex.map(lambda f: synth.frame(seed + 31, f, n_az)[0], range(n_frames)))
+    # pcl::PointXYZ layout (x, y, z, pad): 16 B per point like the reference's input cloud
+    scans = [np.ascontiguousarray(np.concatenate([c, np.zeros((len(c), 1), np.float32)], axis=1)) for c in scans]
+    out = {}
+    for mode in ("sequential", "overlapped"):
+        sr, od, mp = ScanRegistration(device=device), BatchOdometry(1, device=device), BatchMapper(1, device=device)
+        t0 = None
+        if mode == "overlapped":
+            sr.input_async(scans[0])
+        for f in range(n_frames):
+            if f == n_frames - timed:
+                t0 = time.perf_counter()
+            if mode == "sequential":
+                sr.input(scans[f])
+            else:
+                sr.wait()
+            ptrs, counts = zip(*(sr.device_ptr(w) for w in (1, 2, 3, 4)))
+            od.input_device(0, ptrs, counts)
+            od.solve()
+            q, t, _, _, _ = od.output(0)
+            (pc, nc), (ps, ns) = od.last_cloud_device(0, 0), od.last_cloud_device(0, 1)
+            mp.input_device(0, pc, nc, ps, ns, q, t)
+            if mode == "overlapped" and f + 1 < n_frames:
+                sr.input_async(scans[f + 1])
+            mp.solve()
+        dt = time.perf_counter() - t0
+        out[mode] = {"ms_per_frame": round(1e3 * dt / timed, 4), "frames_per_s": round(timed / dt, 1)}
+        for h in (sr, od, mp):
+            h.close()
+    out["frames"] = f"{timed} timed after {n_frames - timed}, {n_az} azimuths x 64 rings, one stream"
+    return out
+
+
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
 
 
@@ -510,6 +555,7 @@ def main():
         if not args.no_depth and world == 1:
             stages["depth_association"] = depth_stage(args.seed, local, with_cpu=not args.no_cpu)
             stages["vo_solve"] = vo_stage(args.seed, local, with_cpu=not args.no_cpu)
+            stages["pipeline_one_stream"] = pipeline_stage(args.seed, local)
         out["stages"] = stages
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(out["value"] / cpu["value"], 2)

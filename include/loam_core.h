@@ -91,6 +91,17 @@ int32_t loam_scanreg_destroy(loam_scanreg* h);
  * point (x, y, z first), host or device memory */
 int32_t loam_scanreg_input(loam_scanreg* h, const float* xyz, int32_t n, int32_t stride);
 int32_t loam_scanreg_input_device(loam_scanreg* h, const float* d_xyz, int32_t n, int32_t stride);
+/* ingest (the PointCloud2 -> pcl conversion of vloam_main_node.cpp:160):
+ * a page-locked host buffer of cap_points x 4 floats owned by the handle.  A PointCloud2's
+ * data can be written there directly; its point_step / 4 is the stride. */
+int32_t loam_scanreg_host_buffer(loam_scanreg* h, float** ptr, int32_t* cap_points);
+/* loam_scanreg_input without waiting: the H2D copy and the kernels are queued on the handle's
+ * stream and overlap whatever the caller does next (e.g. the previous frame's
+ * loam_mapper_solve).  Host memory must stay untouched until loam_scanreg_wait.  The copy is
+ * asynchronous only from loam_scanreg_host_buffer memory; every other loam_scanreg_* call
+ * waits first. */
+int32_t loam_scanreg_input_async(loam_scanreg* h, const float* xyz, int32_t n, int32_t stride);
+int32_t loam_scanreg_wait(loam_scanreg* h);
 /* ScanRegistration::output (scan_registration.cpp:566-577): which = 0 laserCloud,
  * 1 cornerPointsSharp, 2 cornerPointsLessSharp, 3 surfPointsFlat, 4 surfPointsLessFlat */
 int32_t loam_scanreg_counts(loam_scanreg* h, int32_t* counts5);

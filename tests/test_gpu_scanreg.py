@@ -90,3 +90,28 @@ def test_scanreg_small_and_empty():
     gpu.input(xyz)
     for a, b in zip(gpu.output(), ref.output()):
         _same_points(a, b, _ori_span(xyz))
+
+
+def test_async_pinned_ingest_and_overlap():
+    """loam_scanreg_input_async from the pinned buffer, overlapped with a
+    mapper solve of the previous frame: the same features as the synchronous path"""
+    from loam_amd.mapping import BatchMapper
+    from loam_amd.scanreg import ScanRegistration
+    frames = [synth.frame(4, f, 1000)[0] for f in range(4)]
+    ref = ScanRegistration()
+    want = []
+    for xyz in frames:
+        ref.input(xyz)
+        want.append([ref.cloud(w) for w in range(5)])
+    sr = ScanRegistration()
+    m = BatchMapper(1)
+    sr.input_async(frames[0])
+    for f in range(len(frames)):
+        got = [sr.cloud(w) for w in range(5)]  # waits for the frame
+        for a, b in zip(got, want[f]):
+            assert np.array_equal(a, b)
+        m.input(0, got[2], got[4], np.array([0, 0, 0, 1.0]), np.zeros(3))
+        if f + 1 < len(frames):
+            sr.input_async(frames[f + 1])  # next frame's copy + kernels overlap this solve
+        m.solve()
+    sr.wait()

@@ -575,6 +575,11 @@ struct loam_scanreg {
   SrDev D{};
   SrFrame hf{};
   float* d_in = nullptr;
+  float* h_pinned = nullptr;  // loam_scanreg_host_buffer: page-locked ingest buffer (cap x 4 floats)
+  SrFrame* hf_pinned = nullptr;  // D2H target of the frame record (page-locked: the copy stays async)
+  int pending = 0;            // loam_scanreg_input_async launched, loam_scanreg_wait not yet called
+  int pending_stride = 4;
+  const float* pending_xyz = nullptr;
   std::vector<void*> allocs;
   float ms = 0.f;
 };
@@ -592,6 +597,9 @@ int32_t sralloc(loam_scanreg* h, T** p, size_t n) {
   return LOAM_OK;
 }
 void sr_free(loam_scanreg* h) {
+  if (h->st) (void)hipStreamSynchronize(h->st);  // an input_async still in flight
+  if (h->h_pinned) (void)hipHostFree(h->h_pinned);
+  if (h->hf_pinned) (void)hipHostFree(h->hf_pinned);
   for (void* p : h->allocs) (void)hipFree(p);
   h->allocs.clear();
   for (auto& e : h->ev)
@@ -664,7 +672,11 @@ int32_t loam_scanreg_destroy(loam_scanreg* h) {
   return LOAM_OK;
 }
 
-static int32_t sr_run(loam_scanreg* h, const float* xyz, int32_t n, int32_t stride, bool on_device) {
+static int32_t sr_finish(loam_scanreg* h);
+
+// enqueue one frame (H2D when host memory, then every kernel and the D2H of the frame
+// record) on the handle's stream; sr_finish waits for it
+static int32_t sr_launch(loam_scanreg* h, const float* xyz, int32_t n, int32_t stride, bool on_device) {
   if (!h || n < 0 || (n > 0 && !xyz) || stride < 3) {
     set_error("loam_scanreg_input: bad arguments");
     return LOAM_ERR_ARG;
@@ -708,17 +720,36 @@ static int32_t sr_run(loam_scanreg* h, const float* xyz, int32_t n, int32_t stri
     LOAM_HIP(hipGetLastError());
   }
   LOAM_HIP(hipEventRecord(h->ev[1], st));
-  LOAM_HIP(hipMemcpyAsync(&h->hf, D.fr, sizeof(SrFrame), hipMemcpyDeviceToHost, st));
-  LOAM_HIP(hipStreamSynchronize(st));
+  if (!h->hf_pinned)
+    LOAM_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->hf_pinned), sizeof(SrFrame), hipHostMallocDefault));
+  LOAM_HIP(hipMemcpyAsync(h->hf_pinned, D.fr, sizeof(SrFrame), hipMemcpyDeviceToHost, st));
+  h->pending = 1;
+  h->pending_xyz = D.xyz;
+  h->pending_stride = stride;
+  return LOAM_OK;
+}
+
+static int32_t sr_finish(loam_scanreg* h) {
+  if (!h->pending) return LOAM_OK;
+  h->pending = 0;
+  LOAM_HIP(hipSetDevice(h->dev));
+  LOAM_HIP(hipStreamSynchronize(h->st));
+  h->hf = *h->hf_pinned;
   LOAM_HIP(hipEventElapsedTime(&h->ms, h->ev[0], h->ev[1]));
-  h->D.xyz = D.xyz;
-  h->D.stride = stride;
+  h->D.xyz = h->pending_xyz;
+  h->D.stride = h->pending_stride;
   if (h->hf.err) {
     set_error("loam_scanreg_input: ring or sector larger than the LDS capacity (err " +
               std::to_string(h->hf.err) + ")");
     return LOAM_ERR_CAPACITY;
   }
   return LOAM_OK;
+}
+
+static int32_t sr_run(loam_scanreg* h, const float* xyz, int32_t n, int32_t stride, bool on_device) {
+  if (h && h->pending) TRY(sr_finish(h));
+  TRY(sr_launch(h, xyz, n, stride, on_device));
+  return sr_finish(h);
 }
 
 int32_t loam_scanreg_input(loam_scanreg* h, const float* xyz, int32_t n, int32_t stride) {
@@ -729,14 +760,38 @@ int32_t loam_scanreg_input_device(loam_scanreg* h, const float* d_xyz, int32_t n
   return sr_run(h, d_xyz, n, stride, true);
 }
 
+int32_t loam_scanreg_host_buffer(loam_scanreg* h, float** ptr, int32_t* cap_points) {
+  if (!h || !ptr) return LOAM_ERR_ARG;
+  if (!h->h_pinned) {
+    LOAM_HIP(hipSetDevice(h->dev));
+    LOAM_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->h_pinned), sizeof(float) * 4 * (size_t)h->D.cap,
+                           hipHostMallocDefault));
+  }
+  *ptr = h->h_pinned;
+  if (cap_points) *cap_points = h->D.cap;
+  return LOAM_OK;
+}
+
+int32_t loam_scanreg_input_async(loam_scanreg* h, const float* xyz, int32_t n, int32_t stride) {
+  if (h && h->pending) TRY(sr_finish(h));
+  return sr_launch(h, xyz, n, stride, false);
+}
+
+int32_t loam_scanreg_wait(loam_scanreg* h) {
+  if (!h) return LOAM_ERR_ARG;
+  return sr_finish(h);
+}
+
 int32_t loam_scanreg_counts(loam_scanreg* h, int32_t* counts) {
   if (!h || !counts) return LOAM_ERR_ARG;
+  TRY(sr_finish(h));  // an input_async in flight completes first
   for (int k = 0; k < 5; ++k) counts[k] = h->hf.n_in > 0 ? h->hf.out_n[k] : 0;
   return LOAM_OK;
 }
 
 int32_t loam_scanreg_copy(loam_scanreg* h, int32_t which, float* out, int32_t cap) {
   if (!h || which < 0 || which > 4 || (cap > 0 && !out)) return LOAM_ERR_ARG;
+  TRY(sr_finish(h));  // an input_async in flight completes first
   LOAM_HIP(hipSetDevice(h->dev));
   const int n = h->hf.n_in > 0 ? h->hf.out_n[which] : 0;
   if (n > cap) {
@@ -749,12 +804,14 @@ int32_t loam_scanreg_copy(loam_scanreg* h, int32_t which, float* out, int32_t ca
 
 int32_t loam_scanreg_device_ptr(loam_scanreg* h, int32_t which, const float** ptr) {
   if (!h || which < 0 || which > 4 || !ptr) return LOAM_ERR_ARG;
+  TRY(sr_finish(h));  // an input_async in flight completes first
   *ptr = reinterpret_cast<const float*>(h->D.out[which]);
   return h->hf.n_in > 0 ? h->hf.out_n[which] : 0;
 }
 
 int32_t loam_scanreg_curvature(loam_scanreg* h, float* curv, int32_t* label, int32_t cap) {
   if (!h || (cap > 0 && (!curv || !label))) return LOAM_ERR_ARG;
+  TRY(sr_finish(h));  // an input_async in flight completes first
   LOAM_HIP(hipSetDevice(h->dev));
   const int n = h->hf.n_in > 0 ? h->hf.n_cloud : 0;
   if (n > cap) return LOAM_ERR_CAPACITY;

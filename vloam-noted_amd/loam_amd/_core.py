@@ -75,6 +75,9 @@ SIGNATURES = {
     "loam_scanreg_destroy": (c_i32, [vp]),
     "loam_scanreg_input": (c_i32, [vp, vp, c_i32, c_i32]),
     "loam_scanreg_input_device": (c_i32, [vp, vp, c_i32, c_i32]),
+    "loam_scanreg_host_buffer": (c_i32, [vp, ctypes.POINTER(vp), ctypes.POINTER(c_i32)]),
+    "loam_scanreg_input_async": (c_i32, [vp, vp, c_i32, c_i32]),
+    "loam_scanreg_wait": (c_i32, [vp]),
     "loam_scanreg_counts": (c_i32, [vp, vp]),
     "loam_scanreg_copy": (c_i32, [vp, c_i32, vp, c_i32]),
     "loam_scanreg_device_ptr": (c_i32, [vp, c_i32, ctypes.POINTER(vp)]),

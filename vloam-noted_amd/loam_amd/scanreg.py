@@ -47,6 +47,32 @@ class ScanRegistration:
     def input_device(self, d_ptr, n, stride):
         check(lib().loam_scanreg_input_device(self.h, d_ptr, n, stride))
 
+    def host_buffer(self):
+        """the handle's page-locked ingest buffer as a (cap, 4) float32 array (write a frame
+        there, then input_async(n=...) copies from it without staging)"""
+        p = ctypes.c_void_p()
+        cap = ctypes.c_int32()
+        check(lib().loam_scanreg_host_buffer(self.h, ctypes.byref(p), ctypes.byref(cap)))
+        buf = (ctypes.c_float * (4 * cap.value)).from_address(p.value)
+        return np.ctypeslib.as_array(buf).reshape(cap.value, 4)
+
+    def input_async(self, cloud=None, n=None):
+        """queue one frame (cloud is copied into the pinned buffer first; or n points already
+        written there by the caller) and return; wait() or any accessor completes it"""
+        check(lib().loam_scanreg_wait(self.h))  # the buffer is free once the last frame is done
+        buf = self.host_buffer()
+        if cloud is not None:
+            c = np.asarray(cloud, dtype=np.float32)
+            n = len(c)
+            if c.shape[1] == 4:
+                buf[:n] = c  # one contiguous copy
+            else:
+                buf[:n, :3] = c[:, :3]
+        check(lib().loam_scanreg_input_async(self.h, buf.ctypes.data, int(n), 4))
+
+    def wait(self):
+        check(lib().loam_scanreg_wait(self.h))
+
     def counts(self):
         c = np.zeros(5, dtype=np.int32)
         check(lib().loam_scanreg_counts(self.h, ptr(c)))
