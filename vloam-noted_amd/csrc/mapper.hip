@@ -52,6 +52,7 @@ constexpr int MAP_ERR_SUBMAP = 4, MAP_ERR_EXTRA = 8, MAP_ERR_HASH = 16, MAP_ERR_
 struct StreamFrame {
   double pose[7];  // in: initial guess (transformAssociateToMap); out: optimised pose
   int active;
+  uint32_t epoch;  // frame counter of the handle (marks the cubes outside the window touched this frame)
   int nc_in, ns_in;
   int nc_stack, ns_stack;
   int sub_n[2];
@@ -701,7 +702,7 @@ __global__ void k_insert(MapperDev D) {
                              ck >= F.center[2] - 1 && ck <= F.center[2] + 1;
       if (!in_window) {
         uint32_t* fl = D.extra_flag + sm_index(s, m) * NCUBE + tag;
-        if (atomicExch(fl, D.epoch) != D.epoch) {
+        if (atomicExch(fl, F.epoch) != F.epoch) {
           int e = atomicAdd(&F.extra_n[m], 1);
           if (e < EXTRA_CAP) F.extra_list[m][e] = tag;
           else atomicOr(&F.err, MAP_ERR_EXTRA);
@@ -1195,6 +1196,10 @@ struct loam_mapper {
   loam_comm* comm = nullptr;  // sharded mode (loam_mapper_create_sharded)
   PinnedArray<int> q_off;     // [B + 1] query offsets of the sharded kNN exchange
   int* d_q_off = nullptr;
+  // hipGraph of the whole per-frame sequence (default for <= 4 streams; LOAM_MAPPER_GRAPH): one per cube-table parity,
+  // used for frames without recentering, profiling, groups or sharding
+  int use_graph = 0;
+  hipGraphExec_t gexec[2] = {nullptr, nullptr};
   // publish-side buffers (grown on demand)
   uint32_t* d_map_off = nullptr;  // [2 * NCUBE + 1]
   float4* d_pub = nullptr;
@@ -1228,6 +1233,8 @@ void free_all(loam_mapper* h) {
   if (h->d_pub) (void)hipFree(h->d_pub);
   h->d_pub = nullptr;
   h->pub_cap = 0;
+  for (auto& g : h->gexec)
+    if (g) (void)hipGraphExecDestroy(g);
   for (auto& e : h->ev_pool) (void)hipEventDestroy(e);
   h->ev_pool.clear();
   for (auto& e : h->ev)
@@ -1379,6 +1386,10 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     }
     const char* senv = std::getenv("LOAM_MAPPER_STAGGER");
     h->stagger = (senv && senv[0] == '1') ? 1 : 0;
+    // graphs pay off where launch gaps are the cost (B = 1: 0.750 -> 0.733 ms per frame); with
+    // two handles of 64 streams, graph launches measured 20% slower (375k vs 470k iterations/s)
+    const char* genv2 = std::getenv("LOAM_MAPPER_GRAPH");
+    h->use_graph = genv2 ? (genv2[0] == '1' ? 1 : 0) : (n_streams <= 4 ? 1 : 0);
     const char* oenv = std::getenv("LOAM_KNN_ORDER");
     D.knn_order = (oenv && oenv[0] == '1') ? 1 : 0;
     // 2 lanes per query when few streams leave the chip idle (B = 1: 0.254 -> 0.190 ms of
@@ -1661,6 +1672,7 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   if (!any) return LOAM_OK;
   h->frame_counter++;
   D.epoch = h->frame_counter;
+  for (int s = 0; s < B; ++s) h->hf[s].epoch = h->frame_counter;
   std::vector<uint32_t> tail0(2 * B);
   for (int s = 0; s < B; ++s) {
     tail0[2 * s] = h->hf[s].arena_tail[0];
@@ -1669,6 +1681,48 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   }
   D.cube_tab = h->cube_tab[h->parity];
   hipStream_t st = h->st;
+  const bool graph = h->use_graph && !h->prof && !any_shift && h->groups == 1 && !D.rv_split && !D.sharded &&
+                     h->lm_G > 0;
+  if (graph) {
+    // the frame's whole sequence as one graph launch: records H2D, stack VoxelGrid (forked
+    // stream) beside the submap prep, 2 x (kNN, geometry, LM round), insertion, re-VoxelGrid,
+    // records D2H.  Every kernel argument is fixed per (handle, parity): the frame's values
+    // travel in the stream records.
+    hipGraphExec_t& ge = h->gexec[h->parity];
+    if (!ge) {
+      hipStream_t s2 = h->st2;
+      hipGraph_t gr = nullptr;
+      LOAM_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+      LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(StreamFrame) * B, hipMemcpyHostToDevice, st));
+      LOAM_HIP(hipEventRecord(h->ev_fork, st));
+      LOAM_HIP(hipStreamWaitEvent(s2, h->ev_fork, 0));
+      k_stack_ds<<<B * 2, VX_THREADS, 0, s2>>>(D);
+      LOAM_HIP(hipEventRecord(h->ev_join, s2));
+      k_submap_prep<<<B, 128, 0, st>>>(D);
+      LOAM_HIP(hipStreamWaitEvent(st, h->ev_join, 0));
+      for (int round = 0; round < 2; ++round) {
+        if (h->knn_lanes == 2) k_knn<2><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
+        else if (h->knn_lanes == 4) k_knn<4><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
+        else if (h->knn_lanes == 8) k_knn<8><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
+        else k_knn<1><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
+        k_geom<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
+        k_lm_round<<<B * h->lm_G, LM_THREADS, 0, st>>>(D, round, h->lm_G);
+      }
+      k_insert<<<dim3(16, B), 256, 0, st>>>(D);
+      k_bucket<<<B * 2, VX_THREADS, 0, st>>>(D);
+      k_revox<<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D);
+      LOAM_HIP(hipMemcpyAsync(h->hf.data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
+      LOAM_HIP(hipStreamEndCapture(st, &gr));
+      const hipError_t ie = hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(gr);
+      LOAM_HIP(ie);
+    }
+    LOAM_HIP(hipEventRecord(h->ev[0], st));
+    LOAM_HIP(hipGraphLaunch(ge, st));
+    LOAM_HIP(hipEventRecord(h->ev[3], st));
+    LOAM_HIP(hipStreamSynchronize(st));
+  }
+  if (!graph) {
   LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(StreamFrame) * B, hipMemcpyHostToDevice, st));
   LOAM_HIP(hipEventRecord(h->ev[0], st));
   // The streams run in h->groups groups, each on its own HIP streams (gst[g], and gst2[g] for
@@ -1807,9 +1861,11 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   LOAM_HIP(hipEventRecord(h->ev[3], st));
   LOAM_HIP(hipMemcpyAsync(h->hf.data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
   LOAM_HIP(hipStreamSynchronize(st));
+  }  // !graph
   float ms_total = 0, ms_opt = 0;
   LOAM_HIP(hipEventElapsedTime(&ms_total, h->ev[0], h->ev[3]));
-  LOAM_HIP(hipEventElapsedTime(&ms_opt, h->ev[1], h->ev[2]));
+  if (graph) ms_opt = ms_total;  // no event inside the graph (the optimisation block is most of it)
+  else LOAM_HIP(hipEventElapsedTime(&ms_opt, h->ev[1], h->ev[2]));
   if (h->prof) {
     for (size_t k = 0; k < h->ev_fam.size(); ++k) {
       float ms = 0;
@@ -2052,6 +2108,8 @@ static int32_t pub_reserve(loam_mapper* h, size_t n) {
   if (h->d_pub) (void)hipFree(h->d_pub);
   h->d_pub = nullptr;
   h->pub_cap = 0;
+  for (auto& g : h->gexec)
+    if (g) (void)hipGraphExecDestroy(g);
   LOAM_HIP(hipMalloc(&h->d_pub, sizeof(float4) * std::max<size_t>(n, 1)));
   h->pub_cap = n;
   return LOAM_OK;
