@@ -181,3 +181,21 @@ def test_publish_outputs(seq):
     reg = m.register_cloud(0, cloud)
     assert np.array_equal(reg, _to_map_np(m.pose(0), cloud))
     assert len(m.register_cloud(0, np.zeros((0, 4), np.float32))) == 0
+
+
+def test_stack_split_option_bit_exact(monkeypatch):
+    """LOAM_STACK_SPLIT=1 (the stack VoxelGrid cut into voxel-row ranges): the same stacks"""
+    import loam_oracle as O
+    monkeypatch.setenv("LOAM_STACK_SPLIT", "1")
+    rng = np.random.default_rng(3)
+    n = 30000
+    xyz = np.c_[rng.uniform(-60, 60, (n, 2)), rng.normal(-1.7, 0.3, n)]
+    c = np.c_[xyz, rng.uniform(0, 64, n)].astype(np.float32)
+    m = BatchMapper(2)
+    for s in range(2):
+        m.input(s, c[: n // (s + 1)], c, np.array([0, 0, 0, 1.0]), np.zeros(3))
+    m.solve()
+    for s in range(2):
+        for which, (cl, leaf) in enumerate([(c[: n // (s + 1)], 0.4), (c, 0.8)]):
+            got, ref = m.stack(s, which), O.voxel_grid(cl, leaf)
+            assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))

@@ -125,6 +125,12 @@ struct MapperDev {
   // sharded mode (loam_mapper_create_sharded): this rank of nrank; map points are stored by
   // the rank owning their 4 m block (comm.h, shard_owner); blk_v: voxels per block edge
   int knn_order = 0;  // corr_block ordering (LOAM_KNN_ORDER)
+  int stack_split = 0;   // k_stack_part / k_stack_gather around k_stack_ds (few streams)
+  uint32_t* part_off;    // [B][2][SP_PARTS + 1]
+  uint32_t* part_cnt;    // [B][2][SP_PARTS]
+  int* part_split;       // [B][2] 1: the cloud was split this frame
+  float4* part_in;       // [B][2][max_in] the cloud ordered by range
+  float4* part_out;      // [B][2][max_in] every range's VoxelGrid output at its input offset
   int rank = 0, nrank = 1, sharded = 0;
   int blk_v[2] = {1, 1};
   uint32_t* wcnt;        // [B][2][WIN_MAX] window cube counts (all-reduced over the ranks)
@@ -183,31 +189,202 @@ __global__ void k_shift_cubes(MapperDev D, const uint2* __restrict__ old_tab, ui
 // ---------------------------------------------------------------------------------------
 // VoxelGrid of the incoming feature clouds -> CornerStack / SurfStack (:492-500)
 // ---------------------------------------------------------------------------------------
+// Split mode (handles of few streams, where one workgroup per cloud leaves the chip idle):
+// k_stack_part cuts a cloud into SP_PARTS contiguous ranges of voxel rows (z, y) of about equal
+// point counts, scattering the points stably (input order kept within a range); k_stack_ds
+// filters every range in its own workgroup; k_stack_gather concatenates the results.  PCL's
+// output order is lexicographic in (z, y, x) voxel index whatever the grid origin, and every
+// voxel lies in one range with its members in input order, so the concatenation is the
+// unsplit VoxelGrid bit for bit.  Clouds below SP_MIN points or with more than SP_ROWCAP rows
+// stay whole (partition 0 filters the input in place).
+constexpr int SP_PARTS = 8;
+constexpr int SP_MIN = 8192;
+constexpr int SP_ROWCAP = 24576;
+
+__global__ void __launch_bounds__(VX_THREADS) k_stack_part(MapperDev D) {
+  __shared__ uint32_t rows[SP_ROWCAP];
+  __shared__ uint32_t ws[VX_WAVES + 1];
+  __shared__ float bbs[VX_WAVES][4];
+  __shared__ int geo[4];
+  __shared__ uint32_t pbase[SP_PARTS];
+  __shared__ uint32_t wcnt[VX_WAVES][SP_PARTS];
+  const int s = D.s0 + (blockIdx.x >> 1), m = blockIdx.x & 1;
+  const StreamFrame& F = D.fr[s];
+  if (!F.active) return;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  const int n = m == 0 ? F.nc_in : F.ns_in;
+  const float4* src = F.in_ptr[m];
+  const size_t sm = sm_index(s, m);
+  uint32_t* po = D.part_off + sm * (SP_PARTS + 1);
+  float4* dst = D.part_in + sm * D.max_in;
+  const float inv = 1.0f / D.leaf[m];
+  // 1. y / z extent -> the (z, y) voxel rows
+  float y0 = 3.402823466e38f, z0 = 3.402823466e38f, y1 = -3.402823466e38f, z1 = -3.402823466e38f;
+  for (int i = tid; i < n; i += VX_THREADS) {
+    const float4 p = src[i];
+    y0 = fminf(y0, p.y); y1 = fmaxf(y1, p.y);
+    z0 = fminf(z0, p.z); z1 = fmaxf(z1, p.z);
+  }
+  y0 = wave_min_f(y0); z0 = wave_min_f(z0); y1 = wave_max_f(y1); z1 = wave_max_f(z1);
+  if (lane == 0) { bbs[wid][0] = y0; bbs[wid][1] = z0; bbs[wid][2] = y1; bbs[wid][3] = z1; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < VX_WAVES; ++w) {
+      y0 = fminf(y0, bbs[w][0]); z0 = fminf(z0, bbs[w][1]); y1 = fmaxf(y1, bbs[w][2]); z1 = fmaxf(z1, bbs[w][3]);
+    }
+    const int jmin = (int)floorf(y0 * inv), jmax = (int)floorf(y1 * inv);
+    const int kmin = (int)floorf(z0 * inv), kmax = (int)floorf(z1 * inv);
+    const long long R = (long long)(kmax - kmin + 1) * (long long)(jmax - jmin + 1);
+    const bool split = n >= SP_MIN && R > 0 && R <= SP_ROWCAP;
+    geo[0] = kmin; geo[1] = jmin; geo[2] = jmax - jmin + 1; geo[3] = split ? (int)R : 0;
+    D.part_split[sm] = split ? 1 : 0;
+    if (!split) {
+      po[0] = 0;
+      for (int p = 1; p <= SP_PARTS; ++p) po[p] = (uint32_t)n;
+    }
+  }
+  __syncthreads();
+  const int R = geo[3];
+  if (R == 0) return;
+  const int kmin = geo[0], jmin = geo[1], Jn = geo[2];
+  auto row_of = [&](const float4& p) { return ((int)floorf(p.z * inv) - kmin) * Jn + ((int)floorf(p.y * inv) - jmin); };
+  // 2. points per row, 3. exclusive prefix -> the range of each row
+  for (int r = tid; r < R; r += VX_THREADS) rows[r] = 0;
+  __syncthreads();
+  for (int i = tid; i < n; i += VX_THREADS) atomicAdd(&rows[row_of(src[i])], 1u);
+  __syncthreads();
+  const int per = (R + VX_THREADS - 1) / VX_THREADS, r0 = tid * per;
+  uint32_t sum = 0;
+  for (int k = 0; k < per; ++k)
+    if (r0 + k < R) sum += rows[r0 + k];
+  uint32_t tot;
+  uint32_t pre = vx_block_scan(sum, ws, &tot);
+  for (int k = 0; k < per; ++k)
+    if (r0 + k < R) {
+      const uint32_t c = rows[r0 + k];
+      rows[r0 + k] = min((uint32_t)(SP_PARTS - 1), (uint32_t)(((unsigned long long)pre * SP_PARTS) / (unsigned)n));
+      pre += c;
+    }
+  if (tid < SP_PARTS) pbase[tid] = 0;
+  __syncthreads();
+  // 4. stable counting sort of the points by range (one pass: counts, then ranks per chunk)
+  for (int i = tid; i < n; i += VX_THREADS) atomicAdd(&pbase[rows[row_of(src[i])]], 1u);
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (int p = 0; p < SP_PARTS; ++p) {
+      const uint32_t c = pbase[p];
+      po[p] = acc;
+      pbase[p] = acc;
+      acc += c;
+    }
+    po[SP_PARTS] = acc;
+  }
+  __syncthreads();
+  for (int c0 = 0; c0 < n; c0 += VX_THREADS) {
+    const int i = c0 + tid;
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+    int pr = -1;
+    if (i < n) {
+      p = src[i];
+      pr = (int)rows[row_of(p)];
+    }
+    for (int k = tid; k < VX_WAVES * SP_PARTS; k += VX_THREADS) (&wcnt[0][0])[k] = 0;
+    __syncthreads();
+    uint32_t rank = 0;
+#pragma unroll
+    for (int q = 0; q < SP_PARTS; ++q) {
+      const uint64_t mk = __ballot(pr == q);
+      if (pr == q) rank = __popcll(mk & lanemask_lt());
+      if (lane == 0) wcnt[wid][q] = __popcll(mk);
+    }
+    __syncthreads();
+    if (tid < SP_PARTS) {
+      uint32_t acc = pbase[tid];
+      for (int w = 0; w < VX_WAVES; ++w) {
+        const uint32_t c = wcnt[w][tid];
+        wcnt[w][tid] = acc;
+        acc += c;
+      }
+      pbase[tid] = acc;
+    }
+    __syncthreads();
+    if (pr >= 0) dst[wcnt[wid][pr] + rank] = p;
+    __syncthreads();
+  }
+}
+
+// grid B * 2 (whole clouds) or B * 2 * SP_PARTS (split mode, D.stack_split)
 __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
-  const int s = D.s0 + (blockIdx.x >> 1), m = blockIdx.x & 1;
+  const int P = D.stack_split ? SP_PARTS : 1;
+  const int b = blockIdx.x / P, part = blockIdx.x % P;
+  const int s = D.s0 + (b >> 1), m = b & 1;
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
+  const size_t sm = sm_index(s, m);
+  const bool split = D.stack_split && D.part_split[sm];
+  if (!split && part > 0) return;
   VoxSeg S;
-  S.src0 = F.in_ptr[m];
-  S.n0 = m == 0 ? F.nc_in : F.ns_in;
   S.src1 = nullptr;
   S.tag1 = nullptr;
   S.n1 = 0;
   S.tag = 0;
   S.leaf = D.leaf[m];
   S.append_only = 0;
-  S.out = D.stack[m] + (size_t)s * D.max_in;
   S.tail = nullptr;
-  S.cap = D.max_in;
   S.res_off = nullptr;
-  S.res_cnt = reinterpret_cast<uint32_t*>(m == 0 ? &F.nc_stack : &F.ns_stack);
-  S.scratch_pts = D.vx_pts + sm_index(s, m) * D.scratch_cap;
-  S.scratch_idx = D.vx_idx + sm_index(s, m) * D.scratch_cap;
   S.scratch_tail = nullptr;
-  S.scratch_cap = D.scratch_cap;
   S.err = &F.err;
+  if (!split) {
+    S.src0 = F.in_ptr[m];
+    S.n0 = m == 0 ? F.nc_in : F.ns_in;
+    S.out = D.stack[m] + (size_t)s * D.max_in;
+    S.cap = D.max_in;
+    S.res_cnt = reinterpret_cast<uint32_t*>(m == 0 ? &F.nc_stack : &F.ns_stack);
+    S.scratch_pts = D.vx_pts + sm * D.scratch_cap;
+    S.scratch_idx = D.vx_idx + sm * D.scratch_cap;
+    S.scratch_cap = D.scratch_cap;
+  } else {  // range `part` of the split cloud, into its own slice of part_out
+    const uint32_t* po = D.part_off + sm * (SP_PARTS + 1);
+    const uint32_t o = po[part];
+    S.src0 = D.part_in + sm * D.max_in + o;
+    S.n0 = (int)(po[part + 1] - o);
+    S.out = D.part_out + sm * D.max_in + o;
+    S.cap = po[part + 1] - o;
+    S.res_cnt = D.part_cnt + sm * SP_PARTS + part;
+    S.scratch_pts = D.vx_pts + sm * D.scratch_cap + o;
+    S.scratch_idx = D.vx_idx + sm * D.scratch_cap + o;
+    S.scratch_cap = S.cap;
+  }
   voxel_segment(S, lds);
+}
+
+// split mode: the ranges' outputs, concatenated in range order, become the stack
+__global__ void __launch_bounds__(VX_THREADS) k_stack_gather(MapperDev D) {
+  __shared__ uint32_t dst_off[SP_PARTS + 1];
+  const int s = D.s0 + (blockIdx.x >> 1), m = blockIdx.x & 1;
+  StreamFrame& F = D.fr[s];
+  const size_t sm = sm_index(s, m);
+  if (!F.active || !D.part_split[sm]) return;
+  const uint32_t* po = D.part_off + sm * (SP_PARTS + 1);
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int p = 0; p < SP_PARTS; ++p) {
+      dst_off[p] = acc;
+      acc += D.part_cnt[sm * SP_PARTS + p];
+    }
+    dst_off[SP_PARTS] = acc;
+    if (m == 0) F.nc_stack = (int)acc;
+    else F.ns_stack = (int)acc;
+  }
+  __syncthreads();
+  float4* out = D.stack[m] + (size_t)s * D.max_in;
+  const float4* in = D.part_out + sm * D.max_in;
+  for (int p = 0; p < SP_PARTS; ++p) {
+    const uint32_t c = dst_off[p + 1] - dst_off[p];
+    for (uint32_t i = threadIdx.x; i < c; i += VX_THREADS) out[dst_off[p] + i] = in[po[p] + i];
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1441,6 +1618,19 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   ALLOC(D.lm_xpub, B * 2 * 8);
   ALLOC(D.tickets, B);
   ALLOC(h->d_map_off, 2 * NCUBE + 1);
+  {
+    // split stack VoxelGrid (LOAM_STACK_SPLIT=1): measured slower, B = 1 0.733 -> 0.789 ms
+    // per frame (the single-workgroup partition pass costs more than the ranges save), B = 128
+    // 480k -> 316k iterations/s; kept as an option, bit-exact (tests/test_gpu_mapping.py)
+    const char* senv2 = std::getenv("LOAM_STACK_SPLIT");
+    D.stack_split = (senv2 && senv2[0] == '1') ? 1 : 0;
+    const size_t np = D.stack_split ? B : 1;
+    ALLOC(D.part_off, np * 2 * (SP_PARTS + 1));
+    ALLOC(D.part_cnt, np * 2 * SP_PARTS);
+    ALLOC(D.part_split, np * 2);
+    ALLOC(D.part_in, D.stack_split ? B * 2 * (size_t)D.max_in : 1);
+    ALLOC(D.part_out, D.stack_split ? B * 2 * (size_t)D.max_in : 1);
+  }
   ALLOC(h->d_pairs, B * 2);
   ALLOC(h->d_new_off, B * 2 * (NCUBE + 1));
   if (D.sharded) {
@@ -1696,7 +1886,9 @@ int32_t loam_mapper_solve(loam_mapper* h) {
       LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(StreamFrame) * B, hipMemcpyHostToDevice, st));
       LOAM_HIP(hipEventRecord(h->ev_fork, st));
       LOAM_HIP(hipStreamWaitEvent(s2, h->ev_fork, 0));
-      k_stack_ds<<<B * 2, VX_THREADS, 0, s2>>>(D);
+      if (D.stack_split) k_stack_part<<<B * 2, VX_THREADS, 0, s2>>>(D);
+      k_stack_ds<<<B * 2 * (D.stack_split ? SP_PARTS : 1), VX_THREADS, 0, s2>>>(D);
+      if (D.stack_split) k_stack_gather<<<B * 2, VX_THREADS, 0, s2>>>(D);
       LOAM_HIP(hipEventRecord(h->ev_join, s2));
       k_submap_prep<<<B, 128, 0, st>>>(D);
       LOAM_HIP(hipStreamWaitEvent(st, h->ev_join, 0));
@@ -1751,7 +1943,9 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     LOAM_HIP(hipEventRecord(h->gfork[g], sg));
     LOAM_HIP(hipStreamWaitEvent(s2, h->gfork[g], 0));
     LOAM_HIP(before(g, 0, s2));
-    LAUNCH_ON(s2, FAM_STACK, k_stack_ds<<<Bg * 2, VX_THREADS, 0, s2>>>(Dg[g]));
+    if (D.stack_split) LAUNCH_ON(s2, FAM_STACK, k_stack_part<<<Bg * 2, VX_THREADS, 0, s2>>>(Dg[g]));
+    LAUNCH_ON(s2, FAM_STACK, k_stack_ds<<<Bg * 2 * (D.stack_split ? SP_PARTS : 1), VX_THREADS, 0, s2>>>(Dg[g]));
+    if (D.stack_split) LAUNCH_ON(s2, FAM_STACK, k_stack_gather<<<Bg * 2, VX_THREADS, 0, s2>>>(Dg[g]));
     LOAM_HIP(after(g, 0, s2));
     LOAM_HIP(hipEventRecord(h->gjoin[g], s2));
   }
