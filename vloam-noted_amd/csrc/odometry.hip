@@ -494,6 +494,9 @@ int32_t loam_odometry_create(const loam_params* p, int32_t device, int32_t n_str
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_od_lm, OD_LM_THREADS, 0) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess)
       h->G = std::min(OD_PBLK, std::min(4, std::min(occ, 1) * cus / n_streams));  // 1 block/CU (256 VGPRs)
+    const char* genv = std::getenv("LOAM_OD_LM_G");  // measurement override (within the residency cap)
+    if (h->G >= 1 && genv && std::atoi(genv) > 0)
+      h->G = std::min(std::min(OD_PBLK, std::min(occ, 1) * cus / n_streams), std::atoi(genv));
     if (h->G < 1) {
       set_error("loam_odometry_create: too many streams for one resident LM launch");
       return fail(LOAM_ERR_CAPACITY);
