@@ -1,0 +1,4 @@
+#!/bin/bash
+cd "$(dirname "$0")/../.."
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_shard_mp.py -m gpu -x -v --timeout 400 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
