@@ -432,7 +432,7 @@ def main():
     if H > 1:
         # every handle's persistent LM grid must be resident at once: G <= CUs / all streams
         cus = torch.cuda.get_device_properties(local).multi_processor_count
-        os.environ["LOAM_LM_G"] = str(max(1, cus // B))
+        os.environ["LOAM_LM_G"] = os.environ.get("BENCH_LM_G") or str(max(1, cus // B))
     mappers = [BatchMapper(Bh, device=local, max_map_points=args.map_points, comm=comm) for _ in range(H)]
     os.environ.pop("LOAM_LM_G", None) if H > 1 else None  # read at create; not for later handles
     mapper = mappers[0]

@@ -5,5 +5,5 @@
 set -e
 cd "$(dirname "$0")/../vloam-noted_amd"
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wall -Wno-unused-function \
-  -Wno-unused-variable -I../include -shared -o "loam_amd/_lib/$1.so" csrc/*.hip
+  -Wno-unused-variable ${EXTRA:-} -I../include -shared -o "loam_amd/_lib/$1.so" csrc/*.hip
 echo "loam_amd/_lib/$1.so"

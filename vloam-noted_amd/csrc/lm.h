@@ -235,10 +235,8 @@ __host__ __device__ inline bool lm_solve_step(LmState& S, double* step) {
     b[i] = S.scaling[i] * S.g[i];
   }
   S.reuse_diag = 1;
-  // Cholesky A = L L^T
-  double L[6][6];
-  for (int i = 0; i < 6; ++i)
-    for (int j = 0; j < 6; ++j) L[i][j] = 0;
+  // Cholesky A = L L^T, L in A's lower triangle (the upper triangle is not read again)
+  double (&L)[6][6] = A;
   for (int j = 0; j < 6; ++j) {
     double s = A[j][j];
     for (int k = 0; k < j; ++k) s -= L[j][k] * L[j][k];
@@ -416,8 +414,8 @@ __device__ inline void lm_eval_sum(const LmRecView& R, int nrec, const double* X
   };
   double Rm[9];
   lm_rotmat(X, Rm);
-  Rec cur[2], nxt[2];
   const int r0 = blk * kThreads + tid;
+  Rec cur[2], nxt[2];
   load(cur, r0);
   for (int r = r0; r < nrec; r += 2 * stride) {
     load(nxt, r + 2 * stride);
