@@ -86,3 +86,30 @@ def test_cxx_shim_compiles_and_links(tmp_path):
     r = subprocess.run([exe, "1" if gpu_available() else "0"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "version" in r.stdout
+
+
+def test_new_entry_points_validate_arguments():
+    """argument checks of the sharding, depth and VO entry points (before any device work)"""
+    L = _core.lib()
+    h = ctypes.c_void_p()
+    assert L.loam_comm_create(0, 2, None, ctypes.byref(h)) == -1       # 2 ranks need callbacks
+    assert L.loam_comm_create(2, 2, None, ctypes.byref(h)) == -1       # rank out of range
+    assert L.loam_comm_create(0, 1, None, ctypes.byref(h)) == 0        # one rank: no callbacks needed
+    assert L.loam_comm_destroy(h) == 0
+    assert L.loam_mapper_create_sharded(None, 0, 1, None, ctypes.byref(h)) == -1
+    xyz = (ctypes.c_float * 3)(1.0, 2.0, 3.0)
+    assert L.loam_shard_owner(xyz, ctypes.c_float(0.4), 0) == -1
+    assert L.loam_shard_owner(xyz, ctypes.c_float(0.0), 2) == -1
+    assert L.loam_shard_owner(xyz, ctypes.c_float(0.4), 1) == 0
+    dp = _core.DepthParams()
+    L.loam_depth_params_default(ctypes.byref(dp))
+    assert (dp.grid, dp.img_width, dp.img_height) == (5, 1242, 375)
+    dp.grid = 0
+    assert L.loam_depth_create(ctypes.byref(dp), 0, 1, ctypes.byref(h)) == -1
+    off = (ctypes.c_int32 * 2)(0, 1)
+    x = (ctypes.c_double * 6)()
+    assert L.loam_vo_solve(0, 1, off, None, x, 100, None) == -1        # records missing
+    assert L.loam_vo_solve(0, 1, off, None, x, 100000, None) == -1     # iteration cap
+    bad = (ctypes.c_int32 * 2)(1, 0)
+    assert L.loam_vo_solve(0, 1, bad, None, x, 100, None) == -1        # offsets must start at 0
+    assert L.loam_vo_solve(0, 0, None, None, None, 100, None) == 0      # nothing to do
