@@ -199,3 +199,29 @@ def test_stack_split_option_bit_exact(monkeypatch):
         for which, (cl, leaf) in enumerate([(c[: n // (s + 1)], 0.4), (c, 0.8)]):
             got, ref = m.stack(s, which), O.voxel_grid(cl, leaf)
             assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_recentering_frame():
+    """a frame whose pose crosses the cube-grid recentering threshold (laser_mapping.cpp:252-444:
+    the grid shifts by one cube, wrapped slabs cleared), teacher-forced from the oracle state:
+    pose, counts, grid centre and the shifted map"""
+    frames = (384, 385, 386, 387, 388)
+    seq = run_sequence(seed=11, n_frames=frames[-1] + 1, n_az=600, snapshot_frames=frames)
+    shifted = [f for f in frames if not np.array_equal(seq[f]["before"]["cen"], seq[f]["after"]["cen"])]
+    assert shifted, "no recentering in the probed frames"
+    rec = seq[shifted[0]]
+    m = BatchMapper(1)
+    load_state(m, 0, rec["before"])
+    m.input(0, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+    m.solve()
+    _check_frame(m, 0, rec)
+    cen, _, _ = m.get_state(0)
+    assert np.array_equal(cen, rec["after"]["cen"])
+    _check_map(m, 0, rec["after"])
+    # and the frame after it, free-running on the device
+    nxt = seq[shifted[0] + 1] if shifted[0] + 1 < len(seq) else None
+    if nxt is not None:
+        m.input(0, nxt["corner"], nxt["surf"], nxt["q_wodom"], nxt["t_wodom"])
+        m.solve()
+        q, t = m.pose(0)
+        assert np.linalg.norm(t - nxt["pose"][1]) < 1e-4 and quat_angle(q, nxt["pose"][0]) < 1e-4
