@@ -172,7 +172,9 @@ __device__ inline void cube_corner(int c, const int* cen, int corner[3]) {
 // ring-buffer recentering (laser_mapping.cpp:252-444): content moves by shift[axis] cube
 // indices, the slabs that wrap around are cleared.
 // ---------------------------------------------------------------------------------------
-__global__ void k_shift_cubes(MapperDev D, const uint2* __restrict__ old_tab, uint2* new_tab) {
+// The fixed-point tokens move with their cubes (into tok_tmp, copied back on the same stream):
+// a token left at the old index would send every moved cube through a full re-filter.
+__global__ void k_shift_cubes(MapperDev D, const uint2* __restrict__ old_tab, uint2* new_tab, uint32_t* tok_tmp) {
   int s = D.s0 + blockIdx.y;
   const StreamFrame& F = D.fr[s];
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < 2 * NCUBE; t += gridDim.x * blockDim.x) {
@@ -180,9 +182,14 @@ __global__ void k_shift_cubes(MapperDev D, const uint2* __restrict__ old_tab, ui
     int i = c % CW, j = (c / CW) % CH, k = c / (CW * CH);
     int oi = i - F.shift[0], oj = j - F.shift[1], ok = k - F.shift[2];
     uint2 v = make_uint2(0, 0);
-    if (oi >= 0 && oi < CW && oj >= 0 && oj < CH && ok >= 0 && ok < CD)
-      v = old_tab[sm_index(s, m) * NCUBE + oi + CW * oj + CW * CH * ok];
+    uint32_t tok = 0;
+    if (oi >= 0 && oi < CW && oj >= 0 && oj < CH && ok >= 0 && ok < CD) {
+      const size_t o = sm_index(s, m) * NCUBE + oi + CW * oj + CW * CH * ok;
+      v = old_tab[o];
+      tok = D.stable_tok[o];
+    }
     new_tab[sm_index(s, m) * NCUBE + c] = v;
+    tok_tmp[sm_index(s, m) * NCUBE + c] = tok;
   }
 }
 
@@ -1360,6 +1367,7 @@ struct loam_mapper {
   uint2* cube_tab[2] = {nullptr, nullptr};
   int parity = 0;
   int* d_pairs = nullptr;
+  uint32_t* tok_tmp = nullptr;  // [B][2][NCUBE] the shifted fixed-point tokens
   uint32_t* d_new_off = nullptr;
   std::vector<void*> allocs;
   uint32_t frame_counter = 0;
@@ -1607,6 +1615,7 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   ALLOC(D.ins_sorted, B * 2 * (size_t)D.max_in);
   ALLOC(D.ins_off, B * 2 * (size_t)(INS_SLOTS + 1));
   ALLOC(D.stable_tok, B * 2 * (size_t)NCUBE);
+  ALLOC(h->tok_tmp, B * 2 * (size_t)NCUBE);
   ALLOC(D.rv_list[0], B * 2 * (size_t)INS_SLOTS);
   ALLOC(D.rv_list[1], B * 2 * (size_t)INS_SLOTS);
   ALLOC(D.rv_count, 2 * MAX_GROUPS);
@@ -1950,9 +1959,13 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     LOAM_HIP(hipEventRecord(h->gjoin[g], s2));
   }
   if (any_shift) {
-    for (int g = 0; g < NG; ++g)
+    for (int g = 0; g < NG; ++g) {
       LAUNCH_ON(h->gst[g], FAM_OTHER, k_shift_cubes<<<dim3(16, Bg), 256, 0, h->gst[g]>>>(
-                                          Dg[g], h->cube_tab[h->parity], h->cube_tab[1 - h->parity]));
+                                          Dg[g], h->cube_tab[h->parity], h->cube_tab[1 - h->parity], h->tok_tmp));
+      const size_t o = (size_t)g * Bg * 2 * NCUBE;
+      LOAM_HIP(hipMemcpyAsync(D.stable_tok + o, h->tok_tmp + o, sizeof(uint32_t) * Bg * 2 * NCUBE,
+                              hipMemcpyDeviceToDevice, h->gst[g]));
+    }
     h->parity ^= 1;
     D.cube_tab = h->cube_tab[h->parity];
     for (int g = 0; g < NG; ++g) Dg[g].cube_tab = D.cube_tab;
