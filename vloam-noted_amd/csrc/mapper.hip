@@ -495,8 +495,11 @@ __device__ inline void corr_block(const MapperDev& D, int* s, int* blk) {
   }
 }
 
+#ifndef KNN_WAVES
+#define KNN_WAVES 7  // 72 VGPRs, 20 B spill outside the cell loop: 6 -> 7 waves, correspondence -8%
+#endif
 template <int L>
-__global__ void __launch_bounds__(CORR_THREADS) k_knn(MapperDev D, int round) {
+__global__ void __launch_bounds__(CORR_THREADS) __attribute__((amdgpu_waves_per_eu(KNN_WAVES, 8))) k_knn(MapperDev D, int round) {
   __shared__ WinMap W[2];
   __shared__ int slot_of[75];  // 5 x 5 x 3 window position -> slot (laserCloudValidInd order)
   int s, blk;
