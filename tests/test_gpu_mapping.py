@@ -225,3 +225,37 @@ def test_recentering_frame():
         m.solve()
         q, t = m.pose(0)
         assert np.linalg.norm(t - nxt["pose"][1]) < 1e-4 and quat_angle(q, nxt["pose"][0]) < 1e-4
+
+
+@pytest.mark.parametrize("n_streams", [1, 8])
+def test_arena_compaction_is_transparent(seq, n_streams):
+    """a small arena compacts several times (queued at the start of the next frame, decided on
+    the device per (stream, map)); poses, statistics and maps stay bit-identical to a mapper
+    whose arena never fills.  One stream runs the graph path (a frame with a compaction due
+    leaves it), eight streams the batched path."""
+    small = dict(max_input_points=32768, max_submap_points=16384, max_map_points=131072)
+    big = dict(max_input_points=32768, max_submap_points=16384)
+    ms, mb = BatchMapper(n_streams, **small), BatchMapper(n_streams, **big)
+    ms.debug_counters(reset=True)
+    for k, rec in enumerate(seq):
+        for m in (ms, mb):
+            for s in range(n_streams):
+                r = seq[(k + s) % len(seq)] if n_streams > 1 else rec
+                m.input(s, r["corner"], r["surf"], r["q_wodom"], r["t_wodom"])
+            m.solve()
+        for s in range(n_streams):
+            (qs, ts), (qb, tb) = ms.pose(s), mb.pose(s)
+            assert np.array_equal(qs, qb) and np.array_equal(ts, tb), (k, s)
+            a, b = ms.stats(s), mb.stats(s)
+            assert (a.corner_map, a.surf_map, list(a.corner_num), list(a.surf_num)) == \
+                (b.corner_map, b.surf_map, list(b.corner_num), list(b.surf_num))
+    assert ms.debug_counters()[41] >= n_streams  # compactions happened
+    assert mb.debug_counters()[41] == 0
+    for s in range(n_streams):
+        for which in range(2):
+            cs, cb = ms.cubes(s, which), mb.cubes(s, which)
+            assert sorted(cs) == sorted(cb)
+            for c in cb:
+                assert np.array_equal(cs[c], cb[c])
+    ms.close()
+    mb.close()

@@ -47,7 +47,7 @@ constexpr int SUBMAP_BLOCKS = 64;
 constexpr int INS_SLOTS = WIN_VALID_MAX + EXTRA_CAP;
 constexpr int MAX_GROUPS = 4;  // stream groups launched on separate HIP streams
 constexpr int MAP_ERR_SUBMAP = 4, MAP_ERR_EXTRA = 8, MAP_ERR_HASH = 16, MAP_ERR_LM_SYNC = 32,
-              MAP_ERR_INDEX = 64;
+              MAP_ERR_INDEX = 64, MAP_ERR_LIVE = 128;
 
 struct StreamFrame {
   double pose[7];  // in: initial guess (transformAssociateToMap); out: optimised pose
@@ -126,6 +126,7 @@ struct MapperDev {
   // the rank owning their 4 m block (comm.h, shard_owner); blk_v: voxels per block edge
   int knn_order = 0;  // corr_block ordering (LOAM_KNN_ORDER)
   int stack_split = 0;   // k_stack_part / k_stack_gather around k_stack_ds (few streams)
+  uint32_t compact_at = 0;  // an arena whose tail passed this is compacted
   uint32_t* part_off;    // [B][2][SP_PARTS + 1]
   uint32_t* part_cnt;    // [B][2][SP_PARTS]
   int* part_split;       // [B][2] 1: the cloud was split this frame
@@ -1179,10 +1180,17 @@ __global__ void __launch_bounds__(VX_THREADS) k_cube_index(MapperDev D, int s, i
 // ---------------------------------------------------------------------------------------
 // arena compaction: live cubes copied, in cube order, into the other arena
 // ---------------------------------------------------------------------------------------
-__global__ void k_compact_scan(MapperDev D, const int* pairs, uint32_t* new_off) {
-  // one workgroup (1024 threads) per (stream, map) pair; pairs[b] = s*2 + m
+// Launched over every (stream, map) pair sm = 2 s0 + b of the handle; a pair whose tail is at
+// or below compact_at exits at once (the decision is taken on the device, from the records)
+__device__ inline bool compact_due(const MapperDev& D, int sm) {
+  return D.fr[sm >> 1].arena_tail[sm & 1] > D.compact_at;
+}
+
+__global__ void k_compact_scan(MapperDev D, uint32_t* new_off) {
+  // one workgroup (1024 threads) per pair
   __shared__ uint32_t ws[VX_WAVES + 1];
-  const int sm = pairs[blockIdx.x];
+  const int sm = 2 * D.s0 + blockIdx.x;
+  if (!compact_due(D, sm)) return;
   const uint2* tab = D.cube_tab + (size_t)sm * NCUBE;
   uint32_t* no = new_off + (size_t)blockIdx.x * (NCUBE + 1);
   constexpr int PER = (NCUBE + VX_THREADS - 1) / VX_THREADS;  // 5
@@ -1205,9 +1213,9 @@ __global__ void k_compact_scan(MapperDev D, const int* pairs, uint32_t* new_off)
   if (threadIdx.x == 0) no[NCUBE] = total;
 }
 
-__global__ void k_compact_copy(MapperDev D, const int* pairs, const uint32_t* new_off) {
-  const int p = blockIdx.y;
-  const int sm = pairs[p];
+__global__ void k_compact_copy(MapperDev D, const uint32_t* new_off) {
+  const int p = blockIdx.y, sm = 2 * D.s0 + p;
+  if (!compact_due(D, sm)) return;
   const int s = sm >> 1, m = sm & 1;
   StreamFrame& F = D.fr[s];
   uint2* tab = D.cube_tab + (size_t)sm * NCUBE;
@@ -1231,10 +1239,12 @@ __global__ void k_compact_copy(MapperDev D, const int* pairs, const uint32_t* ne
   }
 }
 
-__global__ void k_compact_commit(MapperDev D, const int* pairs, int npairs, const uint32_t* new_off) {
-  const int p = blockIdx.x;
-  if (p >= npairs) return;
-  const int sm = pairs[p];
+__global__ void k_compact_commit(MapperDev D, const uint32_t* new_off) {
+  __shared__ int due;
+  const int p = blockIdx.x, sm = 2 * D.s0 + p;
+  if (threadIdx.x == 0) due = compact_due(D, sm);
+  __syncthreads();  // thread 0 moves the tail below
+  if (!due) return;
   const int s = sm >> 1, m = sm & 1;
   StreamFrame& F = D.fr[s];
   uint2* tab = D.cube_tab + (size_t)sm * NCUBE;
@@ -1248,6 +1258,8 @@ __global__ void k_compact_commit(MapperDev D, const int* pairs, int npairs, cons
   if (threadIdx.x == 0) {
     F.arena_tail[m] = no[NCUBE];
     F.arena_active[m] = 1 - F.arena_active[m];
+    if (no[NCUBE] > D.compact_at) atomicOr(&F.err, MAP_ERR_LIVE);  // the live map itself
+    atomicAdd(&D.dbg[41], 1ull);
   }
 }
 
@@ -1369,7 +1381,6 @@ struct loam_mapper {
   std::vector<HostStream> hs;
   uint2* cube_tab[2] = {nullptr, nullptr};
   int parity = 0;
-  int* d_pairs = nullptr;
   uint32_t* tok_tmp = nullptr;  // [B][2][NCUBE] the shifted fixed-point tokens
   uint32_t* d_new_off = nullptr;
   std::vector<void*> allocs;
@@ -1512,6 +1523,7 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   {
     const uint64_t cap = (uint64_t)D.map_cap, margin = (uint64_t)D.sub_cap + 2ull * D.max_in;
     h->compact_at = (uint32_t)std::max<uint64_t>(cap / 2, cap > margin ? cap - margin : 0);
+    D.compact_at = h->compact_at;
   }
   D.max_chunks = LM_EBLK;
   {
@@ -1643,7 +1655,6 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     ALLOC(D.part_in, D.stack_split ? B * 2 * (size_t)D.max_in : 1);
     ALLOC(D.part_out, D.stack_split ? B * 2 * (size_t)D.max_in : 1);
   }
-  ALLOC(h->d_pairs, B * 2);
   ALLOC(h->d_new_off, B * 2 * (NCUBE + 1));
   if (D.sharded) {
     for (int m = 0; m < 2; ++m) D.blk_v[m] = shard_block_voxels(D.leaf[m]);
@@ -1883,7 +1894,10 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   }
   D.cube_tab = h->cube_tab[h->parity];
   hipStream_t st = h->st;
-  const bool graph = h->use_graph && !h->prof && !any_shift && h->groups == 1 && !D.rv_split && !D.sharded &&
+  bool compact_due = false;  // the graph path has no compaction step: such frames run without it
+  for (int s = 0; s < B && !compact_due; ++s)
+    compact_due = h->hf[s].arena_tail[0] > h->compact_at || h->hf[s].arena_tail[1] > h->compact_at;
+  const bool graph = h->use_graph && !h->prof && !any_shift && !compact_due && h->groups == 1 && !D.rv_split && !D.sharded &&
                      h->lm_G > 0;
   if (graph) {
     // the frame's whole sequence as one graph launch: records H2D, stack VoxelGrid (forked
@@ -1929,6 +1943,14 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   if (!graph) {
   LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(StreamFrame) * B, hipMemcpyHostToDevice, st));
   LOAM_HIP(hipEventRecord(h->ev[0], st));
+  // arenas the last frame left past the compaction threshold are compacted here, queued ahead
+  // of this frame (each workgroup checks its own pair's tail), so the host never waits on them
+  if (compact_due) {
+    k_compact_scan<<<B * 2, VX_THREADS, 0, st>>>(D, h->d_new_off);
+    k_compact_copy<<<dim3(128, B * 2), 256, 0, st>>>(D, h->d_new_off);
+    k_compact_commit<<<B * 2, 256, 0, st>>>(D, h->d_new_off);
+    LOAM_HIP(hipGetLastError());
+  }
   // The streams run in h->groups groups, each on its own HIP streams (gst[g], and gst2[g] for
   // the stack VoxelGrid); the launch sequences are issued phase by phase so the groups start
   // together and drift apart as their kernels finish.
@@ -2101,7 +2123,6 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     }
   }
   // host bookkeeping + compaction decisions
-  std::vector<int> pairs;
   int32_t status = LOAM_OK;
   for (int s = 0; s < B; ++s) {
     StreamFrame& F = h->hf[s];
@@ -2136,26 +2157,6 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     if (F.err) {
       set_error("loam_mapper_solve: device capacity exceeded (err flags " + std::to_string(F.err) + ")");
       status = LOAM_ERR_CAPACITY;
-    }
-    for (int m = 0; m < 2; ++m)
-      if (F.arena_tail[m] > h->compact_at) pairs.push_back(s * 2 + m);
-  }
-  if (!pairs.empty()) {
-    const int np = (int)pairs.size();
-    LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(StreamFrame) * B, hipMemcpyHostToDevice, st));
-    LOAM_HIP(hipMemcpyAsync(h->d_pairs, pairs.data(), sizeof(int) * np, hipMemcpyHostToDevice, st));
-    k_compact_scan<<<np, VX_THREADS, 0, st>>>(D, h->d_pairs, h->d_new_off);
-    k_compact_copy<<<dim3(256, np), 256, 0, st>>>(D, h->d_pairs, h->d_new_off);
-    k_compact_commit<<<np, 256, 0, st>>>(D, h->d_pairs, np, h->d_new_off);
-    LOAM_HIP(hipGetLastError());
-    LOAM_HIP(hipMemcpyAsync(h->hf.data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
-    LOAM_HIP(hipStreamSynchronize(st));
-    for (int p : pairs) {
-      const StreamFrame& F = h->hf[p >> 1];
-      if (F.arena_tail[p & 1] > h->compact_at) {
-        set_error("loam_mapper_solve: live map exceeds the compaction threshold of max_map_points");
-        status = LOAM_ERR_CAPACITY;
-      }
     }
   }
   return status;
