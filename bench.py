@@ -430,7 +430,8 @@ def main():
             os.dup2(saved, 1)
             os.close(saved)
     if H > 1:
-        # every handle's persistent LM grid must be resident at once: G <= CUs / all streams
+        # persistent LM grids sized so that every handle's fits at once: G <= CUs / all streams
+        # (speed: 2 beat 4 workgroups per stream; correctness needs no residency, lm.h)
         cus = torch.cuda.get_device_properties(local).multi_processor_count
         os.environ["LOAM_LM_G"] = os.environ.get("BENCH_LM_G") or str(max(1, cus // B))
     mappers = [BatchMapper(Bh, device=local, max_map_points=args.map_points, comm=comm) for _ in range(H)]

@@ -259,3 +259,51 @@ def test_arena_compaction_is_transparent(seq, n_streams):
                 assert np.array_equal(cs[c], cb[c])
     ms.close()
     mb.close()
+
+
+def test_concurrent_handles_share_the_gpu(seq):
+    """two 64-stream handles, each sizing its persistent LM grid for the whole GPU, solve at the
+    same time from two host threads: the LM shares are claimed by whichever workgroups run
+    (lm.h), so neither waits on workgroups the other keeps off the GPU; poses are bit-identical
+    to one handle running alone"""
+    import threading
+    B, n = 64, 6
+    caps = dict(max_input_points=32768, max_submap_points=16384, max_map_points=262144)
+
+    def feed(m, k):
+        for s in range(B):
+            r = seq[(k + s) % len(seq)]
+            m.input(s, r["corner"], r["surf"], r["q_wodom"], r["t_wodom"])
+
+    ref = BatchMapper(B, **caps)
+    want = []
+    for k in range(n):
+        feed(ref, k)
+        ref.solve()
+        want.append([ref.pose(s) for s in range(B)])
+    ref.close()
+    ms = [BatchMapper(B, **caps) for _ in range(2)]
+    got = [[None] * n for _ in ms]
+    errs = []
+
+    def run(i):
+        try:
+            for k in range(n):
+                feed(ms[i], k)
+                ms[i].solve()
+                got[i][k] = [ms[i].pose(s) for s in range(B)]
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs
+    for i in range(2):
+        for k in range(n):
+            for s in range(B):
+                (q, t), (qr, tr) = got[i][k][s], want[k][s]
+                assert np.array_equal(q, qr) and np.array_equal(t, tr), (i, k, s)
+        ms[i].close()

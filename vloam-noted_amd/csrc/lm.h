@@ -497,18 +497,28 @@ __device__ inline bool lm_step_wave(const double* partials, int nblk, LmState& S
 }
 
 // ---------------------------------------------------------------------------------------
-// Persistent LM round: all <= 5 passes of one solve in one launch.  G workgroups evaluate a
-// share of the records each; the leader (g = 0) keeps the trust-region state in its LDS,
-// reduces the workers' partials and runs the step.  Hand-offs follow the agent-scope
+// Persistent LM round: all <= 5 passes of one solve in one launch.  The records are cut into
+// G fixed shares; the partial sums of share c go to part[c] and the leader (g = 0) adds them in
+// share order, so the arithmetic depends on G alone, not on who evaluates a share.  Shares
+// are claimed per pass with an atomic ticket by whichever of the stream's workgroups is
+// running: the leader keeps claiming until every share is taken, then waits only for shares
+// that running workgroups hold.  No workgroup waits for one that may not be resident, so
+// handles sharing the GPU cannot deadlock (the leaders are the first blocks of every grid; a
+// member that starts after the round ended sees DONE and leaves).  The leader keeps the
+// trust-region state in its LDS and runs the step.  Hand-offs follow the agent-scope
 // release/acquire recipe (cdna_hip_programming.md §6 Guideline 16): partials are plain
-// stores + drain + release fence + relaxed ticket; the eval point is published with sc1
-// (atomic) stores + drain + a relaxed flag; consumers poll relaxed and acquire once.  The
-// caller sizes the grid so every workgroup is resident; every spin is bounded (err_code).
+// stores + drain + release fence + relaxed counter; the eval point is published with sc1
+// (atomic) stores + drain + a relaxed generation; consumers poll relaxed and acquire once.
+// Every spin is bounded (err_code).
 // ---------------------------------------------------------------------------------------
 #define RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
 
 constexpr int LM_MAX_PASSES = 8;          // a round needs <= 1 + max_num_iterations = 5
 constexpr uint32_t LM_SPIN_LIMIT = 1u << 21;
+// sync words per solve, zeroed before the launch: [1] generation (pass + 1 of the published
+// evaluation point), [2] its status, [4 + p] claims of pass p's shares 1.. (share 0 is the
+// leader's), [4 + LM_MAX_PASSES + p] shares 1.. of pass p completed
+constexpr int LM_SYNC_WORDS = 4 + 2 * LM_MAX_PASSES;
 
 __device__ inline bool lm_spin_ge(uint32_t* w, uint32_t target) {
   for (uint32_t spins = 0;; ++spins) {
@@ -523,8 +533,8 @@ struct LmJob {
   LmState* S;         // state, initialised by lm_init in an earlier launch
   LmRecView R;        // factor records
   int nrec;
-  double* part;       // [G][LM_NACC] worker partials
-  uint32_t* sync;     // [4] zeroed in an earlier launch: arrivals, generation, status
+  double* part;       // [G][LM_NACC] share partials
+  uint32_t* sync;     // [LM_SYNC_WORDS] zeroed in an earlier launch
   double* xpub;       // [8] published evaluation point
   double* best_out;   // [7] pose written when the solve terminates
   int* err;
@@ -533,21 +543,79 @@ struct LmJob {
                                        // [2] reduce + step, [3] passes, [4] member wait for x
 };
 
+// share c of pass `pass` at X -> part[c], then counted complete (release)
+template <int kThreads>
+__device__ inline void lm_share(const LmJob& J, const double* X, int c, int G, int pass, double* bsum) {
+  const int tid = threadIdx.x;
+  lm_eval_sum<kThreads>(J.R, J.nrec, X, c, G, bsum);
+  if (tid < LM_NACC) J.part[(size_t)c * LM_NACC + tid] = bsum[tid];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(&J.sync[4 + LM_MAX_PASSES + pass], 1u, RLX_AGENT);
+  }
+}
+
 template <int kThreads>
 __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
   __shared__ LmState ls;
   __shared__ double sx[7];
   __shared__ double bsum[LM_NACC];
+  __shared__ double bsum0[LM_NACC];  // the leader's share 0, kept in LDS
   __shared__ double sred[LM_NACC];
-  __shared__ int sstat;
+  __shared__ int sstat, sshare, spass;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   LmState& S = *J.S;
-  const LmRecView& R = J.R;
-  const int nrec = J.nrec;
   uint32_t* sync = J.sync;
   double* xpub = J.xpub;
-  double* part = J.part;
-  if (g == 0) {  // state written by an earlier launch: plain loads
+  const double* part = J.part;
+  unsigned long long t0 = 0;
+  if (g != 0) {  // member: join the pass in progress, evaluate the shares it can claim
+    uint32_t want = 1;
+    while (true) {
+      if (tid == 0) {
+        t0 = __builtin_readcyclecounter();
+        int st = LM_DONE, c = G, p = 0;
+        if (lm_spin_ge(&sync[1], want)) {  // a member that waits too long just leaves
+          const uint32_t gen = __hip_atomic_load(&sync[1], RLX_AGENT);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          st = (int)__hip_atomic_load(&sync[2], RLX_AGENT);
+          p = (int)gen - 1;
+          if (st != LM_DONE && p < LM_MAX_PASSES) {
+            c = 1 + (int)__hip_atomic_fetch_add(&sync[4 + p], 1u, RLX_AGENT);
+            // a claimed share holds the leader in pass p: the published point is pass p's
+            if (c < G)
+              for (int i = 0; i < 7; ++i) sx[i] = __hip_atomic_load(&xpub[i], RLX_AGENT);
+          } else {
+            st = LM_DONE;
+          }
+        }
+        sstat = st;
+        sshare = c;
+        spass = p;
+        if (J.prof) atomicAdd(&J.prof[4], __builtin_readcyclecounter() - t0);
+      }
+      __syncthreads();
+      // LDS broadcasts read as scalars: the branches around barriers must be uniform to the
+      // compiler (a divergent loop here is structured so that some lanes never leave it)
+      if (__builtin_amdgcn_readfirstlane(sstat) == LM_DONE) return;
+      const int c = __builtin_amdgcn_readfirstlane(sshare), p = __builtin_amdgcn_readfirstlane(spass);
+      if (c >= G) {  // pass p fully claimed: wait for the next evaluation point
+        want = (uint32_t)p + 2;
+        __syncthreads();
+        continue;
+      }
+      double X[7];
+#pragma unroll
+      for (int i = 0; i < 7; ++i) X[i] = sx[i];
+      lm_share<kThreads>(J, X, c, G, p, bsum);
+      want = (uint32_t)p + 1;  // more shares of pass p, if any are left
+      __syncthreads();
+    }
+  }
+  {  // leader: state written by an earlier launch, plain loads
     constexpr int NW = sizeof(LmState) / 8;
     const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&S);
     unsigned long long* dst = reinterpret_cast<unsigned long long*>(&ls);
@@ -555,64 +623,46 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
   }
   __syncthreads();
   bool aborted = false;
-  unsigned long long t0 = 0;
   for (int pass = 0; pass < LM_MAX_PASSES; ++pass) {
     // ---- evaluation point of this pass
-    if (g == 0) {
-      if (tid == 0) {
-        sstat = ls.status;
-        for (int i = 0; i < 7; ++i) sx[i] = ls.status == LM_EVAL_X ? ls.x[i] : ls.cand[i];
-      }
-      __syncthreads();
-      if (G > 1 && wid == 0) {  // publish: sc1 stores, drain, relaxed flag
-        if (lane < 7) __hip_atomic_store(&xpub[lane], sx[lane], RLX_AGENT);
-        if (lane == 7) __hip_atomic_store(&sync[2], (uint32_t)sstat, RLX_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_store(&sync[1], (uint32_t)(pass + 1), RLX_AGENT);
-      }
-    } else {
-      if (tid == 0) {
-        t0 = __builtin_readcyclecounter();
-        if (lm_spin_ge(&sync[1], (uint32_t)(pass + 1))) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          sstat = (int)__hip_atomic_load(&sync[2], RLX_AGENT);
-          for (int i = 0; i < 7; ++i) sx[i] = __hip_atomic_load(&xpub[i], RLX_AGENT);
-        } else {
-          atomicOr(J.err, J.err_code);
-          sstat = LM_DONE;
-        }
-        if (J.prof) atomicAdd(&J.prof[4], __builtin_readcyclecounter() - t0);
-      }
-      __syncthreads();
+    if (tid == 0) {
+      sstat = ls.status;
+      for (int i = 0; i < 7; ++i) sx[i] = ls.status == LM_EVAL_X ? ls.x[i] : ls.cand[i];
     }
-    if (sstat == LM_DONE) break;
-    if (g == 0 && tid == 0) t0 = __builtin_readcyclecounter();
+    __syncthreads();
+    if (G > 1 && wid == 0) {  // publish: sc1 stores, drain, relaxed generation
+      if (lane < 7) __hip_atomic_store(&xpub[lane], sx[lane], RLX_AGENT);
+      if (lane == 7) __hip_atomic_store(&sync[2], (uint32_t)sstat, RLX_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(&sync[1], (uint32_t)(pass + 1), RLX_AGENT);
+    }
+    if (__builtin_amdgcn_readfirstlane(sstat) == LM_DONE) break;
+    if (tid == 0) t0 = __builtin_readcyclecounter();
     double X[7];
 #pragma unroll
     for (int i = 0; i < 7; ++i) X[i] = sx[i];
-    // ---- evaluation of this workgroup's share
-    lm_eval_sum<kThreads>(R, nrec, X, g, G, bsum);
-    if (g != 0) {  // publish the partial: plain stores, drain, release, relaxed ticket
-      if (tid < LM_NACC) part[(size_t)g * LM_NACC + tid] = bsum[tid];
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // ---- share 0, then the shares nobody else took
+    lm_eval_sum<kThreads>(J.R, J.nrec, X, 0, G, bsum0);
+    while (G > 1) {
+      if (tid == 0) sshare = 1 + (int)__hip_atomic_fetch_add(&sync[4 + pass], 1u, RLX_AGENT);
       __syncthreads();
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(&sync[0], 1u, RLX_AGENT);
-      }
-      continue;
+      const int c = __builtin_amdgcn_readfirstlane(sshare);
+      __syncthreads();
+      if (c >= G) break;
+      lm_share<kThreads>(J, X, c, G, pass, bsum);
+      // keeps lm_share's tid-0 release apart from the next claim: merged, they let the other
+      // lanes reach the loop's barrier on a shorter path and spin on a stale share forever
+      __syncthreads();
     }
-    // ---- leader: gather the partials, step
     if (tid == 0 && J.prof) {
       const unsigned long long t1 = __builtin_readcyclecounter();
       atomicAdd(&J.prof[0], t1 - t0);
       atomicAdd(&J.prof[3], 1ull);
       t0 = t1;
     }
+    // ---- every share complete (the others are held by running workgroups)
     if (tid == 0 && G > 1) {
-      if (lm_spin_ge(&sync[0], (uint32_t)(pass + 1) * (uint32_t)(G - 1))) {
+      if (lm_spin_ge(&sync[4 + LM_MAX_PASSES + pass], (uint32_t)(G - 1))) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       } else {
@@ -626,15 +676,15 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
       t0 = t1;
     }
     __syncthreads();
-    if (sstat == -1) {
+    if (__builtin_amdgcn_readfirstlane(sstat) == -1) {
       aborted = true;
       break;
     }
     if (wid == 0) {
-      // lane i sums accumulator i over the workgroups in order (G <= 16: one lane per
+      // lane i sums accumulator i over the shares in order (G <= 32: one lane per
       // accumulator beats a shuffle tree per accumulator)
       if (lane < LM_NACC) {
-        double v = bsum[lane];
+        double v = bsum0[lane];
         for (int c = 1; c < G; ++c) v += part[(size_t)c * LM_NACC + lane];
         sred[lane] = v;
       }
@@ -650,7 +700,6 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
     __syncthreads();
     if (tid == 0 && J.prof) atomicAdd(&J.prof[2], __builtin_readcyclecounter() - t0);
   }
-  if (g != 0) return;
   if (aborted && tid == 0) {  // stop this stream's LM where it is (best so far)
     ls.term = 6;
     ls.status = LM_DONE;

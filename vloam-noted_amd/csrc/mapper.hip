@@ -119,7 +119,7 @@ struct MapperDev {
   float4* vx_pts;  // [B][2][scratch_cap]
   int* vx_idx;
   double* partials;  // [B][max_chunks][LM_NACC]
-  uint32_t* lm_sync;   // [B][2 rounds][4]: worker arrivals, eval-point generation, status
+  uint32_t* lm_sync;   // [B][2 rounds][LM_SYNC_WORDS] (lm.h)
   double* lm_xpub;     // [B][2 rounds][8]: eval point published to the workers
   uint32_t* tickets;  // [B]
   // sharded mode (loam_mapper_create_sharded): this rank of nrank; map points are stored by
@@ -510,7 +510,7 @@ __global__ void __launch_bounds__(CORR_THREADS) __attribute__((amdgpu_waves_per_
   double X[7];
 #pragma unroll
   for (int i = 0; i < 7; ++i) X[i] = F.pose[i];
-  if (blk == 0 && threadIdx.x < 4) D.lm_sync[((size_t)s * 2 + round) * 4 + threadIdx.x] = 0;
+  if (blk == 0 && threadIdx.x < LM_SYNC_WORDS) D.lm_sync[((size_t)s * 2 + round) * LM_SYNC_WORDS + threadIdx.x] = 0;
   if (blk == 0 && threadIdx.x == 0) lm_init(F.lm[round], X, 4, F.optimize != 0);
   if (!F.optimize) return;  // k_geom types every record 0
   const int tid = threadIdx.x;
@@ -822,7 +822,7 @@ __global__ void __launch_bounds__(64) k_lm_step(MapperDev D, int round) {
 // agent-scope release/acquire recipe (cdna_hip_programming.md §6 Guideline 16): partials are
 // plain stores + drain + release fence + relaxed ticket; the eval point is published with sc1
 // (atomic) stores + drain + a relaxed flag; every consumer polls relaxed and acquires once.
-// The grid is sized on the host so that every workgroup is resident, and every spin is
+// Shares are claimed per pass by whichever workgroups run (no residency needed), and every spin is
 // bounded (MAP_ERR_LM_SYNC, the stream's LM then stops).
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(LM_THREADS) k_lm_round(MapperDev D, int round, int G) {
@@ -838,7 +838,7 @@ __global__ void __launch_bounds__(LM_THREADS) k_lm_round(MapperDev D, int round,
                   D.r_a[2] + rb, D.r_b[0] + rb, D.r_b[1] + rb, D.r_b[2] + rb};
   J.nrec = F.nc_stack + F.ns_stack;
   J.part = D.partials + (size_t)s * D.max_chunks * LM_NACC;
-  J.sync = D.lm_sync + ((size_t)s * 2 + round) * 4;
+  J.sync = D.lm_sync + ((size_t)s * 2 + round) * LM_SYNC_WORDS;
   J.xpub = D.lm_xpub + ((size_t)s * 2 + round) * 8;
   J.best_out = F.pose;
   J.err = &F.err;
@@ -1527,8 +1527,10 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   }
   D.max_chunks = LM_EBLK;
   {
-    // k_lm_round needs every workgroup resident: G per stream with B * G <= CUs x blocks/CU.
-    // LOAM_LM_PERSISTENT=0 selects the two-kernel path (tests cover both).
+    // k_lm_round: G workgroups per stream, B * G <= CUs x blocks/CU so that one launch fits the
+    // GPU (speed only: the shares are claimed by whichever workgroups run, lm.h, so handles
+    // sharing the GPU cannot deadlock).  LOAM_LM_PERSISTENT=0 selects the two-kernel path
+    // (tests cover both).
     int occ = 0, cus = 0;
     const char* env = std::getenv("LOAM_LM_PERSISTENT");
     const bool allow = !(env && env[0] == '0');
@@ -1541,8 +1543,8 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
       occ = std::min(occ, 1);
       const int cap = occ * cus;
       h->lm_G = std::min(LM_EBLK, std::min(16, cap / n_streams));
-      const char* genv = std::getenv("LOAM_LM_G");  // measurement override (clamped to the cap)
-      if (genv && std::atoi(genv) > 0) h->lm_G = std::min(LM_EBLK, std::min(cap / n_streams, std::atoi(genv)));
+      const char* genv = std::getenv("LOAM_LM_G");  // measurement override
+      if (genv && std::atoi(genv) > 0) h->lm_G = std::min(LM_EBLK, std::atoi(genv));
     }
   }
   D.leaf[0] = (float)h->P.mapping_line_resolution;
@@ -1638,7 +1640,7 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   ALLOC(D.vx_pts, B * 2 * (size_t)D.scratch_cap);
   ALLOC(D.vx_idx, B * 2 * (size_t)D.scratch_cap);
   ALLOC(D.partials, B * (size_t)D.max_chunks * LM_NACC);
-  ALLOC(D.lm_sync, B * 2 * 4);
+  ALLOC(D.lm_sync, B * 2 * LM_SYNC_WORDS);
   ALLOC(D.lm_xpub, B * 2 * 8);
   ALLOC(D.tickets, B);
   ALLOC(h->d_map_off, 2 * NCUBE + 1);

@@ -69,7 +69,7 @@ struct OdomDev {
   double* r_a[3];
   double* r_b[3];
   double* partials;    // [B][OD_PBLK][LM_NACC]
-  uint32_t* lm_sync;   // [B][2][4]
+  uint32_t* lm_sync;   // [B][2][LM_SYNC_WORDS] (lm.h)
   double* lm_xpub;     // [B][2][8]
 };
 
@@ -258,7 +258,7 @@ __global__ void __launch_bounds__(OD_QTHREADS) k_od_corr(OdomDev D, int round, i
   double X[7];
 #pragma unroll
   for (int i = 0; i < 7; ++i) X[i] = F.x[i];
-  if (blk == 0 && threadIdx.x < 4) D.lm_sync[((size_t)s * 2 + round) * 4 + threadIdx.x] = 0;
+  if (blk == 0 && threadIdx.x < LM_SYNC_WORDS) D.lm_sync[((size_t)s * 2 + round) * LM_SYNC_WORDS + threadIdx.x] = 0;
   if (blk == 0 && threadIdx.x == 0) lm_init(F.lm[round], X, 4, true);
   const int ns = F.n_in[0], nf = F.n_in[2];
   const size_t rb = (size_t)s * OD_MAXQ;
@@ -369,7 +369,7 @@ __global__ void __launch_bounds__(OD_LM_THREADS) k_od_lm(OdomDev D, int round, i
                   D.r_a[2] + rb, D.r_b[0] + rb, D.r_b[1] + rb, D.r_b[2] + rb};
   J.nrec = F.n_in[0] + F.n_in[2];
   J.part = D.partials + (size_t)s * OD_PBLK * LM_NACC;
-  J.sync = D.lm_sync + ((size_t)s * 2 + round) * 4;
+  J.sync = D.lm_sync + ((size_t)s * 2 + round) * LM_SYNC_WORDS;
   J.xpub = D.lm_xpub + ((size_t)s * 2 + round) * 8;
   J.best_out = F.x;
   J.err = &F.err;
@@ -483,24 +483,18 @@ int32_t loam_odometry_create(const loam_params* p, int32_t device, int32_t n_str
     OA(D.r_b[k], B * (size_t)OD_MAXQ);
   }
   OA(D.partials, B * (size_t)OD_PBLK * LM_NACC);
-  OA(D.lm_sync, B * 2 * 4);
+  OA(D.lm_sync, B * 2 * LM_SYNC_WORDS);
   OA(D.lm_xpub, B * 2 * 8);
 #undef OA
-  {  // workgroups per stream of the LM round: all resident (lm.h)
+  {  // workgroups per stream of the LM round (lm.h: shares are claimed by whichever workgroups
+     // run, so residency is a speed matter only): one block per CU (256 VGPRs) when they fit
     int occ = 0, cus = 0;
-    h->G = 0;
-    const char* env = std::getenv("LOAM_LM_PERSISTENT");
-    if (!(env && env[0] == '0') &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_od_lm, OD_LM_THREADS, 0) == hipSuccess &&
+    h->G = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_od_lm, OD_LM_THREADS, 0) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess)
-      h->G = std::min(OD_PBLK, std::min(4, std::min(occ, 1) * cus / n_streams));  // 1 block/CU (256 VGPRs)
-    const char* genv = std::getenv("LOAM_OD_LM_G");  // measurement override (within the residency cap)
-    if (h->G >= 1 && genv && std::atoi(genv) > 0)
-      h->G = std::min(std::min(OD_PBLK, std::min(occ, 1) * cus / n_streams), std::atoi(genv));
-    if (h->G < 1) {
-      set_error("loam_odometry_create: too many streams for one resident LM launch");
-      return fail(LOAM_ERR_CAPACITY);
-    }
+      h->G = std::max(1, std::min(OD_PBLK, std::min(4, std::min(occ, 1) * cus / n_streams)));
+    const char* genv = std::getenv("LOAM_OD_LM_G");  // measurement override
+    if (genv && std::atoi(genv) > 0) h->G = std::min(OD_PBLK, std::atoi(genv));
   }
   h->hf.assign(B, OdomFrame{});
   h->hs.assign(B, OdomHost{});
