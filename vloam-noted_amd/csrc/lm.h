@@ -528,6 +528,10 @@ __device__ inline bool lm_spin_ge(uint32_t* w, uint32_t target) {
   }
 }
 
+// streams padded to a multiple of the 8 XCDs: block g * Bp + s of a persistent LM launch runs
+// on XCD s % 8 for every member g (workgroups are dealt to the XCDs round-robin)
+__host__ __device__ inline int lm_padded(int B) { return (B + 7) & ~7; }
+
 // one LM solve (one outer round of one stream) spread over G workgroups
 struct LmJob {
   LmState* S;         // state, initialised by lm_init in an earlier launch

@@ -826,9 +826,12 @@ __global__ void __launch_bounds__(64) k_lm_step(MapperDev D, int round) {
 // bounded (MAP_ERR_LM_SYNC, the stream's LM then stops).
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(LM_THREADS) k_lm_round(MapperDev D, int round, int G) {
-  // block b -> stream b % B, member b / B: with B a multiple of 8 all of a stream's blocks
-  // share an XCD (b % 8), so its hand-offs stay in one L2 (placement is speed only)
-  const int s = D.s0 + blockIdx.x % D.B, g = blockIdx.x / D.B;
+  // block b -> stream b % Bp, member b / Bp with B padded to a multiple of 8 (the padding
+  // blocks leave at once): all of a stream's blocks share an XCD (b % 8), so its hand-offs
+  // stay in one L2 (placement is speed only)
+  const int Bp = lm_padded(D.B), sl = blockIdx.x % Bp, g = blockIdx.x / Bp;
+  if (sl >= D.B) return;
+  const int s = D.s0 + sl;
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
   const size_t rb = (size_t)s * 2 * D.max_in;
@@ -1926,7 +1929,7 @@ int32_t loam_mapper_solve(loam_mapper* h) {
         else if (h->knn_lanes == 8) k_knn<8><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
         else k_knn<1><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
         k_geom<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
-        k_lm_round<<<B * h->lm_G, LM_THREADS, 0, st>>>(D, round, h->lm_G);
+        k_lm_round<<<lm_padded(B) * h->lm_G, LM_THREADS, 0, st>>>(D, round, h->lm_G);
       }
       k_insert<<<dim3(16, B), 256, 0, st>>>(D);
       k_bucket<<<B * 2, VX_THREADS, 0, st>>>(D);
@@ -2043,7 +2046,7 @@ int32_t loam_mapper_solve(loam_mapper* h) {
       hipStream_t sg = h->gst[g];
       LOAM_HIP(before(g, 4 + 3 * round, sg));
       if (h->lm_G > 0) {
-        LAUNCH_ON(sg, FAM_LM, k_lm_round<<<Bg * h->lm_G, LM_THREADS, 0, sg>>>(Dg[g], round, h->lm_G));
+        LAUNCH_ON(sg, FAM_LM, k_lm_round<<<lm_padded(Bg) * h->lm_G, LM_THREADS, 0, sg>>>(Dg[g], round, h->lm_G));
       } else {
         for (int it = 0; it < 5; ++it) {  // iteration 0 + max_num_iterations = 4 candidates
           LAUNCH_ON(sg, FAM_LM, k_lm_eval<<<Bg * LM_EBLK, LM_THREADS, 0, sg>>>(Dg[g], round));

@@ -359,7 +359,9 @@ __global__ void __launch_bounds__(OD_QTHREADS) k_od_corr(OdomDev D, int round, i
 }
 
 __global__ void __launch_bounds__(OD_LM_THREADS) k_od_lm(OdomDev D, int round, int G) {
-  const int s = blockIdx.x / G, g = blockIdx.x % G;
+  // block b -> stream b % Bp, member b / Bp: a stream's blocks share an XCD (lm.h lm_padded)
+  const int Bp = lm_padded(D.B), s = blockIdx.x % Bp, g = blockIdx.x / Bp;
+  if (s >= D.B) return;
   OdomFrame& F = D.fr[s];
   if (!F.active || !F.inited) return;
   const size_t rb = (size_t)s * OD_MAXQ;
@@ -598,7 +600,7 @@ int32_t loam_odometry_solve(loam_odometry* h) {
     const int qblk = std::min(OD_QBLK_MAX, (maxq + OD_QWAVES - 1) / OD_QWAVES);
     for (int round = 0; round < 2; ++round) {
       k_od_corr<<<B * qblk, OD_QTHREADS, 0, st>>>(D, round, qblk);
-      k_od_lm<<<B * h->G, OD_LM_THREADS, 0, st>>>(D, round, h->G);
+      k_od_lm<<<lm_padded(B) * h->G, OD_LM_THREADS, 0, st>>>(D, round, h->G);
     }
   }
   k_od_build<<<B * 2, OD_BUILD_THREADS, 0, st>>>(D);
