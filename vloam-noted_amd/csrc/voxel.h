@@ -13,7 +13,7 @@
 //   1. virtual cloud = src0[0..n0) ++ {src1[i] : tag1[i] == tag}  (stable compaction)
 //   2. bbox reduction
 //   3. LDS open-addressing hash of the voxel idx -> per-voxel counts (ds atomics)
-//   4. compact the U unique voxels, bitonic-sort them in LDS by idx
+//   4. compact the U unique voxels, bitonic-sort them by idx (registers, vx_bitonic_regs)
 //   5. exclusive scan of counts -> output slots; member lists (u16 in LDS when they fit,
 //      else int in global scratch)
 //   6. per voxel: members sorted by input index (insertion sort, lists are short and nearly
@@ -266,6 +266,9 @@ __device__ inline bool vx_centroids(const VxGeom& g, const VxSrc& P, uint32_t N,
 // voxels -> member lists -> centroids written at out[base + j].  out_base == VX_ALLOC:
 // allocate exactly U (at *tail or at 0) once U is known.  Returns U, or VX_OVERFLOW (no side
 // effects on the output) when the unique voxels do not fit the LDS.
+template <int NT, int E, typename KF>
+__device__ inline void vx_bitonic_regs(uint64_t* sk, uint64_t* xb0, uint64_t* xb1, uint32_t npad, const KF& key);
+
 __device__ inline uint32_t vx_group(const VoxSeg& S, const VxGeom& g, const VxSrc& P, uint32_t N,
                                     int* members, uint32_t klo, uint32_t khi, uint32_t out_base,
                                     uint32_t lds_limit, uint32_t* lds, uint32_t* ws, VxMisc& M,
@@ -322,28 +325,41 @@ __device__ inline uint32_t vx_group(const VoxSeg& S, const VxGeom& g, const VxSr
   const int fail = M.sfail;
   __syncthreads();
   if (U > VX_UCAP || fail) return VX_OVERFLOW;
-  uint32_t Upad = 1;
+  uint32_t Upad = 64;
   while (Upad < U) Upad <<= 1;
   uint64_t* s64 = reinterpret_cast<uint64_t*>(lds);  // overlays the (consumed) hash
 #pragma unroll
   for (int s = 0; s < SPT; ++s)
     if (mk[s] != VX_EMPTY) s64[mpos++] = ((uint64_t)mk[s] << 32) | mc[s];
-  for (uint32_t i = U + tid; i < Upad; i += VX_THREADS) s64[i] = 0xFFFFFFFFFFFFFFFFull;
   __syncthreads();
-  for (uint32_t k = 2; k <= Upad; k <<= 1) {
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = tid; i < Upad; i += VX_THREADS) {
-        uint32_t ixj = i ^ j;
-        if (ixj > i) {
-          uint64_t a = s64[i], b = s64[ixj];
-          bool asc = (i & k) == 0;
-          if ((a > b) == asc) {
-            s64[i] = b;
-            s64[ixj] = a;
+  // sort by idx in registers (E keys per thread; cross-wave stages through the hash area, the
+  // one buffer that is free: Upad u64 <= VX_HASH u64); an LDS network above 8192
+  {
+    auto key = [&](uint32_t i) -> uint64_t { return i < U ? s64[i] : ~0ull; };
+    static_assert(8 * VX_THREADS <= VX_HASH, "one-buffer register sort");
+    if (Upad <= 1u * VX_THREADS) vx_bitonic_regs<VX_THREADS, 1>(s64, s64, s64, Upad, key);
+    else if (Upad <= 2u * VX_THREADS) vx_bitonic_regs<VX_THREADS, 2>(s64, s64, s64, Upad, key);
+    else if (Upad <= 4u * VX_THREADS) vx_bitonic_regs<VX_THREADS, 4>(s64, s64, s64, Upad, key);
+    else if (Upad <= 8u * VX_THREADS) vx_bitonic_regs<VX_THREADS, 8>(s64, s64, s64, Upad, key);
+    else {  // > 8192 unique voxels (rare: full re-filters of the largest cubes): in LDS, as 16
+            // keys per thread in registers would spill
+      for (uint32_t i = U + tid; i < Upad; i += VX_THREADS) s64[i] = ~0ull;
+      __syncthreads();
+      for (uint32_t k = 2; k <= Upad; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+          for (uint32_t i = tid; i < Upad; i += VX_THREADS) {
+            const uint32_t ixj = i ^ j;
+            if (ixj > i) {
+              const uint64_t a = s64[i], b = s64[ixj];
+              if ((a > b) == ((i & k) == 0)) {
+                s64[i] = b;
+                s64[ixj] = a;
+              }
+            }
           }
+          __syncthreads();
         }
       }
-      __syncthreads();
     }
   }
   // keys / counts -> exclusive offsets (thread t owns entries [t*EPT, (t+1)*EPT))
@@ -672,8 +688,9 @@ __device__ inline void voxel_segment(const VoxSeg& S, uint32_t* lds) {
 // Block bitonic sort of npad (a power of two, 64 <= npad <= E NT) 64-bit keys held in registers:
 // element i = (wave * E + e) * 64 + lane.  Partners closer than 64 are exchanged by lane
 // shuffles, partners within a lane's E registers directly; only partners in another wave go
-// through LDS (xb0 / xb1: npad u64 each, alternating, one barrier per such stage).  Waves past
-// npad / (64 E) take part in the barriers only.  key(i) gives the key of element i (~0 for
+// through LDS (xb0 / xb1: npad u64 each, alternating, one barrier per such stage; xb0 == xb1:
+// one buffer, two barriers per such stage).  Waves past npad / (64 E) take part in the
+// barriers only.  key(i) gives the key of element i (~0 for
 // padding; it may read LDS that sk / xb0 / xb1 alias); the sorted keys end in sk[0 .. npad).
 template <int NT, int E, typename KF>
 __device__ inline void vx_bitonic_regs(uint64_t* sk, uint64_t* xb0, uint64_t* xb1, uint32_t npad, const KF& key) {
@@ -703,6 +720,7 @@ __device__ inline void vx_bitonic_regs(uint64_t* sk, uint64_t* xb0, uint64_t* xb
             v[e] = keep_min ? (v[e] < p ? v[e] : p) : (v[e] < p ? p : v[e]);
           }
         }
+        if (xb0 == xb1) __syncthreads();  // one buffer: every read before the next write
       } else if (j >= 64) {  // partner in this lane's registers
         const int ej = (int)(j >> 6);
 #pragma unroll
