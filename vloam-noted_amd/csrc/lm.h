@@ -687,9 +687,17 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
     if (wid == 0) {
       // lane i sums accumulator i over the shares in order (G <= 32: one lane per
       // accumulator beats a shuffle tree per accumulator)
-      if (lane < LM_NACC) {
+      if (lane < LM_NACC) {  // loads 8 at a time in flight, added in share order
         double v = bsum0[lane];
-        for (int c = 1; c < G; ++c) v += part[(size_t)c * LM_NACC + lane];
+        int c = 1;
+        for (; c + 8 <= G; c += 8) {
+          double q[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) q[u] = part[(size_t)(c + u) * LM_NACC + lane];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v += q[u];
+        }
+        for (; c < G; ++c) v += part[(size_t)c * LM_NACC + lane];
         sred[lane] = v;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -344,6 +344,7 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
   S.res_off = nullptr;
   S.scratch_tail = nullptr;
   S.err = &F.err;
+  S.prof_seg = D.dbg + 42;  // stack VoxelGrid phases: dbg[42..45]
   if (!split) {
     S.src0 = F.in_ptr[m];
     S.n0 = m == 0 ? F.nc_in : F.ns_in;

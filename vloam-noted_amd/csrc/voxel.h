@@ -55,6 +55,8 @@ struct VoxSeg {
   uint32_t scratch_cap;
   int* err;
   unsigned long long* prof = nullptr;  // optional: merge phase cycles [bbox, sort, runs, pass A, pass B]
+  unsigned long long* prof_seg = nullptr;  // optional: full filter phase cycles [gather + bbox,
+                                           // hash, sort + scan, member lists + centroids]
 };
 
 // thread 0 adds the cycles since *t to prof[k] and restarts *t (phase counters; call after a barrier)
@@ -274,6 +276,7 @@ __device__ inline uint32_t vx_group(const VoxSeg& S, const VxGeom& g, const VxSr
                                     uint32_t lds_limit, uint32_t* lds, uint32_t* ws, VxMisc& M,
                                     int* moved_out) {
   const int tid = threadIdx.x;
+  unsigned long long tp = __builtin_readcyclecounter();
   uint32_t* hkey = lds;
   uint32_t* hcnt = lds + VX_HASH;
   for (int i = tid; i < VX_HASH; i += VX_THREADS) {
@@ -324,6 +327,7 @@ __device__ inline uint32_t vx_group(const VoxSeg& S, const VxGeom& g, const VxSr
   uint32_t mpos = vx_block_scan(nm, ws, &U);
   const int fail = M.sfail;
   __syncthreads();
+  vx_phase(S.prof_seg, 1, &tp);
   if (U > VX_UCAP || fail) return VX_OVERFLOW;
   uint32_t Upad = 64;
   while (Upad < U) Upad <<= 1;
@@ -379,6 +383,7 @@ __device__ inline uint32_t vx_group(const VoxSeg& S, const VxGeom& g, const VxSr
   uint32_t* ukey = lds;  // packed: ukey[U] | uoff[U] | ufill[U] | LDS member lists
   uint32_t* uoff = lds + U;
   uint32_t* ufill = lds + 2 * U;
+  vx_phase(S.prof_seg, 2, &tp);
 #pragma unroll
   for (int e = 0; e < EPT; ++e) {
     uint32_t j = tid * EPT + e;
@@ -419,6 +424,7 @@ __device__ inline uint32_t vx_group(const VoxSeg& S, const VxGeom& g, const VxSr
   }
   if (moved) M.moved = 1;
   __syncthreads();
+  vx_phase(S.prof_seg, 3, &tp);
   *moved_out |= M.moved;
   if (out_base == VX_ALLOC && tid == 0) {
     if (S.res_off) *S.res_off = ob;
@@ -653,8 +659,10 @@ __device__ inline void voxel_segment(const VoxSeg& S, uint32_t* lds) {
   }
 
   // ---- 2. bounding box + geometry
+  unsigned long long tp = __builtin_readcyclecounter();
   vx_geometry(P, N, S.leaf, M);
   const VxGeom g = M.g;
+  vx_phase(S.prof_seg, 0, &tp);
   if (g.overflow) {  // PCL: "Leaf size is too small" -> output = input
     if (tid == 0) {
       uint32_t b = S.tail ? atomicAdd(S.tail, N) : 0;
