@@ -307,3 +307,48 @@ def test_concurrent_handles_share_the_gpu(seq):
                 (q, t), (qr, tr) = got[i][k][s], want[k][s]
                 assert np.array_equal(q, qr) and np.array_equal(t, tr), (i, k, s)
         ms[i].close()
+
+
+def _options_run(seq, n_streams, n_frames):
+    m = BatchMapper(n_streams, max_input_points=32768, max_submap_points=16384, max_map_points=262144)
+    poses, stats = [], []
+    for k in range(n_frames):
+        for s in range(n_streams):
+            r = seq[(k + s) % len(seq)]
+            m.input(s, r["corner"], r["surf"], r["q_wodom"], r["t_wodom"])
+        m.solve()
+        poses.append([m.pose(s) for s in range(n_streams)])
+        stats.append([(m.stats(s).corner_map, m.stats(s).surf_map, tuple(m.stats(s).corner_num),
+                       tuple(m.stats(s).surf_num), m.stats(s).lm[0].iterations, m.stats(s).lm[1].iterations)
+                      for s in range(n_streams)])
+    maps = [[m.cubes(s, w) for w in range(2)] for s in range(n_streams)]
+    m.close()
+    return poses, stats, maps
+
+
+@pytest.fixture(scope="module")
+def options_ref(seq):
+    return _options_run(seq, 8, 8)
+
+
+@pytest.mark.parametrize("env", [{"LOAM_REVOX_SPLIT": "1"}, {"LOAM_MAPPER_GROUPS": "2"},
+                                 {"LOAM_MAPPER_GROUPS": "2", "LOAM_MAPPER_STAGGER": "1"},
+                                 {"LOAM_KNN_LANES": "2"}, {"LOAM_KNN_ORDER": "1"},
+                                 {"LOAM_MAPPER_GRAPH": "1"}, {"LOAM_STACK_SPLIT": "1"}],
+                         ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
+def test_scheduling_options_bit_identical(seq, options_ref, monkeypatch, env):
+    """the measured-and-kept-off options change scheduling only: poses, statistics and maps
+    bit-identical to the default path (8 streams, 8 frames)"""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    poses, stats, maps = _options_run(seq, 8, 8)
+    rp, rs, rm = options_ref
+    for k in range(len(rp)):
+        assert stats[k] == rs[k], k
+        for s in range(8):
+            assert np.array_equal(poses[k][s][0], rp[k][s][0]) and np.array_equal(poses[k][s][1], rp[k][s][1]), (k, s)
+    for s in range(8):
+        for w in range(2):
+            assert sorted(maps[s][w]) == sorted(rm[s][w])
+            for c in rm[s][w]:
+                assert np.array_equal(maps[s][w][c], rm[s][w][c]), (s, w, c)
