@@ -199,7 +199,7 @@ int32_t loam_mapper_stats(loam_mapper* h, int32_t stream, loam_map_stats* st);
  * [32..39] their cycles (filter + index), [40] sharded: pose values that differed from rank 0's
  * after the LM (0 when the all-reduce is bit-identical on every rank), [41] arena compactions
  * ((stream, map) pairs), [42..45] stack VoxelGrid cycles: bounding box, hash, sort + scan,
- * member lists + centroids */
+ * member lists + centroids, [46..47] of the latter: member lists, per-voxel sort + sums */
 #define LOAM_DEBUG_COUNTERS 48
 int32_t loam_mapper_debug_counters(loam_mapper* h, uint64_t* out, int32_t n, int32_t reset);
 /* sum over all streams of the LM iterations (both rounds) of the last solve */

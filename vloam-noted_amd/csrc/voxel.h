@@ -176,8 +176,10 @@ template <typename MT>
 __device__ inline bool vx_centroids(const VxGeom& g, const VxSrc& P, uint32_t N, MT* members,
                                     uint32_t klo, uint32_t khi, uint32_t U, const uint32_t* ukey,
                                     const uint32_t* uoff, uint32_t* ufill, float4* out,
-                                    uint32_t* big_list, uint32_t big_cap, VxMisc& M) {
+                                    uint32_t* big_list, uint32_t big_cap, VxMisc& M,
+                                    unsigned long long* dprof = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  unsigned long long tq = __builtin_readcyclecounter();
   bool moved = false;
   float4 pn = make_float4(0.f, 0.f, 0.f, 0.f);
   if ((uint32_t)tid < N) pn = P(tid);
@@ -201,6 +203,7 @@ __device__ inline bool vx_centroids(const VxGeom& g, const VxSrc& P, uint32_t N,
   }
   if (tid == 0) M.nbig = 0;
   __syncthreads();
+  vx_phase(dprof, 0, &tq);
   for (uint32_t j = tid; j < U; j += VX_THREADS) {
     const uint32_t b = uoff[j];
     const uint32_t n = ufill[j];
@@ -238,6 +241,7 @@ __device__ inline bool vx_centroids(const VxGeom& g, const VxSrc& P, uint32_t N,
     moved |= vx_key(g, cc) != ukey[j];
   }
   __syncthreads();
+  vx_phase(dprof, 1, &tq);
   const uint32_t nbig = min(M.nbig, big_cap);
   for (uint32_t e = wid; e < nbig; e += VX_WAVES) {
     const uint32_t j = big_list[e];
@@ -416,7 +420,7 @@ __device__ inline uint32_t vx_group(const VoxSeg& S, const VxGeom& g, const VxSr
   if (N <= 65536u && 3 * U + mem_words + 64 <= lds_limit) {
     uint32_t* big = lds + 3 * U + mem_words;
     moved = vx_centroids(g, P, N, reinterpret_cast<uint16_t*>(lds + 3 * U), klo, khi, U, ukey, uoff,
-                         ufill, S.out + ob, big, lds_limit - (3 * U + mem_words), M);
+                         ufill, S.out + ob, big, lds_limit - (3 * U + mem_words), M, S.prof_seg ? S.prof_seg + 4 : nullptr);
   } else {
     uint32_t* big = lds + 3 * U;
     const uint32_t cap = lds_limit > 3 * U ? lds_limit - 3 * U : 0u;
