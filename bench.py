@@ -55,7 +55,8 @@ def parse():
                     help="max_map_points per stream and map (arena size; fewer compactions)")
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--n-az", type=int, default=2000)
-    ap.add_argument("--cpu-frames", type=int, default=40, help="cpu_baseline timed frames (after warmup)")
+    ap.add_argument("--cpu-frames", type=int, default=200,
+                    help="cpu_baseline timed frames after warmup (~14 s of single-core oracle work in all)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-prof", action="store_true", help="no per-launch HIP events")
     ap.add_argument("--prior", choices=["odometry", "drift"], default="odometry",
