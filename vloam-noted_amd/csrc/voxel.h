@@ -251,11 +251,11 @@ __device__ inline bool vx_centroids(const VxGeom& g, const VxSrc& P, uint32_t N,
       float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
       if (a + lane < n) p = P((uint32_t)members[b + a + lane]);
       const uint32_t m = min(64u, n - a);
-      for (uint32_t l = 0; l < m; ++l) {
-        sx += __shfl(p.x, l, 64);
-        sy += __shfl(p.y, l, 64);
-        sz += __shfl(p.z, l, 64);
-        si += __shfl(p.w, l, 64);
+      for (uint32_t l = 0; l < m; ++l) {  // lane l's point as scalars (uniform l: v_readlane)
+        sx += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.x), (int)l));
+        sy += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.y), (int)l));
+        sz += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.z), (int)l));
+        si += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.w), (int)l));
       }
     }
     if (lane == 0) {
