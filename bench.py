@@ -11,17 +11,23 @@ Inputs are produced before the timed region, on the GPU: synthetic raw scans
 (vloam-noted_amd/csrc/synth.cpp) -> HIP ScanRegistration -> HIP LaserOdometry -> lessSharp /
 lessFlat clouds kept in HBM + the odometry pose as the mapping prior (--prior drift: ground
 truth plus a seeded random walk instead).  Stream b
-replays the sequence from frame b * --stride.  The W warmup steps build every stream's map
-(the 5x5x3-cube window saturates after ~150 m of travel), so the K timed steps run at the
-steady-state map size of a long stream (BASELINE configs[3], 10k-frame stream).
+replays the sequence from frame b * --stride.  --map-frames M untimed steps (always run,
+independent of --warmup) build every stream's map (the 5x5x3-cube window saturates after
+~150 m of travel; the default M = 300 also puts the window recentering of frames ~386 and
+~436 inside the timed steps), then W untimed warmup steps, then the K timed steps: the timed
+steps run at the steady-state map size of a long stream (BASELINE configs[3], 10k-frame
+stream), whatever W the caller passes.
 
 value = sum of LM iterations of all streams on all ranks / max over ranks of the timed
 wall time.  roofline: the kernel family with the largest device time, algorithmic bytes /
 its average launch duration (HIP events around every launch inside the library, on the
 library's streams, over the timed region).  cpu_baseline (rank 0, N = 1): the CPU oracle
 (single-threaded restatement of the reference: PCL KD-tree + VoxelGrid + Ceres-LM
-semantics) on stream 0's frames: the same W warmup frames untimed, then --cpu-frames
-frames timed (same steady-state regime as the GPU measurement).
+semantics) fed stream 0's inputs: frames 0 .. M+W-1 untimed, then exactly the K frames
+stream 0 processed inside the timed steps, timed.  Its poses give pose_rmse_vs_cpu (the
+second half of the metric): GPU stream 0 against the oracle, both free-running from frame 0
+on identical features and priors.  cpu_all_cores: one oracle replica per core (stream c on
+core c), map building untimed, the K timed frames of every replica bracketed by a barrier.
 
 Usage: python bench.py [--gpus N --steps K --warmup W --streams B]; for N > 1 launch with
 torch.distributed.run, one rank per GPU (streams shard across ranks, no data-path
@@ -46,7 +52,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=150, help="untimed steps; they build the maps")
+    ap.add_argument("--warmup", type=int, default=5, help="untimed steps after --map-frames")
+    ap.add_argument("--map-frames", type=int, default=300,
+                    help="untimed map-building steps, always run before --warmup (steady-state maps)")
     ap.add_argument("--streams", type=int, default=128, help="mapping streams per GPU")
     ap.add_argument("--stride", type=int, default=1, help="frame offset between streams")
     ap.add_argument("--handles", type=int, default=2,
@@ -55,8 +63,8 @@ def parse():
                     help="max_map_points per stream and map (arena size; fewer compactions)")
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--n-az", type=int, default=2000)
-    ap.add_argument("--cpu-frames", type=int, default=200,
-                    help="cpu_baseline timed frames after warmup (~14 s of single-core oracle work in all)")
+    ap.add_argument("--cpu-cores", type=int, default=0,
+                    help="oracle replicas of the all-cores CPU figure (0: min(16, usable cores))")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-prof", action="store_true", help="no per-launch HIP events")
     ap.add_argument("--prior", choices=["odometry", "drift"], default="odometry",
@@ -86,15 +94,17 @@ def drift_priors(seed, n, q_gt, t_gt):
     return q, t
 
 
-def make_frames(seed, n_frames, n_az, device, keep_raw=0, prior="odometry"):
+def make_frames(seed, n_frames, n_az, device, raw_frames=(), prior="odometry"):
     """raw scans (threads) -> HIP ScanRegistration -> HIP LaserOdometry -> features in HBM
-    (torch tensors) + the odometry pose (the mapping prior, laser_odometry.cpp:660-679); the
-    raw scans of the first keep_raw frames are kept for the CPU baseline"""
+    (torch tensors, plus host copies for the CPU legs) + the odometry pose (the mapping prior,
+    laser_odometry.cpp:660-679); the raw scans of the frames in raw_frames are kept for the
+    CPU stage baselines"""
     import torch
     from loam_amd import synth
     from loam_amd.odometry import BatchOdometry
     from loam_amd.scanreg import ScanRegistration
 
+    raw_frames = set(raw_frames)
     sr = ScanRegistration(device=device)
     od = BatchOdometry(1, device=device)
     frames = []
@@ -117,7 +127,8 @@ def make_frames(seed, n_frames, n_az, device, keep_raw=0, prior="odometry"):
                 surf = sr.cloud(4)    # surfPointsLessFlat   -> laserCloudSurfLast
                 frames.append(dict(corner=torch.from_numpy(corner).to(f"cuda:{device}"),
                                    surf=torch.from_numpy(surf).to(f"cuda:{device}"),
-                                   gt=gt, q=q, t=t, raw=xyz if c0 + k < keep_raw else None))
+                                   corner_h=corner, surf_h=surf,
+                                   gt=gt, q=q, t=t, raw=xyz if c0 + k in raw_frames else None))
     sr.close()
     od.close()
     if prior == "drift":
@@ -142,28 +153,32 @@ def step_inputs(frames, streams, stride, k, first=0):
             np.array([f["q"] for f in fs]), np.array([f["t"] for f in fs]))
 
 
-def run_steps(mapper, plan, first, count):
-    """count solveMapping steps from the precomputed per-step input arrays"""
+def run_steps(mapper, plan, first, count, poses=None):
+    """count solveMapping steps from the precomputed per-step input arrays; with `poses`, the
+    pose of the handle's stream 0 after every step is appended (a host read of the records
+    the solve already copied back)"""
     iters = 0
     for k in range(first, first + count):
         mapper.input_device_batch(*plan[k])
         mapper.solve()
         iters += mapper.total_iterations()
+        if poses is not None:
+            poses.append(mapper.pose(0))
     return iters
 
 
-def run_handles(mappers, plans, first, count):
+def run_handles(mappers, plans, first, count, poses=None):
     """run_steps on every handle, one host thread each (ctypes releases the GIL in the
     library calls): one handle's host work overlaps the others' kernels"""
     if len(mappers) == 1:
-        return run_steps(mappers[0], plans[0], first, count)
+        return run_steps(mappers[0], plans[0], first, count, poses)
     import threading
     out = [0] * len(mappers)
     errs = []
 
     def work(h):
         try:
-            out[h] = run_steps(mappers[h], plans[h], first, count)
+            out[h] = run_steps(mappers[h], plans[h], first, count, poses if h == 0 else None)
         except Exception as e:  # surfaced after the join
             errs.append(e)
 
@@ -177,32 +192,113 @@ def run_handles(mappers, plans, first, count):
     return sum(out)
 
 
-def cpu_baseline(frames, warm, n):
-    """oracle pipeline on stream 0's frames (same features and priors as the GPU run): `warm`
-    untimed frames build the map, then n frames timed (solveMapping, the oracle's own
-    steady_clock over the whole call).  The oracle ScanRegistration and LaserOdometry run on
-    every frame too; their own timers over the same n frames give the stage baselines."""
+def _oracle():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import loam_oracle as O
-    sr, od, mp = O.ScanRegistration(), O.LaserOdometry(), O.LaserMapping()
-    iters, ms = 0, 0.0
-    st_ms = {"scan_registration": 0.0, "odometry": 0.0, "odometry_iters": 0}
-    for k, f in enumerate(frames[:warm + n]):
-        sr.input(f["raw"])
-        od.input(*sr.output())
-        od.solve()
-        mp.input(sr.cloud(2), sr.cloud(4), None, f["q"], f["t"])
+    return O
+
+
+def cpu_baseline(frames, pre, n):
+    """oracle LaserMapping fed stream 0's inputs (the GPU's features and priors, host copies):
+    frames 0 .. pre-1 untimed (map building), then frames pre .. pre+n-1 -- exactly the frames
+    stream 0 processed inside the GPU's timed steps -- timed by the oracle's own steady_clock
+    around each solveMapping.  Returns (iterations, ms, poses of every frame)."""
+    O = _oracle()
+    mp = O.LaserMapping()
+    iters, ms, poses = 0, 0.0, []
+    for k, f in enumerate(frames[:pre + n]):
+        mp.input(f["corner_h"], f["surf_h"], None, f["q"], f["t"])
         mp.solve()
-        if k < warm:
+        poses.append(mp.pose())
+        if k < pre:
             continue
         st = mp.stats()
         iters += st.lm[0].iterations + st.lm[1].iterations
         ms += st.ms_total
-        st_ms["scan_registration"] += sr.ms
-        st_ms["odometry"] += od.ms
+    return iters, ms, poses
+
+
+def cpu_stages(frames, first, n):
+    """oracle ScanRegistration and LaserOdometry on the raw scans of frames first-1 ..
+    first+n-1 (the first only primes the odometry's last clouds); their own timers over the
+    last n frames"""
+    O = _oracle()
+    sr, od = O.ScanRegistration(), O.LaserOdometry()
+    st = {"scan_registration": 0.0, "odometry": 0.0, "odometry_iters": 0}
+    for k in range(first - 1, first + n):
+        sr.input(frames[k]["raw"])
+        od.input(*sr.output())
+        od.solve()
+        if k < first:
+            continue
+        st["scan_registration"] += sr.ms
+        st["odometry"] += od.ms
         _, lm = od.stats()
-        st_ms["odometry_iters"] += lm[0].iterations + lm[1].iterations
-    return iters, ms, st_ms
+        st["odometry_iters"] += lm[0].iterations + lm[1].iterations
+    return st
+
+
+def cpu_all_cores(frames, cores, stride, pre, n):
+    """all-cores CPU figure: `cores` independent oracle LaserMapping replicas,
+    one host thread each (ctypes releases the GIL inside the oracle), replica c on stream c's
+    inputs.  Map building (pre frames) is untimed; the n timed frames of all replicas run
+    between two barriers.  Returns (iterations, wall seconds)."""
+    import threading
+    O = _oracle()
+    bar = threading.Barrier(cores + 1)
+    out = [0] * cores
+    errs = []
+
+    def work(c):
+        try:
+            mp = O.LaserMapping()
+            fs = frames[c * stride: c * stride + pre + n]
+            for k, f in enumerate(fs):
+                if k == pre:
+                    bar.wait()
+                mp.input(f["corner_h"], f["surf_h"], None, f["q"], f["t"])
+                mp.solve()
+                if k >= pre:
+                    st = mp.stats()
+                    out[c] += st.lm[0].iterations + st.lm[1].iterations
+        except Exception as e:
+            errs.append(e)
+            bar.abort()
+        finally:
+            try:
+                bar.wait()
+            except threading.BrokenBarrierError:
+                pass
+
+    ts = [threading.Thread(target=work, args=(c,)) for c in range(cores)]
+    for t in ts:
+        t.start()
+    bar.wait()  # every replica has built its map
+    t0 = time.perf_counter()
+    bar.wait()  # every replica has run its timed frames
+    dt = time.perf_counter() - t0
+    for t in ts:
+        t.join()
+    if errs:
+        raise errs[0]
+    return sum(out), dt
+
+
+def quat_angle(q1, q2):
+    """rotation angle (rad) of q1^-1 q2 (xyzw); atan2 form, exact for tiny angles"""
+    q1 = np.asarray(q1, dtype=np.float64) / np.linalg.norm(q1)
+    q2 = np.asarray(q2, dtype=np.float64) / np.linalg.norm(q2)
+    v = q1[3] * q2[:3] - q2[3] * q1[:3] - np.cross(q1[:3], q2[:3])
+    return 2.0 * np.arctan2(float(np.linalg.norm(v)), abs(float(np.dot(q1, q2))))
+
+
+def pose_errors(gpu, cpu):
+    """translation (m) and rotation-angle (rad) differences, RMS and max, of two pose lists"""
+    dt = np.array([np.linalg.norm(np.asarray(g[1]) - np.asarray(c[1])) for g, c in zip(gpu, cpu)])
+    dr = np.array([quat_angle(g[0], c[0]) for g, c in zip(gpu, cpu)])
+    return {"trans_rms_m": float(np.sqrt(np.mean(dt ** 2))), "trans_max_m": float(dt.max()),
+            "rot_rms_rad": float(np.sqrt(np.mean(dr ** 2))), "rot_max_rad": float(dr.max()),
+            "frames": int(len(dt))}
 
 
 def depth_stage(seed, device, n_frames=64, n_queries=2800, n_az=2000, with_cpu=True):
@@ -405,12 +501,15 @@ def main():
 
     from loam_amd.mapping import BatchMapper
 
-    B, K, W = args.streams, args.steps, args.warmup
-    n_frames = (B - 1) * args.stride + W + K
-    cpu_n = 0 if (args.no_cpu or world > 1 or rank != 0) else W + args.cpu_frames
+    B, K, W, M = args.streams, args.steps, args.warmup, args.map_frames
+    pre = M + W  # untimed steps: map building, then warmup
+    n_frames = (B - 1) * args.stride + pre + K
+    with_cpu = not args.no_cpu and world == 1 and rank == 0
+    cores = args.cpu_cores or min(16, len(os.sched_getaffinity(0)))
+    cores = min(cores, B)
     # sharded: every rank runs the same streams (identical inputs, one share of each map)
-    frames, stage_ms = make_frames(stream_seed(args.seed, 0 if args.shard else rank), max(n_frames, cpu_n), args.n_az, local,
-                         keep_raw=cpu_n, prior=args.prior)
+    frames, stage_ms = make_frames(stream_seed(args.seed, 0 if args.shard else rank), n_frames, args.n_az, local,
+                                   raw_frames=range(pre - 1, pre + K) if with_cpu else (), prior=args.prior)
     H = 1 if args.shard else max(1, args.handles)
     if B % H:
         raise SystemExit("--streams must be divisible by --handles")
@@ -444,15 +543,16 @@ def main():
         if world > 1:
             dist.barrier()
 
-    plans = [[step_inputs(frames, Bh, args.stride, k, first=h * Bh) for k in range(W + K)] for h in range(H)]
-    run_handles(mappers, plans, 0, W)
+    plans = [[step_inputs(frames, Bh, args.stride, k, first=h * Bh) for k in range(pre + K)] for h in range(H)]
+    poses0 = []  # stream 0 after every step (free-running trajectory vs the oracle's)
+    run_handles(mappers, plans, 0, pre, poses0)
     for m in mappers:
         if not args.no_prof:
             m.set_profiling(True)
         m.reset_kernel_times()
     barrier()
     t0 = time.perf_counter()
-    iters = run_handles(mappers, plans, W, K)
+    iters = run_handles(mappers, plans, pre, K, poses0)
     barrier()
     dt = time.perf_counter() - t0
     kt = {}
@@ -473,11 +573,11 @@ def main():
     single = None
     if not args.no_single_stream and rank == 0 and world == 1 and not args.shard:
         m1 = BatchMapper(1, device=local)
-        plan1 = [step_inputs(frames, 1, args.stride, k) for k in range(W + K)]
-        run_steps(m1, plan1, 0, W)
+        plan1 = [step_inputs(frames, 1, args.stride, k) for k in range(pre + K)]
+        run_steps(m1, plan1, 0, pre)
         torch.cuda.synchronize(local)
         t1 = time.perf_counter()
-        it1 = run_steps(m1, plan1, W, K)
+        it1 = run_steps(m1, plan1, pre, K)
         torch.cuda.synchronize(local)
         d1 = time.perf_counter() - t1
         single = {"value": it1 / d1, "ms_per_frame": 1e3 * d1 / K, "iterations": it1}
@@ -494,15 +594,26 @@ def main():
                     "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) if traffic is not None else None,
                     "launches": d["launches"], "avg_launch_us": round(1e3 * d["ms"] / max(1, d["launches"]), 3),
                     "algorithmic_bytes_per_launch": round(d["bytes"] / max(1, d["launches"]), 1)}
-        cpu = None
-        cpu_st = None
-        if not args.no_cpu and world == 1:
-            ci, cms, cpu_st = cpu_baseline(frames, W, args.cpu_frames)
+        cpu = cpu_st = rmse = allc = None
+        if with_cpu:
+            ci, cms, cposes = cpu_baseline(frames, pre, K)
             cpu = {"value": round(ci / (cms * 1e-3), 3), "unit": "LM iters/s", "cores": 1, "kind": "port",
-                   "sample": f"stream 0, frames {W}..{W + args.cpu_frames - 1} after {W} untimed map-building "
-                             f"frames: oracle solveMapping (KD-tree, VoxelGrid, Ceres-LM/DENSE_QR restatement), "
-                             f"{ci} LM iterations in {cms / 1e3:.2f} s",
-                   "ms_per_frame": round(cms / args.cpu_frames, 3)}
+                   "sample": f"stream 0's inputs, frames {pre}..{pre + K - 1} (the frames stream 0 processed in "
+                             f"the timed steps) after {pre} untimed map-building frames: oracle solveMapping "
+                             f"(KD-tree, VoxelGrid, Ceres-LM/DENSE_QR restatement), {ci} LM iterations in "
+                             f"{cms / 1e3:.3f} s",
+                   "ms_per_frame": round(cms / K, 3)}
+            rmse = {"timed_frames": pose_errors(poses0[pre:pre + K], cposes[pre:pre + K]),
+                    "all_frames": pose_errors(poses0, cposes),
+                    "mode": "free-running: GPU stream 0 and the oracle each from frame 0 on identical "
+                            "features and priors, no state shared"}
+            cpu_st = cpu_stages(frames, pre, K)
+            ai, adt = cpu_all_cores(frames, cores, args.stride, pre, K)
+            allc = {"value": round(ai / adt, 3), "unit": "LM iters/s", "cores": cores, "kind": "port",
+                    "nproc": os.cpu_count(), "usable_cores": len(os.sched_getaffinity(0)),
+                    "sample": f"{cores} oracle replicas, one thread each, replica c on stream c's inputs: "
+                              f"{pre} untimed map-building frames, then its {K} timed frames between two "
+                              f"barriers; {ai} LM iterations in {adt:.3f} s"}
         out = {
             "metric": "scan-to-map LM iters/sec on 64-ring KITTI-shaped cloud",
             "value": round(iters_all / dt_max, 3),
@@ -517,11 +628,11 @@ def main():
             "dtype": "fp64 pose/normal equations, fp32 points",
             "data": "synthetic HDL-64E street sequence (64 rings x 2000 azimuths); GPU scan registration "
                     f"features; mapping prior from {'GPU LaserOdometry' if args.prior == 'odometry' else 'ground truth + random walk'}; "
-                    "maps built by the warmup steps",
+                    f"maps built by {pre} untimed steps before the timed ones",
             "config": {"workload": "laserMapping solveMapping, voxel-hashed map resident in HBM "
                                    "(BASELINE configs[3])",
                        "streams_per_gpu": B, "frames_per_step": B if args.shard else B * world,
-                       "n_az": args.n_az, "map_frames_before_timing": W,
+                       "n_az": args.n_az, "map_frames_before_timing": pre, "stride": args.stride,
                        "parallelism": (f"{B} streams, each sharded over {world} GPU(s): RCCL all-gather of the "
                                        f"5-NN candidates per round, all-reduce of the normal equations per LM "
                                        f"iteration" if args.shard else
@@ -531,24 +642,27 @@ def main():
             "kernel_ms_per_step": {k: round(v["ms"] / K, 4) for k, v in kt.items()},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "pose_rmse_vs_cpu": rmse,
+            "cpu_all_cores": allc,
         }
         if single is not None:
             out["single_stream"] = {k: round(v, 4) for k, v in single.items()}
         # the stages before the mapper (BASELINE configs[1], configs[2]): one stream, device time
-        # per frame (HIP events around each call) over the frames after the first 10, and the
-        # oracle's own timers over the cpu_baseline frames
+        # per frame (HIP events around each call) over the cpu_baseline frames (all frames after
+        # the first 10 without the CPU leg), and the oracle's own timers over the same frames
         stages = {}
         for name in ("scan_registration", "odometry"):
-            g = np.array(stage_ms[name][10:], dtype=np.float64)
+            sl = slice(pre, pre + K) if cpu_st is not None else slice(10, None)
+            g = np.array(stage_ms[name][sl], dtype=np.float64)
             if not len(g):
                 continue
             e = {"gpu_ms_per_frame": round(float(g.mean()), 4), "gpu_frames": int(len(g)),
                  "gpu_frames_per_s": round(1e3 / float(g.mean()), 1)}
             if name == "odometry":
-                it = float(np.sum(stage_ms["odometry_iters"][10:]))
+                it = float(np.sum(stage_ms["odometry_iters"][sl]))
                 e["gpu_lm_iters_per_s"] = round(it / (float(g.sum()) * 1e-3), 1)
             if cpu_st is not None:
-                c = cpu_st[name] / args.cpu_frames
+                c = cpu_st[name] / K
                 e.update(cpu_ms_per_frame=round(c, 4), cpu_cores=1, cpu_kind="port",
                          speedup=round(c / float(g.mean()), 2))
                 if name == "odometry":
@@ -561,6 +675,9 @@ def main():
         out["stages"] = stages
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(out["value"] / cpu["value"], 2)
+            out["speedup_vs_cpu_all_cores"] = round(out["value"] / allc["value"], 2)
+            if single is not None:
+                out["single_stream"]["speedup_vs_cpu_baseline"] = round(single["value"] / cpu["value"], 2)
         print(json.dumps(out), flush=True)
     for m in mappers:
         m.close()

@@ -12,8 +12,12 @@ def quat_angle(q1, q2):
     """rotation angle (rad) of q1^-1 q2 (xyzw)"""
     q1 = np.asarray(q1, dtype=np.float64)
     q2 = np.asarray(q2, dtype=np.float64)
-    d = abs(float(np.dot(q1, q2))) / (np.linalg.norm(q1) * np.linalg.norm(q2))
-    return 2.0 * np.arccos(min(1.0, d))
+    q1 = q1 / np.linalg.norm(q1)
+    q2 = q2 / np.linalg.norm(q2)
+    # conj(q1) * q2: w = q1.q2, v = w1 v2 - w2 v1 - v1 x v2 (atan2 keeps tiny angles exact)
+    w = float(np.dot(q1, q2))
+    v = q1[3] * q2[:3] - q2[3] * q1[:3] - np.cross(q1[:3], q2[:3])
+    return 2.0 * np.arctan2(float(np.linalg.norm(v)), abs(w))
 
 
 def snapshot(mp):
