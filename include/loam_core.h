@@ -31,6 +31,8 @@ extern "C" {
 #define LOAM_ERR_CAPACITY (-3)  /* a device buffer would overflow (see loam_params caps) */
 #define LOAM_ERR_STATE (-4)     /* call out of order (e.g. solve without input) */
 #define LOAM_ERR_NODEVICE (-5)  /* no HIP device / wrong architecture */
+#define LOAM_ERR_SYNC (-6)      /* a persistent LM round's workgroup hand-off timed out (lm.h spin
+                                   bound); the frame's state is not trustworthy: reset the stream */
 
 /* ROS parameters of loam_velodyne_HDL_64_kitti.launch:3-16 + vloam_main.launch:4, plus
  * device capacities.  loam_params_default() gives the KITTI launch values. */
@@ -41,7 +43,8 @@ typedef struct loam_params {
   int32_t map_pub_number;           /* 20 (laser_mapping.cpp:127) */
   double mapping_line_resolution;   /* 0.4 m (laser_mapping.cpp:99) */
   double mapping_plane_resolution;  /* 0.8 m (laser_mapping.cpp:101) */
-  int32_t detach_vo_lo;             /* 1 (laser_odometry.cpp:47) */
+  int32_t detach_vo_lo;             /* 1 (laser_odometry.cpp:47); 0: coupled mode, loam_odometry_set_prior
+                                       is required before every solve (:237-250) */
   int32_t verbose_level;            /* loam_verbose_level */
   /* device capacities (per stream) */
   int32_t max_input_points;         /* max points per input cloud (default 262144) */
@@ -141,6 +144,11 @@ int32_t loam_odometry_input(loam_odometry* h, int32_t stream, const float* sharp
 int32_t loam_odometry_input_device(loam_odometry* h, int32_t stream, const float* sharp, int32_t n_sharp,
                                    const float* less_sharp, int32_t n_less_sharp, const float* flat,
                                    int32_t n_flat, const float* less_flat, int32_t n_less_flat);
+/* the VO prior of the next solve, vloam_tf->velo_last_VOT_velo_curr (q xyzw, t), with
+ * detach_vo_lo = 0 (laser_odometry.cpp:237-250): both outer rounds start from it.  Required for
+ * every stream with an input when detach_vo_lo = 0 (solve returns LOAM_ERR_STATE otherwise),
+ * rejected (LOAM_ERR_STATE) when detach_vo_lo = 1; consumed by the solve; NULLs clear it. */
+int32_t loam_odometry_set_prior(loam_odometry* h, int32_t stream, const double* q_xyzw, const double* t_xyz);
 /* LaserOdometry::solveLO (laser_odometry.cpp:199-584) */
 int32_t loam_odometry_solve(loam_odometry* h);
 /* LaserOdometry::output (laser_odometry.cpp:660-679): q_w_curr, t_w_curr, q_last_curr,
@@ -185,7 +193,10 @@ int32_t loam_mapper_input_device_batch(loam_mapper* h, int32_t n, const int32_t*
                                        const uint64_t* d_surf, const int32_t* n_surf,
                                        const double* q_wodom, const double* t_wodom);
 /* LaserMapping::solveMapping (laser_mapping.cpp:212-814) for every stream that received an
- * input since the last call (skip_frame inputs only update the high-frequency pose). */
+ * input since the last call (skip_frame inputs only update the high-frequency pose).
+ * A negative status (LOAM_ERR_CAPACITY: a device buffer overflowed; LOAM_ERR_SYNC: an LM hand-off
+ * timed out; loam_last_error names the stream and the cause) still leaves the frame committed
+ * as computed (pose, insertion, re-VoxelGrid): reset the failed stream before relying on it. */
 int32_t loam_mapper_solve(loam_mapper* h);
 /* pose after solveMapping: q_w_curr (xyzw), t_w_curr (laser_mapping.cpp:826-832) */
 int32_t loam_mapper_pose(loam_mapper* h, int32_t stream, double* q_w, double* t_w);
@@ -202,7 +213,7 @@ int32_t loam_mapper_stats(loam_mapper* h, int32_t stream, loam_map_stats* st);
  * member lists + centroids, [46..47] of the latter: member lists, per-voxel sort + sums */
 #define LOAM_DEBUG_COUNTERS 48
 int32_t loam_mapper_debug_counters(loam_mapper* h, uint64_t* out, int32_t n, int32_t reset);
-/* sum over all streams of the LM iterations (both rounds) of the last solve */
+/* sum over the streams solved by the last loam_mapper_solve of their LM iterations (both rounds) */
 int64_t loam_mapper_total_iterations(loam_mapper* h);
 /* stats of streams 0..n-1 */
 int32_t loam_mapper_stats_all(loam_mapper* h, loam_map_stats* out, int32_t n);
@@ -379,6 +390,15 @@ int32_t loam_lm_normal_equations(int32_t device, const double* factors, int32_t 
 /* pcl::VoxelGrid<PointXYZI> (leaf metres) on one cloud; returns count in *n_out */
 int32_t loam_voxel_grid(int32_t device, const float* in, int32_t n, float leaf, float* out,
                         int32_t* n_out);
+/* pcl::VoxelGrid<PointXYZI> with PCL's own within-voxel summation order (the libstdc++
+ * sort permutation of voxel_grid.hpp's (idx, point) pairs) — the order ScanRegistration's
+ * per-ring filter uses (scan_registration.cpp:497-501).  loam_voxel_grid sums in input order
+ * (the mapper's filters). */
+int32_t loam_voxel_grid_pcl(int32_t device, const float* in, int32_t n, float leaf, float* out, int32_t* n_out);
+/* the permutation libstdc++'s introsort gives the elements (keys[i], i) compared by key only
+ * (the sector sort of scan_registration.cpp:365-366 and PCL's VoxelGrid sort), computed on the
+ * device by n_waves (1..16) cooperating waves */
+int32_t loam_sort_perm(int32_t device, const uint32_t* keys, int32_t n, int32_t n_waves, int32_t* perm);
 /* VoxelGrid of fixed ++ added where `fixed` is already a VoxelGrid output of the same leaf
  * whose centroids stayed in their voxels (the per-cube map update, laser_mapping.cpp:795-808):
  * same result as loam_voxel_grid on the concatenation.  *merged = 1 if the merge path ran

@@ -73,10 +73,22 @@ static inline Quat qinv(const Quat& q) {
 // ---------------------------------------------------------------------------------------
 // PCL VoxelGrid<PointXYZI>::applyFilter (pcl/filters/impl/voxel_grid.hpp, PCL 1.10):
 // bbox → leaf ijk = floor(p*inv) - min_b → idx = i + j*dx + k*dx*dy → sort → centroid of
-// x,y,z,intensity (CentroidPoint, float sums / float(n)).  PCL's std::sort is unstable;
-// here the within-voxel order is the input order (std::stable_sort) — the GPU uses the
-// same rule, so the float sums are bit-identical between oracle and kernel.
+// x,y,z,intensity (CentroidPoint, float sums / float(n)).  The sort is PCL's: std::sort of
+// cloud_point_index_idx {idx, cloud_point_index} with operator< comparing idx only, so the
+// order of a voxel's points (its float summation order) is libstdc++'s introsort permutation
+// (GCC 4.9-13 bits/stl_algo.h; this file is built with GCC 11, the same algorithm as the
+// GCC 7 / 9 of the reference's Ubuntu 18.04 / 20.04 ROS builds).
+// g_voxel_order = 1 sums a voxel's points in input order instead (std::stable_sort): the
+// order of the mapper's VoxelGrid kernels (voxel.h), for their bit-exact tests.
 // ---------------------------------------------------------------------------------------
+static int g_voxel_order = 0;  // 0: PCL (std::sort), 1: input order
+
+struct CloudPointIndexIdx {  // pcl::VoxelGrid's cloud_point_index_idx
+  uint32_t idx;
+  uint32_t cloud_point_index;
+  bool operator<(const CloudPointIndexIdx& p) const { return idx < p.idx; }
+};
+
 Cloud voxel_grid(const Cloud& in, float leaf) {
   Cloud out;
   if (in.empty()) return out;
@@ -99,7 +111,7 @@ Cloud voxel_grid(const Cloud& in, float leaf) {
   const int divx = maxbx - minbx + 1;
   const int divy = maxby - minby + 1;
   const int mul1 = divx, mul2 = divx * divy;
-  std::vector<std::pair<uint32_t, uint32_t>> iv(in.size());
+  std::vector<CloudPointIndexIdx> iv(in.size());
   for (size_t i = 0; i < in.size(); ++i) {
     const Pt& p = in[i];
     int i0 = static_cast<int>(std::floor(p.x * inv) - static_cast<float>(minbx));
@@ -108,16 +120,15 @@ Cloud voxel_grid(const Cloud& in, float leaf) {
     int idx = i0 + i1 * mul1 + i2 * mul2;
     iv[i] = {static_cast<uint32_t>(idx), static_cast<uint32_t>(i)};
   }
-  std::stable_sort(iv.begin(), iv.end(),
-                   [](const std::pair<uint32_t, uint32_t>& a,
-                      const std::pair<uint32_t, uint32_t>& b) { return a.first < b.first; });
+  if (g_voxel_order == 0) std::sort(iv.begin(), iv.end(), std::less<CloudPointIndexIdx>());
+  else std::stable_sort(iv.begin(), iv.end());
   size_t s = 0;
   while (s < iv.size()) {
     size_t e = s + 1;
-    while (e < iv.size() && iv[e].first == iv[s].first) ++e;
+    while (e < iv.size() && iv[e].idx == iv[s].idx) ++e;
     float sx = 0, sy = 0, sz = 0, si = 0;
     for (size_t k = s; k < e; ++k) {
-      const Pt& p = in[iv[k].second];
+      const Pt& p = in[iv[k].cloud_point_index];
       sx += p.x; sy += p.y; sz += p.z; si += p.intensity;
     }
     const float n = static_cast<float>(e - s);
@@ -1053,9 +1064,13 @@ struct ScanRegistration {
 };
 
 // ---------------------------------------------------------------------------------------
-// LaserOdometry::solveLO (laser_odometry.cpp:199-584), detach_VO_LO = true
+// LaserOdometry::solveLO (laser_odometry.cpp:199-584).  detach_VO_LO = true unless a VO prior
+// is set for the frame: then (!detach_VO_LO, :237-250) every outer round starts from it
+// (para_q / para_t overwritten with velo_last_VOT_velo_curr before the round's problem).
 // ---------------------------------------------------------------------------------------
 struct LaserOdometry {
+  bool has_prior = false;
+  double prior_q[4] = {0, 0, 0, 1}, prior_t[3] = {0, 0, 0};
   const double DISTANCE_SQ_THRESHOLD = 25;
   const double NEARBY_SCAN = 2.5;
   int mapping_skip_frame = 1;
@@ -1078,6 +1093,10 @@ struct LaserOdometry {
       systemInited = true;
     } else {
       for (int opti = 0; opti < 2; ++opti) {
+        if (has_prior) {  // laser_odometry.cpp:237-250
+          for (int i = 0; i < 4; ++i) para_q[i] = prior_q[i];
+          for (int i = 0; i < 3; ++i) para_t[i] = prior_t[i];
+        }
         std::vector<Factor> fs;
         int corner_c = 0, plane_c = 0;
         Quat q{para_q[0], para_q[1], para_q[2], para_q[3]};
@@ -1407,6 +1426,20 @@ int32_t oracle_voxel_grid(const float* in, int32_t n, float leaf, float* out) {
   return static_cast<int32_t>(c.size());
 }
 
+int32_t oracle_set_voxel_order(int32_t order) {
+  const int32_t old = g_voxel_order;
+  g_voxel_order = order ? 1 : 0;
+  return old;
+}
+
+int32_t oracle_std_sort_perm(const uint32_t* keys, int32_t n, int32_t* perm) {
+  std::vector<CloudPointIndexIdx> v(n);
+  for (int32_t i = 0; i < n; ++i) v[i] = {keys[i], static_cast<uint32_t>(i)};
+  std::sort(v.begin(), v.end(), std::less<CloudPointIndexIdx>());
+  for (int32_t i = 0; i < n; ++i) perm[i] = static_cast<int32_t>(v[i].cloud_point_index);
+  return n;
+}
+
 int32_t oracle_knn(const float* pts, int32_t n, const float* q, int32_t nq, int32_t k,
                    int32_t* idx, float* d2) {
   Cloud c = to_cloud(pts, n);
@@ -1559,6 +1592,14 @@ int32_t oracle_odom_input(oracle_odom* h, const float* full, int32_t nfull, cons
 }
 int32_t oracle_odom_solve(oracle_odom* h) {
   h->o.solve();
+  return 0;
+}
+int32_t oracle_odom_set_prior(oracle_odom* h, const double* q, const double* t) {
+  h->o.has_prior = q && t;
+  if (h->o.has_prior) {
+    for (int i = 0; i < 4; ++i) h->o.prior_q[i] = q[i];
+    for (int i = 0; i < 3; ++i) h->o.prior_t[i] = t[i];
+  }
   return 0;
 }
 int32_t oracle_odom_output(oracle_odom* h, double* q_w, double* t_w, double* q_lc, double* t_lc) {

@@ -26,8 +26,15 @@ extern "C" {
 /* ---- standalone primitives (4 floats per point: x, y, z, intensity) ---- */
 
 /* PCL VoxelGrid<PointXYZI>::filter semantics (leaf in metres); returns output count.
- * out must hold n points.  Within-voxel summation order = input order (stable). */
+ * out must hold n points.  Within-voxel summation order: PCL's (std::sort of (idx, point)
+ * comparing idx only), or input order after oracle_set_voxel_order(1).  Used by every
+ * VoxelGrid of the oracle pipeline (ScanRegistration, LaserMapping). */
 int32_t oracle_voxel_grid(const float* in, int32_t n, float leaf, float* out);
+/* 0: PCL order (default), 1: input order (the mapper kernels' documented order); returns the
+ * previous setting */
+int32_t oracle_set_voxel_order(int32_t order);
+/* the permutation libstdc++ std::sort produces on (keys[i], i) compared by key only */
+int32_t oracle_std_sort_perm(const uint32_t* keys, int32_t n, int32_t* perm);
 
 /* exact kNN (FLANN L2_Simple<float> distances, ties broken by index). */
 int32_t oracle_knn(const float* pts, int32_t n, const float* q, int32_t nq, int32_t k,
@@ -81,6 +88,9 @@ int32_t oracle_odom_input(oracle_odom* h, const float* full, int32_t nfull, cons
                           const float* flat, int32_t nflat, const float* less_flat,
                           int32_t nless_flat);
 int32_t oracle_odom_solve(oracle_odom* h);
+/* the VO prior velo_last_VOT_velo_curr (!detach_VO_LO, laser_odometry.cpp:237-250): q xyzw, t;
+ * used by every following solve until cleared with NULLs */
+int32_t oracle_odom_set_prior(oracle_odom* h, const double* q, const double* t);
 /* q_w[4] xyzw, t_w[3], q_lc[4], t_lc[3]; returns skip_frame */
 int32_t oracle_odom_output(oracle_odom* h, double* q_w, double* t_w, double* q_lc, double* t_lc);
 /* which: 0 cornerLast, 1 surfLast, 2 fullRes */

@@ -38,6 +38,8 @@ def lib():
         L = ctypes.CDLL(path)
         sig = {
             "oracle_voxel_grid": (c_i32, [vp, c_i32, c_f, vp]),
+            "oracle_set_voxel_order": (c_i32, [c_i32]),
+            "oracle_std_sort_perm": (c_i32, [vp, c_i32, vp]),
             "oracle_knn": (c_i32, [vp, c_i32, vp, c_i32, c_i32, vp, vp]),
             "oracle_edge_from_nbrs": (c_i32, [vp, vp, vp]),
             "oracle_plane_from_nbrs": (c_i32, [vp, vp, vp]),
@@ -54,6 +56,7 @@ def lib():
             "oracle_odom_destroy": (None, [vp]),
             "oracle_odom_input": (c_i32, [vp, vp, c_i32, vp, c_i32, vp, c_i32, vp, c_i32, vp, c_i32]),
             "oracle_odom_solve": (c_i32, [vp]),
+            "oracle_odom_set_prior": (c_i32, [vp, vp, vp]),
             "oracle_odom_output": (c_i32, [vp, vp, vp, vp, vp]),
             "oracle_odom_count": (c_i32, [vp, c_i32]),
             "oracle_odom_copy": (c_i32, [vp, c_i32, vp]),
@@ -109,6 +112,34 @@ def voxel_grid(pts, leaf):
     out = np.empty_like(pts)
     n = lib().oracle_voxel_grid(_ptr(pts), len(pts), leaf, _ptr(out))
     return out[:n].copy()
+
+
+def set_voxel_order(order):
+    """0: PCL's std::sort order (default), 1: input order; returns the previous setting"""
+    return int(lib().oracle_set_voxel_order(int(order)))
+
+
+class voxel_order:
+    """context manager: every oracle VoxelGrid inside uses `order` (0 PCL, 1 input order)"""
+
+    def __init__(self, order):
+        self.order = order
+
+    def __enter__(self):
+        self.old = set_voxel_order(self.order)
+        return self
+
+    def __exit__(self, *exc):
+        set_voxel_order(self.old)
+
+
+def std_sort_perm(keys):
+    """the permutation libstdc++ std::sort gives (keys[i], i) compared by key only (u32)"""
+    k = np.ascontiguousarray(keys, dtype=np.uint32)
+    perm = np.empty(len(k), dtype=np.int32)
+    if len(k):
+        lib().oracle_std_sort_perm(_ptr(k), len(k), _ptr(perm))
+    return perm
 
 
 def knn(pts, queries, k):
@@ -231,6 +262,14 @@ class LaserOdometry:
 
     def solve(self):
         lib().oracle_odom_solve(self.h)
+
+    def set_prior(self, q=None, t=None):
+        """VO prior (!detach_VO_LO): every outer round starts from it; None clears"""
+        if q is None:
+            lib().oracle_odom_set_prior(self.h, None, None)
+            return
+        self._prior = (np.ascontiguousarray(q, dtype=np.float64), np.ascontiguousarray(t, dtype=np.float64))
+        lib().oracle_odom_set_prior(self.h, _ptr(self._prior[0]), _ptr(self._prior[1]))
 
     def output(self):
         q = np.empty(4); t = np.empty(3); qlc = np.empty(4); tlc = np.empty(3)

@@ -45,7 +45,11 @@ def voxel_case():
     pts = np.zeros((6000, 4), np.float32)
     pts[:, :3] = rng.normal(0, 3, (6000, 3))
     pts[:, 3] = rng.uniform(0, 64, 6000)
-    return dict(pts=pts, leaf=np.float32(0.4), out=O.voxel_grid(pts, 0.4))
+    with O.voxel_order(1):
+        out_input = O.voxel_grid(pts, 0.4)
+    # out: PCL's summation order (std::sort of (idx, point) by idx); out_input_order: the
+    # mapper kernels' input order (voxel.h)
+    return dict(pts=pts, leaf=np.float32(0.4), out=O.voxel_grid(pts, 0.4), out_input_order=out_input)
 
 
 def lm_case():

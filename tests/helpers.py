@@ -59,3 +59,35 @@ def load_state(mapper, stream, snap):
     for which, key in ((0, "corner"), (1, "surf")):
         for cube, pts in snap[key].items():
             mapper.set_cube(stream, which, cube, pts)
+
+
+def voxel_members(pts, leaf):
+    """PCL VoxelGrid grouping (voxel_grid.hpp): the voxel idx of every point and, per output
+    voxel in increasing idx, its member count and largest |coordinate| (x, y, z, intensity)"""
+    p = np.asarray(pts, np.float32)
+    inv = np.float32(1.0) / np.float32(leaf)
+    mn, mx = p[:, :3].min(0), p[:, :3].max(0)
+    minb = np.floor(mn * inv).astype(np.int64)
+    div = np.floor(mx * inv).astype(np.int64) - minb + 1
+    ijk = (np.floor(p[:, :3] * inv) - minb.astype(np.float32)).astype(np.int64)
+    idx = ijk[:, 0] + ijk[:, 1] * div[0] + ijk[:, 2] * div[0] * div[1]
+    uniq, inverse, counts = np.unique(idx, return_inverse=True, return_counts=True)
+    amax = np.zeros((len(uniq), 4), np.float64)
+    np.maximum.at(amax, inverse, np.abs(p.astype(np.float64)))
+    return counts, amax
+
+
+def assert_centroids_within_order_bound(pts, leaf, got, ref):
+    """got and ref: VoxelGrid outputs of pts that differ only in the order a voxel's points are
+    summed (float32).  Two orders of m float additions differ by at most 2 (m - 1) u sum|x_i|
+    (u = 2^-24), and the division by m adds one rounding to each: per component
+    |got - ref| <= (2 (m - 1) + 2) u max|x_i| * m / m.  Voxels of 1 or 2 points are exact
+    (float addition commutes)."""
+    got, ref = np.asarray(got, np.float32), np.asarray(ref, np.float32)
+    assert got.shape == ref.shape
+    m, amax = voxel_members(pts, leaf)
+    assert len(m) == len(got)
+    d = np.abs(got.astype(np.float64) - ref.astype(np.float64))
+    bound = (2.0 * (m[:, None] - 1) + 2.0) * 2.0 ** -24 * amax
+    assert np.all(d <= bound), float((d - bound).max())
+    assert np.array_equal(got[m <= 2].view(np.uint32), ref[m <= 2].view(np.uint32))

@@ -36,6 +36,8 @@ def test_oracle_knn_fixture():
 def test_oracle_voxel_fixture():
     g = load("voxel")
     assert np.array_equal(O.voxel_grid(g["pts"], float(g["leaf"])), g["out"])
+    with O.voxel_order(1):
+        assert np.array_equal(O.voxel_grid(g["pts"], float(g["leaf"])), g["out_input_order"])
 
 
 def test_oracle_lm_fixture():
@@ -85,9 +87,15 @@ def test_gpu_knn_fixture():
 
 @pytest.mark.gpu
 def test_gpu_voxel_fixture():
+    """PCL-order kernel (voxel_pcl.h) bit-exact against PCL's order; the mapper's kernel
+    (voxel.h) bit-exact against input order and within the summation-order bound of PCL's"""
     from loam_amd import prims
+    from helpers import assert_centroids_within_order_bound
     g = load("voxel")
-    assert np.array_equal(prims.voxel_grid(g["pts"], float(g["leaf"])), g["out"])
+    assert np.array_equal(prims.voxel_grid_pcl(g["pts"], float(g["leaf"])), g["out"])
+    got = prims.voxel_grid(g["pts"], float(g["leaf"]))
+    assert np.array_equal(got, g["out_input_order"])
+    assert_centroids_within_order_bound(g["pts"], float(g["leaf"]), got, g["out"])
 
 
 @pytest.mark.gpu
@@ -113,10 +121,7 @@ def test_gpu_scanreg_fixture():
     sr.close()
     assert [len(x) for x in c] == list(g["counts"])
     for k, name in enumerate(("sharp", "less_sharp", "flat", "less_flat")):
-        # geometry bit-exact; intensity (ring + 0.1 relTime) may differ only by the
-        # whole-revolution wrap documented in tests/test_gpu_scanreg.py
-        assert np.array_equal(c[k + 1][:, :3], g[name][:, :3])
-        assert np.array_equal(np.floor(c[k + 1][:, 3]), np.floor(g[name][:, 3]))
+        assert np.array_equal(c[k + 1].view(np.uint32), g[name].view(np.uint32))  # bit-exact, intensity too
 
 
 @pytest.mark.gpu

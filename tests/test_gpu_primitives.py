@@ -1,7 +1,10 @@
 """GPU parity of the kernels behind the mapping stage, each against the CPU oracle.
 
 Bars: VoxelGrid and kNN are index/integer decisions + float arithmetic written in the same
-order on both sides -> bit-exact.  The LM normal equations are fp64 sums in a different
+order on both sides -> bit-exact.  Two VoxelGrid kernels: voxel_pcl.h sums a voxel's points in
+PCL's order (the libstdc++ std::sort permutation) and is bit-exact against the oracle's PCL
+filter; voxel.h (the mapper's) sums them in input order and is bit-exact against the oracle in
+that order and within the float summation-order bound of PCL's (helpers.py).  The LM normal equations are fp64 sums in a different
 order (device tree reduction vs sequential) -> 1e-10 relative.  The LM solve uses normal
 equations (Cholesky) on the device vs Householder QR (Ceres DENSE_QR) in the oracle ->
 pose within 1e-9 and identical iteration counts.
@@ -10,7 +13,8 @@ import numpy as np
 import pytest
 
 import loam_oracle as O
-from loam_amd import _core, synth
+from helpers import assert_centroids_within_order_bound
+from loam_amd import _core, prims, synth
 from loam_amd._core import lib, ptr, check
 
 pytestmark = pytest.mark.gpu
@@ -37,10 +41,60 @@ def test_voxel_grid_bit_exact(frame_clouds, which, leaf):
     cloud = frame_clouds[which]
     if which == 0:  # one ring-sized cloud, as in scan_registration.cpp:497-501
         cloud = cloud[:1800]
+    with O.voxel_order(1):
+        ref_in = O.voxel_grid(cloud, leaf)
     ref = O.voxel_grid(cloud, leaf)
     got = gpu_voxel(cloud, leaf)
-    assert got.shape == ref.shape
-    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert got.shape == ref_in.shape
+    assert np.array_equal(got.view(np.uint32), ref_in.view(np.uint32))
+    assert_centroids_within_order_bound(cloud, leaf, got, ref)
+    pcl = prims.voxel_grid_pcl(cloud, leaf)
+    assert np.array_equal(pcl.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("n,kv", [(5, 3), (16, 2), (17, 2), (300, 7), (4000, 30), (20000, 1000), (100000, 50)])
+def test_sort_perm_matches_std_sort(n, kv):
+    """the device std::sort emulation (stdsort.h) against libstdc++ itself: heavy ties"""
+    rng = np.random.default_rng(n)
+    keys = rng.integers(0, kv, n).astype(np.uint32)
+    for waves in (1, 16):
+        assert np.array_equal(prims.sort_perm(keys, waves), O.std_sort_perm(keys)), waves
+
+
+@pytest.mark.parametrize("pattern", range(5))
+def test_sort_perm_adversarial(pattern):
+    """sorted, reversed, organ-pipe and median-of-3-killer inputs: the depth-limit heap sort
+    (__partial_sort) and unbalanced partitions"""
+    n = 4096
+    i = np.arange(n)
+    if pattern == 0:
+        k = i
+    elif pattern == 1:
+        k = n - i
+    elif pattern == 2:
+        k = np.where(i < n // 2, i, n - i)
+    elif pattern == 3:
+        k = np.where(i % 2 == 1, i, n - i)
+    else:  # Musser's median-of-3 killer
+        h = n // 2
+        k = np.empty(n, np.int64)
+        k[:h] = np.where(np.arange(h) % 2 == 0, np.arange(h) + 1, h + np.arange(h))
+        k[h:] = 2 * (np.arange(n - h) + 1)
+    keys = k.astype(np.uint32)
+    assert np.array_equal(prims.sort_perm(keys, 16), O.std_sort_perm(keys))
+
+
+def test_voxel_grid_pcl_order_large_and_tied():
+    """PCL-order kernel on a quantized cloud (many points per voxel, coordinates on leaf
+    boundaries) and on a 60k-point cloud (global scratch path)"""
+    xyz, _ = synth.frame(6, 3, 2000, flags=synth.QUANTIZE)
+    pts = np.concatenate([xyz, np.arange(len(xyz), dtype=np.float32)[:, None] % 64], 1)
+    for leaf in (0.2, 0.8):
+        ref = O.voxel_grid(pts, leaf)
+        assert np.array_equal(prims.voxel_grid_pcl(pts, leaf).view(np.uint32), ref.view(np.uint32))
+        with O.voxel_order(1):
+            assert np.array_equal(gpu_voxel(pts, leaf).view(np.uint32), O.voxel_grid(pts, leaf).view(np.uint32))
+        assert_centroids_within_order_bound(pts, leaf, gpu_voxel(pts, leaf), ref)
 
 
 def test_voxel_grid_edge_cases():
@@ -49,10 +103,17 @@ def test_voxel_grid_edge_cases():
     assert np.array_equal(gpu_voxel(one, 0.4), one)
     dup = np.repeat(one, 100, axis=0)  # 100 identical points -> one centroid
     assert np.array_equal(gpu_voxel(dup, 0.4), O.voxel_grid(dup, 0.4))
+    assert np.array_equal(prims.voxel_grid_pcl(dup, 0.4), O.voxel_grid(dup, 0.4))
+    assert prims.voxel_grid_pcl(np.zeros((0, 4), np.float32), 0.4).shape == (0, 4)
     # negative coordinates straddling zero, several points per voxel
     rng = np.random.default_rng(0)
     pts = np.concatenate([rng.uniform(-3, 3, (5000, 3)), rng.uniform(0, 60, (5000, 1))], 1).astype(np.float32)
-    assert np.array_equal(gpu_voxel(pts, 0.4).view(np.uint32), O.voxel_grid(pts, 0.4).view(np.uint32))
+    with O.voxel_order(1):
+        assert np.array_equal(gpu_voxel(pts, 0.4).view(np.uint32), O.voxel_grid(pts, 0.4).view(np.uint32))
+    assert np.array_equal(prims.voxel_grid_pcl(pts, 0.4).view(np.uint32), O.voxel_grid(pts, 0.4).view(np.uint32))
+    # leaf too small for int32 voxel indices: PCL returns the input unchanged
+    far = np.array([[-1e6, 0, 0, 1], [0, 0, 0, 2], [1e6, 1e3, 1e3, 3]], np.float32)
+    assert np.array_equal(prims.voxel_grid_pcl(far, 0.01), far)
 
 
 def test_knn_radius_exact(frame_clouds):
@@ -138,7 +199,8 @@ def test_voxel_grid_many_unique_voxels():
     """more unique voxels than one LDS pass (12288): idx-range groups path"""
     rng = np.random.default_rng(5)
     pts = np.concatenate([rng.uniform(-20, 20, (60000, 3)), rng.uniform(0, 60, (60000, 1))], 1).astype(np.float32)
-    ref = O.voxel_grid(pts, 0.5)
+    with O.voxel_order(1):
+        ref = O.voxel_grid(pts, 0.5)
     got = gpu_voxel(pts, 0.5)
     assert len(ref) > 12288
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
@@ -150,8 +212,10 @@ def test_voxel_merge_bit_exact(frame_clouds, leaf, n_new):
     """map update path: VoxelGrid(fixed ++ added) with `fixed` a VoxelGrid fixed point; the merge
     kernel (n_new <= 4096) must equal the full filter bit for bit"""
     from loam_amd import prims
+    O.set_voxel_order(1)  # the mapper kernels' order (restored below)
     fixed = O.voxel_grid(frame_clouds[4], leaf)
     if not np.array_equal(O.voxel_grid(fixed, leaf), fixed):
+        O.set_voxel_order(0)
         pytest.skip("content is not a fixed point")
     rng = np.random.default_rng(n_new)
     # half the new points land in occupied voxels (jittered copies), half anywhere nearby
@@ -163,6 +227,7 @@ def test_voxel_merge_bit_exact(frame_clouds, leaf, n_new):
     added = np.concatenate([pick, far]).astype(np.float32)
     got, merged = prims.voxel_merge(fixed, added, leaf)
     ref = O.voxel_grid(np.concatenate([fixed, added]), leaf)
+    O.set_voxel_order(0)
     assert merged == (n_new <= 4096)
     assert got.shape == ref.shape
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))

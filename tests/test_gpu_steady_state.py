@@ -1,0 +1,109 @@
+"""GPU parity in the regime the bench times (BASELINE configs[3]): full-density frames
+(64 x 2000), steady-state maps (the 5x5x3-cube window saturated after ~150 m) and the window
+recentering of laser_mapping.cpp:252-444.
+
+One oracle pipeline run (scan registration -> odometry -> mapping, seed 11, 392 frames) feeds:
+  - teacher-forced frames 155 and 160: the oracle's map state before the frame loaded into the
+    device mapper, same inputs -> pose within 1e-4 m / 1e-4 rad, stack / submap /
+    correspondence counts and LM iterations identical, the updated map within 1e-5 m;
+  - the first recentering frame after 380 (grid shift, wrapped slabs cleared), teacher-forced;
+  - a free-running GPU pipeline (HIP scan registration -> HIP odometry -> HIP mapping on the raw
+    scans) over 300 frames against the oracle trajectory: per-scan pose deltas and RMSE.
+The oracle sums VoxelGrid voxels in PCL's order, the mapper's kernels in input order (their
+stacks and cubes differ within the summation-order bound): the pose bar holds.
+"""
+import numpy as np
+import pytest
+
+from helpers import load_state, quat_angle, run_sequence
+from loam_amd.mapping import BatchMapper
+
+pytestmark = pytest.mark.gpu
+
+SEED, N_AZ = 11, 2000
+STEADY = (155, 160)
+RECENTER = tuple(range(380, 392))
+
+
+@pytest.fixture(scope="module")
+def seq():
+    return run_sequence(seed=SEED, n_frames=RECENTER[-1] + 1, n_az=N_AZ, snapshot_frames=STEADY + RECENTER)
+
+
+def _check(m, rec):
+    q, t = m.pose(0)
+    qr, tr = rec["pose"]
+    st, sr = m.stats(0), rec["stats"]
+    assert np.linalg.norm(t - tr) < 1e-4 and quat_angle(q, qr) < 1e-4, (np.linalg.norm(t - tr), quat_angle(q, qr))
+    assert st.optimized == sr.optimized
+    assert (st.corner_stack, st.surf_stack, st.corner_map, st.surf_map) == \
+        (sr.corner_stack, sr.surf_stack, sr.corner_map, sr.surf_map)
+    assert list(st.corner_num) == list(sr.corner_num) and list(st.surf_num) == list(sr.surf_num)
+    assert [st.lm[0].iterations, st.lm[1].iterations] == [sr.lm[0].iterations, sr.lm[1].iterations]
+    assert list(st.center) == list(sr.center)
+
+
+def _check_map(m, after):
+    for which, key in ((0, "corner"), (1, "surf")):
+        got, ref = m.cubes(0, which), after[key]
+        assert sorted(got) == sorted(ref)
+        for c in ref:
+            assert got[c].shape == ref[c].shape, (key, c)
+            assert np.max(np.abs(got[c][:, :3] - ref[c][:, :3])) < 1e-5
+
+
+@pytest.mark.parametrize("fi", STEADY)
+def test_steady_state_teacher_forced(seq, fi):
+    rec = seq[fi]
+    assert rec["stats"].corner_map > 20000 and rec["stats"].surf_map > 10000  # saturated window
+    m = BatchMapper(1)
+    load_state(m, 0, rec["before"])
+    m.input(0, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+    m.solve()
+    _check(m, rec)
+    _check_map(m, rec["after"])
+    m.close()
+
+
+def test_full_density_recentering(seq):
+    shifted = [f for f in RECENTER if not np.array_equal(seq[f]["before"]["cen"], seq[f]["after"]["cen"])]
+    assert shifted, "no recentering in the probed frames"
+    rec = seq[shifted[0]]
+    m = BatchMapper(1)
+    load_state(m, 0, rec["before"])
+    m.input(0, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+    m.solve()
+    _check(m, rec)
+    cen, _, _ = m.get_state(0)
+    assert np.array_equal(cen, rec["after"]["cen"])
+    _check_map(m, rec["after"])
+    m.close()
+
+
+def test_free_running_300_frames(seq):
+    """the whole GPU chain on the raw scans, free-running, against the oracle chain"""
+    from loam_amd import synth
+    from loam_amd.odometry import BatchOdometry
+    from loam_amd.scanreg import ScanRegistration
+    sr, od, mp = ScanRegistration(), BatchOdometry(1), BatchMapper(1)
+    dt, dr = [], []
+    for f in range(300):
+        xyz, _ = synth.frame(SEED, f, N_AZ)
+        sr.input(xyz)
+        ptrs, counts = zip(*(sr.device_ptr(w) for w in (1, 2, 3, 4)))
+        od.input_device(0, ptrs, counts)
+        od.solve()
+        q, t, _, _, _ = od.output(0)
+        (pc, nc), (ps, ns) = od.last_cloud_device(0, 0), od.last_cloud_device(0, 1)
+        mp.input_device(0, pc, nc, ps, ns, q, t)
+        mp.solve()
+        qm, tm = mp.pose(0)
+        qr, tr = seq[f]["pose"]
+        dt.append(float(np.linalg.norm(tm - tr)))
+        dr.append(quat_angle(qm, qr))
+    dt, dr = np.array(dt), np.array(dr)
+    print(f"free-running 300 frames: trans rms {np.sqrt(np.mean(dt ** 2)):.3e} max {dt.max():.3e} m, "
+          f"rot rms {np.sqrt(np.mean(dr ** 2)):.3e} max {dr.max():.3e} rad")
+    assert dt.max() < 1e-4 and dr.max() < 1e-4
+    for h in (sr, od, mp):
+        h.close()

@@ -45,8 +45,10 @@ def test_knn_ties_break_by_index():
 
 
 # ---------------------------------------------------------------------------- VoxelGrid
-def voxel_grid_py(pts, leaf):
-    """pcl::VoxelGrid<PointXYZI>::applyFilter restated in float32 numpy (stable within voxel)"""
+def voxel_grid_py(pts, leaf, pcl_order=False):
+    """pcl::VoxelGrid<PointXYZI>::applyFilter restated in float32 numpy; a voxel's points are
+    summed in input order, or (pcl_order) in the order std::sort leaves (idx, point) pairs
+    compared by idx (the permutation taken from libstdc++ itself, oracle_std_sort_perm)"""
     p = pts.astype(np.float32)
     inv = np.float32(1.0) / np.float32(leaf)
     mn, mx = p[:, :3].min(0), p[:, :3].max(0)
@@ -55,7 +57,7 @@ def voxel_grid_py(pts, leaf):
     div = maxb - minb + 1
     ijk = (np.floor(p[:, :3] * inv) - minb.astype(np.float32)).astype(np.int64)
     idx = ijk[:, 0] + ijk[:, 1] * div[0] + ijk[:, 2] * div[0] * div[1]
-    order = np.argsort(idx, kind="stable")
+    order = O.std_sort_perm(idx.astype(np.uint32)) if pcl_order else np.argsort(idx, kind="stable")
     out = []
     i = 0
     while i < len(order):
@@ -75,9 +77,19 @@ def test_voxel_grid_matches_python(leaf):
     pts = np.zeros((3000, 4), np.float32)
     pts[:, :3] = rng.uniform(-3, 3, (3000, 3))
     pts[:, 3] = rng.uniform(0, 64, 3000)
-    got = O.voxel_grid(pts, leaf)
-    ref = voxel_grid_py(pts, leaf)
-    assert np.array_equal(got, ref)
+    assert np.array_equal(O.voxel_grid(pts, leaf), voxel_grid_py(pts, leaf, pcl_order=True))
+    with O.voxel_order(1):
+        assert np.array_equal(O.voxel_grid(pts, leaf), voxel_grid_py(pts, leaf))
+
+
+def test_std_sort_perm_is_a_sorting_permutation():
+    """the oracle's PCL sort: a permutation, keys ascending, and NOT the stable one on ties"""
+    rng = np.random.default_rng(3)
+    keys = rng.integers(0, 20, 5000).astype(np.uint32)
+    perm = O.std_sort_perm(keys)
+    assert sorted(perm) == list(range(len(keys)))
+    assert np.all(np.diff(keys[perm].astype(np.int64)) >= 0)
+    assert not np.array_equal(perm, np.argsort(keys, kind="stable"))
 
 
 def test_voxel_grid_overflow_returns_input():

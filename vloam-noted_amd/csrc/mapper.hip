@@ -48,7 +48,6 @@ constexpr int LM_THREADS = 256;
 constexpr int LM_EBLK = 32;     // LM evaluation workgroups per stream (grid-stride)
 constexpr int SUBMAP_BLOCKS = 64;
 constexpr int INS_SLOTS = WIN_VALID_MAX + EXTRA_CAP;
-constexpr int MAX_GROUPS = 4;  // stream groups launched on separate HIP streams
 constexpr int MAP_ERR_SUBMAP = 4, MAP_ERR_EXTRA = 8, MAP_ERR_HASH = 16, MAP_ERR_LM_SYNC = 32,
               MAP_ERR_INDEX = 64, MAP_ERR_LIVE = 128;
 
@@ -112,11 +111,6 @@ struct MapperDev {
   float4* ins_sorted;    // [B][2][max_in] inserted points grouped by target cube (input order kept)
   uint32_t* ins_off;     // [B][2][INS_SLOTS + 1] group offsets: window slots, then extra cubes
   unsigned long long* dbg;  // [LOAM_DEBUG_COUNTERS] phase cycle counters (loam_mapper_debug_counters)
-  uint32_t* rv_list[2];  // [B][2][INS_SLOTS] re-VoxelGrid slots for k_revox_merge (0) / k_revox (1),
-                         // a group's entries from 2 s0 INS_SLOTS
-  uint32_t* rv_count;    // [MAX_GROUPS][2] entries of the lists
-  int rv_split;          // 1: k_bucket lists the slots for k_revox_merge + k_revox; 0: k_revox
-                         // takes every slot (one workgroup per slot)
   uint32_t* stable_tok;  // [B][2][NCUBE] arena offset + 1 of content known to be a VoxelGrid
                          // fixed point (re-filtering it is the identity), else 0
   float4* vx_pts;  // [B][2][scratch_cap]
@@ -127,14 +121,7 @@ struct MapperDev {
   uint32_t* tickets;  // [B]
   // sharded mode (loam_mapper_create_sharded): this rank of nrank; map points are stored by
   // the rank owning their 4 m block (comm.h, shard_owner); blk_v: voxels per block edge
-  int knn_order = 0;  // corr_block ordering (LOAM_KNN_ORDER)
-  int stack_split = 0;   // k_stack_part / k_stack_gather around k_stack_ds (few streams)
   uint32_t compact_at = 0;  // an arena whose tail passed this is compacted
-  uint32_t* part_off;    // [B][2][SP_PARTS + 1]
-  uint32_t* part_cnt;    // [B][2][SP_PARTS]
-  int* part_split;       // [B][2] 1: the cloud was split this frame
-  float4* part_in;       // [B][2][max_in] the cloud ordered by range
-  float4* part_out;      // [B][2][max_in] every range's VoxelGrid output at its input offset
   int rank = 0, nrank = 1, sharded = 0;
   int blk_v[2] = {1, 1};
   uint32_t* wcnt;        // [B][2][WIN_MAX] window cube counts (all-reduced over the ranks)
@@ -200,142 +187,13 @@ __global__ void k_shift_cubes(MapperDev D, const uint2* __restrict__ old_tab, ui
 // ---------------------------------------------------------------------------------------
 // VoxelGrid of the incoming feature clouds -> CornerStack / SurfStack (:492-500)
 // ---------------------------------------------------------------------------------------
-// Split mode (handles of few streams, where one workgroup per cloud leaves the chip idle):
-// k_stack_part cuts a cloud into SP_PARTS contiguous ranges of voxel rows (z, y) of about equal
-// point counts, scattering the points stably (input order kept within a range); k_stack_ds
-// filters every range in its own workgroup; k_stack_gather concatenates the results.  PCL's
-// output order is lexicographic in (z, y, x) voxel index whatever the grid origin, and every
-// voxel lies in one range with its members in input order, so the concatenation is the
-// unsplit VoxelGrid bit for bit.  Clouds below SP_MIN points or with more than SP_ROWCAP rows
-// stay whole (partition 0 filters the input in place).
-constexpr int SP_PARTS = 8;
-constexpr int SP_MIN = 8192;
-constexpr int SP_ROWCAP = 24576;
-
-__global__ void __launch_bounds__(VX_THREADS) k_stack_part(MapperDev D) {
-  __shared__ uint32_t rows[SP_ROWCAP];
-  __shared__ uint32_t ws[VX_WAVES + 1];
-  __shared__ float bbs[VX_WAVES][4];
-  __shared__ int geo[4];
-  __shared__ uint32_t pbase[SP_PARTS];
-  __shared__ uint32_t wcnt[VX_WAVES][SP_PARTS];
-  const int s = D.s0 + (blockIdx.x >> 1), m = blockIdx.x & 1;
-  const StreamFrame& F = D.fr[s];
-  if (!F.active) return;
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const int n = m == 0 ? F.nc_in : F.ns_in;
-  const float4* src = F.in_ptr[m];
-  const size_t sm = sm_index(s, m);
-  uint32_t* po = D.part_off + sm * (SP_PARTS + 1);
-  float4* dst = D.part_in + sm * D.max_in;
-  const float inv = 1.0f / D.leaf[m];
-  // 1. y / z extent -> the (z, y) voxel rows
-  float y0 = 3.402823466e38f, z0 = 3.402823466e38f, y1 = -3.402823466e38f, z1 = -3.402823466e38f;
-  for (int i = tid; i < n; i += VX_THREADS) {
-    const float4 p = src[i];
-    y0 = fminf(y0, p.y); y1 = fmaxf(y1, p.y);
-    z0 = fminf(z0, p.z); z1 = fmaxf(z1, p.z);
-  }
-  y0 = wave_min_f(y0); z0 = wave_min_f(z0); y1 = wave_max_f(y1); z1 = wave_max_f(z1);
-  if (lane == 0) { bbs[wid][0] = y0; bbs[wid][1] = z0; bbs[wid][2] = y1; bbs[wid][3] = z1; }
-  __syncthreads();
-  if (tid == 0) {
-    for (int w = 1; w < VX_WAVES; ++w) {
-      y0 = fminf(y0, bbs[w][0]); z0 = fminf(z0, bbs[w][1]); y1 = fmaxf(y1, bbs[w][2]); z1 = fmaxf(z1, bbs[w][3]);
-    }
-    const int jmin = (int)floorf(y0 * inv), jmax = (int)floorf(y1 * inv);
-    const int kmin = (int)floorf(z0 * inv), kmax = (int)floorf(z1 * inv);
-    const long long R = (long long)(kmax - kmin + 1) * (long long)(jmax - jmin + 1);
-    const bool split = n >= SP_MIN && R > 0 && R <= SP_ROWCAP;
-    geo[0] = kmin; geo[1] = jmin; geo[2] = jmax - jmin + 1; geo[3] = split ? (int)R : 0;
-    D.part_split[sm] = split ? 1 : 0;
-    if (!split) {
-      po[0] = 0;
-      for (int p = 1; p <= SP_PARTS; ++p) po[p] = (uint32_t)n;
-    }
-  }
-  __syncthreads();
-  const int R = geo[3];
-  if (R == 0) return;
-  const int kmin = geo[0], jmin = geo[1], Jn = geo[2];
-  auto row_of = [&](const float4& p) { return ((int)floorf(p.z * inv) - kmin) * Jn + ((int)floorf(p.y * inv) - jmin); };
-  // 2. points per row, 3. exclusive prefix -> the range of each row
-  for (int r = tid; r < R; r += VX_THREADS) rows[r] = 0;
-  __syncthreads();
-  for (int i = tid; i < n; i += VX_THREADS) atomicAdd(&rows[row_of(src[i])], 1u);
-  __syncthreads();
-  const int per = (R + VX_THREADS - 1) / VX_THREADS, r0 = tid * per;
-  uint32_t sum = 0;
-  for (int k = 0; k < per; ++k)
-    if (r0 + k < R) sum += rows[r0 + k];
-  uint32_t tot;
-  uint32_t pre = vx_block_scan(sum, ws, &tot);
-  for (int k = 0; k < per; ++k)
-    if (r0 + k < R) {
-      const uint32_t c = rows[r0 + k];
-      rows[r0 + k] = min((uint32_t)(SP_PARTS - 1), (uint32_t)(((unsigned long long)pre * SP_PARTS) / (unsigned)n));
-      pre += c;
-    }
-  if (tid < SP_PARTS) pbase[tid] = 0;
-  __syncthreads();
-  // 4. stable counting sort of the points by range (one pass: counts, then ranks per chunk)
-  for (int i = tid; i < n; i += VX_THREADS) atomicAdd(&pbase[rows[row_of(src[i])]], 1u);
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t acc = 0;
-    for (int p = 0; p < SP_PARTS; ++p) {
-      const uint32_t c = pbase[p];
-      po[p] = acc;
-      pbase[p] = acc;
-      acc += c;
-    }
-    po[SP_PARTS] = acc;
-  }
-  __syncthreads();
-  for (int c0 = 0; c0 < n; c0 += VX_THREADS) {
-    const int i = c0 + tid;
-    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-    int pr = -1;
-    if (i < n) {
-      p = src[i];
-      pr = (int)rows[row_of(p)];
-    }
-    for (int k = tid; k < VX_WAVES * SP_PARTS; k += VX_THREADS) (&wcnt[0][0])[k] = 0;
-    __syncthreads();
-    uint32_t rank = 0;
-#pragma unroll
-    for (int q = 0; q < SP_PARTS; ++q) {
-      const uint64_t mk = __ballot(pr == q);
-      if (pr == q) rank = __popcll(mk & lanemask_lt());
-      if (lane == 0) wcnt[wid][q] = __popcll(mk);
-    }
-    __syncthreads();
-    if (tid < SP_PARTS) {
-      uint32_t acc = pbase[tid];
-      for (int w = 0; w < VX_WAVES; ++w) {
-        const uint32_t c = wcnt[w][tid];
-        wcnt[w][tid] = acc;
-        acc += c;
-      }
-      pbase[tid] = acc;
-    }
-    __syncthreads();
-    if (pr >= 0) dst[wcnt[wid][pr] + rank] = p;
-    __syncthreads();
-  }
-}
-
-// grid B * 2 (whole clouds) or B * 2 * SP_PARTS (split mode, D.stack_split)
+// one 1024-thread workgroup per (stream, map): grid B * 2
 __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
-  const int P = D.stack_split ? SP_PARTS : 1;
-  const int b = blockIdx.x / P, part = blockIdx.x % P;
-  const int s = D.s0 + (b >> 1), m = b & 1;
+  const int s = D.s0 + (blockIdx.x >> 1), m = blockIdx.x & 1;
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
   const size_t sm = sm_index(s, m);
-  const bool split = D.stack_split && D.part_split[sm];
-  if (!split && part > 0) return;
   VoxSeg S;
   S.src1 = nullptr;
   S.tag1 = nullptr;
@@ -348,55 +206,15 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
   S.scratch_tail = nullptr;
   S.err = &F.err;
   S.prof_seg = D.dbg + 42;  // stack VoxelGrid phases: dbg[42..45]
-  if (!split) {
-    S.src0 = F.in_ptr[m];
-    S.n0 = m == 0 ? F.nc_in : F.ns_in;
-    S.out = D.stack[m] + (size_t)s * D.max_in;
-    S.cap = D.max_in;
-    S.res_cnt = reinterpret_cast<uint32_t*>(m == 0 ? &F.nc_stack : &F.ns_stack);
-    S.scratch_pts = D.vx_pts + sm * D.scratch_cap;
-    S.scratch_idx = D.vx_idx + sm * D.scratch_cap;
-    S.scratch_cap = D.scratch_cap;
-  } else {  // range `part` of the split cloud, into its own slice of part_out
-    const uint32_t* po = D.part_off + sm * (SP_PARTS + 1);
-    const uint32_t o = po[part];
-    S.src0 = D.part_in + sm * D.max_in + o;
-    S.n0 = (int)(po[part + 1] - o);
-    S.out = D.part_out + sm * D.max_in + o;
-    S.cap = po[part + 1] - o;
-    S.res_cnt = D.part_cnt + sm * SP_PARTS + part;
-    S.scratch_pts = D.vx_pts + sm * D.scratch_cap + o;
-    S.scratch_idx = D.vx_idx + sm * D.scratch_cap + o;
-    S.scratch_cap = S.cap;
-  }
+  S.src0 = F.in_ptr[m];
+  S.n0 = m == 0 ? F.nc_in : F.ns_in;
+  S.out = D.stack[m] + (size_t)s * D.max_in;
+  S.cap = D.max_in;
+  S.res_cnt = reinterpret_cast<uint32_t*>(m == 0 ? &F.nc_stack : &F.ns_stack);
+  S.scratch_pts = D.vx_pts + sm * D.scratch_cap;
+  S.scratch_idx = D.vx_idx + sm * D.scratch_cap;
+  S.scratch_cap = D.scratch_cap;
   voxel_segment(S, lds);
-}
-
-// split mode: the ranges' outputs, concatenated in range order, become the stack
-__global__ void __launch_bounds__(VX_THREADS) k_stack_gather(MapperDev D) {
-  __shared__ uint32_t dst_off[SP_PARTS + 1];
-  const int s = D.s0 + (blockIdx.x >> 1), m = blockIdx.x & 1;
-  StreamFrame& F = D.fr[s];
-  const size_t sm = sm_index(s, m);
-  if (!F.active || !D.part_split[sm]) return;
-  const uint32_t* po = D.part_off + sm * (SP_PARTS + 1);
-  if (threadIdx.x == 0) {
-    uint32_t acc = 0;
-    for (int p = 0; p < SP_PARTS; ++p) {
-      dst_off[p] = acc;
-      acc += D.part_cnt[sm * SP_PARTS + p];
-    }
-    dst_off[SP_PARTS] = acc;
-    if (m == 0) F.nc_stack = (int)acc;
-    else F.ns_stack = (int)acc;
-  }
-  __syncthreads();
-  float4* out = D.stack[m] + (size_t)s * D.max_in;
-  const float4* in = D.part_out + sm * D.max_in;
-  for (int p = 0; p < SP_PARTS; ++p) {
-    const uint32_t c = dst_off[p + 1] - dst_off[p];
-    for (uint32_t i = threadIdx.x; i < c; i += VX_THREADS) out[dst_off[p] + i] = in[po[p] + i];
-  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -485,19 +303,11 @@ struct WinMap {  // per (stream, map) window cubes, in LDS
 // union's 5th from above, so it is safe), and a butterfly merge leaves the union's 5 nearest in
 // every lane.  The result is the L = 1 result (the minimum over (d, key) of the same
 // candidates); L > 1 shortens each query's chain of dependent loads.
-// block -> (stream, member).  Default: stream b % B, member b / B (a stream's blocks on one XCD,
-// b % 8, when B is a multiple of 8).  knn_order 1: the same XCD per stream, but each XCD runs
-// its streams one after another (b = 8 k + xcd, stream xcd + 8 (k / CORR_BLK)), so fewer
-// streams' cell indexes share an XCD's L2 at a time.
+// block -> (stream, member): stream b % B, member b / B (a stream's blocks on one XCD, b % 8,
+// when B is a multiple of 8: they share that XCD's L2 copy of the stream's cell indexes)
 __device__ inline void corr_block(const MapperDev& D, int* s, int* blk) {
-  if (D.knn_order && (D.B & 7) == 0) {
-    const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
-    *s = D.s0 + x + 8 * (k / CORR_BLK);
-    *blk = k % CORR_BLK;
-  } else {
-    *s = D.s0 + blockIdx.x % D.B;
-    *blk = blockIdx.x / D.B;
-  }
+  *s = D.s0 + blockIdx.x % D.B;
+  *blk = blockIdx.x / D.B;
 }
 
 #ifndef KNN_WAVES
@@ -875,7 +685,6 @@ __global__ void k_pose_adopt(MapperDev D) {
 // insertion of the stacks into the cube grid with the final pose (laser_mapping.cpp:741-788)
 // ---------------------------------------------------------------------------------------
 __global__ void k_insert(MapperDev D) {
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2) D.rv_count[2 * (D.s0 / D.B) + threadIdx.x] = 0;  // k_bucket's lists
   const int s = D.s0 + blockIdx.y;
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
@@ -934,25 +743,6 @@ __device__ inline bool revox_target(const MapperDev& D, int s, int m, int slot, 
   *cube_out = cube;
   *append_out = append;
   return true;
-}
-
-// Re-VoxelGrid of one slot's cube, then its cell index.  MERGE: the merge path only, in a
-// workgroup of NT threads with LW LDS words (merge capacity CAP); returns false, with nothing
-// written, when the merge cannot run (grid overflow).  Otherwise: merge or full filter in a
-// VX_THREADS workgroup with the whole LDS.
-constexpr int RV_NT = 512;                    // k_revox_merge workgroup
-constexpr int RV_CAP = 2048;                  // its merge capacity (new points)
-constexpr int RV_LW = 9 * RV_CAP + 256;       // its LDS words: 74 KiB, two workgroups per CU
-constexpr int RV_MAXT = 16384;                // its LDS cell-index tables
-constexpr int RV_SMALL_N = RV_MAXT / 2;       // k_revox_merge cubes: old + new points below this
-static_assert(RV_MAXT + RV_NT / 64 + 1 <= RV_LW - 256, "k_revox_merge LDS");
-
-__device__ inline bool revox_merge_ok(const MapperDev& D, int s, int m, int slot, int cube, int append) {
-  if (append) return false;
-  const uint32_t* ioff = D.ins_off + sm_index(s, m) * (INS_SLOTS + 1);
-  const uint32_t n_new = ioff[slot + 1] - ioff[slot];
-  const uint2 cv = D.cube_tab[sm_index(s, m) * NCUBE + cube];
-  return n_new > 0 && n_new <= (uint32_t)RV_CAP && cv.y > 0 && D.stable_tok[sm_index(s, m) * NCUBE + cube] == cv.x + 1;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1032,27 +822,16 @@ __global__ void __launch_bounds__(VX_THREADS) k_bucket(MapperDev D) {
     if (sl >= 0) out[wcnt[wid][sl] + rank] = pts[i];
     __syncthreads();
   }
-  // the re-VoxelGrid work of each slot: merges of cubes small enough for k_revox_merge's LDS,
-  // everything else for k_revox
-  if (D.rv_split && tid < INS_SLOTS) {
-    int cube = 0, append = 0;
-    if (revox_target(D, s, m, tid, &cube, &append)) {
-      const uint32_t n_new = off[tid + 1] - off[tid];
-      const uint32_t n0 = D.cube_tab[sm_index(s, m) * NCUBE + cube].y;
-      const int k = revox_merge_ok(D, s, m, tid, cube, append) && n0 + n_new < (uint32_t)RV_SMALL_N ? 0 : 1;
-      const int g = D.s0 / D.B;
-      D.rv_list[k][2 * (size_t)D.s0 * INS_SLOTS + atomicAdd(&D.rv_count[2 * g + k], 1u)] =
-          (uint32_t)(sm * INS_SLOTS + tid);
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------------------
 // re-VoxelGrid of every window cube (old content ++ inserted points, :795-808); cubes outside
-// the window that received points get them appended raw (:762).  One workgroup per cube.
+// the window that received points get them appended raw (:762).  One workgroup per cube:
+// the merge path (a fixed-point cube plus a few new points, voxel.h vx_merge_fixed_point) or
+// the full filter in a VX_THREADS workgroup with the whole LDS, then the cube's cell index.
 // ---------------------------------------------------------------------------------------
-template <int NT, int CAP, int LW, int MAXT, bool MERGE>
 __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube, int append, uint32_t* lds) {
+  constexpr int LW = VX_LDS_WORDS;
   StreamFrame& F = D.fr[s];
   const uint32_t* ioff = D.ins_off + sm_index(s, m) * (INS_SLOTS + 1);
   const uint32_t i0 = ioff[slot], n_new = ioff[slot + 1] - i0;
@@ -1083,18 +862,12 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
   S.prof = D.dbg + 11;  // merge phases: dbg[11..14]
   bool merged = false;
   const unsigned long long t0 = __builtin_readcyclecounter();
-  if (MERGE) {
-    merged = vx_merge_fixed_point<NT, CAP, LW>(S, lds);
-    __syncthreads();
-    if (!merged) vx_copy_through<NT>(S, lds + LW - 3);  // grid overflow: output = input (PCL)
-  } else {
-    if (!append && n_new > 0 && n_new <= VX_MERGE_CAP && cv.y > 0 && *tok == cv.x + 1) {
-      merged = vx_merge_fixed_point(S, lds);
-      __syncthreads();  // false: grid overflow, full filter below
-    }
-    if (!merged) voxel_segment(S, lds);
-    __syncthreads();
+  if (!append && n_new > 0 && n_new <= VX_MERGE_CAP && cv.y > 0 && *tok == cv.x + 1) {
+    merged = vx_merge_fixed_point(S, lds);
+    __syncthreads();  // false: grid overflow, full filter below
   }
+  if (!merged) voxel_segment(S, lds);
+  __syncthreads();
   const unsigned long long t1 = __builtin_readcyclecounter();
   // the cube's new content -> its cell index (cubeindex.h)
   uint32_t* res = lds + LW - 2;
@@ -1108,7 +881,7 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
   __syncthreads();  // res may lie in the index build's LDS
   int corner[3];
   cube_corner(cube, F.cen, corner);
-  if (!cube_index_build<NT, MAXT>(ar + off, n, corner, carena_base(D, s, m, F.arena_active[m]) + off,
+  if (!cube_index_build<VX_THREADS, CI_LDS_MAX_T>(ar + off, n, corner, carena_base(D, s, m, F.arena_active[m]) + off,
                                   ctab_base(D, s, m, F.arena_active[m]) + 4 * (size_t)off, lds, D.dbg + 16) &&
       threadIdx.x == 0)
     atomicOr(&F.err, MAP_ERR_INDEX);
@@ -1129,39 +902,19 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
     atomicAdd(&D.dbg[32 + hb], t2 - t0);
     if (merged) {
       atomicAdd(&D.dbg[3], (unsigned long long)n_new);  // new points of merged cubes
-      if (!MERGE) atomicAdd(&D.dbg[7], 1ull);          // merges run by the full-size kernel
+      atomicAdd(&D.dbg[7], 1ull);                       // merges
     }
   }
 }
 
-// The slots listed by k_bucket: merges of small cubes in 512-thread workgroups, two per CU
-// (k_revox_merge), the rest in VX_THREADS workgroups with the whole LDS (k_revox).  The two
-// run side by side on a group's two HIP streams.  Blocks past a list's end exit at once (a
-// grid-stride loop over the list spills k_revox's registers).
-__global__ void __launch_bounds__(RV_NT, 2) k_revox_merge(MapperDev D) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[RV_LW];
-  const uint32_t e = blockIdx.x;
-  if (e >= D.rv_count[2 * (D.s0 / D.B)]) return;
-  const uint32_t item = D.rv_list[0][2 * (size_t)D.s0 * INS_SLOTS + e];
-  const int slot = (int)(item % INS_SLOTS), sm = (int)(item / INS_SLOTS);
-  int cube = 0, append = 0;
-  revox_target(D, sm >> 1, sm & 1, slot, &cube, &append);
-  revox_item<RV_NT, RV_CAP, RV_LW, RV_MAXT, true>(D, sm >> 1, sm & 1, slot, cube, append, lds);
-}
-
+// one workgroup per (stream, map, slot): block = slot item
 __global__ void __launch_bounds__(VX_THREADS) k_revox(MapperDev D) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
-  const uint32_t e = blockIdx.x;
-  uint32_t item = 2 * (uint32_t)D.s0 * INS_SLOTS + e;  // rv_split 0: block = slot
-  if (D.rv_split) {
-    if (e >= D.rv_count[2 * (D.s0 / D.B) + 1]) return;
-    item = D.rv_list[1][2 * (size_t)D.s0 * INS_SLOTS + e];
-  }
+  const uint32_t item = 2 * (uint32_t)D.s0 * INS_SLOTS + blockIdx.x;
   const int slot = (int)(item % INS_SLOTS), sm = (int)(item / INS_SLOTS);
   int cube = 0, append = 0;
   if (!revox_target(D, sm >> 1, sm & 1, slot, &cube, &append)) return;
-  revox_item<VX_THREADS, (int)VX_MERGE_CAP, VX_LDS_WORDS, CI_LDS_MAX_T, false>(D, sm >> 1, sm & 1, slot, cube, append,
-                                                                              lds);
+  revox_item(D, sm >> 1, sm & 1, slot, cube, append, lds);
 }
 
 // cell index of one cube whose content was set through the API (cen: the host's grid centre)
@@ -1351,9 +1104,27 @@ struct HostStream {
   double pose[7] = {0, 0, 0, 1, 0, 0, 0};
   double q_hf[4] = {0, 0, 0, 1}, t_hf[3] = {0, 0, 0};
   bool pending = false, skip = false;
+  bool solved_last = false;  // solved by the last loam_mapper_solve (loam_mapper_total_iterations)
   int frame = 0;
   loam_map_stats st{};
 };
+
+// device error flags of a stream -> message (VX_ERR_* of voxel.h, MAP_ERR_* above)
+inline std::string map_err_text(int e) {
+  std::string m;
+  auto add = [&](int bit, const char* what) {
+    if (e & bit) m += (m.empty() ? "" : ", ") + std::string(what);
+  };
+  add(VX_ERR_CAPACITY, "VoxelGrid scratch full");
+  add(VX_ERR_OUTPUT, "map arena full (max_map_points)");
+  add(MAP_ERR_SUBMAP, "submap larger than max_submap_points");
+  add(MAP_ERR_EXTRA, "too many out-of-window insertions");
+  add(MAP_ERR_HASH, "cell table full");
+  add(MAP_ERR_LM_SYNC, "LM workgroup hand-off timed out");
+  add(MAP_ERR_INDEX, "cube cell index capacity");
+  add(MAP_ERR_LIVE, "live map larger than the arena's compaction bound");
+  return m + " (flags " + std::to_string(e) + ")";
+}
 
 }  // namespace loam
 
@@ -1372,16 +1143,6 @@ struct loam_mapper {
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;  // stack VoxelGrid, concurrent with the submap / hash build
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  // stream groups: group g > 0 runs its launch sequence on its own HIP streams, so the
-  // groups' phases (memory-bound kNN, fp64 LM, LDS-bound re-VoxelGrid) overlap on the CUs
-  int groups = 1;
-  hipStream_t gst[MAX_GROUPS] = {}, gst2[MAX_GROUPS] = {};
-  hipEvent_t gfork[MAX_GROUPS] = {}, gjoin[MAX_GROUPS] = {}, gdone[MAX_GROUPS] = {};
-  // stagger: phase p of group g waits for phase p of group g - 1, keeping the groups one
-  // kernel apart (LOAM_MAPPER_STAGGER=1)
-  int stagger = 0;
-  static constexpr int NPHASE = 10;
-  hipEvent_t gph[MAX_GROUPS][NPHASE] = {};
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   MapperDev D{};
   PinnedArray<StreamFrame> hf;  // pinned: the per-frame H2D / D2H of the stream records
@@ -1398,12 +1159,12 @@ struct loam_mapper {
   // the window that receive points; a write past the capacity is reported (err flags)
   uint32_t compact_at = 0;
   int lm_G = 0;  // workgroups per stream of k_lm_round (0: two-kernel path k_lm_eval / k_lm_step)
-  int knn_lanes = 1;  // lanes per query of k_knn (LOAM_KNN_LANES: 1, 2, 4, 8)
+  int knn_lanes = 1;  // lanes per query of k_knn (1, or 2 for handles of <= 4 streams)
   loam_comm* comm = nullptr;  // sharded mode (loam_mapper_create_sharded)
   PinnedArray<int> q_off;     // [B + 1] query offsets of the sharded kNN exchange
   int* d_q_off = nullptr;
-  // hipGraph of the whole per-frame sequence (default for <= 4 streams; LOAM_MAPPER_GRAPH): one per cube-table parity,
-  // used for frames without recentering, profiling, groups or sharding
+  // hipGraph of the whole per-frame sequence (handles of <= 4 streams): one per cube-table
+  // parity, used for frames without recentering, compaction, profiling or sharding
   int use_graph = 0;
   hipGraphExec_t gexec[2] = {nullptr, nullptr};
   // publish-side buffers (grown on demand)
@@ -1449,17 +1210,6 @@ void free_all(loam_mapper* h) {
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->st) (void)hipStreamDestroy(h->st);
   if (h->st2) (void)hipStreamDestroy(h->st2);
-  for (int g = 1; g < MAX_GROUPS; ++g) {  // group 0 uses st / st2 / ev_fork / ev_join
-    if (h->gst[g]) (void)hipStreamDestroy(h->gst[g]);
-    if (h->gst2[g]) (void)hipStreamDestroy(h->gst2[g]);
-    if (h->gfork[g]) (void)hipEventDestroy(h->gfork[g]);
-    if (h->gjoin[g]) (void)hipEventDestroy(h->gjoin[g]);
-  }
-  for (int g = 0; g < MAX_GROUPS; ++g) {
-    if (h->gdone[g]) (void)hipEventDestroy(h->gdone[g]);
-    for (auto& e : h->gph[g])
-      if (e) (void)hipEventDestroy(e);
-  }
 }
 
 void host_initial_guess(HostStream& H, double* pose) {
@@ -1572,47 +1322,12 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     return fail(LOAM_ERR_HIP);
   for (auto& e : h->ev)
     if (hipEventCreate(&e) != hipSuccess) return fail(LOAM_ERR_HIP);
-  {
-    // LOAM_MAPPER_GROUPS: stream groups on separate HIP streams (B divisible by the count)
-    const char* genv = std::getenv("LOAM_MAPPER_GROUPS");
-    int ng = (genv && !comm) ? std::atoi(genv) : 1;  // sharded: one group (collectives on st)
-    ng = std::max(1, std::min(ng, MAX_GROUPS));
-    while (ng > 1 && B % ng != 0) --ng;
-    h->groups = ng;
-    h->gst[0] = h->st;
-    h->gst2[0] = h->st2;
-    h->gfork[0] = h->ev_fork;
-    h->gjoin[0] = h->ev_join;
-    for (int g = 0; g < ng; ++g) {
-      if (g > 0 && (hipStreamCreateWithFlags(&h->gst[g], hipStreamNonBlocking) != hipSuccess ||
-                    hipStreamCreateWithFlags(&h->gst2[g], hipStreamNonBlocking) != hipSuccess ||
-                    hipEventCreateWithFlags(&h->gfork[g], hipEventDisableTiming) != hipSuccess ||
-                    hipEventCreateWithFlags(&h->gjoin[g], hipEventDisableTiming) != hipSuccess))
-        return fail(LOAM_ERR_HIP);
-      if (hipEventCreateWithFlags(&h->gdone[g], hipEventDisableTiming) != hipSuccess) return fail(LOAM_ERR_HIP);
-      for (auto& e : h->gph[g])
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(LOAM_ERR_HIP);
-    }
-    const char* senv = std::getenv("LOAM_MAPPER_STAGGER");
-    h->stagger = (senv && senv[0] == '1') ? 1 : 0;
-    // graphs pay off where launch gaps are the cost (B = 1: 0.750 -> 0.733 ms per frame); with
-    // two handles of 64 streams, graph launches measured 20% slower (375k vs 470k iterations/s)
-    const char* genv2 = std::getenv("LOAM_MAPPER_GRAPH");
-    h->use_graph = genv2 ? (genv2[0] == '1' ? 1 : 0) : (n_streams <= 4 ? 1 : 0);
-    const char* oenv = std::getenv("LOAM_KNN_ORDER");
-    D.knn_order = (oenv && oenv[0] == '1') ? 1 : 0;
-    // 2 lanes per query when few streams leave the chip idle (B = 1: 0.254 -> 0.190 ms of
-    // correspondence per frame); 1 lane once the streams fill it (B = 64: 2 lanes are 1.4x
-    // slower).  LOAM_KNN_LANES overrides.
-    h->knn_lanes = n_streams <= 4 ? 2 : 1;
-    const char* kenv = std::getenv("LOAM_KNN_LANES");
-    if (kenv) {
-      const int l = std::atoi(kenv);
-      h->knn_lanes = (l == 2 || l == 4 || l == 8) ? l : 1;
-    }
-    const char* renv = std::getenv("LOAM_REVOX_SPLIT");  // 1: k_revox_merge + k_revox
-    D.rv_split = (renv && renv[0] == '1') ? 1 : 0;
-  }
+  // graphs pay off where launch gaps are the cost (B = 1: 0.750 -> 0.733 ms per frame); with
+  // two handles of 64 streams, graph launches measured 20% slower (375k vs 470k iterations/s)
+  h->use_graph = n_streams <= 4 ? 1 : 0;
+  // 2 lanes per query when few streams leave the chip idle (B = 1: 0.254 -> 0.190 ms of
+  // correspondence per frame); 1 lane once the streams fill it (B = 64: 2 lanes are 1.4x slower)
+  h->knn_lanes = n_streams <= 4 ? 2 : 1;
   ALLOC(D.fr, B);
   for (int m = 0; m < 2; ++m) {
     ALLOC(D.in_pts[m], B * D.max_in);
@@ -1640,9 +1355,6 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   ALLOC(D.ins_off, B * 2 * (size_t)(INS_SLOTS + 1));
   ALLOC(D.stable_tok, B * 2 * (size_t)NCUBE);
   ALLOC(h->tok_tmp, B * 2 * (size_t)NCUBE);
-  ALLOC(D.rv_list[0], B * 2 * (size_t)INS_SLOTS);
-  ALLOC(D.rv_list[1], B * 2 * (size_t)INS_SLOTS);
-  ALLOC(D.rv_count, 2 * MAX_GROUPS);
   ALLOC(D.dbg, LOAM_DEBUG_COUNTERS);
   ALLOC(D.vx_pts, B * 2 * (size_t)D.scratch_cap);
   ALLOC(D.vx_idx, B * 2 * (size_t)D.scratch_cap);
@@ -1651,19 +1363,6 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   ALLOC(D.lm_xpub, B * 2 * 8);
   ALLOC(D.tickets, B);
   ALLOC(h->d_map_off, 2 * NCUBE + 1);
-  {
-    // split stack VoxelGrid (LOAM_STACK_SPLIT=1): measured slower, B = 1 0.733 -> 0.789 ms
-    // per frame (the single-workgroup partition pass costs more than the ranges save), B = 128
-    // 480k -> 316k iterations/s; kept as an option, bit-exact (tests/test_gpu_mapping.py)
-    const char* senv2 = std::getenv("LOAM_STACK_SPLIT");
-    D.stack_split = (senv2 && senv2[0] == '1') ? 1 : 0;
-    const size_t np = D.stack_split ? B : 1;
-    ALLOC(D.part_off, np * 2 * (SP_PARTS + 1));
-    ALLOC(D.part_cnt, np * 2 * SP_PARTS);
-    ALLOC(D.part_split, np * 2);
-    ALLOC(D.part_in, D.stack_split ? B * 2 * (size_t)D.max_in : 1);
-    ALLOC(D.part_out, D.stack_split ? B * 2 * (size_t)D.max_in : 1);
-  }
   ALLOC(h->d_new_off, B * 2 * (NCUBE + 1));
   if (D.sharded) {
     for (int m = 0; m < 2; ++m) D.blk_v[m] = shard_block_voxels(D.leaf[m]);
@@ -1839,7 +1538,8 @@ int32_t loam_mapper_input_device_batch(loam_mapper* h, int32_t n, const int32_t*
 int64_t loam_mapper_total_iterations(loam_mapper* h) {
   if (!h) return LOAM_ERR_ARG;
   int64_t it = 0;
-  for (int s = 0; s < h->B; ++s) it += h->hs[s].st.lm[0].iterations + h->hs[s].st.lm[1].iterations;
+  for (int s = 0; s < h->B; ++s)
+    if (h->hs[s].solved_last) it += h->hs[s].st.lm[0].iterations + h->hs[s].st.lm[1].iterations;
   return it;
 }
 
@@ -1906,8 +1606,7 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   bool compact_due = false;  // the graph path has no compaction step: such frames run without it
   for (int s = 0; s < B && !compact_due; ++s)
     compact_due = h->hf[s].arena_tail[0] > h->compact_at || h->hf[s].arena_tail[1] > h->compact_at;
-  const bool graph = h->use_graph && !h->prof && !any_shift && !compact_due && h->groups == 1 && !D.rv_split && !D.sharded &&
-                     h->lm_G > 0;
+  const bool graph = h->use_graph && !h->prof && !any_shift && !compact_due && !D.sharded && h->lm_G > 0;
   if (graph) {
     // the frame's whole sequence as one graph launch: records H2D, stack VoxelGrid (forked
     // stream) beside the submap prep, 2 x (kNN, geometry, LM round), insertion, re-VoxelGrid,
@@ -1921,16 +1620,12 @@ int32_t loam_mapper_solve(loam_mapper* h) {
       LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(StreamFrame) * B, hipMemcpyHostToDevice, st));
       LOAM_HIP(hipEventRecord(h->ev_fork, st));
       LOAM_HIP(hipStreamWaitEvent(s2, h->ev_fork, 0));
-      if (D.stack_split) k_stack_part<<<B * 2, VX_THREADS, 0, s2>>>(D);
-      k_stack_ds<<<B * 2 * (D.stack_split ? SP_PARTS : 1), VX_THREADS, 0, s2>>>(D);
-      if (D.stack_split) k_stack_gather<<<B * 2, VX_THREADS, 0, s2>>>(D);
+      k_stack_ds<<<B * 2, VX_THREADS, 0, s2>>>(D);
       LOAM_HIP(hipEventRecord(h->ev_join, s2));
       k_submap_prep<<<B, 128, 0, st>>>(D);
       LOAM_HIP(hipStreamWaitEvent(st, h->ev_join, 0));
       for (int round = 0; round < 2; ++round) {
         if (h->knn_lanes == 2) k_knn<2><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
-        else if (h->knn_lanes == 4) k_knn<4><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
-        else if (h->knn_lanes == 8) k_knn<8><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
         else k_knn<1><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
         k_geom<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
         k_lm_round<<<lm_padded(B) * h->lm_G, LM_THREADS, 0, st>>>(D, round, h->lm_G);
@@ -1960,57 +1655,27 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     k_compact_commit<<<B * 2, 256, 0, st>>>(D, h->d_new_off);
     LOAM_HIP(hipGetLastError());
   }
-  // The streams run in h->groups groups, each on its own HIP streams (gst[g], and gst2[g] for
-  // the stack VoxelGrid); the launch sequences are issued phase by phase so the groups start
-  // together and drift apart as their kernels finish.
-  const int NG = h->groups, Bg = B / NG;
-  MapperDev Dg[MAX_GROUPS];
-  for (int g = 0; g < NG; ++g) {
-    Dg[g] = D;
-    Dg[g].B = Bg;
-    Dg[g].s0 = g * Bg;
-  }
-  // phase bracketing for the stagger: before(g, p) / after(g, p) around group g's phase p
-  auto before = [&](int g, int p, hipStream_t q) -> hipError_t {
-    return (h->stagger && g > 0) ? hipStreamWaitEvent(q, h->gph[g - 1][p], 0) : hipSuccess;
-  };
-  auto after = [&](int g, int p, hipStream_t q) -> hipError_t {
-    return (h->stagger && g + 1 < NG) ? hipEventRecord(h->gph[g][p], q) : hipSuccess;
-  };
-  LOAM_HIP(hipEventRecord(h->gdone[0], st));  // the frame records are on the device
-  for (int g = 0; g < NG; ++g) {
-    hipStream_t sg = h->gst[g], s2 = h->gst2[g];
-    if (g > 0) LOAM_HIP(hipStreamWaitEvent(sg, h->gdone[0], 0));
-    // stack VoxelGrid (reads only this frame's inputs) on the second stream, overlapping the
-    // cube shift and submap gather; joined before the correspondences
-    LOAM_HIP(hipEventRecord(h->gfork[g], sg));
-    LOAM_HIP(hipStreamWaitEvent(s2, h->gfork[g], 0));
-    LOAM_HIP(before(g, 0, s2));
-    if (D.stack_split) LAUNCH_ON(s2, FAM_STACK, k_stack_part<<<Bg * 2, VX_THREADS, 0, s2>>>(Dg[g]));
-    LAUNCH_ON(s2, FAM_STACK, k_stack_ds<<<Bg * 2 * (D.stack_split ? SP_PARTS : 1), VX_THREADS, 0, s2>>>(Dg[g]));
-    if (D.stack_split) LAUNCH_ON(s2, FAM_STACK, k_stack_gather<<<Bg * 2, VX_THREADS, 0, s2>>>(Dg[g]));
-    LOAM_HIP(after(g, 0, s2));
-    LOAM_HIP(hipEventRecord(h->gjoin[g], s2));
-  }
+  // stack VoxelGrid (reads only this frame's inputs) on the second stream, overlapping the cube
+  // shift and submap preparation; joined before the correspondences
+  hipStream_t s2 = h->st2;
+  LOAM_HIP(hipEventRecord(h->ev_fork, st));
+  LOAM_HIP(hipStreamWaitEvent(s2, h->ev_fork, 0));
+  LAUNCH_ON(s2, FAM_STACK, k_stack_ds<<<B * 2, VX_THREADS, 0, s2>>>(D));
+  LOAM_HIP(hipEventRecord(h->ev_join, s2));
   if (any_shift) {
-    for (int g = 0; g < NG; ++g) {
-      LAUNCH_ON(h->gst[g], FAM_OTHER, k_shift_cubes<<<dim3(16, Bg), 256, 0, h->gst[g]>>>(
-                                          Dg[g], h->cube_tab[h->parity], h->cube_tab[1 - h->parity], h->tok_tmp));
-      const size_t o = (size_t)g * Bg * 2 * NCUBE;
-      LOAM_HIP(hipMemcpyAsync(D.stable_tok + o, h->tok_tmp + o, sizeof(uint32_t) * Bg * 2 * NCUBE,
-                              hipMemcpyDeviceToDevice, h->gst[g]));
-    }
+    LAUNCH(FAM_OTHER, k_shift_cubes<<<dim3(16, B), 256, 0, st>>>(D, h->cube_tab[h->parity],
+                                                                 h->cube_tab[1 - h->parity], h->tok_tmp));
+    LOAM_HIP(hipMemcpyAsync(D.stable_tok, h->tok_tmp, sizeof(uint32_t) * B * 2 * NCUBE, hipMemcpyDeviceToDevice, st));
     h->parity ^= 1;
     D.cube_tab = h->cube_tab[h->parity];
-    for (int g = 0; g < NG; ++g) Dg[g].cube_tab = D.cube_tab;
   }
-  if (D.sharded) {  // the submap sizes over all ranks (NG = 1)
+  if (D.sharded) {  // the submap sizes over all ranks
     LAUNCH(FAM_OTHER, k_submap_count<<<B, 256, 0, st>>>(D));
     TRY(comm_allreduce(h->comm, D.wcnt, (int64_t)B * 2 * WIN_MAX, LOAM_DT_I32, st));
   }
-  for (int g = 0; g < NG; ++g) LAUNCH_ON(h->gst[g], FAM_OTHER, k_submap_prep<<<Bg, 128, 0, h->gst[g]>>>(Dg[g]));
+  LAUNCH(FAM_OTHER, k_submap_prep<<<B, 128, 0, st>>>(D));
   LOAM_HIP(hipEventRecord(h->ev[1], st));
-  for (int g = 0; g < NG; ++g) LOAM_HIP(hipStreamWaitEvent(h->gst[g], h->gjoin[g], 0));
+  LOAM_HIP(hipStreamWaitEvent(st, h->ev_join, 0));
   size_t q_tot = 0;
   if (D.sharded) {
     // the stack sizes (identical on every rank) place each stream's queries in the exchange
@@ -2025,43 +1690,24 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     LOAM_HIP(hipMemcpyAsync(h->d_q_off, h->q_off.data(), sizeof(int) * (B + 1), hipMemcpyHostToDevice, st));
   }
   for (int round = 0; round < 2; ++round) {
-    for (int g = 0; g < NG; ++g) {
-      hipStream_t sg = h->gst[g];
-      LOAM_HIP(before(g, 2 + 3 * round, sg));
-      switch (h->knn_lanes) {
-        case 1: LAUNCH_ON(sg, FAM_CORR, k_knn<1><<<Bg * CORR_BLK, CORR_THREADS, 0, sg>>>(Dg[g], round)); break;
-        case 2: LAUNCH_ON(sg, FAM_CORR, k_knn<2><<<Bg * CORR_BLK, CORR_THREADS, 0, sg>>>(Dg[g], round)); break;
-        case 4: LAUNCH_ON(sg, FAM_CORR, k_knn<4><<<Bg * CORR_BLK, CORR_THREADS, 0, sg>>>(Dg[g], round)); break;
-        default: LAUNCH_ON(sg, FAM_CORR, k_knn<8><<<Bg * CORR_BLK, CORR_THREADS, 0, sg>>>(Dg[g], round)); break;
-      }
-      LOAM_HIP(after(g, 2 + 3 * round, sg));
-    }
+    if (h->knn_lanes == 2) LAUNCH(FAM_CORR, k_knn<2><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round));
+    else LAUNCH(FAM_CORR, k_knn<1><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round));
     if (D.sharded) {  // every rank's candidates -> the exact 5-NN on every rank
       TRY(comm_allgather(h->comm, D.nn_send, const_cast<NnRec*>(D.nn_recv), (int64_t)(q_tot * sizeof(NnRec)), st));
       LAUNCH(FAM_CORR, k_nn_merge<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D));
     }
-    for (int g = 0; g < NG; ++g) {
-      hipStream_t sg = h->gst[g];
-      LOAM_HIP(before(g, 3 + 3 * round, sg));
-      LAUNCH_ON(sg, FAM_CORR, k_geom<<<Bg * CORR_BLK, CORR_THREADS, 0, sg>>>(Dg[g], round));
-      LOAM_HIP(after(g, 3 + 3 * round, sg));
-    }
-    for (int g = 0; g < NG; ++g) {
-      hipStream_t sg = h->gst[g];
-      LOAM_HIP(before(g, 4 + 3 * round, sg));
-      if (h->lm_G > 0) {
-        LAUNCH_ON(sg, FAM_LM, k_lm_round<<<lm_padded(Bg) * h->lm_G, LM_THREADS, 0, sg>>>(Dg[g], round, h->lm_G));
-      } else {
-        for (int it = 0; it < 5; ++it) {  // iteration 0 + max_num_iterations = 4 candidates
-          LAUNCH_ON(sg, FAM_LM, k_lm_eval<<<Bg * LM_EBLK, LM_THREADS, 0, sg>>>(Dg[g], round));
-          if (D.sharded) {  // per Ceres iteration: all-reduce of the 6x6 normal equations
-            LAUNCH_ON(sg, FAM_LM, k_lm_reduce<<<Bg, 64, 0, sg>>>(Dg[g], round));
-            TRY(comm_allreduce(h->comm, D.lm_red, (int64_t)B * LM_NACC, LOAM_DT_F64, sg));
-          }
-          LAUNCH_ON(sg, FAM_LM, k_lm_step<<<Bg, 64, 0, sg>>>(Dg[g], round));
+    LAUNCH(FAM_CORR, k_geom<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round));
+    if (h->lm_G > 0) {
+      LAUNCH(FAM_LM, k_lm_round<<<lm_padded(B) * h->lm_G, LM_THREADS, 0, st>>>(D, round, h->lm_G));
+    } else {
+      for (int it = 0; it < 5; ++it) {  // iteration 0 + max_num_iterations = 4 candidates
+        LAUNCH(FAM_LM, k_lm_eval<<<B * LM_EBLK, LM_THREADS, 0, st>>>(D, round));
+        if (D.sharded) {  // per Ceres iteration: all-reduce of the 6x6 normal equations
+          LAUNCH(FAM_LM, k_lm_reduce<<<B, 64, 0, st>>>(D, round));
+          TRY(comm_allreduce(h->comm, D.lm_red, (int64_t)B * LM_NACC, LOAM_DT_F64, st));
         }
+        LAUNCH(FAM_LM, k_lm_step<<<B, 64, 0, st>>>(D, round));
       }
-      LOAM_HIP(after(g, 4 + 3 * round, sg));
     }
   }
   if (D.sharded) {  // pose agreement across ranks before anything is stored (k_pose_adopt)
@@ -2070,34 +1716,9 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     LAUNCH(FAM_OTHER, k_pose_adopt<<<B, 64, 0, st>>>(D));
   }
   LOAM_HIP(hipEventRecord(h->ev[2], st));
-  for (int g = 0; g < NG; ++g) {
-    hipStream_t sg = h->gst[g];
-    LOAM_HIP(before(g, 8, sg));
-    LAUNCH_ON(sg, FAM_INSERT, k_insert<<<dim3(16, Bg), 256, 0, sg>>>(Dg[g]));
-    LAUNCH_ON(sg, FAM_INSERT, k_bucket<<<Bg * 2, VX_THREADS, 0, sg>>>(Dg[g]));
-    LOAM_HIP(after(g, 8, sg));
-  }
-  for (int g = 0; g < NG; ++g) {
-    hipStream_t sg = h->gst[g];
-    LOAM_HIP(before(g, 9, sg));
-    // the long items (k_revox, whole-CU workgroups) start first on the second stream; the
-    // merges fill the other CUs beside them
-    if (D.rv_split) {
-      hipStream_t s2 = h->gst2[g];
-      LOAM_HIP(hipEventRecord(h->gfork[g], sg));
-      LOAM_HIP(hipStreamWaitEvent(s2, h->gfork[g], 0));
-      LAUNCH_ON(s2, FAM_REVOX, k_revox<<<Bg * 2 * INS_SLOTS, VX_THREADS, 0, s2>>>(Dg[g]));
-      LOAM_HIP(hipEventRecord(h->gjoin[g], s2));
-      LAUNCH_ON(sg, FAM_REVOX, k_revox_merge<<<Bg * 2 * INS_SLOTS, RV_NT, 0, sg>>>(Dg[g]));
-      LOAM_HIP(hipStreamWaitEvent(sg, h->gjoin[g], 0));
-    } else {
-      LAUNCH_ON(sg, FAM_REVOX, k_revox<<<Bg * 2 * INS_SLOTS, VX_THREADS, 0, sg>>>(Dg[g]));
-    }
-    if (g > 0) {
-      LOAM_HIP(hipEventRecord(h->gdone[g], sg));
-      LOAM_HIP(hipStreamWaitEvent(st, h->gdone[g], 0));
-    }
-  }
+  LAUNCH(FAM_INSERT, k_insert<<<dim3(16, B), 256, 0, st>>>(D));
+  LAUNCH(FAM_INSERT, k_bucket<<<B * 2, VX_THREADS, 0, st>>>(D));
+  LAUNCH(FAM_REVOX, k_revox<<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D));
   LOAM_HIP(hipGetLastError());
   LOAM_HIP(hipEventRecord(h->ev[3], st));
   LOAM_HIP(hipMemcpyAsync(h->hf.data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
@@ -2136,6 +1757,7 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   for (int s = 0; s < B; ++s) {
     StreamFrame& F = h->hf[s];
     HostStream& H = h->hs[s];
+    H.solved_last = F.active != 0;
     if (!F.active) continue;
     H.pending = false;
     for (int i = 0; i < 7; ++i) H.pose[i] = F.pose[i];
@@ -2164,8 +1786,11 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     S.ms_opt = ms_opt;
     if (h->prof) h->fam_bytes[FAM_REVOX] += (double)F.vx_bytes;  // counted by k_revox
     if (F.err) {
-      set_error("loam_mapper_solve: device capacity exceeded (err flags " + std::to_string(F.err) + ")");
-      status = LOAM_ERR_CAPACITY;
+      // the frame is committed as computed (pose, insertion, re-VoxelGrid ran on the device);
+      // the status says it is not trustworthy: the caller resets the stream (include/loam_core.h)
+      set_error("loam_mapper_solve: stream " + std::to_string(s) + ": " + map_err_text(F.err));
+      const int32_t st = (F.err & MAP_ERR_LM_SYNC) ? LOAM_ERR_SYNC : LOAM_ERR_CAPACITY;
+      if (status == LOAM_OK || st == LOAM_ERR_SYNC) status = st;
     }
   }
   return status;

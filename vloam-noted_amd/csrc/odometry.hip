@@ -3,20 +3,26 @@
 // One handle = B independent odometry streams; every launch covers all of them.  Per frame:
 //   2 x { k_od_corr   one wave per query (cornerPointsSharp, surfPointsFlat): TransformToStart
 //                     (:152-173, s = 1), exact 1-NN in the last cloud (KdTreeFLANN, d2 < 25,
-//                     :292/:398) and the second / third point of the reference's ring scans
-//                     (:303-349 corner, :407-468 surf) as a ring-filtered nearest search over
-//                     the same cell grid -> factor records (LidarEdgeFactor / LidarPlaneFactor)
+//                     :292/:398) over a 2 m cell grid, then the second / third point by the
+//                     reference's own linear scans of the last cloud from the 1-NN
+//                     (:309-355 corner, :407-456 surf), 64 points per wave step
+//                     -> factor records (LidarEdgeFactor / LidarPlaneFactor)
 //         k_od_lm     Ceres TR-LM on the records (lm.h, one launch per round) }
 //   k_od_build        laserCloudCornerLast / SurfLast <- lessSharp / lessFlat (:559-569) and
 //                     their 2 m cell tables (replaces kdtree->setInputCloud, :571-572)
 // The pose composition t_w += q_w t_lc, q_w = q_w q_lc (:524-527) runs on the host with the
 // oracle's operation order.
 //
-// Ring scans as a nearest search: the last clouds are ring-major (int(intensity) is the
-// scanID, non-decreasing along the cloud), so the reference's forward scan from the 1-NN
-// `c` visits exactly the points after c up to ring cid + 2 and the backward scan the points
-// before c down to ring cid - 2.  The minimum under strict '<' in that visiting order is the
-// minimum of (d2, order) with order = j - c for j > c and (c - j) + 2^30 for j < c.
+// The ring scans are restated literally, not as a ring-filtered nearest search: int(intensity)
+// is not monotone along a last cloud (points before the halfPassed latch with relTime < 0 carry
+// scanID - 1, scan_registration.cpp:263-296; the lessSharp picks follow curvature order and
+// lessFlat voxel order), and the reference's `continue` / `break` tests (:312-317, :337-342,
+// :410, :436) decide which points are visited.  A wave steps 64 consecutive points at a time;
+// the first lane whose point triggers the `break` ends the scan, the lanes before it are the
+// visited points.  Each lane keeps its own running minimum under strict '<' (its points come
+// in scan order), and the lanes' minima are merged with the scan order as the tie rule: the
+// forward scan's earliest j, then the backward scan's latest j, the backward one only if
+// strictly nearer (minPointSqDis2 / 3 carry over from the forward loop).
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -52,6 +58,8 @@ struct OdomFrame {
   int n_last[2];  // cornerLast, surfLast
   int corr[4];    // corner / plane correspondences, rounds 0 and 1
   int err;
+  int has_prior;   // !detach_VO_LO: every outer round starts from `prior` (laser_odometry.cpp:237-250)
+  double prior[7];
   LmState lm[2];
 };
 
@@ -249,15 +257,102 @@ __device__ inline void od_visit(const uint4* tab, float qx, float qy, float qz, 
   }
 }
 
+// squared distance of the reference's scans (laser_odometry.cpp:319-322): float differences,
+// float products and sums, widened to double only for the comparison (same outcome)
+__device__ inline float od_scan_d2(const float4& p, const float4& q) {
+  const float dx = p.x - q.x, dy = p.y - q.y, dz = p.z - q.z;
+  return dx * dx + dy * dy + dz * dz;
+}
+
+// lanes' running minima -> the wave's (every lane ends with it); `later` = larger j wins a
+// tie (the backward scan meets larger j first)
+__device__ inline OdNear od_merge_lanes(OdNear b, bool later) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float d = __shfl_xor(b.d, o, 64);
+    const int j = __shfl_xor(b.j, o, 64);
+    const bool take = j >= 0 && (b.j < 0 || d < b.d || (d == b.d && (later ? j > b.j : j < b.j)));
+    if (take) {
+      b.d = d;
+      b.j = j;
+    }
+  }
+  return b;
+}
+
+// The second (corner) / second and third (surf) points: the reference's forward scan
+// j = cl+1 .. n-1 and backward scan j = cl-1 .. 0 over the last cloud in its own order.
+//   corner (:309-355): skip int(I) <= cid (fwd) / >= cid (bwd); stop at int(I) > cid + 2 (fwd)
+//                      / < cid - 2 (bwd); nearest under '<' starting from 25
+//   surf   (:407-456): stop at int(I) > cid + 2 (fwd) / < cid - 2 (bwd); int(I) <= cid (fwd) /
+//                      >= cid (bwd) -> minPointInd2, else -> minPointInd3
+// b2 / b3: j = -1 when none (d < 25 never met).
+__device__ inline void od_ring_scans(const float4* last, int nl, int cl, int cid, int c, const float4& sel, int lane,
+                                     OdNear& b2, OdNear& b3) {
+  OdNear f2{OD_THR, 0, -1}, f3{OD_THR, 0, -1};
+  for (int j0 = cl + 1; j0 < nl; j0 += 64) {  // forward
+    const int j = j0 + lane;
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (j < nl) p = last[j];
+    const int r = (int)p.w;
+    const uint64_t brk = __ballot(j < nl && r > cid + 2);
+    const int stop = brk ? __ffsll((long long)brk) - 1 : 64;
+    if (j < nl && lane < stop) {
+      const float d = od_scan_d2(p, sel);
+      if (c == 0) {
+        if (r > cid && d < f2.d) f2 = OdNear{d, 0, j};
+      } else if (r <= cid) {
+        if (d < f2.d) f2 = OdNear{d, 0, j};
+      } else if (d < f3.d) {
+        f3 = OdNear{d, 0, j};
+      }
+    }
+    if (brk) break;
+  }
+  OdNear k2{OD_THR, 0, -1}, k3{OD_THR, 0, -1};
+  for (int j0 = cl - 1; j0 >= 0; j0 -= 64) {  // backward
+    const int j = j0 - lane;
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (j >= 0) p = last[j];
+    const int r = (int)p.w;
+    const uint64_t brk = __ballot(j >= 0 && r < cid - 2);
+    const int stop = brk ? __ffsll((long long)brk) - 1 : 64;
+    if (j >= 0 && lane < stop) {
+      const float d = od_scan_d2(p, sel);
+      if (c == 0) {
+        if (r < cid && d < k2.d) k2 = OdNear{d, 0, j};
+      } else if (r >= cid) {
+        if (d < k2.d) k2 = OdNear{d, 0, j};
+      } else if (d < k3.d) {
+        k3 = OdNear{d, 0, j};
+      }
+    }
+    if (brk) break;
+  }
+  f2 = od_merge_lanes(f2, false);
+  k2 = od_merge_lanes(k2, true);
+  b2 = (k2.j >= 0 && (f2.j < 0 || k2.d < f2.d)) ? k2 : f2;
+  if (c == 1) {
+    f3 = od_merge_lanes(f3, false);
+    k3 = od_merge_lanes(k3, true);
+    b3 = (k3.j >= 0 && (f3.j < 0 || k3.d < f3.d)) ? k3 : f3;
+  } else {
+    b3 = OdNear{OD_THR, 0, -1};
+  }
+}
+
 constexpr int OD_QWAVES = OD_QTHREADS / 64;  // queries in flight per workgroup (one per wave)
 
 __global__ void __launch_bounds__(OD_QTHREADS) k_od_corr(OdomDev D, int round, int qblk) {
   const int s = blockIdx.x / qblk, blk = blockIdx.x % qblk;
   OdomFrame& F = D.fr[s];
   if (!F.active || !F.inited) return;
+  // para_q / para_t at the start of the round: the VO prior when coupled (:237-250), else the
+  // previous frame's (round 0) or round 0's result (round 1)
+  const double* x0 = F.has_prior ? F.prior : F.x;
   double X[7];
 #pragma unroll
-  for (int i = 0; i < 7; ++i) X[i] = F.x[i];
+  for (int i = 0; i < 7; ++i) X[i] = x0[i];
   if (blk == 0 && threadIdx.x < LM_SYNC_WORDS) D.lm_sync[((size_t)s * 2 + round) * LM_SYNC_WORDS + threadIdx.x] = 0;
   if (blk == 0 && threadIdx.x == 0) lm_init(F.lm[round], X, 4, true);
   const int ns = F.n_in[0], nf = F.n_in[2];
@@ -288,29 +383,10 @@ __global__ void __launch_bounds__(OD_QTHREADS) k_od_corr(OdomDev D, int round, i
     });
     if (n1.j >= 0 && n1.d < OD_THR) {
       const int cl = n1.j;
-      const int cid = (int)last[cl].w;
-      OdNear b2{OD_THR, 0xFFFFFFFFu, -1}, b3{OD_THR, 0xFFFFFFFFu, -1};
-      od_visit(tab, sel.x, sel.y, sel.z, OD_THR * 1.01f + 1e-5f, [&](const uint4& e) {
-        for (uint32_t k = lane; k < e.z; k += 64) {
-          const float4 p = srt[e.y + k];
-          const int j = sidx[e.y + k];
-          if (j == cl) continue;
-          const int r = (int)p.w;
-          if (r > cid + 2 || r < cid - 2) continue;  // NEARBY_SCAN = 2.5
-          const float d = fdist2(sel.x, sel.y, sel.z, p.x, p.y, p.z);
-          const uint32_t ord = j > cl ? (uint32_t)(j - cl) : (uint32_t)(cl - j) + (1u << 30);
-          if (c == 0) {
-            if (r != cid) od_offer(b2, d, ord, j);  // corner: rings cid +- 1, 2
-          } else if (r == cid) {
-            od_offer(b2, d, ord, j);                // surf ind2: same ring
-          } else {
-            od_offer(b3, d, ord, j);                // surf ind3: rings cid +- 1, 2
-          }
-        }
-        b2 = od_wave_min(b2);
-        if (c == 1) b3 = od_wave_min(b3);
-        return fmaxf(b2.d, c == 0 ? 0.0f : b3.d) * 1.01f + 1e-5f;
-      });
+      const int cid = (int)last[cl].w;  // closestPointScanID = int(intensity)
+      const int nl = F.n_last[c];
+      OdNear b2, b3;
+      od_ring_scans(last, nl, cl, cid, c, sel, lane, b2, b3);
       const float4 pa = last[cl];
       if (c == 0 && b2.j >= 0) {
         // LidarEdgeFactor(curr, a = last[cl], b = last[ind2]): r = (lp - a) x e, e = (a - b)/|a - b|
@@ -386,6 +462,8 @@ struct OdomHost {
   double q_w[4] = {0, 0, 0, 1}, t_w[3] = {0, 0, 0};
   int frame_count = 0;
   bool pending = false;
+  bool prior_set = false;  // loam_odometry_set_prior for the next solve
+  double prior[7] = {0, 0, 0, 1, 0, 0, 0};
   loam_odom_stats st{};
 };
 
@@ -581,7 +659,19 @@ int32_t loam_odometry_solve(loam_odometry* h) {
   bool any = false, any_inited = false;
   for (int s = 0; s < B; ++s) {
     OdomFrame& F = h->hf[s];
-    F.active = h->hs[s].pending ? 1 : 0;
+    OdomHost& H = h->hs[s];
+    if (H.pending && F.inited && !h->P.detach_vo_lo && !H.prior_set) {
+      set_error("loam_odometry_solve: detach_vo_lo = 0 needs loam_odometry_set_prior for every stream with an "
+                "input (laser_odometry.cpp:237-250)");
+      return LOAM_ERR_STATE;
+    }
+  }
+  for (int s = 0; s < B; ++s) {
+    OdomFrame& F = h->hf[s];
+    OdomHost& H = h->hs[s];
+    F.active = H.pending ? 1 : 0;
+    F.has_prior = (F.active && H.prior_set) ? 1 : 0;
+    for (int i = 0; i < 7; ++i) F.prior[i] = H.prior[i];
     F.err = 0;
     for (int k = 0; k < 4; ++k) F.corr[k] = 0;
     any |= F.active != 0;
@@ -641,15 +731,41 @@ int32_t loam_odometry_solve(loam_odometry* h) {
     F.inited = 1;
     H.frame_count++;
     H.pending = false;
+    H.prior_set = false;  // velo_last_VOT_velo_curr is the VO estimate of this frame pair only
     F.active = 0;
     S.n_corner_last = F.n_last[0];
     S.n_surf_last = F.n_last[1];
     S.ms = ms;
   }
+  if (err & OD_ERR_LM_SYNC) {
+    set_error("loam_odometry_solve: the LM round's workgroup hand-off timed out (lm.h spin bound; flags " +
+              std::to_string(err) + ")");
+    return LOAM_ERR_SYNC;
+  }
   if (err) {
-    set_error("loam_odometry_solve: device capacity / synchronisation error (flags " + std::to_string(err) + ")");
+    set_error(std::string("loam_odometry_solve: ") +
+              ((err & OD_ERR_TABLE) ? "last-cloud cell table full" : "device capacity exceeded") + " (flags " +
+              std::to_string(err) + ")");
     return LOAM_ERR_CAPACITY;
   }
+  return LOAM_OK;
+}
+
+int32_t loam_odometry_set_prior(loam_odometry* h, int32_t s, const double* q_xyzw, const double* t_xyz) {
+  TRY(od_check(h, s));
+  if (h->P.detach_vo_lo) {
+    set_error("loam_odometry_set_prior: detach_vo_lo = 1 (the reference ignores the VO prior, "
+              "laser_odometry.cpp:237)");
+    return LOAM_ERR_STATE;
+  }
+  OdomHost& H = h->hs[s];
+  if (!q_xyzw || !t_xyz) {
+    H.prior_set = false;
+    return LOAM_OK;
+  }
+  for (int i = 0; i < 4; ++i) H.prior[i] = q_xyzw[i];
+  for (int i = 0; i < 3; ++i) H.prior[4 + i] = t_xyz[i];
+  H.prior_set = true;
   return LOAM_OK;
 }
 

@@ -15,16 +15,23 @@
 //                   per sector, register bitonic), then the greedy sharp / lessSharp / flat
 //                   picks with +-5 neighbour suppression (:352-493): one wave runs the
 //                   (inherently sequential) greedy scan with 64-wide ballots, all in LDS
-//   k_sr_ringvox    VoxelGrid 0.2 m of each ring's lessFlat candidates (:497-503)
+//   k_sr_ringvox    VoxelGrid 0.2 m of each ring's lessFlat candidates (:497-503), in PCL's
+//                   summation order (voxel_pcl.h)
 //   k_sr_gather     concatenation of the per-ring outputs in ring order
-// The reference sorts each sector with std::sort (unstable); the kernel sorts by
-// (curvature, index), which is the same order whenever curvatures are distinct.
+// The reference sorts each sector with std::sort (unstable).  The bitonic sort by (curvature,
+// index) is std::sort's order whenever a sector's curvatures are distinct; a sector with a tie
+// is re-sorted by the exact libstdc++ permutation (stdsort.h) before the picks.  Azimuths and
+// elevations use glibc's atan2f / atanf restated (libm_f32.h), so ring ids and intensity carry
+// the reference's bits.
 #include <algorithm>
 #include <cmath>
 #include <vector>
 
 #include "common.h"
+#include "libm_f32.h"
+#include "stdsort.h"
 #include "voxel.h"
+#include "voxel_pcl.h"
 
 namespace loam {
 
@@ -33,7 +40,7 @@ constexpr int SR_BLOCK = 256;
 constexpr int SR_RING_CAP = 16384;  // points per ring handled in LDS
 constexpr int SR_SECT_CAP = 4096;   // points per sector (bitonic in LDS)
 constexpr int SR_SHARP = 2, SR_LESS_SHARP = 20, SR_FLAT = 4;
-constexpr int SR_ERR_RING = 1, SR_ERR_VOXEL = 2;
+constexpr int SR_ERR_RING = 1, SR_ERR_VOXEL = 2, SR_ERR_SORT = 4;
 
 struct SrFrame {
   int n_in;
@@ -72,12 +79,17 @@ struct SrDev {
   float4* vx_pts;
   int* vx_idx;
   float4* out[5];        // laserCloud alias, sharp, lessSharp, flat, lessFlat
+  // std::sort emulation scratch for sectors / rings too long for LDS, indexed by cloud position
+  uint64_t* ss_e;
+  uint32_t* ss_a;
+  uint32_t* ss_b;
+  uint64_t* ss_s;
 };
 
 // scan_registration.cpp:217-259 (float atan/sqrt like the reference's float overloads)
 __device__ inline int sr_scan_id(float x, float y, float z, int n_scans) {
   // float atan(float) * 180 -> float, / M_PI -> double, stored as float
-  const float angle = (float)((double)(atanf(z / sqrtf(x * x + y * y)) * 180) / M_PI);
+  const float angle = (float)((double)(glibc_atanf(z / sqrtf(x * x + y * y)) * 180) / M_PI);
   int scanID = 0;
   if (n_scans == 16) {
     scanID = int((angle + 15) / 2 + 0.5);
@@ -128,7 +140,7 @@ __global__ void __launch_bounds__(SR_BLOCK) k_sr_ring(SrDev D, int nblocks) {
     D.ring_of[i] = sid;
     if (sid >= 0) {
       atomicAdd(&hist[sid], 1);
-      const float ori = sr_ori_branch1(-atan2f(y, x), F.start_ori);
+      const float ori = sr_ori_branch1(-glibc_atan2f(y, x), F.start_ori);
       if (ori - F.start_ori > M_PI) atomicMin(&F.latch, i);
     }
   }
@@ -142,8 +154,8 @@ __global__ void k_sr_oris(SrDev D) {
   if (F.first > F.last) return;
   const float* p0 = D.xyz + (size_t)F.first * D.stride;
   const float* p1 = D.xyz + (size_t)F.last * D.stride;
-  float startOri = -atan2f(p0[1], p0[0]);
-  float endOri = (float)(-atan2f(p1[1], p1[0]) + 2 * M_PI);
+  float startOri = -glibc_atan2f(p0[1], p0[0]);
+  float endOri = (float)(-glibc_atan2f(p1[1], p1[0]) + 2 * M_PI);
   if (endOri - startOri > 3 * M_PI) endOri = (float)(endOri - 2 * M_PI);
   else if (endOri - startOri < M_PI) endOri = (float)(endOri + 2 * M_PI);
   F.start_ori = startOri;
@@ -216,7 +228,7 @@ __global__ void __launch_bounds__(SR_BLOCK) k_sr_scatter(SrDev D, int nblocks) {
   const int pos = D.blk_off[sid * nblocks + blockIdx.x] + before + rank;
   const float x = D.xyz[(size_t)i * D.stride], y = D.xyz[(size_t)i * D.stride + 1],
               z = D.xyz[(size_t)i * D.stride + 2];
-  float ori = -atan2f(y, x);
+  float ori = -glibc_atan2f(y, x);
   const float startOri = F.start_ori, endOri = F.end_ori;
   if (i <= F.latch) {
     ori = sr_ori_branch1(ori, startOri);
@@ -311,6 +323,41 @@ __device__ inline void sr_wave_sort(const float* curv, int sp, int len, uint64_t
 
 constexpr int SR_SEL_THREADS = 512;
 constexpr int SR_WSORT_MAX = 1024;  // register sort (one wave per sector) up to this length
+constexpr int SR_SS_LDS = 512;      // tied sectors re-sorted in LDS up to this length (else global)
+constexpr int SR_SS_STK = 48;       // segment stack of one wave (depth <= 2 log2(n) + 1)
+
+struct SrCurvLess {  // the reference's comparator: cloudCurvature[i] < cloudCurvature[j]
+  __device__ bool operator()(uint64_t a, uint64_t b) const {
+    return __uint_as_float((uint32_t)(a >> 32)) < __uint_as_float((uint32_t)(b >> 32));
+  }
+};
+
+// K[0, len): one sector's keys (curvature bits << 32 | cloud index) sorted by (curvature,
+// index).  If two curvatures are equal, std::sort's order differs from that one: the wave
+// recomputes the exact libstdc++ permutation of the sector (cloudSortInd[sp..ep] starts as
+// the identity, :341) into K.  One wave; E/A/B in LDS for short sectors, else the global
+// scratch at the sector's cloud positions.
+__device__ inline void sr_exact_sector(const SrDev& D, int sp, int len, uint64_t* K, uint64_t* lE, uint32_t* lA,
+                                       uint32_t* lB, SsCtl* ctl, int* stk) {
+  const int lane = threadIdx.x & 63;
+  ss_wave_fence();
+  bool tie = false;
+  for (int k = lane; k + 1 < len; k += 64) tie |= (uint32_t)(K[k] >> 32) == (uint32_t)(K[k + 1] >> 32);
+  if (!__ballot(tie)) return;
+  const bool lds = len <= SR_SS_LDS;
+  uint64_t* E = lds ? lE : D.ss_e + sp;
+  uint32_t* A = lds ? lA : D.ss_a + sp;
+  uint32_t* B = lds ? lB : D.ss_b + sp;
+  for (int k = lane; k < len; k += 64)
+    E[k] = ((uint64_t)__float_as_uint(D.curv[sp + k]) << 32) | (uint32_t)(sp + k);
+  if (lane == 0) ss_init(ctl, stk, len);
+  ss_wave_fence();
+  const SrCurvLess less;
+  ss_loop(E, A, B, ctl, stk, SR_SS_STK, less);
+  ss_final(E, A, B, len, K, lane, 64, less);
+  if (lane == 0 && ctl->err) atomicOr(&D.fr->err, SR_ERR_SORT);
+  ss_wave_fence();
+}
 
 // sharp / lessSharp (descending curvature, :371-431) and flat (ascending, :439-483) picks of
 // one sector from its sorted keys K[0, len): one wave, 64 candidates tested per ballot
@@ -407,6 +454,10 @@ __global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(SrDev D) {
   __shared__ int8_t lab[SR_RING_CAP];
   __shared__ uint8_t gapok[SR_RING_CAP];
   __shared__ uint32_t ws[SR_SEL_THREADS / 64];
+  __shared__ uint64_t ssE[6][SR_SS_LDS];  // exact re-sort of tied sectors (one wave each)
+  __shared__ uint32_t ssA[6][SR_SS_LDS], ssB[6][SR_SS_LDS];
+  __shared__ int ssStk[6][3 * SR_SS_STK];
+  __shared__ SsCtl ssCtl[6];
   const int r = blockIdx.x;
   SrFrame& F = *D.fr;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
@@ -448,6 +499,8 @@ __global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(SrDev D) {
   if (fast && wid < 6) {
     if (maxlen <= 512) sr_wave_sort<8>(D.curv, sp[wid], len[wid], keys + wid * SR_WSORT_MAX);
     else sr_wave_sort<16>(D.curv, sp[wid], len[wid], keys + wid * SR_WSORT_MAX);
+    sr_exact_sector(D, sp[wid], len[wid], keys + wid * SR_WSORT_MAX, ssE[wid], ssA[wid], ssB[wid], &ssCtl[wid],
+                    ssStk[wid]);
   }
   __syncthreads();
   int nsh = 0, nls = 0, nfl = 0;  // valid in wave 0
@@ -477,6 +530,8 @@ __global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(SrDev D) {
           __syncthreads();
         }
       }
+      if (wid == 0) sr_exact_sector(D, sp[j], len[j], keys, nullptr, nullptr, nullptr, &ssCtl[0], ssStk[0]);
+      __syncthreads();
     }
     if (wid == 0) sr_greedy(D, r, base, K, len[j], picked, lab, gapok, nsh, nls, nfl);
     if (!fast) __syncthreads();
@@ -510,27 +565,28 @@ __global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(SrDev D) {
   }
 }
 
-__global__ void __launch_bounds__(VX_THREADS) k_sr_ringvox(SrDev D) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
+// PCL VoxelGrid of one ring's lessFlat candidates in PCL's summation order (voxel_pcl.h): the
+// std::sort emulation in LDS up to SRV_LDS points, else in the global scratch
+constexpr int SRV_THREADS = 512;
+constexpr int SRV_LDS = 4096;
+constexpr int SRV_STK = 1024;  // pending segments (<= n / 17 + 1)
+
+__global__ void __launch_bounds__(SRV_THREADS) k_sr_ringvox(SrDev D) {
+  __shared__ uint64_t sE[SRV_LDS], sS[SRV_LDS];
+  __shared__ uint32_t sA[SRV_LDS], sB[SRV_LDS];
+  __shared__ int stk[3 * SRV_STK];
+  __shared__ SsCtl ctl;
+  __shared__ VxMisc M;
+  __shared__ uint32_t ws[SRV_THREADS / 64 + 1];
   const int r = blockIdx.x;
   SrFrame& F = *D.fr;
   const int base = F.ring_off[r];
   const int n = F.n_less_flat_scan[r];
-  if (threadIdx.x == 0) F.n_less_flat[r] = 0;
-  if (n == 0) return;
-  __syncthreads();
-  VoxSeg S{};
-  S.src0 = D.less_flat_scan + base;
-  S.n0 = n;
-  S.leaf = 0.2f;
-  S.out = D.less_flat_ds + base;
-  S.cap = (uint32_t)n;
-  S.res_cnt = &F.n_less_flat[r];
-  S.scratch_pts = D.vx_pts + base;
-  S.scratch_idx = D.vx_idx + base;
-  S.scratch_cap = (uint32_t)n;
-  S.err = &F.err;
-  voxel_segment(S, lds);
+  const bool lds = n <= SRV_LDS;
+  const VxPclScratch X{lds ? sE : D.ss_e + base, lds ? sA : D.ss_a + base, lds ? sB : D.ss_b + base,
+                       lds ? sS : D.ss_s + base, &ctl, stk, SRV_STK};
+  voxel_grid_pcl<SRV_THREADS>(D.less_flat_scan + base, n, 0.2f, D.less_flat_ds + base, &F.n_less_flat[r], X, M, ws,
+                              &F.err);
 }
 
 // concatenation of the per-ring outputs in ring order
@@ -656,6 +712,10 @@ int32_t loam_scanreg_create(const loam_params* p, int32_t device, loam_scanreg**
   SRA(D.vx_pts, cap);
   SRA(D.vx_idx, cap);
   for (int k = 1; k < 5; ++k) SRA(D.out[k], cap);
+  SRA(D.ss_e, cap);
+  SRA(D.ss_a, cap);
+  SRA(D.ss_b, cap);
+  SRA(D.ss_s, cap);
 #undef SRA
   D.out[0] = D.cloud;
   D.sort_ind = nullptr;
@@ -715,7 +775,7 @@ static int32_t sr_launch(loam_scanreg* h, const float* xyz, int32_t n, int32_t s
     k_sr_scatter<<<nblocks, SR_BLOCK, 0, st>>>(D, nblocks);
     k_sr_curv<<<std::min(nblocks, 1024), SR_BLOCK, 0, st>>>(D);
     k_sr_select<<<SR_MAX_RINGS, SR_SEL_THREADS, 0, st>>>(D);
-    k_sr_ringvox<<<SR_MAX_RINGS, VX_THREADS, 0, st>>>(D);
+    k_sr_ringvox<<<SR_MAX_RINGS, SRV_THREADS, 0, st>>>(D);
     k_sr_gather<<<SR_MAX_RINGS, 256, 0, st>>>(D);
     LOAM_HIP(hipGetLastError());
   }
@@ -739,8 +799,9 @@ static int32_t sr_finish(loam_scanreg* h) {
   h->D.xyz = h->pending_xyz;
   h->D.stride = h->pending_stride;
   if (h->hf.err) {
-    set_error("loam_scanreg_input: ring or sector larger than the LDS capacity (err " +
-              std::to_string(h->hf.err) + ")");
+    set_error(std::string("loam_scanreg_input: ") +
+              ((h->hf.err & SR_ERR_SORT) ? "std::sort emulation stack overflow" : "ring or sector larger than the LDS capacity") +
+              " (err " + std::to_string(h->hf.err) + ")");
     return LOAM_ERR_CAPACITY;
   }
   return LOAM_OK;

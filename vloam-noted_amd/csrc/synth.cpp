@@ -9,6 +9,8 @@
 // hundredths of a degree from the reference's scanID boundaries so the ring rule of
 // scan_registration.cpp:241-254 is unambiguous), n_az azimuths per revolution clockwise,
 // range noise N(0, 0.02 m), max range 100 m.  Output order is ring-major (KITTI-like).
+// synth_frame_ex's flags switch on the edge cases (boundary elevations, per-laser azimuth
+// offsets, azimuth-interleaved order, 1 cm quantization) for the parity tests.
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -225,10 +227,34 @@ void synth_pose(uint64_t seed, double frame, double speed, double* q_xyzw, doubl
   t_xyz[2] = 0.0;
 }
 
+// Edge-case modes of synth_frame_ex (flags), the input shapes the reference's scan
+// registration and odometry see on real sensors but the default street avoids:
+//   SYNTH_COLUMN_MAJOR  azimuth-interleaved output (one column of 64 lasers after another, the
+//                       order of raw HDL-64E packets) instead of ring-major
+//   SYNTH_LASER_AZ      per-laser azimuth offsets of up to +-4 deg (the HDL-64E rotational
+//                       corrections): rings start at different azimuths, so with column-major
+//                       order points before the halfPassed latch fall below startOri and get
+//                       relTime < 0, int(intensity) = scanID - 1 (scan_registration.cpp:263-296)
+//   SYNTH_BOUNDARY      laser elevations exactly on the ring rule's boundaries and cut-offs
+//                       (scan_registration.cpp:241-254: 2 - (k + 1/2)/3, -8.83 - (k + 1/2)/2,
+//                       2, -8.83, -24.33): a point's ring is decided by the last bits of
+//                       atan / sqrt / the division
+//   SYNTH_QUANTIZE      coordinates rounded to 1 cm: equal curvatures (std::sort ties of
+//                       :365-366) and points on VoxelGrid leaf boundaries
+constexpr int32_t SYNTH_COLUMN_MAJOR = 1, SYNTH_LASER_AZ = 2, SYNTH_BOUNDARY = 4, SYNTH_QUANTIZE = 8;
+
+int32_t synth_frame_ex(uint64_t seed, int32_t frame, int32_t n_az, double speed, int32_t flags, float* out_xyz,
+                       double* pose7);
+
 // one revolution: writes up to 64*n_az points (x,y,z, stride 3) in the SENSOR frame,
 // ring-major; returns the number of returns.  pose7 = q(x,y,z,w), t(x,y,z) ground truth.
 int32_t synth_frame(uint64_t seed, int32_t frame, int32_t n_az, double speed, float* out_xyz,
                     double* pose7) {
+  return synth_frame_ex(seed, frame, n_az, speed, 0, out_xyz, pose7);
+}
+
+int32_t synth_frame_ex(uint64_t seed, int32_t frame, int32_t n_az, double speed, int32_t flags, float* out_xyz,
+                       double* pose7) {
   Scene S{seed};
   double q[4], t[3];
   synth_pose(seed, frame, speed, q, t);
@@ -243,14 +269,31 @@ int32_t synth_frame(uint64_t seed, int32_t frame, int32_t n_az, double speed, fl
                     {2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)}};
   Rng rng{mix64(seed * 1000003ULL + (uint64_t)frame)};
   double az0 = 2.0 * M_PI * u01(mix64(seed ^ (uint64_t)frame * 77ULL)) / n_az;
-  int32_t n = 0;
+  double ce[64], se[64], daz[64];
   for (int ring = 0; ring < 64; ++ring) {
     double elev = ring < 32 ? (1.98 - ring / 3.0) : (-8.87 - (ring - 32) * 0.5);
-    double el = elev * M_PI / 180.0;
-    double ce = std::cos(el), se = std::sin(el);
-    for (int a = 0; a < n_az; ++a) {
-      double az = -(az0 + 2.0 * M_PI * a / n_az);  // clockwise
-      double ds[3] = {ce * std::cos(az), ce * std::sin(az), se};
+    if (flags & SYNTH_BOUNDARY) {
+      elev = ring < 32 ? 2.0 - (ring + 0.5) / 3.0 : -8.83 - (ring - 32 + 0.5) / 2.0;
+      if (ring == 0) elev = 2.0;
+      if (ring == 32) elev = -8.83;
+      if (ring == 63) elev = -24.33;
+    }
+    const double el = elev * M_PI / 180.0;
+    ce[ring] = std::cos(el);
+    se[ring] = std::sin(el);
+    // offsets falling with the laser index (plus jitter): in a column-major frame the first
+    // returning laser leads, and the first columns of the lasers after it lie before startOri
+    daz[ring] = (flags & SYNTH_LASER_AZ)
+                    ? (M_PI / 180.0) * (4.0 - 8.0 * ring / 63.0 + 0.5 * (2.0 * hrand(seed, 900, ring) - 1.0))
+                    : 0.0;
+  }
+  int32_t n = 0;
+  const bool cm = (flags & SYNTH_COLUMN_MAJOR) != 0;
+  for (int outer = 0; outer < (cm ? n_az : 64); ++outer) {
+    for (int inner = 0; inner < (cm ? 64 : n_az); ++inner) {
+      const int ring = cm ? inner : outer, a = cm ? outer : inner;
+      double az = -(az0 + 2.0 * M_PI * a / n_az + daz[ring]);  // clockwise
+      double ds[3] = {ce[ring] * std::cos(az), ce[ring] * std::sin(az), se[ring]};
       double dw[3] = {R[0][0] * ds[0] + R[0][1] * ds[1] + R[0][2] * ds[2],
                       R[1][0] * ds[0] + R[1][1] * ds[1] + R[1][2] * ds[2],
                       R[2][0] * ds[0] + R[2][1] * ds[1] + R[2][2] * ds[2]};
@@ -258,9 +301,12 @@ int32_t synth_frame(uint64_t seed, int32_t frame, int32_t n_az, double speed, fl
       double noise = 0.02 * rng.gauss();
       if (!(r < kMaxRange)) continue;
       r += noise;
-      out_xyz[3 * n + 0] = static_cast<float>(r * ds[0]);
-      out_xyz[3 * n + 1] = static_cast<float>(r * ds[1]);
-      out_xyz[3 * n + 2] = static_cast<float>(r * ds[2]);
+      float p[3] = {static_cast<float>(r * ds[0]), static_cast<float>(r * ds[1]), static_cast<float>(r * ds[2])};
+      if (flags & SYNTH_QUANTIZE)
+        for (float& v : p) v = static_cast<float>(std::round(static_cast<double>(v) * 100.0) / 100.0);
+      out_xyz[3 * n + 0] = p[0];
+      out_xyz[3 * n + 1] = p[1];
+      out_xyz[3 * n + 2] = p[2];
       ++n;
     }
   }

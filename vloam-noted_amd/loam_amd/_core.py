@@ -89,6 +89,7 @@ SIGNATURES = {
     "loam_odometry_input": (c_i32, [vp, c_i32, vp, c_i32, vp, c_i32, vp, c_i32, vp, c_i32]),
     "loam_odometry_input_device": (c_i32, [vp, c_i32, vp, c_i32, vp, c_i32, vp, c_i32, vp, c_i32]),
     "loam_odometry_solve": (c_i32, [vp]),
+    "loam_odometry_set_prior": (c_i32, [vp, c_i32, vp, vp]),
     "loam_odometry_output": (c_i32, [vp, c_i32, vp, vp, vp, vp, ctypes.POINTER(c_i32)]),
     "loam_odometry_last_cloud": (c_i32, [vp, c_i32, c_i32, ctypes.POINTER(vp)]),
     "loam_odometry_copy_last": (c_i32, [vp, c_i32, c_i32, vp, c_i32]),
@@ -141,6 +142,8 @@ SIGNATURES = {
     "loam_lm_solve": (c_i32, [c_i32, vp, c_i32, vp, c_i32, ctypes.POINTER(LMStats)]),
     "loam_lm_normal_equations": (c_i32, [c_i32, vp, c_i32, vp, vp, vp, vp]),
     "loam_voxel_grid": (c_i32, [c_i32, vp, c_i32, c_f, vp, ctypes.POINTER(c_i32)]),
+    "loam_voxel_grid_pcl": (c_i32, [c_i32, vp, c_i32, c_f, vp, ctypes.POINTER(c_i32)]),
+    "loam_sort_perm": (c_i32, [c_i32, vp, c_i32, c_i32, vp]),
     "loam_voxel_merge": (c_i32, [c_i32, vp, c_i32, vp, c_i32, c_f, vp, ctypes.POINTER(c_i32),
                                  ctypes.POINTER(c_i32)]),
     "loam_knn_radius": (c_i32, [c_i32, vp, c_i32, vp, c_i32, c_i32, c_f, vp, vp]),

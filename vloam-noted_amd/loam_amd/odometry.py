@@ -49,6 +49,16 @@ class BatchOdometry:
             args += [p, n]
         check(lib().loam_odometry_input_device(self.h, stream, *args))
 
+    def set_prior(self, stream, q=None, t=None):
+        """VO prior velo_last_VOT_velo_curr for the next solve (detach_vo_lo = 0 only,
+        laser_odometry.cpp:237-250); None clears it"""
+        if q is None:
+            check(lib().loam_odometry_set_prior(self.h, stream, None, None))
+            return
+        q = np.ascontiguousarray(q, dtype=np.float64)
+        t = np.ascontiguousarray(t, dtype=np.float64)
+        check(lib().loam_odometry_set_prior(self.h, stream, ptr(q), ptr(t)))
+
     def solve(self):
         check(lib().loam_odometry_solve(self.h))
 

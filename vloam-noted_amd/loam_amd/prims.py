@@ -1,7 +1,10 @@
 """Standalone HIP primitives behind the mapping stage (C-ABI, include/loam_core.h).
 
 Same argument meaning as the pieces of the reference they replace:
-  voxel_grid   pcl::VoxelGrid<PointXYZI>::filter (laser_mapping.cpp:492-500, :795-808)
+  voxel_grid   pcl::VoxelGrid<PointXYZI>::filter (laser_mapping.cpp:492-500, :795-808), a voxel's
+               points summed in input order (the mapper's kernels)
+  voxel_grid_pcl  the same with PCL's summation order (scan_registration.cpp:497-501's kernel)
+  sort_perm    std::sort's permutation under a key-only comparator (stdsort.h)
   knn_radius   pcl::KdTreeFLANN::nearestKSearch restricted to d2 < radius2 (:554, :633)
   lm_solve     ceres::Solve with the reference's options (:709-717) on factor records
   lm_normal_equations  cost, J^T J, J^T r at x (Huber-corrected, local 6-dof)
@@ -21,6 +24,23 @@ def voxel_grid(pts, leaf, device=0):
     n = _core.c_i32()
     check(lib().loam_voxel_grid(device, ptr(pts), len(pts), float(leaf), ptr(out), ctypes.byref(n)))
     return out[: n.value].copy()
+
+
+def voxel_grid_pcl(pts, leaf, device=0):
+    """VoxelGrid with PCL's own within-voxel summation order (std::sort permutation)"""
+    pts = f32x4(pts)
+    out = np.empty_like(pts)
+    n = _core.c_i32()
+    check(lib().loam_voxel_grid_pcl(device, ptr(pts), len(pts), float(leaf), ptr(out), ctypes.byref(n)))
+    return out[: n.value].copy()
+
+
+def sort_perm(keys, n_waves=16, device=0):
+    """the libstdc++ std::sort permutation of (keys[i], i) compared by key, computed on the GPU"""
+    k = np.ascontiguousarray(keys, dtype=np.uint32)
+    perm = np.empty(len(k), dtype=np.int32)
+    check(lib().loam_sort_perm(device, ptr(k), len(k), int(n_waves), ptr(perm)))
+    return perm
 
 
 def voxel_merge(fixed, added, leaf, device=0):

@@ -21,6 +21,9 @@ def _lib():
         lib.synth_frame.restype = ctypes.c_int32
         lib.synth_frame.argtypes = [ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32, ctypes.c_double,
                                     ctypes.c_void_p, ctypes.c_void_p]
+        lib.synth_frame_ex.restype = ctypes.c_int32
+        lib.synth_frame_ex.argtypes = [ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32, ctypes.c_double,
+                                       ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]
         lib.synth_pose.restype = None
         lib.synth_pose.argtypes = [ctypes.c_uint64, ctypes.c_double, ctypes.c_double,
                                    ctypes.c_void_p, ctypes.c_void_p]
@@ -28,11 +31,16 @@ def _lib():
     return _LIB
 
 
-def frame(seed: int, index: int, n_az: int = 2000, speed: float = 1.0):
+# edge-case modes (csrc/synth.cpp): azimuth-interleaved order, per-laser azimuth offsets,
+# elevations on the ring-rule boundaries, 1 cm coordinate quantization
+COLUMN_MAJOR, LASER_AZ, BOUNDARY, QUANTIZE = 1, 2, 4, 8
+
+
+def frame(seed: int, index: int, n_az: int = 2000, speed: float = 1.0, flags: int = 0):
     """Return (xyz float32 [n, 3] in the sensor frame, ground-truth pose7 = q xyzw + t)."""
     buf = np.empty((64 * n_az, 3), dtype=np.float32)
     pose = np.empty(7, dtype=np.float64)
-    n = _lib().synth_frame(seed, index, n_az, speed, buf.ctypes.data, pose.ctypes.data)
+    n = _lib().synth_frame_ex(seed, index, n_az, speed, flags, buf.ctypes.data, pose.ctypes.data)
     return buf[:n].copy(), pose
 
 
