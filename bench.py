@@ -72,6 +72,9 @@ def parse():
     ap.add_argument("--no-single-stream", action="store_true",
                     help="skip the single-stream (latency view) timing")
     ap.add_argument("--no-depth", action="store_true", help="skip the VO depth-association stage")
+    ap.add_argument("--exact-voxel-order", type=int, choices=[0, 1], default=1,
+                    help="mapper VoxelGrids in PCL's summation order (1, the reference's arithmetic) or input "
+                         "order (0, faster; maps differ by summation-order ulps)")
     ap.add_argument("--shard", action="store_true",
                     help="sharded mapping (SURVEY.md §8e): every stream split over all N ranks, map "
                          "blocks owned per rank, RCCL all-gather of 5-NN candidates per round and "
@@ -534,7 +537,8 @@ def main():
         # (speed: 2 beat 4 workgroups per stream; correctness needs no residency, lm.h)
         cus = torch.cuda.get_device_properties(local).multi_processor_count
         os.environ["LOAM_LM_G"] = os.environ.get("BENCH_LM_G") or str(max(1, cus // B))
-    mappers = [BatchMapper(Bh, device=local, max_map_points=args.map_points, comm=comm) for _ in range(H)]
+    mappers = [BatchMapper(Bh, device=local, max_map_points=args.map_points, comm=comm,
+                           exact_voxel_order=args.exact_voxel_order) for _ in range(H)]
     os.environ.pop("LOAM_LM_G", None) if H > 1 else None  # read at create; not for later handles
     mapper = mappers[0]
 
@@ -572,7 +576,7 @@ def main():
 
     single = None
     if not args.no_single_stream and rank == 0 and world == 1 and not args.shard:
-        m1 = BatchMapper(1, device=local)
+        m1 = BatchMapper(1, device=local, exact_voxel_order=args.exact_voxel_order)
         plan1 = [step_inputs(frames, 1, args.stride, k) for k in range(pre + K)]
         run_steps(m1, plan1, 0, pre)
         torch.cuda.synchronize(local)
@@ -633,6 +637,7 @@ def main():
                                    "(BASELINE configs[3])",
                        "streams_per_gpu": B, "frames_per_step": B if args.shard else B * world,
                        "n_az": args.n_az, "map_frames_before_timing": pre, "stride": args.stride,
+                       "voxel_order": "PCL (exact)" if args.exact_voxel_order else "input order",
                        "parallelism": (f"{B} streams, each sharded over {world} GPU(s): RCCL all-gather of the "
                                        f"5-NN candidates per round, all-reduce of the normal equations per LM "
                                        f"iteration" if args.shard else

@@ -50,6 +50,12 @@ typedef struct loam_params {
   int32_t max_input_points;         /* max points per input cloud (default 262144) */
   int32_t max_map_points;           /* arena capacity per map (corner/surf) (default 2097152) */
   int32_t max_submap_points;        /* 5x5x3-cube submap capacity per map (default 524288) */
+  /* the mapper's VoxelGrids (stacks, laser_mapping.cpp:492-500; cube re-filter, :795-808):
+   * 1 = PCL's within-voxel summation order (the libstdc++ sort permutation of voxel_grid.hpp;
+   * bit-exact with the reference arithmetic), 0 = input order (no sort emulation, merge path for
+   * cubes that gain a few points; centroids differ from PCL's within the float summation-order
+   * bound).  ScanRegistration's per-ring filter always uses PCL's order.  Default 1. */
+  int32_t exact_voxel_order;
 } loam_params;
 
 void loam_params_default(loam_params* p);

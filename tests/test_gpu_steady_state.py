@@ -49,14 +49,15 @@ def _check_map(m, after):
         assert sorted(got) == sorted(ref)
         for c in ref:
             assert got[c].shape == ref[c].shape, (key, c)
-            assert np.max(np.abs(got[c][:, :3] - ref[c][:, :3])) < 1e-5
+            assert np.all(np.abs(got[c][:, :3] - ref[c][:, :3]) <= 1e-5 + 4e-7 * np.abs(ref[c][:, :3]))
 
 
+@pytest.mark.parametrize("exact", [1, 0])
 @pytest.mark.parametrize("fi", STEADY)
-def test_steady_state_teacher_forced(seq, fi):
+def test_steady_state_teacher_forced(seq, fi, exact):
     rec = seq[fi]
     assert rec["stats"].corner_map > 20000 and rec["stats"].surf_map > 10000  # saturated window
-    m = BatchMapper(1)
+    m = BatchMapper(1, exact_voxel_order=exact)
     load_state(m, 0, rec["before"])
     m.input(0, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
     m.solve()
@@ -80,12 +81,16 @@ def test_full_density_recentering(seq):
     m.close()
 
 
-def test_free_running_300_frames(seq):
-    """the whole GPU chain on the raw scans, free-running, against the oracle chain"""
+@pytest.mark.parametrize("exact", [1, 0])
+def test_free_running_300_frames(seq, exact):
+    """the whole GPU chain on the raw scans, free-running, against the oracle chain.  PCL's
+    VoxelGrid order (default): every per-scan pose within 1e-4 of the oracle's.  Input order
+    (exact_voxel_order = 0): the maps differ from the oracle's by summation-order ulps, which a
+    free-running chain amplifies through threshold decisions; reported, bounded loosely"""
     from loam_amd import synth
     from loam_amd.odometry import BatchOdometry
     from loam_amd.scanreg import ScanRegistration
-    sr, od, mp = ScanRegistration(), BatchOdometry(1), BatchMapper(1)
+    sr, od, mp = ScanRegistration(), BatchOdometry(1), BatchMapper(1, exact_voxel_order=exact)
     dt, dr = [], []
     for f in range(300):
         xyz, _ = synth.frame(SEED, f, N_AZ)
@@ -102,8 +107,11 @@ def test_free_running_300_frames(seq):
         dt.append(float(np.linalg.norm(tm - tr)))
         dr.append(quat_angle(qm, qr))
     dt, dr = np.array(dt), np.array(dr)
-    print(f"free-running 300 frames: trans rms {np.sqrt(np.mean(dt ** 2)):.3e} max {dt.max():.3e} m, "
-          f"rot rms {np.sqrt(np.mean(dr ** 2)):.3e} max {dr.max():.3e} rad")
-    assert dt.max() < 1e-4 and dr.max() < 1e-4
+    print(f"free-running 300 frames (exact_voxel_order={exact}): trans rms {np.sqrt(np.mean(dt ** 2)):.3e} "
+          f"max {dt.max():.3e} m, rot rms {np.sqrt(np.mean(dr ** 2)):.3e} max {dr.max():.3e} rad")
+    if exact:
+        assert dt.max() < 1e-4 and dr.max() < 1e-4
+    else:
+        assert dt.max() < 0.1 and dr.max() < 0.01
     for h in (sr, od, mp):
         h.close()

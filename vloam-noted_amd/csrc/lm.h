@@ -645,18 +645,30 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
     double X[7];
 #pragma unroll
     for (int i = 0; i < 7; ++i) X[i] = sx[i];
-    // ---- share 0, then the shares nobody else took
+    // ---- share 0, then the shares nobody else took.  Structure (member loop too): every
+    // thread-0 region is bracketed by barriers, and every branch that skips a barrier tests an
+    // LDS word written in such a region and read through readfirstlane, so the control flow
+    // around barriers is uniform whatever the compiler does with the regions.  A share's
+    // completion (release) and the next claim are one thread-0 region.
     lm_eval_sum<kThreads>(J.R, J.nrec, X, 0, G, bsum0);
-    while (G > 1) {
+    if (G > 1) {
       if (tid == 0) sshare = 1 + (int)__hip_atomic_fetch_add(&sync[4 + pass], 1u, RLX_AGENT);
       __syncthreads();
-      const int c = __builtin_amdgcn_readfirstlane(sshare);
-      __syncthreads();
-      if (c >= G) break;
-      lm_share<kThreads>(J, X, c, G, pass, bsum);
-      // keeps lm_share's tid-0 release apart from the next claim: merged, they let the other
-      // lanes reach the loop's barrier on a shorter path and spin on a stale share forever
-      __syncthreads();
+      while (true) {
+        const int c = __builtin_amdgcn_readfirstlane(sshare);
+        if (c >= G) break;
+        lm_eval_sum<kThreads>(J.R, J.nrec, X, c, G, bsum);
+        if (tid < LM_NACC) J.part[(size_t)c * LM_NACC + tid] = bsum[tid];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // every thread has read sshare and stored its part
+        if (tid == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_fetch_add(&sync[4 + LM_MAX_PASSES + pass], 1u, RLX_AGENT);
+          sshare = 1 + (int)__hip_atomic_fetch_add(&sync[4 + pass], 1u, RLX_AGENT);
+        }
+        __syncthreads();
+      }
     }
     if (tid == 0 && J.prof) {
       const unsigned long long t1 = __builtin_readcyclecounter();

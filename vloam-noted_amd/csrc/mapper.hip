@@ -32,6 +32,7 @@
 #include "cubeindex.h"
 #include "lm.h"
 #include "voxel.h"
+#include "voxel_pcl.h"
 
 namespace loam {
 
@@ -49,7 +50,7 @@ constexpr int LM_EBLK = 32;     // LM evaluation workgroups per stream (grid-str
 constexpr int SUBMAP_BLOCKS = 64;
 constexpr int INS_SLOTS = WIN_VALID_MAX + EXTRA_CAP;
 constexpr int MAP_ERR_SUBMAP = 4, MAP_ERR_EXTRA = 8, MAP_ERR_HASH = 16, MAP_ERR_LM_SYNC = 32,
-              MAP_ERR_INDEX = 64, MAP_ERR_LIVE = 128;
+              MAP_ERR_INDEX = 64, MAP_ERR_LIVE = 128, MAP_ERR_SORT = 256;
 
 struct StreamFrame {
   double pose[7];  // in: initial guess (transformAssociateToMap); out: optimised pose
@@ -122,6 +123,13 @@ struct MapperDev {
   // sharded mode (loam_mapper_create_sharded): this rank of nrank; map points are stored by
   // the rank owning their 4 m block (comm.h, shard_owner); blk_v: voxels per block edge
   uint32_t compact_at = 0;  // an arena whose tail passed this is compacted
+  // exact_voxel_order: the stack and cube VoxelGrids in PCL's summation order (voxel_pcl.h);
+  // sort scratch [B][2][scratch_cap] (the stack at offset 0, the cubes from scratch_tail)
+  int pcl_order = 0;
+  uint64_t* pe;
+  uint32_t* pa;
+  uint32_t* pb;
+  uint64_t* ps;
   int rank = 0, nrank = 1, sharded = 0;
   int blk_v[2] = {1, 1};
   uint32_t* wcnt;        // [B][2][WIN_MAX] window cube counts (all-reduced over the ranks)
@@ -184,6 +192,41 @@ __global__ void k_shift_cubes(MapperDev D, const uint2* __restrict__ old_tab, ui
   }
 }
 
+// PCL-order VoxelGrid (voxel_pcl.h) in a VX_THREADS workgroup owning the whole LDS: the sort's
+// level lists in LDS (inputs up to ~115k points); the elements E and the stop lists A / B in LDS
+// too for inputs up to MP_LDS_N points (the sort's dependent accesses are LDS latency, not L2),
+// else at offset `so` of the (stream, map) sort scratch, where the sorted copy S always goes.
+// Returns false (MAP_ERR_SORT) when the input is too large for the lists.
+constexpr int MP_LDS_N = 8192;                                    // E 64 KiB + A, B 32 KiB each
+constexpr int MP_SEG_LDS = (VX_LDS_WORDS - 256 - 16 - 4 * MP_LDS_N) / 6;  // level lists beside them
+constexpr int MP_SEG_CAP = (VX_LDS_WORDS - 256 - 16) / 6;
+static_assert(MP_SEG_LDS >= MP_LDS_N / (SS_THRESHOLD + 1) + 2, "level lists of an LDS-resident sort");
+template <typename PF>
+__device__ inline bool map_voxel_pcl(const MapperDev& D, size_t sm, uint32_t so, const PF& P, int n, float leaf,
+                                     const VxPclOut& O, uint32_t* lds, int* err) {
+  if (n / (SS_THRESHOLD + 1) + 2 > MP_SEG_CAP || so + (uint32_t)n > (uint32_t)D.scratch_cap) {
+    if (threadIdx.x == 0) atomicOr(err, MAP_ERR_SORT);
+    return false;
+  }
+  VxMisc& M = *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192);
+  uint32_t* ws = lds + VX_LDS_WORDS - 256;
+  SsLevels* lev = reinterpret_cast<SsLevels*>(lds + VX_LDS_WORDS - 256 - 16);
+  const size_t b = sm * D.scratch_cap + so;
+  if (n <= MP_LDS_N) {
+    uint64_t* E = reinterpret_cast<uint64_t*>(lds);
+    uint32_t* A = lds + 2 * MP_LDS_N;
+    uint32_t* B = A + MP_LDS_N;
+    int* seg0 = reinterpret_cast<int*>(B + MP_LDS_N);
+    const VxPclScratch X{E, A, B, D.ps + b, lev, {seg0, seg0 + 3 * MP_SEG_LDS}, MP_SEG_LDS};
+    voxel_grid_pcl<VX_THREADS>(P, n, leaf, O, X, M, ws, err);
+  } else {
+    int* seg0 = reinterpret_cast<int*>(lds);
+    const VxPclScratch X{D.pe + b, D.pa + b, D.pb + b, D.ps + b, lev, {seg0, seg0 + 3 * MP_SEG_CAP}, MP_SEG_CAP};
+    voxel_grid_pcl<VX_THREADS>(P, n, leaf, O, X, M, ws, err);
+  }
+  return true;
+}
+
 // ---------------------------------------------------------------------------------------
 // VoxelGrid of the incoming feature clouds -> CornerStack / SurfStack (:492-500)
 // ---------------------------------------------------------------------------------------
@@ -194,6 +237,14 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
   StreamFrame& F = D.fr[s];
   if (!F.active) return;
   const size_t sm = sm_index(s, m);
+  if (D.pcl_order) {
+    VxPclOut O;
+    O.out = D.stack[m] + (size_t)s * D.max_in;
+    O.cap = D.max_in;
+    O.res_cnt = reinterpret_cast<uint32_t*>(m == 0 ? &F.nc_stack : &F.ns_stack);
+    map_voxel_pcl(D, sm, 0u, VxPtrSrc{F.in_ptr[m]}, m == 0 ? F.nc_in : F.ns_in, D.leaf[m], O, lds, &F.err);
+    return;
+  }
   VoxSeg S;
   S.src1 = nullptr;
   S.tag1 = nullptr;
@@ -862,12 +913,33 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
   S.prof = D.dbg + 11;  // merge phases: dbg[11..14]
   bool merged = false;
   const unsigned long long t0 = __builtin_readcyclecounter();
-  if (!append && n_new > 0 && n_new <= VX_MERGE_CAP && cv.y > 0 && *tok == cv.x + 1) {
-    merged = vx_merge_fixed_point(S, lds);
-    __syncthreads();  // false: grid overflow, full filter below
+  if (D.pcl_order && !append && n_new > 0) {
+    // PCL's summation order: the sort of old content ++ new points (voxel_pcl.h); the merge
+    // path (input order) does not apply
+    uint32_t* sb = lds + LW - 3;
+    const uint32_t n = cv.y + n_new;
+    if (threadIdx.x == 0) *sb = atomicAdd(&F.scratch_tail[m], n);
+    __syncthreads();
+    const uint32_t so = *sb;
+    __syncthreads();
+    VxPclOut O;
+    O.out = ar;
+    O.tail = &F.arena_tail[m];
+    O.cap = D.map_cap;
+    O.res_off = &tab[cube].x;
+    O.res_cnt = &tab[cube].y;
+    O.stable_out = tok;
+    map_voxel_pcl(D, sm_index(s, m), so, VxSrc{ar + cv.x, (int)cv.y, D.ins_sorted + sm_index(s, m) * D.max_in + i0},
+                  (int)n, D.leaf[m], O, lds, &F.err);
+    __syncthreads();
+  } else {
+    if (!append && n_new > 0 && n_new <= VX_MERGE_CAP && cv.y > 0 && *tok == cv.x + 1) {
+      merged = vx_merge_fixed_point(S, lds);
+      __syncthreads();  // false: grid overflow, full filter below
+    }
+    if (!merged) voxel_segment(S, lds);
+    __syncthreads();
   }
-  if (!merged) voxel_segment(S, lds);
-  __syncthreads();
   const unsigned long long t1 = __builtin_readcyclecounter();
   // the cube's new content -> its cell index (cubeindex.h)
   uint32_t* res = lds + LW - 2;
@@ -1123,6 +1195,7 @@ inline std::string map_err_text(int e) {
   add(MAP_ERR_LM_SYNC, "LM workgroup hand-off timed out");
   add(MAP_ERR_INDEX, "cube cell index capacity");
   add(MAP_ERR_LIVE, "live map larger than the arena's compaction bound");
+  add(MAP_ERR_SORT, "PCL-order VoxelGrid input larger than its sort lists / scratch");
   return m + " (flags " + std::to_string(e) + ")";
 }
 
@@ -1304,6 +1377,7 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
       if (genv && std::atoi(genv) > 0) h->lm_G = std::min(LM_EBLK, std::atoi(genv));
     }
   }
+  D.pcl_order = h->P.exact_voxel_order ? 1 : 0;
   D.leaf[0] = (float)h->P.mapping_line_resolution;
   D.leaf[1] = (float)h->P.mapping_plane_resolution;
   const size_t B = n_streams;
@@ -1357,6 +1431,12 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   ALLOC(h->tok_tmp, B * 2 * (size_t)NCUBE);
   ALLOC(D.dbg, LOAM_DEBUG_COUNTERS);
   ALLOC(D.vx_pts, B * 2 * (size_t)D.scratch_cap);
+  if (D.pcl_order) {
+    ALLOC(D.pe, B * 2 * (size_t)D.scratch_cap);
+    ALLOC(D.pa, B * 2 * (size_t)D.scratch_cap);
+    ALLOC(D.pb, B * 2 * (size_t)D.scratch_cap);
+    ALLOC(D.ps, B * 2 * (size_t)D.scratch_cap);
+  }
   ALLOC(D.vx_idx, B * 2 * (size_t)D.scratch_cap);
   ALLOC(D.partials, B * (size_t)D.max_chunks * LM_NACC);
   ALLOC(D.lm_sync, B * 2 * LM_SYNC_WORDS);

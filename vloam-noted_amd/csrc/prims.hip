@@ -72,16 +72,19 @@ __global__ void __launch_bounds__(VX_THREADS) k_voxel_one(VoxSeg S) {
 // merge path ran, 0 if it fell back to the full filter
 // PCL-order VoxelGrid (voxel_pcl.h) of one cloud in global scratch (any size)
 constexpr int P_PCL_THREADS = 1024;
-constexpr int P_PCL_STK = 8192;
+inline int ss_cap(int n) { return n / (SS_THRESHOLD + 1) + 2; }
 __global__ void __launch_bounds__(P_PCL_THREADS) k_voxel_pcl_one(const float4* src, int n, float leaf, float4* out,
                                                                  uint32_t* out_n, uint64_t* E, uint32_t* A,
-                                                                 uint32_t* B, uint64_t* S, int* err) {
-  __shared__ int stk[3 * P_PCL_STK];
-  __shared__ SsCtl ctl;
+                                                                 uint32_t* B, uint64_t* S, int* seg, int cap,
+                                                                 int* err) {
+  __shared__ SsLevels lev;
   __shared__ VxMisc M;
   __shared__ uint32_t ws[P_PCL_THREADS / 64 + 1];
-  const VxPclScratch X{E, A, B, S, &ctl, stk, P_PCL_STK};
-  voxel_grid_pcl<P_PCL_THREADS>(src, n, leaf, out, out_n, X, M, ws, err);
+  const VxPclScratch X{E, A, B, S, &lev, {seg, seg + 3 * cap}, cap};
+  VxPclOut O;
+  O.out = out;
+  O.res_cnt = out_n;
+  voxel_grid_pcl<P_PCL_THREADS>(VxPtrSrc{src}, n, leaf, O, X, M, ws, err);
 }
 
 struct PKeyLess {
@@ -90,18 +93,16 @@ struct PKeyLess {
 
 // std::sort permutation of (keys[i], i) by key (stdsort.h), NT threads cooperating
 __global__ void __launch_bounds__(P_PCL_THREADS) k_sort_perm(const uint32_t* keys, int n, int32_t* perm, uint64_t* E,
-                                                             uint32_t* A, uint32_t* B, uint64_t* S, int nwaves,
-                                                             int* err) {
-  __shared__ int stk[3 * P_PCL_STK];
-  __shared__ SsCtl ctl;
+                                                             uint32_t* A, uint32_t* B, uint64_t* S, int* seg, int cap,
+                                                             int nwaves, int* err) {
+  __shared__ SsLevels lev;
   const int tid = threadIdx.x;
   for (int i = tid; i < n; i += P_PCL_THREADS) E[i] = ((uint64_t)keys[i] << 32) | (uint32_t)i;
-  if (tid == 0) ss_init(&ctl, stk, n);
-  __syncthreads();
+  if (tid == 0) ss_levels_init(&lev, n, seg, seg + 3 * cap, cap);
   const PKeyLess less;
-  if ((tid >> 6) < nwaves) ss_loop(E, A, B, &ctl, stk, P_PCL_STK, less);
+  ss_levels<true>(E, A, B, &lev, tid >> 6, nwaves, less);
   __syncthreads();
-  if (tid == 0 && ctl.err) *err = ctl.err;
+  if (tid == 0 && lev.err) err[0] = lev.err;
   ss_final(E, A, B, n, S, tid, P_PCL_THREADS, less);
   __syncthreads();
   for (int i = tid; i < n; i += P_PCL_THREADS) perm[i] = (int32_t)(uint32_t)S[i];
@@ -373,7 +374,9 @@ int32_t loam_voxel_grid_pcl(int32_t device, const float* in, int32_t n, float le
   int32_t rc = ensure_device(device);
   if (rc != LOAM_OK) return rc;
   LOAM_HIP(hipSetDevice(device));
-  DevBuf din, dout, de, da, db, ds, dcnt, derr;
+  DevBuf din, dout, de, da, db, ds, dseg, dcnt, derr;
+  const int cap = ss_cap(n);
+  LOAM_HIP(dmalloc<int>(dseg, 6 * (size_t)cap));
   LOAM_HIP(dmalloc<float4>(din, n));
   LOAM_HIP(dmalloc<float4>(dout, n));
   LOAM_HIP(dmalloc<uint64_t>(de, n));
@@ -385,14 +388,14 @@ int32_t loam_voxel_grid_pcl(int32_t device, const float* in, int32_t n, float le
   if (n) LOAM_HIP(hipMemcpy(din.p, in, sizeof(float4) * n, hipMemcpyHostToDevice));
   k_voxel_pcl_one<<<1, P_PCL_THREADS>>>((const float4*)din.p, n, leaf, (float4*)dout.p, (uint32_t*)dcnt.p,
                                         (uint64_t*)de.p, (uint32_t*)da.p, (uint32_t*)db.p, (uint64_t*)ds.p,
-                                        (int*)derr.p);
+                                        (int*)dseg.p, cap, (int*)derr.p);
   LOAM_HIP(hipGetLastError());
   uint32_t cnt = 0;
   int err = 0;
   LOAM_HIP(hipMemcpy(&cnt, dcnt.p, sizeof(uint32_t), hipMemcpyDeviceToHost));
   LOAM_HIP(hipMemcpy(&err, derr.p, sizeof(int), hipMemcpyDeviceToHost));
   if (err) {
-    set_error("loam_voxel_grid_pcl: std::sort emulation stack overflow");
+    set_error("loam_voxel_grid_pcl: std::sort emulation level list overflow");
     return LOAM_ERR_CAPACITY;
   }
   if (cnt) LOAM_HIP(hipMemcpy(out, dout.p, sizeof(float4) * cnt, hipMemcpyDeviceToHost));
@@ -409,7 +412,9 @@ int32_t loam_sort_perm(int32_t device, const uint32_t* keys, int32_t n, int32_t 
   if (rc != LOAM_OK) return rc;
   LOAM_HIP(hipSetDevice(device));
   if (n == 0) return LOAM_OK;
-  DevBuf dk, dp, de, da, db, ds, derr;
+  DevBuf dk, dp, de, da, db, ds, dseg, derr;
+  const int cap = ss_cap(n);
+  LOAM_HIP(dmalloc<int>(dseg, 6 * (size_t)cap));
   LOAM_HIP(dmalloc<uint32_t>(dk, n));
   LOAM_HIP(dmalloc<int32_t>(dp, n));
   LOAM_HIP(dmalloc<uint64_t>(de, n));
@@ -419,12 +424,12 @@ int32_t loam_sort_perm(int32_t device, const uint32_t* keys, int32_t n, int32_t 
   LOAM_HIP(dmalloc<int>(derr, 1));
   LOAM_HIP(hipMemcpy(dk.p, keys, sizeof(uint32_t) * n, hipMemcpyHostToDevice));
   k_sort_perm<<<1, P_PCL_THREADS>>>((const uint32_t*)dk.p, n, (int32_t*)dp.p, (uint64_t*)de.p, (uint32_t*)da.p,
-                                    (uint32_t*)db.p, (uint64_t*)ds.p, n_waves, (int*)derr.p);
+                                    (uint32_t*)db.p, (uint64_t*)ds.p, (int*)dseg.p, cap, n_waves, (int*)derr.p);
   LOAM_HIP(hipGetLastError());
   int err = 0;
   LOAM_HIP(hipMemcpy(&err, derr.p, sizeof(int), hipMemcpyDeviceToHost));
   if (err) {
-    set_error("loam_sort_perm: std::sort emulation stack overflow");
+    set_error("loam_sort_perm: std::sort emulation level list overflow");
     return LOAM_ERR_CAPACITY;
   }
   LOAM_HIP(hipMemcpy(perm, dp.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost));

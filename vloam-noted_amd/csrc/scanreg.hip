@@ -84,6 +84,7 @@ struct SrDev {
   uint32_t* ss_a;
   uint32_t* ss_b;
   uint64_t* ss_s;
+  int* ss_seg;  // [2][3 * SR_SS_GSEG] level lists of the long-sector path (one sector at a time)
 };
 
 // scan_registration.cpp:217-259 (float atan/sqrt like the reference's float overloads)
@@ -324,7 +325,8 @@ __device__ inline void sr_wave_sort(const float* curv, int sp, int len, uint64_t
 constexpr int SR_SEL_THREADS = 512;
 constexpr int SR_WSORT_MAX = 1024;  // register sort (one wave per sector) up to this length
 constexpr int SR_SS_LDS = 512;      // tied sectors re-sorted in LDS up to this length (else global)
-constexpr int SR_SS_STK = 48;       // segment stack of one wave (depth <= 2 log2(n) + 1)
+constexpr int SR_SS_SEG = SR_WSORT_MAX / 17 + 2;  // level list of one wave-sorted sector
+constexpr int SR_SS_GSEG = 6 * SR_WSORT_MAX / 17 + 2;  // long sectors: global level lists
 
 struct SrCurvLess {  // the reference's comparator: cloudCurvature[i] < cloudCurvature[j]
   __device__ bool operator()(uint64_t a, uint64_t b) const {
@@ -338,7 +340,7 @@ struct SrCurvLess {  // the reference's comparator: cloudCurvature[i] < cloudCur
 // the identity, :341) into K.  One wave; E/A/B in LDS for short sectors, else the global
 // scratch at the sector's cloud positions.
 __device__ inline void sr_exact_sector(const SrDev& D, int sp, int len, uint64_t* K, uint64_t* lE, uint32_t* lA,
-                                       uint32_t* lB, SsCtl* ctl, int* stk) {
+                                       uint32_t* lB, SsLevels* lev, int* seg0, int* seg1, int cap) {
   const int lane = threadIdx.x & 63;
   ss_wave_fence();
   bool tie = false;
@@ -350,12 +352,11 @@ __device__ inline void sr_exact_sector(const SrDev& D, int sp, int len, uint64_t
   uint32_t* B = lds ? lB : D.ss_b + sp;
   for (int k = lane; k < len; k += 64)
     E[k] = ((uint64_t)__float_as_uint(D.curv[sp + k]) << 32) | (uint32_t)(sp + k);
-  if (lane == 0) ss_init(ctl, stk, len);
-  ss_wave_fence();
+  if (lane == 0) ss_levels_init(lev, len, seg0, seg1, cap);
   const SrCurvLess less;
-  ss_loop(E, A, B, ctl, stk, SR_SS_STK, less);
+  ss_levels<false>(E, A, B, lev, 0, 1, less);
   ss_final(E, A, B, len, K, lane, 64, less);
-  if (lane == 0 && ctl->err) atomicOr(&D.fr->err, SR_ERR_SORT);
+  if (lane == 0 && lev->err) atomicOr(&D.fr->err, SR_ERR_SORT);
   ss_wave_fence();
 }
 
@@ -456,8 +457,8 @@ __global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(SrDev D) {
   __shared__ uint32_t ws[SR_SEL_THREADS / 64];
   __shared__ uint64_t ssE[6][SR_SS_LDS];  // exact re-sort of tied sectors (one wave each)
   __shared__ uint32_t ssA[6][SR_SS_LDS], ssB[6][SR_SS_LDS];
-  __shared__ int ssStk[6][3 * SR_SS_STK];
-  __shared__ SsCtl ssCtl[6];
+  __shared__ int ssSeg[6][2][3 * SR_SS_SEG];
+  __shared__ SsLevels ssLev[6];
   const int r = blockIdx.x;
   SrFrame& F = *D.fr;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
@@ -499,8 +500,8 @@ __global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(SrDev D) {
   if (fast && wid < 6) {
     if (maxlen <= 512) sr_wave_sort<8>(D.curv, sp[wid], len[wid], keys + wid * SR_WSORT_MAX);
     else sr_wave_sort<16>(D.curv, sp[wid], len[wid], keys + wid * SR_WSORT_MAX);
-    sr_exact_sector(D, sp[wid], len[wid], keys + wid * SR_WSORT_MAX, ssE[wid], ssA[wid], ssB[wid], &ssCtl[wid],
-                    ssStk[wid]);
+    sr_exact_sector(D, sp[wid], len[wid], keys + wid * SR_WSORT_MAX, ssE[wid], ssA[wid], ssB[wid], &ssLev[wid],
+                    ssSeg[wid][0], ssSeg[wid][1], SR_SS_SEG);
   }
   __syncthreads();
   int nsh = 0, nls = 0, nfl = 0;  // valid in wave 0
@@ -530,7 +531,9 @@ __global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(SrDev D) {
           __syncthreads();
         }
       }
-      if (wid == 0) sr_exact_sector(D, sp[j], len[j], keys, nullptr, nullptr, nullptr, &ssCtl[0], ssStk[0]);
+      if (wid == 0)
+        sr_exact_sector(D, sp[j], len[j], keys, nullptr, nullptr, nullptr, &ssLev[0], D.ss_seg, D.ss_seg + 3 * SR_SS_GSEG,
+                        SR_SS_GSEG);
       __syncthreads();
     }
     if (wid == 0) sr_greedy(D, r, base, K, len[j], picked, lab, gapok, nsh, nls, nfl);
@@ -569,13 +572,13 @@ __global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(SrDev D) {
 // std::sort emulation in LDS up to SRV_LDS points, else in the global scratch
 constexpr int SRV_THREADS = 512;
 constexpr int SRV_LDS = 4096;
-constexpr int SRV_STK = 1024;  // pending segments (<= n / 17 + 1)
+constexpr int SRV_SEG = SR_RING_CAP / 17 + 2;  // level list (<= n / 17 + 1 segments per level)
 
 __global__ void __launch_bounds__(SRV_THREADS) k_sr_ringvox(SrDev D) {
   __shared__ uint64_t sE[SRV_LDS], sS[SRV_LDS];
   __shared__ uint32_t sA[SRV_LDS], sB[SRV_LDS];
-  __shared__ int stk[3 * SRV_STK];
-  __shared__ SsCtl ctl;
+  __shared__ int seg[2][3 * SRV_SEG];
+  __shared__ SsLevels lev;
   __shared__ VxMisc M;
   __shared__ uint32_t ws[SRV_THREADS / 64 + 1];
   const int r = blockIdx.x;
@@ -584,9 +587,11 @@ __global__ void __launch_bounds__(SRV_THREADS) k_sr_ringvox(SrDev D) {
   const int n = F.n_less_flat_scan[r];
   const bool lds = n <= SRV_LDS;
   const VxPclScratch X{lds ? sE : D.ss_e + base, lds ? sA : D.ss_a + base, lds ? sB : D.ss_b + base,
-                       lds ? sS : D.ss_s + base, &ctl, stk, SRV_STK};
-  voxel_grid_pcl<SRV_THREADS>(D.less_flat_scan + base, n, 0.2f, D.less_flat_ds + base, &F.n_less_flat[r], X, M, ws,
-                              &F.err);
+                       lds ? sS : D.ss_s + base, &lev, {seg[0], seg[1]}, SRV_SEG};
+  VxPclOut O;
+  O.out = D.less_flat_ds + base;
+  O.res_cnt = &F.n_less_flat[r];
+  voxel_grid_pcl<SRV_THREADS>(VxPtrSrc{D.less_flat_scan + base}, n, 0.2f, O, X, M, ws, &F.err);
 }
 
 // concatenation of the per-ring outputs in ring order
@@ -716,6 +721,7 @@ int32_t loam_scanreg_create(const loam_params* p, int32_t device, loam_scanreg**
   SRA(D.ss_a, cap);
   SRA(D.ss_b, cap);
   SRA(D.ss_s, cap);
+  SRA(D.ss_seg, 6 * SR_SS_GSEG);
 #undef SRA
   D.out[0] = D.cloud;
   D.sort_ind = nullptr;
@@ -800,7 +806,7 @@ static int32_t sr_finish(loam_scanreg* h) {
   h->D.stride = h->pending_stride;
   if (h->hf.err) {
     set_error(std::string("loam_scanreg_input: ") +
-              ((h->hf.err & SR_ERR_SORT) ? "std::sort emulation stack overflow" : "ring or sector larger than the LDS capacity") +
+              ((h->hf.err & SR_ERR_SORT) ? "std::sort emulation level list overflow" : "ring or sector larger than the LDS capacity") +
               " (err " + std::to_string(h->hf.err) + ")");
     return LOAM_ERR_CAPACITY;
   }

@@ -19,8 +19,8 @@
 //           __introsort_loop(cut, last, depth_limit); last = cut
 //   __final_insertion_sort(first, last)
 // and this header reproduces its output permutation exactly:
-//   * segments are independent, so any processing order gives the same result; waves pop
-//     segments from a shared LDS stack (one wave per segment);
+//   * segments are independent, so any processing order gives the same result: the waves
+//     take the segments level by level (one wave per segment, a barrier between levels);
 //   * the Hoare scan is computed in parallel: with l_k the k-th position (ascending) in
 //     [first+1, last) whose key is !(key < pivot) and r_k the k-th position (descending) in
 //     [first, last) whose key is !(pivot < key) (first itself, the pivot, is the last r), the
@@ -43,34 +43,25 @@ namespace loam {
 
 constexpr int SS_THRESHOLD = 16;  // _S_threshold
 
-// Shared state of one sort (LDS): a stack of pending segments guarded by a lock, and the
-// count of segments not yet finished (the exit condition every wave reaches).
-struct SsCtl {
-  int lock;
-  int top;
-  int pending;
+// Pending segments of one sort, level by level: the segments of depth level `lev` are in
+// seg[lev & 1][0 .. cnt[lev & 1]); every one longer than 16 elements.  Segments of one level are
+// disjoint, so a level holds at most n / 17 + 1 of them (cap).
+struct SsLevels {
+  int cnt[2];
   int err;
+  int cap;
+  int* seg[2];  // [cap][3] (lo, hi, depth budget), LDS or global
 };
 
 // Elements are 64-bit; Less compares two elements (the reference's comparator).  Per sort:
 //   E[n]    the elements, permuted in place by the partitions (LDS or global)
-//   A[n+1], B[n+1]  u32 scratch: partition stop lists, then the small-segment bounds
-//   stk     3 * stk_cap ints of LDS
+//   A[n], B[n]  u32 scratch: partition stop lists, then the final segments' bounds
 // the wave's lanes see each other's writes (LDS or global: workgroup scope waits for the
 // stores; the CU's L1 is write-through, so no invalidation is needed at this scope)
 __device__ inline void ss_wave_fence() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-__device__ inline void ss_lock(SsCtl* c) {
-  while (atomicCAS(&c->lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(1);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-__device__ inline void ss_unlock(SsCtl* c) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  atomicExch(&c->lock, 0);
 }
 
 // libstdc++ __adjust_heap + __push_heap on E[first ..], one lane
@@ -198,103 +189,69 @@ __device__ inline void ss_mark(uint32_t* A, uint32_t* B, int lo, int hi, bool so
   }
 }
 
-// The introsort loop over [0, n), run by every wave that shares `ctl` (nw waves call it);
-// the caller initialised ctl (ss_init) and a barrier separates that from this call.
-// stk_cap: stack entries.  max_spins bounds the idle waiting (ctl->err set when exceeded).
-template <typename T, typename Less>
-__device__ inline void ss_loop(T* E, uint32_t* A, uint32_t* B, SsCtl* ctl, int* stk, int stk_cap,
-                               const Less& less) {
-  const int lane = threadIdx.x & 63;
-  int spins = 0;
-  while (true) {
-    int lo = 0, hi = 0, d = -1, state = 0;  // state: 0 got a segment, 1 idle, 2 done
-    if (lane == 0) {
-      ss_lock(ctl);
-      if (ctl->top > 0) {
-        const int t = --ctl->top;
-        lo = stk[3 * t];
-        hi = stk[3 * t + 1];
-        d = stk[3 * t + 2];
-      } else {
-        state = ctl->pending == 0 ? 2 : 1;
-      }
-      ss_unlock(ctl);
-    }
-    state = __builtin_amdgcn_readfirstlane(state);
-    if (state == 2) break;
-    if (state == 1) {
-      if (++spins > (1 << 22)) {  // cannot happen while the waves progress; never hang
-        if (lane == 0) atomicOr(&ctl->err, 1);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-      continue;
-    }
-    lo = __builtin_amdgcn_readfirstlane(lo);
-    hi = __builtin_amdgcn_readfirstlane(hi);
-    d = __builtin_amdgcn_readfirstlane(d);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    // run this segment down its left spine, pushing the right parts
-    while (true) {
-      if (hi - lo <= SS_THRESHOLD) {
-        ss_mark(A, B, lo, hi, false);
-        break;
-      }
-      if (d == 0) {
-        if (lane == 0) ss_heap_sort(E, lo, hi, less);
-        ss_wave_fence();
-        ss_mark(A, B, lo, hi, true);
-        break;
-      }
-      --d;
-      const int cut = ss_partition(E, A, B, lo, hi, less);
-      // right part [cut, hi) to the stack (other waves may take it), continue with the left
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (hi - cut > SS_THRESHOLD) {
-        if (lane == 0) {
-          ss_lock(ctl);
-          const int t = ctl->top;
-          if (t < stk_cap) {
-            stk[3 * t] = cut;
-            stk[3 * t + 1] = hi;
-            stk[3 * t + 2] = d;
-            ctl->top = t + 1;
-            ctl->pending += 1;
-          } else {
-            ctl->err |= 2;
-          }
-          ss_unlock(ctl);
-        }
-      } else {
-        ss_mark(A, B, cut, hi, false);
-      }
-      hi = cut;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) {
-      ss_lock(ctl);
-      ctl->pending -= 1;
-      ss_unlock(ctl);
-    }
-    spins = 0;
+// Init with the root segment [0, n) (one thread; a barrier / wave fence before ss_levels).
+__device__ inline void ss_levels_init(SsLevels* L, int n, int* seg0, int* seg1, int cap) {
+  L->seg[0] = seg0;
+  L->seg[1] = seg1;
+  L->cap = cap;
+  L->err = 0;
+  L->cnt[1] = 0;
+  L->cnt[0] = n > SS_THRESHOLD ? 1 : 0;
+  if (n > SS_THRESHOLD) {
+    seg0[0] = 0;
+    seg0[1] = n;
+    seg0[2] = 2 * (31 - __clz(n));  // 2 * __lg(n)
   }
 }
 
-// Init of the shared state with the root segment [0, n), by one thread (then a barrier / wave
-// fence before ss_loop)
-__device__ inline void ss_init(SsCtl* ctl, int* stk, int n) {
-  ctl->lock = 0;
-  ctl->err = 0;
-  if (n > SS_THRESHOLD) {
-    int lg = 31 - __clz(n);
-    stk[0] = 0;
-    stk[1] = n;
-    stk[2] = 2 * lg;
-    ctl->top = 1;
-    ctl->pending = 1;
-  } else {
-    ctl->top = 0;
-    ctl->pending = 0;
+// The introsort loop over [0, n), level by level.  Every wave of the group calls it (WG: the
+// whole workgroup, barriers are __syncthreads; else one wave alone); waves w < nw take the
+// level's segments w, w + nw, ...  No waiting on other waves outside the barriers, and at most
+// 2 * __lg(n) + 1 levels (each level lowers the depth budget by one).
+template <bool WG, typename T, typename Less>
+__device__ inline void ss_levels(T* E, uint32_t* A, uint32_t* B, SsLevels* L, int wave, int nw, const Less& less) {
+  const int lane = threadIdx.x & 63;
+  auto barrier = [] {
+    if (WG) __syncthreads();
+    else ss_wave_fence();
+  };
+  for (int lev = 0;; ++lev) {
+    barrier();
+    const int cur = lev & 1, nxt = cur ^ 1;
+    const int cnt = L->cnt[cur];
+    if (cnt == 0) break;
+    const int* sg = L->seg[cur];
+    for (int k = wave; wave < nw && k < cnt; k += nw) {
+      const int lo = sg[3 * k], hi = sg[3 * k + 1], d = sg[3 * k + 2];
+      if (d == 0) {  // depth limit: __partial_sort(first, last, last)
+        if (lane == 0) ss_heap_sort(E, lo, hi, less);
+        ss_wave_fence();
+        ss_mark(A, B, lo, hi, true);
+        continue;
+      }
+      const int cut = ss_partition(E, A, B, lo, hi, less);
+      const int parts[2][2] = {{lo, cut}, {cut, hi}};
+      for (int q = 0; q < 2; ++q) {
+        const int a = parts[q][0], b = parts[q][1];
+        if (b - a > SS_THRESHOLD) {
+          if (lane == 0) {
+            const int t = atomicAdd(&L->cnt[nxt], 1);
+            if (t < L->cap) {
+              int* o = L->seg[nxt] + 3 * t;
+              o[0] = a;
+              o[1] = b;
+              o[2] = d - 1;
+            } else {
+              atomicOr(&L->err, 2);
+            }
+          }
+        } else {
+          ss_mark(A, B, a, b, false);
+        }
+      }
+    }
+    barrier();  // every append to level lev + 1 done, every read of this level's count done
+    if (wave == 0 && lane == 0) L->cnt[cur] = 0;
   }
 }
 

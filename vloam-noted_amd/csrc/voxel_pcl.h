@@ -22,9 +22,9 @@ struct VxPclScratch {
   uint32_t* A;   // n
   uint32_t* B;   // n
   uint64_t* S;   // n: sorted
-  SsCtl* ctl;    // LDS
-  int* stk;      // LDS, 3 * stk_cap
-  int stk_cap;
+  SsLevels* lev;  // LDS
+  int* seg[2];    // 3 * cap ints each (LDS or global)
+  int cap;        // >= n / 17 + 1
 };
 
 struct VxPtrSrc {
@@ -36,30 +36,62 @@ struct VxIdxLess {
   __device__ bool operator()(uint64_t a, uint64_t b) const { return (uint32_t)(a >> 32) < (uint32_t)(b >> 32); }
 };
 
-// All NT threads call it.  out receives the centroids (at most n), *out_n their count.
-// ws: >= NT / 64 + 1 words of LDS; M: LDS misc.
-template <int NT>
-__device__ inline void voxel_grid_pcl(const float4* src, int n, float leaf, float4* out, uint32_t* out_n,
-                                      const VxPclScratch& X, VxMisc& M, uint32_t* ws, int* err) {
+// Where the centroids go: out[0 ..) (tail == nullptr), or a block of exactly the output
+// count allocated at *tail (the mapper's arena).  res_off / res_cnt / stable_out optional:
+// the block's offset and count, and (offset + 1) when the output is a VoxelGrid fixed point
+// (every centroid inside its own voxel: re-filtering it is the identity), else 0.
+struct VxPclOut {
+  float4* out;
+  uint32_t* tail = nullptr;
+  uint32_t cap = 0xFFFFFFFFu;
+  uint32_t* res_off = nullptr;
+  uint32_t* res_cnt = nullptr;
+  uint32_t* stable_out = nullptr;
+};
+
+// All NT threads call it.  P(i): the i-th input point (i < n).  ws: >= NT / 64 + 1 words of
+// LDS; M: LDS misc.  err |= 4: level list overflow, |= 2 (VX_ERR_OUTPUT): output block past cap.
+template <int NT, typename PF>
+__device__ inline void voxel_grid_pcl(const PF& P, int n, float leaf, const VxPclOut& O, const VxPclScratch& X,
+                                      VxMisc& M, uint32_t* ws, int* err) {
   const int tid = threadIdx.x;
+  auto finish = [&](uint32_t base, uint32_t cnt, bool fixed) {
+    if (O.res_off) *O.res_off = base;
+    if (O.res_cnt) *O.res_cnt = cnt;
+    if (O.stable_out) *O.stable_out = fixed ? base + 1 : 0u;
+  };
+  auto alloc = [&](uint32_t cnt) {  // thread 0; 0xFFFFFFFF: no room
+    uint32_t b = O.tail ? atomicAdd(O.tail, cnt) : 0u;
+    if (b + cnt > O.cap) {
+      atomicOr(err, VX_ERR_OUTPUT);
+      b = 0xFFFFFFFFu;
+    }
+    return b;
+  };
   if (n <= 0) {
-    if (tid == 0) *out_n = 0;
+    if (tid == 0) finish(0, 0, false);
     return;
   }
-  vx_geometry<VxPtrSrc, NT>(VxPtrSrc{src}, (uint32_t)n, leaf, M);
+  vx_geometry<PF, NT>(P, (uint32_t)n, leaf, M);
   const VxGeom g = M.g;
   if (g.overflow) {  // "Leaf size is too small for the input dataset": output = input
-    for (int i = tid; i < n; i += NT) out[i] = src[i];
-    if (tid == 0) *out_n = (uint32_t)n;
+    if (tid == 0) M.sbase[1] = alloc((uint32_t)n);
+    __syncthreads();
+    const uint32_t b = M.sbase[1];
+    if (b == 0xFFFFFFFFu) return;
+    for (int i = tid; i < n; i += NT) O.out[b + i] = P((uint32_t)i);
+    if (tid == 0) finish(b, (uint32_t)n, false);
     return;
   }
-  for (int i = tid; i < n; i += NT) X.E[i] = ((uint64_t)vx_key(g, src[i]) << 32) | (uint32_t)i;
-  if (tid == 0) ss_init(X.ctl, X.stk, n);
-  __syncthreads();
+  for (int i = tid; i < n; i += NT) X.E[i] = ((uint64_t)vx_key(g, P((uint32_t)i)) << 32) | (uint32_t)i;
+  if (tid == 0) {
+    ss_levels_init(X.lev, n, X.seg[0], X.seg[1], X.cap);
+    M.moved = 0;
+  }
   const VxIdxLess less;
-  ss_loop(X.E, X.A, X.B, X.ctl, X.stk, X.stk_cap, less);
+  ss_levels<true>(X.E, X.A, X.B, X.lev, tid >> 6, NT / 64, less);
   __syncthreads();
-  if (tid == 0 && X.ctl->err) atomicOr(err, 4);
+  if (tid == 0 && X.lev->err) atomicOr(err, 4);
   ss_final(X.E, X.A, X.B, n, X.S, tid, NT, less);
   __syncthreads();
   // runs of equal idx: thread t owns positions [t * per, (t + 1) * per)
@@ -70,22 +102,31 @@ __device__ inline void voxel_grid_pcl(const float4* src, int n, float leaf, floa
     starts += (i == 0 || (uint32_t)(X.S[i] >> 32) != (uint32_t)(X.S[i - 1] >> 32)) ? 1u : 0u;
   uint32_t tot;
   uint32_t o = vx_block_scan_t<NT>(starts, ws, &tot);
+  if (tid == 0) M.sbase[1] = alloc(tot);
+  __syncthreads();
+  const uint32_t b = M.sbase[1];
+  if (b == 0xFFFFFFFFu) return;
+  bool moved = false;
   for (int i = p0; i < p1; ++i) {
     const uint32_t key = (uint32_t)(X.S[i] >> 32);
     if (i > 0 && (uint32_t)(X.S[i - 1] >> 32) == key) continue;
     float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
     int j = i;
     for (; j < n && (uint32_t)(X.S[j] >> 32) == key; ++j) {
-      const float4 p = src[(uint32_t)X.S[j]];
+      const float4 p = P((uint32_t)X.S[j]);
       sx += p.x;
       sy += p.y;
       sz += p.z;
       si += p.w;
     }
     const float c = (float)(j - i);
-    out[o++] = make_float4(sx / c, sy / c, sz / c, si / c);
+    const float4 cen = make_float4(sx / c, sy / c, sz / c, si / c);
+    moved |= vx_key(g, cen) != key;
+    O.out[b + o++] = cen;
   }
-  if (tid == 0) *out_n = tot;
+  if (moved) M.moved = 1;
+  __syncthreads();
+  if (tid == 0) finish(b, tot, M.moved == 0);
 }
 
 }  // namespace loam

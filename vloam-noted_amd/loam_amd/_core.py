@@ -33,7 +33,7 @@ class Params(ctypes.Structure):
                 ("map_pub_number", c_i32), ("mapping_line_resolution", c_d),
                 ("mapping_plane_resolution", c_d), ("detach_vo_lo", c_i32),
                 ("verbose_level", c_i32), ("max_input_points", c_i32),
-                ("max_map_points", c_i32), ("max_submap_points", c_i32)]
+                ("max_map_points", c_i32), ("max_submap_points", c_i32), ("exact_voxel_order", c_i32)]
 
 
 class LMStats(ctypes.Structure):
