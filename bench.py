@@ -72,9 +72,11 @@ def parse():
     ap.add_argument("--no-single-stream", action="store_true",
                     help="skip the single-stream (latency view) timing")
     ap.add_argument("--no-depth", action="store_true", help="skip the VO depth-association stage")
-    ap.add_argument("--exact-voxel-order", type=int, choices=[0, 1], default=1,
-                    help="mapper VoxelGrids in PCL's summation order (1, the reference's arithmetic) or input "
-                         "order (0, faster; maps differ by summation-order ulps)")
+    ap.add_argument("--exact-voxel-order", type=int, choices=[0, 1], default=0,
+                    help="mapper VoxelGrids of the headline in PCL's summation order (1) or input order (0, the "
+                         "library default; maps differ by summation-order ulps)")
+    ap.add_argument("--no-exact-leg", action="store_true",
+                    help="skip the second (exact_voxel_order = 1) measurement of the same workload")
     ap.add_argument("--shard", action="store_true",
                     help="sharded mapping (SURVEY.md §8e): every stream split over all N ranks, map "
                          "blocks owned per rank, RCCL all-gather of 5-NN candidates per round and "
@@ -532,15 +534,42 @@ def main():
         finally:
             os.dup2(saved, 1)
             os.close(saved)
-    if H > 1:
-        # persistent LM grids sized so that every handle's fits at once: G <= CUs / all streams
-        # (speed: 2 beat 4 workgroups per stream; correctness needs no residency, lm.h)
-        cus = torch.cuda.get_device_properties(local).multi_processor_count
-        os.environ["LOAM_LM_G"] = os.environ.get("BENCH_LM_G") or str(max(1, cus // B))
-    mappers = [BatchMapper(Bh, device=local, max_map_points=args.map_points, comm=comm,
-                           exact_voxel_order=args.exact_voxel_order) for _ in range(H)]
-    os.environ.pop("LOAM_LM_G", None) if H > 1 else None  # read at create; not for later handles
-    mapper = mappers[0]
+
+    def timed_run(exact):
+        """map building (untimed), then the K timed steps; returns (iterations, seconds, kernel
+        family totals, stream 0's pose after every step)"""
+        if H > 1:
+            # persistent LM grids sized so that every handle's fits at once: G <= CUs / all streams
+            # (speed: 2 beat 4 workgroups per stream; correctness needs no residency, lm.h)
+            cus = torch.cuda.get_device_properties(local).multi_processor_count
+            os.environ["LOAM_LM_G"] = os.environ.get("BENCH_LM_G") or str(max(1, cus // B))
+        mappers = [BatchMapper(Bh, device=local, max_map_points=args.map_points, comm=comm,
+                               exact_voxel_order=exact) for _ in range(H)]
+        os.environ.pop("LOAM_LM_G", None) if H > 1 else None  # read at create; not for later handles
+        poses = []  # stream 0 after every step (free-running trajectory vs the oracle's)
+        run_handles(mappers, plans, 0, pre, poses)
+        for m in mappers:
+            if not args.no_prof:
+                m.set_profiling(True)
+            m.reset_kernel_times()
+        barrier()
+        t0 = time.perf_counter()
+        it = run_handles(mappers, plans, pre, K, poses)
+        barrier()
+        secs = time.perf_counter() - t0
+        fam = {}
+        for m in mappers:
+            for f, v in m.kernel_times().items():
+                acc = fam.setdefault(f, {"ms": 0.0, "bytes": 0.0, "launches": 0})
+                for key in acc:
+                    acc[key] += v[key]
+            m.set_profiling(False)
+        if os.environ.get("BENCH_DEBUG_COUNTERS"):
+            print(json.dumps({"debug_counters": [int(v) for v in mappers[0].debug_counters()]}), file=sys.stderr,
+                  flush=True)
+        for m in mappers:
+            m.close()
+        return it, secs, fam, poses
 
     def barrier():
         torch.cuda.synchronize(local)
@@ -548,31 +577,17 @@ def main():
             dist.barrier()
 
     plans = [[step_inputs(frames, Bh, args.stride, k, first=h * Bh) for k in range(pre + K)] for h in range(H)]
-    poses0 = []  # stream 0 after every step (free-running trajectory vs the oracle's)
-    run_handles(mappers, plans, 0, pre, poses0)
-    for m in mappers:
-        if not args.no_prof:
-            m.set_profiling(True)
-        m.reset_kernel_times()
-    barrier()
-    t0 = time.perf_counter()
-    iters = run_handles(mappers, plans, pre, K, poses0)
-    barrier()
-    dt = time.perf_counter() - t0
-    kt = {}
-    for m in mappers:
-        for fam, v in m.kernel_times().items():
-            acc = kt.setdefault(fam, {"ms": 0.0, "bytes": 0.0, "launches": 0})
-            for key in acc:
-                acc[key] += v[key]
-        m.set_profiling(False)
-    if os.environ.get("BENCH_DEBUG_COUNTERS"):
-        dc = mapper.debug_counters()
-        print(json.dumps({"debug_counters": [int(v) for v in dc]}), file=sys.stderr, flush=True)
-
+    iters, dt, kt, poses0 = timed_run(args.exact_voxel_order)
     iters_all, dt_max = aggregate(iters, dt, world, f"cuda:{local}")
     if args.shard:  # every rank counted the same iterations of the same streams
         iters_all = iters_all / world
+
+    exact_leg = None
+    if not args.no_exact_leg and not args.shard and not args.exact_voxel_order:
+        ei, edt, ekt, eposes = timed_run(1)
+        ei_all, edt_max = aggregate(ei, edt, world, f"cuda:{local}")
+        exact_leg = {"value": ei_all / edt_max, "ms_per_step": 1e3 * edt_max / K, "poses": eposes,
+                     "kernel_ms_per_step": {k: round(v["ms"] / K, 4) for k, v in ekt.items()}}
 
     single = None
     if not args.no_single_stream and rank == 0 and world == 1 and not args.shard:
@@ -610,7 +625,21 @@ def main():
             rmse = {"timed_frames": pose_errors(poses0[pre:pre + K], cposes[pre:pre + K]),
                     "all_frames": pose_errors(poses0, cposes),
                     "mode": "free-running: GPU stream 0 and the oracle each from frame 0 on identical "
-                            "features and priors, no state shared"}
+                            "features and priors, no state shared; oracle VoxelGrids in PCL's order, GPU "
+                            f"mapper in {'PCL' if args.exact_voxel_order else 'input'} order"}
+            if exact_leg is not None:
+                exact_leg["pose_rmse_vs_cpu"] = {"timed_frames": pose_errors(exact_leg["poses"][pre:pre + K],
+                                                                             cposes[pre:pre + K]),
+                                                 "all_frames": pose_errors(exact_leg["poses"], cposes)}
+            # the reference against itself: the same oracle with VoxelGrid voxels summed in input
+            # order instead of libstdc++'s sort permutation (a build of the reference whose sort
+            # differs); the divergence a different summation order alone produces free-running
+            O = _oracle()
+            with O.voxel_order(1):
+                _, _, cposes_in = cpu_baseline(frames, pre, K)
+            rmse["reference_self_divergence"] = {
+                **pose_errors(cposes_in, cposes),
+                "mode": "oracle with input-order VoxelGrid sums vs oracle with PCL's order, free-running"}
             cpu_st = cpu_stages(frames, pre, K)
             ai, adt = cpu_all_cores(frames, cores, args.stride, pre, K)
             allc = {"value": round(ai / adt, 3), "unit": "LM iters/s", "cores": cores, "kind": "port",
@@ -652,6 +681,13 @@ def main():
         }
         if single is not None:
             out["single_stream"] = {k: round(v, 4) for k, v in single.items()}
+        if exact_leg is not None:
+            exact_leg.pop("poses")
+            exact_leg["value"] = round(exact_leg["value"], 3)
+            exact_leg["ms_per_step"] = round(exact_leg["ms_per_step"], 4)
+            exact_leg["mode"] = ("the same workload with exact_voxel_order = 1 (the mapper's VoxelGrids in PCL's "
+                                 "summation order: free-running poses follow the oracle bit for bit)")
+            out["exact_voxel_order"] = exact_leg
         # the stages before the mapper (BASELINE configs[1], configs[2]): one stream, device time
         # per frame (HIP events around each call) over the cpu_baseline frames (all frames after
         # the first 10 without the CPU leg), and the oracle's own timers over the same frames
@@ -684,8 +720,6 @@ def main():
             if single is not None:
                 out["single_stream"]["speedup_vs_cpu_baseline"] = round(single["value"] / cpu["value"], 2)
         print(json.dumps(out), flush=True)
-    for m in mappers:
-        m.close()
     if comm is not None:
         comm.close()
     if world > 1:

@@ -54,7 +54,9 @@ typedef struct loam_params {
    * 1 = PCL's within-voxel summation order (the libstdc++ sort permutation of voxel_grid.hpp;
    * bit-exact with the reference arithmetic), 0 = input order (no sort emulation, merge path for
    * cubes that gain a few points; centroids differ from PCL's within the float summation-order
-   * bound).  ScanRegistration's per-ring filter always uses PCL's order.  Default 1. */
+   * bound).  ScanRegistration's per-ring filter always uses PCL's order.  Default 0: the exact
+   * order costs ~7x in mapping throughput; teacher-forced per-scan poses agree
+   * with the reference within 1e-4 either way, free-running trajectories bit-for-bit only with 1. */
   int32_t exact_voxel_order;
 } loam_params;
 

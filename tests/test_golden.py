@@ -131,7 +131,7 @@ def test_gpu_mapping_fixture():
     from loam_amd.scanreg import ScanRegistration
     g = load("mapping")
     seed, n_frames, n_az = g["params"]
-    sr, mp = ScanRegistration(), LaserMapping()
+    sr, mp = ScanRegistration(), LaserMapping(exact_voxel_order=1)  # free-running: PCL's VoxelGrid order
     for f in range(n_frames):
         xyz, gt = synth_frame(seed, f, n_az)
         sr.input(xyz)

@@ -1,0 +1,30 @@
+"""exact-mode phase counters: one mapping stream over a synthetic sequence (device-side
+voxel_grid_pcl phase cycles of the stack [42..45] and cube [11..14] filters)"""
+import sys, time
+import numpy as np
+sys.path[:0] = ['vloam-noted_amd', 'oracle', 'tests']
+from loam_amd import synth
+from loam_amd.scanreg import ScanRegistration
+from loam_amd.odometry import BatchOdometry
+from loam_amd.mapping import BatchMapper
+for exact in (1, 0):
+    sr, od, mp = ScanRegistration(), BatchOdometry(1), BatchMapper(1, exact_voxel_order=exact)
+    t_all = 0.0
+    for f in range(170):
+        xyz, _ = synth.frame(11, f, 2000)
+        sr.input(xyz)
+        ptrs, counts = zip(*(sr.device_ptr(w) for w in (1, 2, 3, 4)))
+        od.input_device(0, ptrs, counts); od.solve()
+        q, t, _, _, _ = od.output(0)
+        (pc, nc), (ps, ns) = od.last_cloud_device(0, 0), od.last_cloud_device(0, 1)
+        if f == 150:
+            mp.debug_counters(reset=True)
+        mp.input_device(0, pc, nc, ps, ns, q, t)
+        t0 = time.perf_counter(); mp.solve(); dt = time.perf_counter() - t0
+        if f >= 150:
+            t_all += dt
+    dc = mp.debug_counters()
+    st = mp.stats(0)
+    print(f"exact={exact}: {1e3 * t_all / 20:.3f} ms/frame; stack phases (Mcycles/frame) {[round(int(v) / 20e6, 3) for v in dc[42:46]]}; "
+          f"cube phases {[round(int(v) / 20e6, 3) for v in dc[11:15]]}; revox items {[int(v) for v in dc[4:7]]} "
+          f"sizes {[int(v) for v in dc[24:32]]}; stacks {st.corner_stack},{st.surf_stack}", flush=True)

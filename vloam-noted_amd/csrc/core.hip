@@ -51,7 +51,7 @@ void loam_params_default(loam_params* p) {
   p->max_input_points = 262144;
   p->max_map_points = 2097152;
   p->max_submap_points = 524288;
-  p->exact_voxel_order = 1;
+  p->exact_voxel_order = 0;
 }
 
 const char* loam_last_error(void) { return loam::g_last_error.c_str(); }

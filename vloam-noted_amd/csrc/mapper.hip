@@ -130,6 +130,7 @@ struct MapperDev {
   uint32_t* pa;
   uint32_t* pb;
   uint64_t* ps;
+  int* pseg;  // level lists of global-memory sorts
   int rank = 0, nrank = 1, sharded = 0;
   int blk_v[2] = {1, 1};
   uint32_t* wcnt;        // [B][2][WIN_MAX] window cube counts (all-reduced over the ranks)
@@ -198,30 +199,40 @@ __global__ void k_shift_cubes(MapperDev D, const uint2* __restrict__ old_tab, ui
 // else at offset `so` of the (stream, map) sort scratch, where the sorted copy S always goes.
 // Returns false (MAP_ERR_SORT) when the input is too large for the lists.
 constexpr int MP_LDS_N = 8192;                                    // E 64 KiB + A, B 32 KiB each
-constexpr int MP_SEG_LDS = (VX_LDS_WORDS - 256 - 16 - 4 * MP_LDS_N) / 6;  // level lists beside them
-constexpr int MP_SEG_CAP = (VX_LDS_WORDS - 256 - 16) / 6;
+constexpr int MP_LEV_W = 32;  // SsLevels words
+static_assert(sizeof(SsLevels) <= 4 * MP_LEV_W, "SsLevels area");
+constexpr int MP_SEG_LDS = (VX_LDS_WORDS - 256 - MP_LEV_W - 4 * MP_LDS_N) / 6;  // level lists beside them
 static_assert(MP_SEG_LDS >= MP_LDS_N / (SS_THRESHOLD + 1) + 2, "level lists of an LDS-resident sort");
+static_assert(VX_THREADS / 64 * SS_LOC_WORDS + 256 + MP_LEV_W <= VX_LDS_WORDS, "wave-local sort buffers");
+// sort scratch of a (stream, map): the stack at 0, the cubes' blocks of n + MP_SLACK from the
+// frame's scratch_tail; the level lists of a global-memory sort at 6 (offset / 16) ints
+constexpr uint32_t MP_SLACK = 64;
+inline size_t mp_scratch(const MapperDev& D) { return (size_t)D.scratch_cap + MP_SLACK * (INS_SLOTS + 1); }
 template <typename PF>
 __device__ inline bool map_voxel_pcl(const MapperDev& D, size_t sm, uint32_t so, const PF& P, int n, float leaf,
                                      const VxPclOut& O, uint32_t* lds, int* err) {
-  if (n / (SS_THRESHOLD + 1) + 2 > MP_SEG_CAP || so + (uint32_t)n > (uint32_t)D.scratch_cap) {
+  const size_t ps = (size_t)D.scratch_cap + MP_SLACK * (INS_SLOTS + 1);
+  if ((size_t)so + (uint32_t)n + MP_SLACK > ps) {
     if (threadIdx.x == 0) atomicOr(err, MAP_ERR_SORT);
     return false;
   }
   VxMisc& M = *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192);
   uint32_t* ws = lds + VX_LDS_WORDS - 256;
-  SsLevels* lev = reinterpret_cast<SsLevels*>(lds + VX_LDS_WORDS - 256 - 16);
-  const size_t b = sm * D.scratch_cap + so;
+  SsLevels* lev = reinterpret_cast<SsLevels*>(lds + VX_LDS_WORDS - 256 - MP_LEV_W);
+  const size_t b = sm * ps + so;
   if (n <= MP_LDS_N) {
     uint64_t* E = reinterpret_cast<uint64_t*>(lds);
     uint32_t* A = lds + 2 * MP_LDS_N;
     uint32_t* B = A + MP_LDS_N;
     int* seg0 = reinterpret_cast<int*>(B + MP_LDS_N);
-    const VxPclScratch X{E, A, B, D.ps + b, lev, {seg0, seg0 + 3 * MP_SEG_LDS}, MP_SEG_LDS};
+    const VxPclScratch X{E, A, B, D.ps + b, lev, {seg0, seg0 + 3 * MP_SEG_LDS}, MP_SEG_LDS, nullptr,
+                         so == 0 ? D.dbg + 42 : D.dbg + 11};
     voxel_grid_pcl<VX_THREADS>(P, n, leaf, O, X, M, ws, err);
-  } else {
-    int* seg0 = reinterpret_cast<int*>(lds);
-    const VxPclScratch X{D.pe + b, D.pa + b, D.pb + b, D.ps + b, lev, {seg0, seg0 + 3 * MP_SEG_CAP}, MP_SEG_CAP};
+  } else {  // level lists in global memory, the LDS holds the waves' subtree sorts
+    const int cap = (int)((n + MP_SLACK) / 16);
+    int* seg0 = D.pseg + sm * (6 * (ps / 16) + 6) + 6 * (so / 16);
+    const VxPclScratch X{D.pe + b, D.pa + b, D.pb + b, D.ps + b, lev, {seg0, seg0 + 3 * cap}, cap, lds,
+                         so == 0 ? D.dbg + 42 : D.dbg + 11};
     voxel_grid_pcl<VX_THREADS>(P, n, leaf, O, X, M, ws, err);
   }
   return true;
@@ -918,7 +929,7 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
     // path (input order) does not apply
     uint32_t* sb = lds + LW - 3;
     const uint32_t n = cv.y + n_new;
-    if (threadIdx.x == 0) *sb = atomicAdd(&F.scratch_tail[m], n);
+    if (threadIdx.x == 0) *sb = atomicAdd(&F.scratch_tail[m], n + MP_SLACK);
     __syncthreads();
     const uint32_t so = *sb;
     __syncthreads();
@@ -1432,10 +1443,12 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   ALLOC(D.dbg, LOAM_DEBUG_COUNTERS);
   ALLOC(D.vx_pts, B * 2 * (size_t)D.scratch_cap);
   if (D.pcl_order) {
-    ALLOC(D.pe, B * 2 * (size_t)D.scratch_cap);
-    ALLOC(D.pa, B * 2 * (size_t)D.scratch_cap);
-    ALLOC(D.pb, B * 2 * (size_t)D.scratch_cap);
-    ALLOC(D.ps, B * 2 * (size_t)D.scratch_cap);
+    const size_t ps = mp_scratch(D);
+    ALLOC(D.pe, B * 2 * ps);
+    ALLOC(D.pa, B * 2 * ps);
+    ALLOC(D.pb, B * 2 * ps);
+    ALLOC(D.ps, B * 2 * ps);
+    ALLOC(D.pseg, B * 2 * (6 * (ps / 16) + 6));
   }
   ALLOC(D.vx_idx, B * 2 * (size_t)D.scratch_cap);
   ALLOC(D.partials, B * (size_t)D.max_chunks * LM_NACC);

@@ -44,14 +44,28 @@ namespace loam {
 constexpr int SS_THRESHOLD = 16;  // _S_threshold
 
 // Pending segments of one sort, level by level: the segments of depth level `lev` are in
-// seg[lev & 1][0 .. cnt[lev & 1]); every one longer than 16 elements.  Segments of one level are
-// disjoint, so a level holds at most n / 17 + 1 of them (cap).
+// seg[lev & 1]: the ones for one wave each at [0, cnt), the long ones (more than SS_BIG elements,
+// depth budget left) from the end, at cap - 1 - t for t < nbig; every one longer than 16
+// elements.  Segments of one level are disjoint, so a level holds at most n / 17 + 1 (cap).
 struct SsLevels {
   int cnt[2];
+  int nbig[2];
   int err;
   int cap;
   int* seg[2];  // [cap][3] (lo, hi, depth budget), LDS or global
+  uint32_t ws[17];  // block-scan scratch of the cooperative partition
+  int sh[2];
+  uint32_t* loc;  // optional LDS for wave-local subtree sorts (SS_LOC_WORDS per wave), else nullptr
 };
+
+// Wave-local subtree sort: a segment of at most SS_LOCAL elements whose array lives in global
+// memory is copied into the wave's LDS, its whole introsort subtree runs there (a wave-local
+// LIFO, no level barriers), and the result goes back with identity annotations.
+constexpr int SS_LOCAL = 512;
+constexpr int SS_LOC_STK = 24;  // >= 2 __lg(SS_LOCAL) + 2 pending right parts
+constexpr int SS_LOC_WORDS = 2 * SS_LOCAL + 2 * SS_LOCAL + 3 * SS_LOC_STK;
+
+constexpr int SS_BIG = 1024;  // longer segments are partitioned by the whole workgroup
 
 // Elements are 64-bit; Less compares two elements (the reference's comparator).  Per sort:
 //   E[n]    the elements, permuted in place by the partitions (LDS or global)
@@ -180,6 +194,89 @@ __device__ inline int ss_partition(T* E, uint32_t* A, uint32_t* B, int lo, int h
   return cut;
 }
 
+// The same partition of one segment by all NT threads of the workgroup (segments longer than
+// SS_BIG, the first levels of a large sort, where one wave per segment would leave the others
+// idle): the stop lists are built tile by tile with a block scan (left / right counts packed in
+// one word), then the prefix length S, the cut and the swaps.
+template <int NT, typename T, typename Less>
+__device__ inline int ss_partition_wg(T* E, uint32_t* A, uint32_t* B, int lo, int hi, SsLevels* L, const Less& less) {
+  constexpr int NW = NT / 64;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  if (tid == 0) {  // __move_median_to_first(lo, lo + 1, mid, hi - 1)
+    const int a = lo + 1, b = lo + (hi - lo) / 2, c = hi - 1;
+    const T ea = E[a], eb = E[b], ec = E[c];
+    int m;
+    if (less(ea, eb)) {
+      if (less(eb, ec)) m = b;
+      else if (less(ea, ec)) m = c;
+      else m = a;
+    } else if (less(ea, ec)) {
+      m = a;
+    } else if (less(eb, ec)) {
+      m = c;
+    } else {
+      m = b;
+    }
+    const T t = E[lo];
+    E[lo] = E[m];
+    E[m] = t;
+    B[lo] = (uint32_t)lo;
+  }
+  __syncthreads();
+  const T p = E[lo];
+  uint32_t nl = 0, nr = 1;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  for (int c0 = lo + 1; c0 < hi; c0 += NT) {
+    const int i = c0 + tid;
+    bool isl = false, isr = false;
+    if (i < hi) {
+      const T e = E[i];
+      isl = !less(e, p);
+      isr = !less(p, e);
+    }
+    const uint64_t bl = __ballot(isl), br = __ballot(isr);
+    if (lane == 0) L->ws[wid] = (uint32_t)__popcll(bl) | ((uint32_t)__popcll(br) << 16);
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (int w = 0; w < NW; ++w) {
+      const uint32_t v = L->ws[w];
+      off += w < wid ? v : 0u;
+      tot += v;
+    }
+    if (isl) A[lo + 1 + nl + (off & 0xFFFFu) + __popcll(bl & lt)] = (uint32_t)i;
+    if (isr) B[lo + nr + (off >> 16) + __popcll(br & lt)] = (uint32_t)i;
+    nl += tot & 0xFFFFu;
+    nr += tot >> 16;
+    __syncthreads();  // ws is rewritten by the next tile
+  }
+  const int kmax = min((int)nl, (int)nr);
+  if (tid == 0) L->sh[0] = kmax + 1;  // first k with !(l_k < r_k)
+  __syncthreads();
+  for (int k0 = 1; k0 <= kmax; k0 += NT) {
+    const int k = k0 + tid;
+    if (k <= kmax && !(A[lo + k] < B[lo + nr - k])) atomicMin(&L->sh[0], k);
+    __syncthreads();
+    const int ff = L->sh[0];
+    __syncthreads();
+    if (ff <= kmax) break;
+  }
+  const int S = L->sh[0] - 1;
+  const int lK = S + 1 <= (int)nl ? (int)A[lo + S + 1] : 0x7FFFFFFF;
+  const int rS = S >= 1 ? (int)B[lo + nr - S] : hi;
+  const int cut = min(lK, rS);
+  for (int k0 = 1; k0 <= S; k0 += NT) {
+    const int k = k0 + tid;
+    if (k <= S) {
+      const int x = (int)A[lo + k], y = (int)B[lo + nr - k];
+      const T ex = E[x], ey = E[y];
+      E[x] = ey;
+      E[y] = ex;
+    }
+  }
+  __syncthreads();
+  return cut;
+}
+
 // Record a final segment for the stable per-segment pass
 __device__ inline void ss_mark(uint32_t* A, uint32_t* B, int lo, int hi, bool sorted) {
   const int lane = threadIdx.x & 63;
@@ -189,18 +286,91 @@ __device__ inline void ss_mark(uint32_t* A, uint32_t* B, int lo, int hi, bool so
   }
 }
 
+template <typename T, typename Less>
+__device__ inline void ss_local_sort(T* E, uint32_t* A, uint32_t* B, int lo, int hi, int d, uint32_t* loc,
+                                     const Less& less) {
+  const int lane = threadIdx.x & 63;
+  const int m = hi - lo;
+  T* lE = reinterpret_cast<T*>(loc);
+  uint32_t* lA = loc + 2 * SS_LOCAL;
+  uint32_t* lB = lA + SS_LOCAL;
+  int* stk = reinterpret_cast<int*>(lB + SS_LOCAL);
+  for (int i = lane; i < m; i += 64) lE[i] = E[lo + i];
+  if (lane == 0) {
+    stk[0] = 0;
+    stk[1] = m;
+    stk[2] = d;
+  }
+  int top = 1;
+  ss_wave_fence();
+  while (top > 0) {
+    --top;
+    int a = __builtin_amdgcn_readfirstlane(stk[3 * top]);
+    int b = __builtin_amdgcn_readfirstlane(stk[3 * top + 1]);
+    int dd = __builtin_amdgcn_readfirstlane(stk[3 * top + 2]);
+    while (true) {
+      if (b - a <= SS_THRESHOLD) {
+        ss_mark(lA, lB, a, b, false);
+        break;
+      }
+      if (dd == 0) {
+        if (lane == 0) ss_heap_sort(lE, a, b, less);
+        ss_wave_fence();
+        ss_mark(lA, lB, a, b, true);
+        break;
+      }
+      --dd;
+      const int cut = __builtin_amdgcn_readfirstlane(ss_partition(lE, lA, lB, a, b, less));
+      if (b - cut > SS_THRESHOLD) {
+        if (lane == 0) {
+          stk[3 * top] = cut;
+          stk[3 * top + 1] = b;
+          stk[3 * top + 2] = dd;
+        }
+        ++top;
+      } else {
+        ss_mark(lA, lB, cut, b, false);
+      }
+      ss_wave_fence();
+      b = cut;
+    }
+  }
+  ss_wave_fence();
+  // the final insertion sort of the subtree (stable within each final segment) -> E[lo ..)
+  for (int i = lane; i < m; i += 64) {
+    const int a = (int)lA[i], b = (int)lB[i];
+    const T ei = lE[i];
+    int r = 0;
+    for (int j = a; j < b; ++j) {
+      const T ej = lE[j];
+      r += (less(ej, ei) || (j < i && !less(ei, ej))) ? 1 : 0;
+    }
+    E[lo + a + r] = ei;
+  }
+  for (int i = lane; i < m; i += 64) {  // sorted in place: ss_final copies it through
+    A[lo + i] = (uint32_t)(lo + i);
+    B[lo + i] = (uint32_t)(lo + i + 1);
+  }
+  ss_wave_fence();
+}
+
 // Init with the root segment [0, n) (one thread; a barrier / wave fence before ss_levels).
 __device__ inline void ss_levels_init(SsLevels* L, int n, int* seg0, int* seg1, int cap) {
   L->seg[0] = seg0;
   L->seg[1] = seg1;
   L->cap = cap;
   L->err = 0;
-  L->cnt[1] = 0;
-  L->cnt[0] = n > SS_THRESHOLD ? 1 : 0;
+  L->cnt[0] = L->cnt[1] = L->nbig[0] = L->nbig[1] = 0;
+  L->loc = nullptr;
   if (n > SS_THRESHOLD) {
-    seg0[0] = 0;
-    seg0[1] = n;
-    seg0[2] = 2 * (31 - __clz(n));  // 2 * __lg(n)
+    const int d = 2 * (31 - __clz(n));  // 2 * __lg(n)
+    const bool big = n > SS_BIG && d > 0;
+    int* o = seg0 + 3 * (big ? cap - 1 : 0);
+    o[0] = 0;
+    o[1] = n;
+    o[2] = d;
+    if (big) L->nbig[0] = 1;
+    else L->cnt[0] = 1;
   }
 }
 
@@ -208,21 +378,65 @@ __device__ inline void ss_levels_init(SsLevels* L, int n, int* seg0, int* seg1, 
 // whole workgroup, barriers are __syncthreads; else one wave alone); waves w < nw take the
 // level's segments w, w + nw, ...  No waiting on other waves outside the barriers, and at most
 // 2 * __lg(n) + 1 levels (each level lowers the depth budget by one).
-template <bool WG, typename T, typename Less>
+template <bool WG, int NT = 64, typename T, typename Less>
 __device__ inline void ss_levels(T* E, uint32_t* A, uint32_t* B, SsLevels* L, int wave, int nw, const Less& less) {
   const int lane = threadIdx.x & 63;
   auto barrier = [] {
     if (WG) __syncthreads();
     else ss_wave_fence();
   };
+  auto push = [&](int nxt, int a, int b, int d) {  // one lane
+    const bool big = b - a > SS_BIG && d > 0;
+    const int t = atomicAdd(big ? &L->nbig[nxt] : &L->cnt[nxt], 1);
+    const int slot = big ? L->cap - 1 - t : t;
+    if (t < L->cap && slot >= 0) {
+      int* o = L->seg[nxt] + 3 * slot;
+      o[0] = a;
+      o[1] = b;
+      o[2] = d;
+    } else {
+      atomicOr(&L->err, 2);
+    }
+  };
   for (int lev = 0;; ++lev) {
     barrier();
     const int cur = lev & 1, nxt = cur ^ 1;
-    const int cnt = L->cnt[cur];
-    if (cnt == 0) break;
+    const int cnt = L->cnt[cur], nb = L->nbig[cur];
+    if (cnt + nb == 0) break;
+    if (cnt + nb > L->cap) {  // the two ends met: the lists were overwritten (cannot happen with cap >= n / 17 + 1)
+      if (threadIdx.x == 0) atomicOr(&L->err, 2);
+      break;
+    }
     const int* sg = L->seg[cur];
-    for (int k = wave; wave < nw && k < cnt; k += nw) {
-      const int lo = sg[3 * k], hi = sg[3 * k + 1], d = sg[3 * k + 2];
+    if (WG) {  // long segments: the whole workgroup on each in turn
+      for (int t = 0; t < nb; ++t) {
+        const int* e = sg + 3 * (L->cap - 1 - t);
+        const int lo = e[0], hi = e[1], d = e[2];
+        const int cut = ss_partition_wg<NT>(E, A, B, lo, hi, L, less);
+        const int parts[2][2] = {{lo, cut}, {cut, hi}};
+        for (int q = 0; q < 2; ++q) {
+          const int a = parts[q][0], b = parts[q][1];
+          if (b - a > SS_THRESHOLD) {
+            if (threadIdx.x == 0) push(nxt, a, b, d - 1);
+          } else {
+            for (int i = a + (int)threadIdx.x; i < b; i += NT) {
+              A[i] = (uint32_t)a;
+              B[i] = (uint32_t)b;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // one wave per segment (and, for a single wave, the long ones too)
+    const int tot = WG ? cnt : cnt + nb;
+    for (int k = wave; wave < nw && k < tot; k += nw) {
+      const int* e = sg + 3 * (k < cnt ? k : L->cap - 1 - (k - cnt));
+      const int lo = e[0], hi = e[1], d = e[2];
+      if (L->loc && hi - lo <= SS_LOCAL) {
+        ss_local_sort(E, A, B, lo, hi, d, L->loc + wave * SS_LOC_WORDS, less);
+        continue;
+      }
       if (d == 0) {  // depth limit: __partial_sort(first, last, last)
         if (lane == 0) ss_heap_sort(E, lo, hi, less);
         ss_wave_fence();
@@ -234,24 +448,14 @@ __device__ inline void ss_levels(T* E, uint32_t* A, uint32_t* B, SsLevels* L, in
       for (int q = 0; q < 2; ++q) {
         const int a = parts[q][0], b = parts[q][1];
         if (b - a > SS_THRESHOLD) {
-          if (lane == 0) {
-            const int t = atomicAdd(&L->cnt[nxt], 1);
-            if (t < L->cap) {
-              int* o = L->seg[nxt] + 3 * t;
-              o[0] = a;
-              o[1] = b;
-              o[2] = d - 1;
-            } else {
-              atomicOr(&L->err, 2);
-            }
-          }
+          if (lane == 0) push(nxt, a, b, d - 1);
         } else {
           ss_mark(A, B, a, b, false);
         }
       }
     }
     barrier();  // every append to level lev + 1 done, every read of this level's count done
-    if (wave == 0 && lane == 0) L->cnt[cur] = 0;
+    if (wave == 0 && lane == 0) L->cnt[cur] = L->nbig[cur] = 0;
   }
 }
 

@@ -25,6 +25,9 @@ struct VxPclScratch {
   SsLevels* lev;  // LDS
   int* seg[2];    // 3 * cap ints each (LDS or global)
   int cap;        // >= n / 17 + 1
+  uint32_t* loc = nullptr;  // LDS for the waves' subtree sorts (SS_LOC_WORDS each) when E is global
+  unsigned long long* prof = nullptr;  // optional phase cycles: [0] bbox + keys, [1] sort levels,
+                                       // [2] final pass, [3] centroids
 };
 
 struct VxPtrSrc {
@@ -83,17 +86,23 @@ __device__ inline void voxel_grid_pcl(const PF& P, int n, float leaf, const VxPc
     if (tid == 0) finish(b, (uint32_t)n, false);
     return;
   }
+  unsigned long long tp = __builtin_readcyclecounter();
   for (int i = tid; i < n; i += NT) X.E[i] = ((uint64_t)vx_key(g, P((uint32_t)i)) << 32) | (uint32_t)i;
   if (tid == 0) {
     ss_levels_init(X.lev, n, X.seg[0], X.seg[1], X.cap);
+    X.lev->loc = X.loc;
     M.moved = 0;
   }
   const VxIdxLess less;
-  ss_levels<true>(X.E, X.A, X.B, X.lev, tid >> 6, NT / 64, less);
   __syncthreads();
+  vx_phase(X.prof, 0, &tp);
+  ss_levels<true, NT>(X.E, X.A, X.B, X.lev, tid >> 6, NT / 64, less);
+  __syncthreads();
+  vx_phase(X.prof, 1, &tp);
   if (tid == 0 && X.lev->err) atomicOr(err, 4);
   ss_final(X.E, X.A, X.B, n, X.S, tid, NT, less);
   __syncthreads();
+  vx_phase(X.prof, 2, &tp);
   // runs of equal idx: thread t owns positions [t * per, (t + 1) * per)
   const int per = (n + NT - 1) / NT;
   const int p0 = min(n, tid * per), p1 = min(n, p0 + per);
@@ -126,6 +135,7 @@ __device__ inline void voxel_grid_pcl(const PF& P, int n, float leaf, const VxPc
   }
   if (moved) M.moved = 1;
   __syncthreads();
+  vx_phase(X.prof, 3, &tp);
   if (tid == 0) finish(b, tot, M.moved == 0);
 }
 
