@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--exact-voxel-order", type=int, choices=[0, 1], default=0,
                     help="mapper VoxelGrids of the headline in PCL's summation order (1) or input order (0, the "
                          "library default; maps differ by summation-order ulps)")
+    ap.add_argument("--shard-streams", type=int, default=32,
+                    help="streams of the sharded leg (every stream split over all ranks; 0: skip the leg)")
     ap.add_argument("--no-exact-leg", action="store_true",
                     help="skip the second (exact_voxel_order = 1) measurement of the same workload")
     ap.add_argument("--shard", action="store_true",
@@ -589,6 +591,48 @@ def main():
         exact_leg = {"value": ei_all / edt_max, "ms_per_step": 1e3 * edt_max / K, "poses": eposes,
                      "kernel_ms_per_step": {k: round(v["ms"] / K, 4) for k, v in ekt.items()}}
 
+    # the north-star multi-GPU design beside the replica headline: Bs streams, each
+    # split over all ranks (block-owned map shards, RCCL all-gather of the 5-NN candidates per
+    # round, all-reduce of the normal equations per LM iteration): strong scaling of a fixed load
+    shard_leg = None
+    if args.shard_streams > 0 and not args.shard:
+        Bs = args.shard_streams
+        n_s = (Bs - 1) * args.stride + pre + K
+        if world == 1 and n_s <= len(frames):
+            sframes = frames
+        else:  # identical inputs on every rank
+            sframes, _ = make_frames(stream_seed(args.seed, 0), n_s, args.n_az, local, prior=args.prior)
+        from loam_amd.comm import Comm
+        uid = [Comm.rccl_unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)  # RCCL's banner stays off the JSON line
+        try:
+            scomm = Comm.rccl(rank, world, uid[0], local)
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
+        sm = BatchMapper(Bs, device=local, max_map_points=args.map_points, comm=scomm)
+        splan = [step_inputs(sframes, Bs, args.stride, k) for k in range(pre + K)]
+        run_steps(sm, splan, 0, pre)
+        barrier()
+        t0 = time.perf_counter()
+        sit = run_steps(sm, splan, pre, K)
+        barrier()
+        sdt = time.perf_counter() - t0
+        sm.close()
+        scomm.close()
+        sit_all, sdt_max = aggregate(sit, sdt, world, f"cuda:{local}")
+        shard_leg = {"value": round(sit_all / world / sdt_max, 3), "unit": "LM iters/s",
+                     "ms_per_step": round(1e3 * sdt_max / K, 4), "streams": Bs, "ranks": world, "scaling": "strong",
+                     "frames_per_step": Bs,
+                     "transport": "RCCL" if world > 1 else "one rank: every collective is the identity",
+                     "mode": "every stream split over all ranks (block-owned map shards, per-round 5-NN all-gather, "
+                             "per-LM-iteration normal-equation all-reduce); iterations counted once per stream"}
+        del sframes
+
     single = None
     if not args.no_single_stream and rank == 0 and world == 1 and not args.shard:
         m1 = BatchMapper(1, device=local, exact_voxel_order=args.exact_voxel_order)
@@ -681,6 +725,8 @@ def main():
         }
         if single is not None:
             out["single_stream"] = {k: round(v, 4) for k, v in single.items()}
+        if shard_leg is not None:
+            out["sharded"] = shard_leg
         if exact_leg is not None:
             exact_leg.pop("poses")
             exact_leg["value"] = round(exact_leg["value"], 3)

@@ -100,6 +100,9 @@ class LaserOdometry {
                     int32_t nf, const float* less_flat, int32_t nlf) {
     check(loam_odometry_input_device(h_, 0, sharp, ns, less_sharp, nls, flat, nf, less_flat, nlf));
   }
+  // vloam_tf->velo_last_VOT_velo_curr for the next solveLO (detach_vo_lo = 0,
+  // laser_odometry.cpp:237-250)
+  void set_vo_prior(const double q_xyzw[4], const double t_xyz[3]) { check(loam_odometry_set_prior(h_, 0, q_xyzw, t_xyz)); }
   void solveLO() { check(loam_odometry_solve(h_)); }
   // q_w_curr, t_w_curr, q_last_curr, t_last_curr, skip_frame (laser_odometry.cpp:660-679)
   bool output(double q_w[4], double t_w[3], double q_lc[4] = nullptr, double t_lc[3] = nullptr) const {

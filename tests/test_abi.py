@@ -75,17 +75,22 @@ def test_no_device_fails_loudly():
 
 
 def test_cxx_shim_compiles_and_links(tmp_path):
-    """include/loam_core.hpp with plain g++ (the reference nodes' compiler), linked to the library"""
+    """include/loam_core.hpp with plain g++ (the reference nodes' compiler), linked to the library;
+    on a GPU box it runs frames through the shim's three stages (tests/cxx/shim_check.cpp)"""
     import subprocess
     lib_dir = os.path.dirname(_core.LIB_PATH)
     exe = str(tmp_path / "shim_check")
+    oracle_dir = os.path.join(ROOT, "oracle", "_build")
     subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
                     os.path.join(ROOT, "tests", "cxx", "shim_check.cpp"), "-o", exe, "-L", lib_dir,
-                    "-lloam_core", f"-Wl,-rpath,{lib_dir}", "-Wl,-rpath,/opt/rocm/lib"],
+                    "-lloam_core", "-lloam_synth", "-L", oracle_dir, "-lloam_oracle", f"-Wl,-rpath,{lib_dir}",
+                    f"-Wl,-rpath,{oracle_dir}", "-Wl,-rpath,/opt/rocm/lib"],
                    check=True, capture_output=True, text=True)
     r = subprocess.run([exe, "1" if gpu_available() else "0"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "version" in r.stdout
+    if gpu_available():  # four frames through the shim's three stages against the oracle
+        assert "frame 3" in r.stdout
 
 
 def test_new_entry_points_validate_arguments():

@@ -56,3 +56,24 @@ def test_pipeline_zero_copy():
     sr.close()
     od.close()
     mp.close()
+
+
+def test_cxx_shim_frames(tmp_path):
+    """the header-only C++ shim (include/loam_core.hpp) driving four frames through
+    ScanRegistration -> LaserOdometry -> LaserMapping with host clouds between the stages, as the
+    reference nodes would (tests/cxx/shim_check.cpp), against the oracle pipeline: within 1e-4"""
+    import os
+    import subprocess
+    from conftest import ROOT
+    from loam_amd import _core
+    lib_dir = os.path.dirname(_core.LIB_PATH)
+    oracle_dir = os.path.join(ROOT, "oracle", "_build")
+    exe = str(tmp_path / "shim_check")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cxx", "shim_check.cpp"), "-o", exe, "-L", lib_dir, "-lloam_core",
+                    "-lloam_synth", "-L", oracle_dir, "-lloam_oracle", f"-Wl,-rpath,{lib_dir}",
+                    f"-Wl,-rpath,{oracle_dir}", "-Wl,-rpath,/opt/rocm/lib"], check=True, capture_output=True, text=True)
+    r = subprocess.run([exe, "1"], capture_output=True, text=True, timeout=120)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "frame 3" in r.stdout

@@ -1,7 +1,9 @@
 """GPU: the sharded LaserMapping with one process per rank (the deployment model), ranks
-exchanging through torch.distributed gloo (loam_amd.comm.TorchDistComm, host buffers); both
-processes share the box's one GPU.  Every rank's pose equals the unsharded mapper's within 1e-6
-and the ranks agree bit for bit."""
+exchanging through torch.distributed gloo, either as host-buffer callbacks
+(loam_amd.comm.TorchDistComm) or as device-pointer callbacks on the mapper's HIP stream
+(TorchDistStagedComm, the C-ABI's host_buffers = 0 transport); both processes share the box's one
+GPU.  Every rank's pose equals the unsharded mapper's within 1e-6 and the ranks agree bit for
+bit."""
 import os
 import socket
 import sys
@@ -24,16 +26,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank(rank, world, port, frames, q):
+def _rank(rank, world, port, frames, q, transport="host"):
     for p in (os.path.join(ROOT, "vloam-noted_amd"), os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
     import torch.distributed as dist
-    from loam_amd.comm import TorchDistComm
+    from loam_amd.comm import TorchDistComm, TorchDistStagedComm
     from loam_amd.mapping import BatchMapper
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        comm = TorchDistComm.create()
+        comm = TorchDistComm.create() if transport == "host" else TorchDistStagedComm.create()
         m = BatchMapper(1, comm=comm)
         poses = []
         for corner, surf, qo, to in frames:
@@ -49,7 +51,8 @@ def _rank(rank, world, port, frames, q):
         dist.destroy_process_group()
 
 
-def test_two_processes_gloo():
+@pytest.mark.parametrize("transport", ["host", "device"])
+def test_two_processes_gloo(transport):
     seq = run_sequence(seed=11, n_frames=N_FRAMES)
     frames = [(r["corner"], r["surf"], r["q_wodom"], r["t_wodom"]) for r in seq]
     ref = BatchMapper(1)
@@ -63,7 +66,7 @@ def test_two_processes_gloo():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, 2, port, frames, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, frames, q, transport)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted((q.get(timeout=240) for _ in range(2)), key=lambda x: x[0])

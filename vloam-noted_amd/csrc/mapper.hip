@@ -1377,7 +1377,10 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     const bool allow = !(env && env[0] == '0');
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
       h->n_cu = cus;
-    if (allow && !comm && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_lm_round, LM_THREADS, 0) == hipSuccess &&
+    // sharded over several ranks: the per-pass all-reduce needs the two-kernel path; at one
+    // rank every collective is the identity and the round stays one persistent launch
+    if (allow && (!comm || comm->size == 1) &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_lm_round, LM_THREADS, 0) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess) {
       // 256 threads x 256 VGPRs: exactly one block per CU; the API can over-report by one
       // block per CU at some SGPR counts (MI355X_MICROARCH.md, correctness boundaries)
@@ -1463,14 +1466,24 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     NnRec* recv = nullptr;
     ALLOC(D.wcnt, B * 2 * (size_t)WIN_MAX);
     ALLOC(D.nn_send, nq);
-    ALLOC(recv, nq * D.nrank);
-    D.nn_recv = recv;
+    if (D.nrank > 1) {
+      ALLOC(recv, nq * D.nrank);
+      D.nn_recv = recv;
+    } else {
+      D.nn_recv = D.nn_send;  // one rank: the all-gather is the identity
+    }
     ALLOC(D.nn_xyz, 5 * nq);
     ALLOC(D.lm_red, B * (size_t)LM_NACC);
     ALLOC(D.pose_x, (size_t)D.nrank * B * 8);
     ALLOC(h->d_q_off, B + 1);
     D.q_off = h->d_q_off;
     if (!h->q_off.assign(B + 1, 0)) return fail(LOAM_ERR_HIP);
+    if (D.nrank == 1) {  // fixed query slots: no per-frame host read of the stack sizes
+      for (size_t s = 0; s <= B; ++s) h->q_off[s] = (int)(s * 2 * (size_t)D.max_in);
+      if (hipMemcpyAsync(h->d_q_off, h->q_off.data(), sizeof(int) * (B + 1), hipMemcpyHostToDevice, h->st) !=
+          hipSuccess)
+        return fail(LOAM_ERR_HIP);
+    }
   }
 #undef ALLOC
   D.cube_tab = h->cube_tab[0];
@@ -1762,15 +1775,16 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     h->parity ^= 1;
     D.cube_tab = h->cube_tab[h->parity];
   }
+  const bool multi = D.sharded && D.nrank > 1;  // collectives that are not the identity
   if (D.sharded) {  // the submap sizes over all ranks
     LAUNCH(FAM_OTHER, k_submap_count<<<B, 256, 0, st>>>(D));
-    TRY(comm_allreduce(h->comm, D.wcnt, (int64_t)B * 2 * WIN_MAX, LOAM_DT_I32, st));
+    if (multi) TRY(comm_allreduce(h->comm, D.wcnt, (int64_t)B * 2 * WIN_MAX, LOAM_DT_I32, st));
   }
   LAUNCH(FAM_OTHER, k_submap_prep<<<B, 128, 0, st>>>(D));
   LOAM_HIP(hipEventRecord(h->ev[1], st));
   LOAM_HIP(hipStreamWaitEvent(st, h->ev_join, 0));
   size_t q_tot = 0;
-  if (D.sharded) {
+  if (multi) {
     // the stack sizes (identical on every rank) place each stream's queries in the exchange
     LOAM_HIP(hipMemcpyAsync(h->hf.data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
     LOAM_HIP(hipStreamSynchronize(st));
@@ -1786,7 +1800,8 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     if (h->knn_lanes == 2) LAUNCH(FAM_CORR, k_knn<2><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round));
     else LAUNCH(FAM_CORR, k_knn<1><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round));
     if (D.sharded) {  // every rank's candidates -> the exact 5-NN on every rank
-      TRY(comm_allgather(h->comm, D.nn_send, const_cast<NnRec*>(D.nn_recv), (int64_t)(q_tot * sizeof(NnRec)), st));
+      if (multi)
+        TRY(comm_allgather(h->comm, D.nn_send, const_cast<NnRec*>(D.nn_recv), (int64_t)(q_tot * sizeof(NnRec)), st));
       LAUNCH(FAM_CORR, k_nn_merge<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D));
     }
     LAUNCH(FAM_CORR, k_geom<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round));
@@ -1805,7 +1820,8 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   }
   if (D.sharded) {  // pose agreement across ranks before anything is stored (k_pose_adopt)
     LAUNCH(FAM_OTHER, k_pose_publish<<<B, 64, 0, st>>>(D));
-    TRY(comm_allgather(h->comm, D.pose_x + (size_t)D.rank * B * 8, D.pose_x, (int64_t)B * 8 * sizeof(double), st));
+    if (multi)
+      TRY(comm_allgather(h->comm, D.pose_x + (size_t)D.rank * B * 8, D.pose_x, (int64_t)B * 8 * sizeof(double), st));
     LAUNCH(FAM_OTHER, k_pose_adopt<<<B, 64, 0, st>>>(D));
   }
   LOAM_HIP(hipEventRecord(h->ev[2], st));

@@ -12,6 +12,10 @@ sums.  Transports:
   host-buffer callbacks meeting at a barrier, summed in rank order.
 - ``TorchDistComm.create()`` — host-buffer callbacks over an initialised torch.distributed group
   (gloo), all-gather + ordered sum so every rank gets bit-identical sums.
+- ``TorchDistStagedComm.create()`` — the same collectives behind device-pointer callbacks
+  (``host_buffers = 0``: the library hands over HBM pointers and its HIP stream); the callback
+  waits for the stream and stages through host memory.  It exercises the device-pointer
+  transport path of the C-ABI, which a caller's own device collectives would use.
 
 Every allreduce must give bit-identical results on all ranks (every rank then takes the same
 trust-region step and stores points with the same pose); RCCL's ring / tree algorithms reduce
@@ -94,6 +98,33 @@ class Comm:
         ops = CommOps()
         ops.user = None
         ops.host_buffers = 1
+        ops.allreduce_sum = ALLREDUCE_FN(ar)
+        ops.allgather = ALLGATHER_FN(ag)
+        h = ctypes.c_void_p()
+        check(lib().loam_comm_create(rank, size, ctypes.byref(ops), ctypes.byref(h)))
+        return cls(h, rank, size, keep=(ops, ops.allreduce_sum, ops.allgather, ar, ag))
+
+    @classmethod
+    def from_device_callbacks(cls, rank, size, allreduce, allgather):
+        """device-pointer callbacks: allreduce(d_buf, count, dtype, hip_stream) sums in place over
+        the ranks, allgather(d_send, d_recv, nbytes, hip_stream) fills d_recv with every rank's
+        send in rank order; both return 0 on success"""
+
+        def ar(user, buf, count, dtype, stream):
+            try:
+                return int(allreduce(buf, count, dtype, stream) or 0)
+            except Exception:  # noqa: BLE001
+                return 1
+
+        def ag(user, send, recv, nbytes, stream):
+            try:
+                return int(allgather(send, recv, nbytes, stream) or 0)
+            except Exception:  # noqa: BLE001
+                return 1
+
+        ops = CommOps()
+        ops.user = None
+        ops.host_buffers = 0
         ops.allreduce_sum = ALLREDUCE_FN(ar)
         ops.allgather = ALLGATHER_FN(ag)
         h = ctypes.c_void_p()
@@ -185,3 +216,38 @@ class TorchDistComm:
 
         return Comm.from_host_callbacks(dist.get_rank(), dist.get_world_size(), dist_allreduce_ordered,
                                         dist_allgather_bytes)
+
+
+class TorchDistStagedComm:
+    """Device-pointer callbacks over the default torch.distributed group: wait for the mapper's
+    HIP stream, copy the device buffer to host memory, run the ordered gloo collective, copy back.
+    The library side is its device-pointer (host_buffers = 0) transport."""
+
+    @staticmethod
+    def create():
+        import torch.distributed as dist
+
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        d2h, h2d = 2, 1  # hipMemcpyDeviceToHost, hipMemcpyHostToDevice
+
+        def allreduce(buf, count, dtype, stream):
+            if hip.hipStreamSynchronize(stream) != 0:
+                return 1
+            arr = np.empty(count, dtype=np.float64 if dtype == DT_F64 else np.int32)
+            if hip.hipMemcpy(arr.ctypes.data, buf, arr.nbytes, d2h) != 0:
+                return 1
+            dist_allreduce_ordered(arr)
+            return hip.hipMemcpy(buf, arr.ctypes.data, arr.nbytes, h2d)
+
+        def allgather(send, recv, nbytes, stream):
+            if hip.hipStreamSynchronize(stream) != 0:
+                return 1
+            arr = np.empty(nbytes, dtype=np.uint8)
+            if nbytes and hip.hipMemcpy(arr.ctypes.data, send, nbytes, d2h) != 0:
+                return 1
+            out = np.ascontiguousarray(dist_allgather_bytes(arr))
+            return hip.hipMemcpy(recv, out.ctypes.data, out.nbytes, h2d) if out.nbytes else 0
+
+        return Comm.from_device_callbacks(dist.get_rank(), dist.get_world_size(), allreduce, allgather)
