@@ -18,8 +18,8 @@ from loam_amd.odometry import BatchOdometry
 pytestmark = pytest.mark.gpu
 
 
-def features(seed, n_frames, n_az=2000, flags=0, with_gt=False):
-    sr = O.ScanRegistration()
+def features(seed, n_frames, n_az=2000, flags=0, with_gt=False, n_scans=64):
+    sr = O.ScanRegistration(n_scans=n_scans)
     out, gts = [], []
     for f in range(n_frames):
         xyz, gt = synth.frame(seed, f, n_az, flags=flags)
@@ -156,6 +156,13 @@ def test_odometry_edge_case_sequence(flags):
     if flags & synth.COLUMN_MAJOR:
         last = frames[2][2]  # a lessSharp cloud (next frame's laserCloudCornerLast)
         assert (np.diff(last[:, 3].astype(np.int32)) < 0).sum() > 5
+    _check_sequence(frames)
+
+
+@pytest.mark.parametrize("lasers", [16, 32])
+def test_odometry_16_and_32_lines(lasers):
+    """VLP-16 / HDL-32E clouds (N_SCANS 16 / 32): sparser rings, the same scan-to-scan path"""
+    frames = features(6, 5, flags=synth.VLP16 if lasers == 16 else synth.HDL32, n_scans=lasers)
     _check_sequence(frames)
 
 

@@ -23,8 +23,8 @@ def _same_points(a, b):
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
-def _check_frame(xyz, gpu=None):
-    ref = O.ScanRegistration()
+def _check_frame(xyz, gpu=None, n_scans=64):
+    ref = O.ScanRegistration(n_scans=n_scans)
     ref.input(xyz)
     gpu = gpu or ScanRegistration()
     gpu.input(xyz)
@@ -58,6 +58,17 @@ def test_scanreg_edge_cases(mode, seed, frame):
     if mode in ("quantized", "all"):  # tied curvatures inside the sectors
         c, _ = ref.curvature()
         assert len(c) - len(np.unique(c)) > 300
+
+
+@pytest.mark.parametrize("lasers,flags", [(16, 0), (16, synth.BOUNDARY), (32, 0), (32, synth.BOUNDARY),
+                                          (16, synth.COLUMN_MAJOR | synth.LASER_AZ | synth.QUANTIZE)])
+def test_scanreg_16_and_32_lines(lasers, flags):
+    """the N_SCANS == 16 / 32 ring rules (scan_registration.cpp:225-236) on VLP-16 / HDL-32E
+    elevations, also exactly on the rules' boundaries"""
+    xyz, _ = synth.frame(5, 21, 2000, flags=flags | (synth.VLP16 if lasers == 16 else synth.HDL32))
+    ref = _check_frame(xyz, ScanRegistration(scan_line=lasers), n_scans=lasers)
+    ids = np.floor(ref.cloud(0)[:, 3]).astype(int)
+    assert ids.max() < lasers and len(np.unique(ids)) >= (12 if lasers == 16 else 20)
 
 
 @pytest.mark.parametrize("n_az", [4000, 5000])

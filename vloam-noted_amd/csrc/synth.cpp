@@ -241,12 +241,20 @@ void synth_pose(uint64_t seed, double frame, double speed, double* q_xyzw, doubl
 //                       atan / sqrt / the division
 //   SYNTH_QUANTIZE      coordinates rounded to 1 cm: equal curvatures (std::sort ties of
 //                       :365-366) and points on VoxelGrid leaf boundaries
-constexpr int32_t SYNTH_COLUMN_MAJOR = 1, SYNTH_LASER_AZ = 2, SYNTH_BOUNDARY = 4, SYNTH_QUANTIZE = 8;
+//   SYNTH_VLP16         a 16-laser sensor (VLP-16: -15 + 2k deg), for the N_SCANS == 16 ring rule
+//                       (scan_registration.cpp:225-230); with SYNTH_BOUNDARY the elevations sit
+//                       on its boundaries (-16 + 2k: (angle + 15) / 2 + 0.5 = k exactly) and the
+//                       +15 deg cut-off
+//   SYNTH_HDL32         a 32-laser sensor (HDL-32E: -92/3 + 4k/3 deg) for N_SCANS == 32
+//                       (:231-236); without SYNTH_BOUNDARY offset by half a ring pitch, with it
+//                       exactly HDL-32E's, where (angle + 92/3) * 3/4 = k is the boundary
+constexpr int32_t SYNTH_COLUMN_MAJOR = 1, SYNTH_LASER_AZ = 2, SYNTH_BOUNDARY = 4, SYNTH_QUANTIZE = 8,
+                  SYNTH_VLP16 = 16, SYNTH_HDL32 = 32;
 
 int32_t synth_frame_ex(uint64_t seed, int32_t frame, int32_t n_az, double speed, int32_t flags, float* out_xyz,
                        double* pose7);
 
-// one revolution: writes up to 64*n_az points (x,y,z, stride 3) in the SENSOR frame,
+// one revolution: writes up to 64*n_az points (16 / 32 * n_az for SYNTH_VLP16 / SYNTH_HDL32) (x,y,z, stride 3) in the SENSOR frame,
 // ring-major; returns the number of returns.  pose7 = q(x,y,z,w), t(x,y,z) ground truth.
 int32_t synth_frame(uint64_t seed, int32_t frame, int32_t n_az, double speed, float* out_xyz,
                     double* pose7) {
@@ -269,10 +277,16 @@ int32_t synth_frame_ex(uint64_t seed, int32_t frame, int32_t n_az, double speed,
                     {2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)}};
   Rng rng{mix64(seed * 1000003ULL + (uint64_t)frame)};
   double az0 = 2.0 * M_PI * u01(mix64(seed ^ (uint64_t)frame * 77ULL)) / n_az;
+  const int lasers = (flags & SYNTH_VLP16) ? 16 : (flags & SYNTH_HDL32) ? 32 : 64;
+  const bool bnd = (flags & SYNTH_BOUNDARY) != 0;
   double ce[64], se[64], daz[64];
-  for (int ring = 0; ring < 64; ++ring) {
+  for (int ring = 0; ring < lasers; ++ring) {
     double elev = ring < 32 ? (1.98 - ring / 3.0) : (-8.87 - (ring - 32) * 0.5);
-    if (flags & SYNTH_BOUNDARY) {
+    if (lasers == 16) {
+      elev = bnd ? -16.0 + 2.0 * (ring + 1) : -15.0 + 2.0 * ring + 0.01;
+    } else if (lasers == 32) {
+      elev = -92.0 / 3.0 + (ring + (bnd ? 0.0 : 0.5)) * 4.0 / 3.0;
+    } else if (bnd) {
       elev = ring < 32 ? 2.0 - (ring + 0.5) / 3.0 : -8.83 - (ring - 32 + 0.5) / 2.0;
       if (ring == 0) elev = 2.0;
       if (ring == 32) elev = -8.83;
@@ -284,13 +298,13 @@ int32_t synth_frame_ex(uint64_t seed, int32_t frame, int32_t n_az, double speed,
     // offsets falling with the laser index (plus jitter): in a column-major frame the first
     // returning laser leads, and the first columns of the lasers after it lie before startOri
     daz[ring] = (flags & SYNTH_LASER_AZ)
-                    ? (M_PI / 180.0) * (4.0 - 8.0 * ring / 63.0 + 0.5 * (2.0 * hrand(seed, 900, ring) - 1.0))
+                    ? (M_PI / 180.0) * (4.0 - 8.0 * ring / (lasers - 1.0) + 0.5 * (2.0 * hrand(seed, 900, ring) - 1.0))
                     : 0.0;
   }
   int32_t n = 0;
   const bool cm = (flags & SYNTH_COLUMN_MAJOR) != 0;
-  for (int outer = 0; outer < (cm ? n_az : 64); ++outer) {
-    for (int inner = 0; inner < (cm ? 64 : n_az); ++inner) {
+  for (int outer = 0; outer < (cm ? n_az : lasers); ++outer) {
+    for (int inner = 0; inner < (cm ? lasers : n_az); ++inner) {
       const int ring = cm ? inner : outer, a = cm ? outer : inner;
       double az = -(az0 + 2.0 * M_PI * a / n_az + daz[ring]);  // clockwise
       double ds[3] = {ce[ring] * std::cos(az), ce[ring] * std::sin(az), se[ring]};

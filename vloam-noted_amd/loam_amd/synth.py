@@ -32,8 +32,8 @@ def _lib():
 
 
 # edge-case modes (csrc/synth.cpp): azimuth-interleaved order, per-laser azimuth offsets,
-# elevations on the ring-rule boundaries, 1 cm coordinate quantization
-COLUMN_MAJOR, LASER_AZ, BOUNDARY, QUANTIZE = 1, 2, 4, 8
+# elevations on the ring-rule boundaries, 1 cm coordinate quantization, 16- and 32-laser sensors
+COLUMN_MAJOR, LASER_AZ, BOUNDARY, QUANTIZE, VLP16, HDL32 = 1, 2, 4, 8, 16, 32
 
 
 def frame(seed: int, index: int, n_az: int = 2000, speed: float = 1.0, flags: int = 0):
