@@ -15,6 +15,7 @@ import pytest
 import loam_oracle as O
 from helpers import quat_angle
 from loam_amd import synth
+from loam_amd.trajectory import KittiTrajectoryWriter, parse_rows
 from loam_amd.mapping import BatchMapper
 from loam_amd.odometry import BatchOdometry
 from loam_amd.scanreg import ScanRegistration
@@ -27,6 +28,8 @@ def test_pipeline_zero_copy():
     sr_o, od_o, mp_o = O.ScanRegistration(), O.LaserOdometry(), O.LaserMapping()
     sr, od, mp = ScanRegistration(), BatchOdometry(1), BatchMapper(1, exact_voxel_order=1)
     worst = [0.0, 0.0, 0.0, 0.0]
+    # LO / MO trajectory files as the driver writes them (vloam_main_node.cpp:192-198)
+    lo, mo, lo_o, mo_o = (KittiTrajectoryWriter(None) for _ in range(4))
     for f in range(n_frames):
         xyz, _ = synth.frame(seed, f)
         # oracle
@@ -48,11 +51,16 @@ def test_pipeline_zero_copy():
         mp.input_device(0, pc, nc, ps, ns, q, t, skip)
         mp.solve()
         qm, tm = mp.pose(0)
+        for w, (qq, tt) in zip((lo, mo, lo_o, mo_o), ((q, t), (qm, tm), (qo, to), (qm_o, tm_o))):
+            w.write(f, qq, tt)
         worst[0] = max(worst[0], float(np.linalg.norm(t - to)))
         worst[1] = max(worst[1], quat_angle(q, qo))
         worst[2] = max(worst[2], float(np.linalg.norm(tm - tm_o)))
         worst[3] = max(worst[3], quat_angle(qm, qm_o))
     assert max(worst) < 1e-4, worst
+    for a, b in ((lo, lo_o), (mo, mo_o)):
+        assert len(a.rows) == n_frames
+        assert np.abs(parse_rows("".join(a.rows)) - parse_rows("".join(b.rows))).max() < 2e-4
     sr.close()
     od.close()
     mp.close()
