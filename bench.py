@@ -625,9 +625,20 @@ def main():
         sm.close()
         scomm.close()
         sit_all, sdt_max = aggregate(sit, sdt, world, f"cuda:{local}")
+        # the same streams and frames through an unsharded handle on this GPU (the reference
+        # point of the sharding overhead at one rank)
+        um = BatchMapper(Bs, device=local, max_map_points=args.map_points)
+        run_steps(um, splan, 0, pre)
+        torch.cuda.synchronize(local)
+        t0 = time.perf_counter()
+        uit = run_steps(um, splan, pre, K)
+        torch.cuda.synchronize(local)
+        udt = time.perf_counter() - t0
+        um.close()
         shard_leg = {"value": round(sit_all / world / sdt_max, 3), "unit": "LM iters/s",
                      "ms_per_step": round(1e3 * sdt_max / K, 4), "streams": Bs, "ranks": world, "scaling": "strong",
-                     "frames_per_step": Bs,
+                     "frames_per_step": Bs, "unsharded_same_streams": round(uit / udt, 3),
+                     "sharded_over_unsharded": round((sit_all / world / sdt_max) / (uit / udt), 4),
                      "transport": "RCCL" if world > 1 else "one rank: every collective is the identity",
                      "mode": "every stream split over all ranks (block-owned map shards, per-round 5-NN all-gather, "
                              "per-LM-iteration normal-equation all-reduce); iterations counted once per stream"}

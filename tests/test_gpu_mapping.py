@@ -336,3 +336,66 @@ def test_graph_path_bit_identical(seq):
             assert sorted(ma[s][w]) == sorted(mb[s][w])
             for c in ma[s][w]:
                 assert np.array_equal(ma[s][w][c], mb[s][w][c])
+
+
+def _cube_of(v, cen):
+    """laser_mapping.cpp:747-756: int((v + 25) / 50) + cen, one less when v + 25 < 0"""
+    c = int((np.float32(v) + np.float32(25.0)) / np.float32(50.0)) + int(cen)
+    return c - 1 if np.float32(v) + np.float32(25.0) < 0 else c
+
+
+def edge_state(rec, axis_bounds=((0, -75.0), (1, -75.0), (0, -125.0), (1, -125.0))):
+    """the frame's map with every point within 0.5 m of the busiest plane v = B (B + 25 a negative
+    multiple of 50) moved onto it and re-filed by the reference's cube rule: cells at v = B hold
+    points in two cubes (the cube above at local 0, the cube below at local 50 for v == B)"""
+    from scipy.spatial.transform import Rotation as R
+    import loam_oracle as O
+    before = rec["before"]
+    x0 = rec["round_pose"][0]
+    qs = np.concatenate([O.voxel_grid(rec["corner"], 0.4), O.voxel_grid(rec["surf"], 0.8)])[:, :3]
+    qm = R.from_quat(x0[:4]).apply(qs.astype(np.float64)) + x0[4:]
+    axis, b = max(axis_bounds, key=lambda ab: int((np.abs(qm[:, ab[0]] - ab[1]) < 1.0).sum()))
+    cen = before["cen"]
+    out = dict(cen=cen, q=before["q"], t=before["t"])
+    moved = 0
+    for key in ("corner", "surf"):
+        cubes = {}
+        for c, pts in before[key].items():
+            for p in pts:
+                p = p.copy()
+                ijk = [c % 21, (c // 21) % 21, c // 441]
+                if abs(float(p[axis]) - b) < 0.5:
+                    p[axis] = np.float32(b)
+                    ijk[axis] = _cube_of(p[axis], cen[axis])
+                    moved += 1
+                cubes.setdefault(ijk[0] + 21 * ijk[1] + 441 * ijk[2], []).append(p)
+        out[key] = {c: np.array(v, np.float32) for c, v in cubes.items()}
+    near = int((np.abs(qm[:, axis] - b) < 1.0).sum())
+    return out, moved, near
+
+
+def test_cube_edge_filing():
+    """queries next to a plane v = B where B + 25 is a negative multiple of 50: map points with
+    v == B exactly sit in the cube below at local coordinate 50 (laser_mapping.cpp:747-756) while
+    the rest of the cell is in the cube above; k_knn scans both.  Against the oracle from the
+    same modified state: identical counts and iterations, pose within 1e-4"""
+    import loam_oracle as O
+    seq = run_sequence(seed=23, n_frames=3, snapshot_frames=(2,))
+    rec = seq[2]
+    state, moved, near = edge_state(rec)
+    assert moved > 20 and near > 40, (moved, near)
+    ref = O.LaserMapping()
+    ref.set_state(state["cen"], state["q"], state["t"])
+    for which, key in ((0, "corner"), (1, "surf")):
+        for c, pts in state[key].items():
+            ref.set_cube(which, c, pts)
+    ref.input(rec["corner"], rec["surf"], None, rec["q_wodom"], rec["t_wodom"])
+    ref.solve()
+    want = dict(pose=ref.pose(), stats=ref.stats())
+    for exact in (1, 0):
+        m = BatchMapper(1, exact_voxel_order=exact)
+        load_state(m, 0, state)
+        m.input(0, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+        m.solve()
+        _check_frame(m, 0, want)
+        m.close()
