@@ -464,7 +464,7 @@ def pipeline_stage(seed, device, n_frames=160, timed=80, n_az=2000):
     return out
 
 
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r2_pmc_traffic.json")
 
 
 def pmc_traffic(family):
