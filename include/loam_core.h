@@ -124,6 +124,11 @@ int32_t loam_scanreg_device_ptr(loam_scanreg* h, int32_t which, const float** pt
 int32_t loam_scanreg_curvature(loam_scanreg* h, float* curv, int32_t* label, int32_t cap);
 /* device time of the last input (ms) */
 double loam_scanreg_ms(loam_scanreg* h);
+/* cumulative device cycle counters of the per-ring PCL-order VoxelGrid (k_sr_ringvox), summed
+ * over rings and frames: [0] bounding box + keys, [1] sort levels, [2] final sort pass,
+ * [3] centroids; reset = 1 zeroes them after the copy */
+#define LOAM_SR_DEBUG_COUNTERS 8
+int32_t loam_scanreg_debug_counters(loam_scanreg* h, uint64_t* out, int32_t n, int32_t reset);
 
 /* --------------------------------------------------------------------------------------
  * LaserOdometry (laser_odometry.h:70-84) — scan-to-scan odometry, n_streams independent

@@ -100,7 +100,7 @@ __global__ void __launch_bounds__(P_PCL_THREADS) k_sort_perm(const uint32_t* key
   for (int i = tid; i < n; i += P_PCL_THREADS) E[i] = ((uint64_t)keys[i] << 32) | (uint32_t)i;
   if (tid == 0) ss_levels_init(&lev, n, seg, seg + 3 * cap, cap);
   const PKeyLess less;
-  ss_levels<true, P_PCL_THREADS>(E, A, B, &lev, tid >> 6, nwaves, less);
+  ss_levels<true, P_PCL_THREADS>(E, A, B, &lev, tid >> 6, nwaves, less, seg, seg + 3 * cap, nullptr);
   __syncthreads();
   if (tid == 0 && lev.err) err[0] = lev.err;
   ss_final(E, A, B, n, S, tid, P_PCL_THREADS, less);

@@ -85,6 +85,7 @@ struct SrDev {
   uint32_t* ss_b;
   uint64_t* ss_s;
   int* ss_seg;  // [2][3 * SR_SS_GSEG] level lists of the long-sector path (one sector at a time)
+  unsigned long long* dbg;  // [LOAM_SR_DEBUG_COUNTERS] (loam_scanreg_debug_counters)
 };
 
 // scan_registration.cpp:217-259 (float atan/sqrt like the reference's float overloads)
@@ -354,7 +355,7 @@ __device__ inline void sr_exact_sector(const SrDev& D, int sp, int len, uint64_t
     E[k] = ((uint64_t)__float_as_uint(D.curv[sp + k]) << 32) | (uint32_t)(sp + k);
   if (lane == 0) ss_levels_init(lev, len, seg0, seg1, cap);
   const SrCurvLess less;
-  ss_levels<false>(E, A, B, lev, 0, 1, less);
+  ss_levels<false>(E, A, B, lev, 0, 1, less, seg0, seg1, nullptr);
   ss_final(E, A, B, len, K, lane, 64, less);
   if (lane == 0 && lev->err) atomicOr(&D.fr->err, SR_ERR_SORT);
   ss_wave_fence();
@@ -586,12 +587,21 @@ __global__ void __launch_bounds__(SRV_THREADS) k_sr_ringvox(SrDev D) {
   const int base = F.ring_off[r];
   const int n = F.n_less_flat_scan[r];
   const bool lds = n <= SRV_LDS;
-  const VxPclScratch X{lds ? sE : D.ss_e + base, lds ? sA : D.ss_a + base, lds ? sB : D.ss_b + base,
-                       lds ? sS : D.ss_s + base, &lev, {seg[0], seg[1]}, SRV_SEG};
   VxPclOut O;
   O.out = D.less_flat_ds + base;
   O.res_cnt = &F.n_less_flat[r];
-  voxel_grid_pcl<SRV_THREADS>(VxPtrSrc{D.less_flat_scan + base}, n, 0.2f, O, X, M, ws, &F.err);
+  // two inlined copies: with the sort arrays named directly as __shared__ the compiler emits
+  // LDS instructions (ds_*) for the sort, where a pointer selected between LDS and global
+  // memory would be generic (flat_*, slower)
+  if (lds) {
+    VxPclScratch X{sE, sA, sB, sS, &lev, {seg[0], seg[1]}, SRV_SEG};
+    X.prof = D.dbg;  // ring VoxelGrid phase cycles, summed over the rings
+    voxel_grid_pcl<SRV_THREADS>(VxPtrSrc{D.less_flat_scan + base}, n, 0.2f, O, X, M, ws, &F.err);
+  } else {
+    VxPclScratch X{D.ss_e + base, D.ss_a + base, D.ss_b + base, D.ss_s + base, &lev, {seg[0], seg[1]}, SRV_SEG};
+    X.prof = D.dbg;
+    voxel_grid_pcl<SRV_THREADS>(VxPtrSrc{D.less_flat_scan + base}, n, 0.2f, O, X, M, ws, &F.err);
+  }
 }
 
 // concatenation of the per-ring outputs in ring order
@@ -722,6 +732,7 @@ int32_t loam_scanreg_create(const loam_params* p, int32_t device, loam_scanreg**
   SRA(D.ss_b, cap);
   SRA(D.ss_s, cap);
   SRA(D.ss_seg, 6 * SR_SS_GSEG);
+  SRA(D.dbg, LOAM_SR_DEBUG_COUNTERS);
 #undef SRA
   D.out[0] = D.cloud;
   D.sort_ind = nullptr;
@@ -890,5 +901,15 @@ int32_t loam_scanreg_curvature(loam_scanreg* h, float* curv, int32_t* label, int
 }
 
 double loam_scanreg_ms(loam_scanreg* h) { return h ? (double)h->ms : 0.0; }
+
+int32_t loam_scanreg_debug_counters(loam_scanreg* h, uint64_t* out, int32_t n, int32_t reset) {
+  if (!h || !out || n < 0) return set_error("loam_scanreg_debug_counters: bad argument"), LOAM_ERR_ARG;
+  LOAM_HIP(hipSetDevice(h->dev));
+  LOAM_HIP(hipStreamSynchronize(h->st));
+  const int k = std::min<int>(n, LOAM_SR_DEBUG_COUNTERS);
+  LOAM_HIP(hipMemcpy(out, h->D.dbg, sizeof(uint64_t) * k, hipMemcpyDeviceToHost));
+  if (reset) LOAM_HIP(hipMemset(h->D.dbg, 0, sizeof(uint64_t) * LOAM_SR_DEBUG_COUNTERS));
+  return LOAM_OK;
+}
 
 }  // extern "C"

@@ -378,9 +378,14 @@ __device__ inline void ss_levels_init(SsLevels* L, int n, int* seg0, int* seg1, 
 // whole workgroup, barriers are __syncthreads; else one wave alone); waves w < nw take the
 // level's segments w, w + nw, ...  No waiting on other waves outside the barriers, and at most
 // 2 * __lg(n) + 1 levels (each level lowers the depth budget by one).
+// The list / buffer pointers are arguments (not read back from L, which lives in LDS): named
+// directly from __shared__ arrays at the call site they keep their LDS address space, so the
+// compiler emits ds_* instead of flat_* accesses.
 template <bool WG, int NT = 64, typename T, typename Less>
-__device__ inline void ss_levels(T* E, uint32_t* A, uint32_t* B, SsLevels* L, int wave, int nw, const Less& less) {
+__device__ inline void ss_levels(T* E, uint32_t* A, uint32_t* B, SsLevels* L, int wave, int nw, const Less& less,
+                                 int* seg0, int* seg1, uint32_t* loc) {
   const int lane = threadIdx.x & 63;
+  int* const segs[2] = {seg0, seg1};
   auto barrier = [] {
     if (WG) __syncthreads();
     else ss_wave_fence();
@@ -390,7 +395,7 @@ __device__ inline void ss_levels(T* E, uint32_t* A, uint32_t* B, SsLevels* L, in
     const int t = atomicAdd(big ? &L->nbig[nxt] : &L->cnt[nxt], 1);
     const int slot = big ? L->cap - 1 - t : t;
     if (t < L->cap && slot >= 0) {
-      int* o = L->seg[nxt] + 3 * slot;
+      int* o = segs[nxt] + 3 * slot;
       o[0] = a;
       o[1] = b;
       o[2] = d;
@@ -407,7 +412,7 @@ __device__ inline void ss_levels(T* E, uint32_t* A, uint32_t* B, SsLevels* L, in
       if (threadIdx.x == 0) atomicOr(&L->err, 2);
       break;
     }
-    const int* sg = L->seg[cur];
+    const int* sg = segs[cur];
     if (WG) {  // long segments: the whole workgroup on each in turn
       for (int t = 0; t < nb; ++t) {
         const int* e = sg + 3 * (L->cap - 1 - t);
@@ -433,8 +438,8 @@ __device__ inline void ss_levels(T* E, uint32_t* A, uint32_t* B, SsLevels* L, in
     for (int k = wave; wave < nw && k < tot; k += nw) {
       const int* e = sg + 3 * (k < cnt ? k : L->cap - 1 - (k - cnt));
       const int lo = e[0], hi = e[1], d = e[2];
-      if (L->loc && hi - lo <= SS_LOCAL) {
-        ss_local_sort(E, A, B, lo, hi, d, L->loc + wave * SS_LOC_WORDS, less);
+      if (loc && hi - lo <= SS_LOCAL) {
+        ss_local_sort(E, A, B, lo, hi, d, loc + wave * SS_LOC_WORDS, less);
         continue;
       }
       if (d == 0) {  // depth limit: __partial_sort(first, last, last)

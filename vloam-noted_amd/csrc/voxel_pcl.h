@@ -96,7 +96,7 @@ __device__ inline void voxel_grid_pcl(const PF& P, int n, float leaf, const VxPc
   const VxIdxLess less;
   __syncthreads();
   vx_phase(X.prof, 0, &tp);
-  ss_levels<true, NT>(X.E, X.A, X.B, X.lev, tid >> 6, NT / 64, less);
+  ss_levels<true, NT>(X.E, X.A, X.B, X.lev, tid >> 6, NT / 64, less, X.seg[0], X.seg[1], X.loc);
   __syncthreads();
   vx_phase(X.prof, 1, &tp);
   if (tid == 0 && X.lev->err) atomicOr(err, 4);

@@ -102,3 +102,9 @@ class ScanRegistration:
     @property
     def ms(self):
         return lib().loam_scanreg_ms(self.h)
+
+    def debug_counters(self, reset=False):
+        """ring VoxelGrid phase cycles (include/loam_core.h LOAM_SR_DEBUG_COUNTERS)"""
+        out = np.zeros(8, np.uint64)
+        check(lib().loam_scanreg_debug_counters(self.h, ptr(out), 8, int(reset)))
+        return out
