@@ -62,7 +62,8 @@ struct SsLevels {
 // memory is copied into the wave's LDS, its whole introsort subtree runs there (a wave-local
 // LIFO, no level barriers), and the result goes back with identity annotations.
 constexpr int SS_LOCAL = 512;
-constexpr int SS_LOC_STK = 24;  // >= 2 __lg(SS_LOCAL) + 2 pending right parts
+// pending right parts are disjoint and longer than 16 elements: at most SS_LOCAL / 17 + 1
+constexpr int SS_LOC_STK = SS_LOCAL / (SS_THRESHOLD + 1) + 2;
 constexpr int SS_LOC_WORDS = 2 * SS_LOCAL + 2 * SS_LOCAL + 3 * SS_LOC_STK;
 
 constexpr int SS_BIG = 1024;  // longer segments are partitioned by the whole workgroup
