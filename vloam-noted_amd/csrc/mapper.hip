@@ -140,6 +140,10 @@ struct MapperDev {
   float4* nn_xyz;        // [5][B][2*max_in] merged neighbours (k_geom input in sharded mode)
   double* pose_x;        // [nrank][B][8] every rank's optimised pose (agreement check)
   double* lm_red;        // [B][LM_NACC] this rank's normal-equation sums, then the all-reduced
+  // few streams: the stack VoxelGrid of a (stream, map) split over stack_k workgroups by voxel
+  // idx range (k_stack_part + k_stack_cat), else one workgroup (k_stack_ds)
+  int stack_k = 0;
+  uint2* stk_part;       // [B][2][STACK_K_MAX] (staging offset, centroids) of each range
 };
 
 // one query's 5 nearest candidates on one rank (d: FLANN L2_Simple float distance, id: global
@@ -277,6 +281,130 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
   S.scratch_idx = D.vx_idx + sm * D.scratch_cap;
   S.scratch_cap = D.scratch_cap;
   voxel_segment(S, lds);
+}
+
+// Few streams: the input-order stack VoxelGrid of a (stream, map) over stack_k workgroups.
+// Every workgroup computes the same geometry and idx histogram (VX_NB buckets) from all the
+// points, cuts the idx range into stack_k ranges of about equal point counts, and filters its
+// own range (vx_group: hash, sorted unique voxels, member lists in input order, centroids) into
+// the (stream, map) staging area at the point-count prefix of its range.  k_stack_cat then
+// concatenates the ranges in idx order.  Same voxels, same member order, same sums: the bits of
+// the one-workgroup filter.
+constexpr int STACK_K_MAX = 16;
+__global__ void __launch_bounds__(VX_THREADS) k_stack_part(MapperDev D) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
+  const int K = D.stack_k;
+  const int j = blockIdx.x % K, pm = blockIdx.x / K;
+  const int s = D.s0 + (pm >> 1), m = pm & 1;
+  StreamFrame& F = D.fr[s];
+  if (!F.active) return;
+  const size_t sm = sm_index(s, m);
+  uint2* part = D.stk_part + sm * STACK_K_MAX;
+  const uint32_t N = (uint32_t)(m == 0 ? F.nc_in : F.ns_in);
+  const VxSrc P{F.in_ptr[m], (int)N, nullptr};
+  float4* stage = D.vx_pts + sm * D.scratch_cap;
+  uint32_t* ws = lds + VX_LDS_WORDS - 256;
+  VxMisc& M = *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192);
+  const int tid = threadIdx.x;
+  if (N == 0) {
+    if (tid == 0) part[j] = make_uint2(0, 0);
+    return;
+  }
+  vx_geometry(P, N, D.leaf[m], M);
+  const VxGeom g = M.g;
+  if (g.overflow) {  // PCL: "Leaf size is too small" -> output = input (range 0 copies it)
+    if (j == 0)
+      for (uint32_t i = tid; i < N; i += VX_THREADS) stage[i] = P(i);
+    if (tid == 0) part[j] = make_uint2(0, j == 0 ? N : 0u);
+    return;
+  }
+  // idx histogram -> the ranges' bucket cuts by cumulative point count
+  uint32_t* hist = lds + VX_HIST_WORD;
+  const unsigned long long V = g.nvox;
+  auto bucket = [&](uint32_t k) { return (uint32_t)(((unsigned long long)k * VX_NB) / V); };
+  auto blo = [&](uint32_t b) { return (uint32_t)(((unsigned long long)b * V + VX_NB - 1) / VX_NB); };
+  for (int b = tid; b < VX_NB; b += VX_THREADS) hist[b] = 0;
+  __syncthreads();
+  for (uint32_t i = tid; i < N; i += VX_THREADS) atomicAdd(&hist[bucket(vx_key(g, P(i)))], 1u);
+  __syncthreads();
+  // range r starts at the first bucket whose points-before count reaches r N / K: a block scan
+  // of the histogram (two buckets per thread) and a test at every bucket
+  static_assert(VX_NB == 2 * VX_THREADS, "two buckets per thread");
+  const uint32_t h0 = hist[2 * tid], h1 = hist[2 * tid + 1];
+  uint32_t tot;
+  const uint32_t a0 = vx_block_scan(h0 + h1, ws, &tot), a1 = a0 + h0;  // points before buckets 2t, 2t+1
+  const uint64_t thr0 = (uint64_t)j * N / K, thr1 = (uint64_t)(j + 1) * N / K;
+  if (tid == 0) {
+    M.sbase[0] = j == 0 ? 0u : (uint32_t)VX_NB;
+    M.sbase[1] = j == K - 1 ? (uint32_t)VX_NB : (uint32_t)VX_NB;
+    M.sfail = j == 0 ? 0 : (int)N;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const uint32_t bb = 2 * tid + u, acc = u ? a1 : a0, prev = u ? a0 : a0 - (tid ? hist[2 * tid - 1] : 0u);
+    const bool first = bb == 0;
+    if (j > 0 && acc >= thr0 && (first || prev < thr0)) {
+      M.sbase[0] = bb;
+      M.sfail = (int)acc;
+    }
+    if (j < K - 1 && acc >= thr1 && (first || prev < thr1)) M.sbase[1] = bb;
+  }
+  __syncthreads();
+  const uint32_t b0 = M.sbase[0], b1 = max(M.sbase[0], M.sbase[1]), base = (uint32_t)M.sfail;
+  __syncthreads();  // vx_group reuses M
+  if (b0 >= b1) {  // empty range
+    if (tid == 0) part[j] = make_uint2(base, 0);
+    return;
+  }
+  VoxSeg S;
+  S.src0 = F.in_ptr[m];
+  S.n0 = (int)N;
+  S.src1 = nullptr;
+  S.tag1 = nullptr;
+  S.n1 = 0;
+  S.tag = 0;
+  S.leaf = D.leaf[m];
+  S.append_only = 0;
+  S.out = stage;
+  S.tail = nullptr;
+  S.cap = (uint32_t)D.scratch_cap;
+  S.res_off = nullptr;
+  S.res_cnt = nullptr;
+  S.scratch_pts = nullptr;
+  S.scratch_idx = D.vx_idx + sm * D.scratch_cap;
+  S.scratch_tail = nullptr;
+  S.scratch_cap = (uint32_t)D.scratch_cap;
+  S.err = &F.err;
+  int moved = 0;
+  const uint32_t klo = blo(b0), khi = b1 >= (uint32_t)VX_NB ? 0xFFFFFFFFu : blo(b1);
+  const uint32_t U = vx_group(S, g, P, N, D.vx_idx + sm * D.scratch_cap + base, klo, khi, base,
+                              VX_LDS_WORDS - 256, lds, ws, M, &moved);
+  if (tid == 0) {
+    if (U == VX_OVERFLOW) atomicOr(&F.err, MAP_ERR_SORT);
+    part[j] = make_uint2(base, U == VX_OVERFLOW ? 0u : U);
+  }
+}
+
+// the ranges of k_stack_part in idx order -> the stack and its count
+__global__ void __launch_bounds__(VX_THREADS) k_stack_cat(MapperDev D) {
+  const int s = D.s0 + (blockIdx.x >> 1), m = blockIdx.x & 1;
+  StreamFrame& F = D.fr[s];
+  if (!F.active) return;
+  const size_t sm = sm_index(s, m);
+  const uint2* part = D.stk_part + sm * STACK_K_MAX;
+  const float4* stage = D.vx_pts + sm * D.scratch_cap;
+  float4* out = D.stack[m] + (size_t)s * D.max_in;
+  uint32_t o = 0;
+  for (int j = 0; j < D.stack_k; ++j) {
+    const uint2 pj = part[j];
+    for (uint32_t i = threadIdx.x; i < pj.y; i += VX_THREADS) out[o + i] = stage[pj.x + i];
+    o += pj.y;
+  }
+  if (threadIdx.x == 0) {
+    if (m == 0) F.nc_stack = (int)o;
+    else F.ns_stack = (int)o;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1392,6 +1520,12 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     }
   }
   D.pcl_order = h->P.exact_voxel_order ? 1 : 0;
+  {  // few streams: the stack VoxelGrid over 8 workgroups per (stream, map) (k_stack_part)
+    const char* kenv = std::getenv("LOAM_STACK_K");  // measurement override
+    int k = (n_streams <= 4 && !D.pcl_order) ? 8 : 0;
+    if (kenv) k = std::atoi(kenv);
+    D.stack_k = D.pcl_order ? 0 : std::max(0, std::min(STACK_K_MAX, k));
+  }
   D.leaf[0] = (float)h->P.mapping_line_resolution;
   D.leaf[1] = (float)h->P.mapping_plane_resolution;
   const size_t B = n_streams;
@@ -1454,6 +1588,7 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     ALLOC(D.pseg, B * 2 * (6 * (ps / 16) + 6));
   }
   ALLOC(D.vx_idx, B * 2 * (size_t)D.scratch_cap);
+  ALLOC(D.stk_part, B * 2 * (size_t)STACK_K_MAX);
   ALLOC(D.partials, B * (size_t)D.max_chunks * LM_NACC);
   ALLOC(D.lm_sync, B * 2 * LM_SYNC_WORDS);
   ALLOC(D.lm_xpub, B * 2 * 8);
@@ -1726,7 +1861,12 @@ int32_t loam_mapper_solve(loam_mapper* h) {
       LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(StreamFrame) * B, hipMemcpyHostToDevice, st));
       LOAM_HIP(hipEventRecord(h->ev_fork, st));
       LOAM_HIP(hipStreamWaitEvent(s2, h->ev_fork, 0));
-      k_stack_ds<<<B * 2, VX_THREADS, 0, s2>>>(D);
+      if (D.stack_k) {
+        k_stack_part<<<B * 2 * D.stack_k, VX_THREADS, 0, s2>>>(D);
+        k_stack_cat<<<B * 2, VX_THREADS, 0, s2>>>(D);
+      } else {
+        k_stack_ds<<<B * 2, VX_THREADS, 0, s2>>>(D);
+      }
       LOAM_HIP(hipEventRecord(h->ev_join, s2));
       k_submap_prep<<<B, 128, 0, st>>>(D);
       LOAM_HIP(hipStreamWaitEvent(st, h->ev_join, 0));
@@ -1766,7 +1906,12 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   hipStream_t s2 = h->st2;
   LOAM_HIP(hipEventRecord(h->ev_fork, st));
   LOAM_HIP(hipStreamWaitEvent(s2, h->ev_fork, 0));
-  LAUNCH_ON(s2, FAM_STACK, k_stack_ds<<<B * 2, VX_THREADS, 0, s2>>>(D));
+  if (D.stack_k) {
+    LAUNCH_ON(s2, FAM_STACK, k_stack_part<<<B * 2 * D.stack_k, VX_THREADS, 0, s2>>>(D));
+    LAUNCH_ON(s2, FAM_STACK, k_stack_cat<<<B * 2, VX_THREADS, 0, s2>>>(D));
+  } else {
+    LAUNCH_ON(s2, FAM_STACK, k_stack_ds<<<B * 2, VX_THREADS, 0, s2>>>(D));
+  }
   LOAM_HIP(hipEventRecord(h->ev_join, s2));
   if (any_shift) {
     LAUNCH(FAM_OTHER, k_shift_cubes<<<dim3(16, B), 256, 0, st>>>(D, h->cube_tab[h->parity],
