@@ -217,8 +217,10 @@ int32_t loam_mapper_stats(loam_mapper* h, int32_t stream, loam_map_stats* st);
 /* device phase counters (diagnostics, n <= LOAM_DEBUG_COUNTERS): [0..2] re-VoxelGrid cycles
  * merge / full / append, [3] new points of merged cubes, [4..6] items of each, [7] merges with
  * more than 1024 new points, [8] cell-index build cycles, [9] points indexed, [10] old points,
- * [11..14] merge phases (bounding box, hash + pass A, new-voxel sort, pass B), [16] cell-index
- * hash phase, [17..21] LM round: leader eval, leader wait, reduce + step, passes, member wait,
+ * [11..14] merge phases (bounding box, hash + pass A, new-voxel sort, pass B), [15] LM step
+ * alone (lane 0), [16] cell-index hash phase, [17..21] LM round: leader eval, leader wait,
+ * reduce + step, passes, member wait, [22..23] the leader's share-0 evaluation: record loop,
+ * block reduction,
  * [24..31] re-VoxelGrid items by output size (< 1k, 2k, 4k, 8k, 16k, 32k, 64k, more),
  * [32..39] their cycles (filter + index), [40] sharded: pose values that differed from rank 0's
  * after the LM (0 when the all-reduce is bit-identical on every rank), [41] arena compactions

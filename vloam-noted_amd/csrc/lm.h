@@ -386,9 +386,8 @@ struct LmRecView {
 // thread are loaded before either is evaluated, so their loads are in flight together.
 template <int kThreads>
 __device__ inline void lm_eval_sum(const LmRecView& R, int nrec, const double* X, int blk, int nblk,
-                                   double* sum) {
-  __shared__ double red[kThreads / 64][LM_NACC];
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+                                   double* sum, unsigned long long* prof = nullptr) {
+  const int tid = threadIdx.x;
   double acc[LM_NACC];
 #pragma unroll
   for (int i = 0; i < LM_NACC; ++i) acc[i] = 0.0;
@@ -412,6 +411,7 @@ __device__ inline void lm_eval_sum(const LmRecView& R, int nrec, const double* X
       }
     }
   };
+  const unsigned long long tp0 = prof ? __builtin_readcyclecounter() : 0ull;
   double Rm[9];
   lm_rotmat(X, Rm);
   const int r0 = blk * kThreads + tid;
@@ -427,19 +427,34 @@ __device__ inline void lm_eval_sum(const LmRecView& R, int nrec, const double* X
 #pragma unroll
     for (int u = 0; u < 2; ++u) cur[u] = nxt[u];
   }
-#pragma unroll
-  for (int i = 0; i < LM_NACC; ++i) {
-    double v = wave_sum_d(acc[i]);
-    if (lane == 0) red[wid][i] = v;
+  unsigned long long tp1 = 0;
+  if (prof) {
+    __syncthreads();
+    tp1 = __builtin_readcyclecounter();
+    if (tid == 0) atomicAdd(&prof[0], tp1 - tp0);
   }
-  __syncthreads();
-  if (tid < LM_NACC) {
-    double v = 0.0;
+  // block sum of the 29 accumulators through an LDS transpose: every thread stores its row,
+  // then thread 8a + q sums the 32 values of segment q of accumulator a in thread order and
+  // the 8 segment sums combine in a fixed butterfly (29 wave butterflies of 6 dependent
+  // shuffles each took ~15k cycles per block, the transpose ~2k)
+  static_assert(kThreads % 64 == 0 && LM_NACC * 8 <= kThreads, "transpose reduction layout");
+  constexpr int SEG = 8, PER = kThreads / SEG;
+  __shared__ double tr[LM_NACC][kThreads + 1];
 #pragma unroll
-    for (int w = 0; w < kThreads / 64; ++w) v += red[w][tid];
-    sum[tid] = v;
-  }
+  for (int i = 0; i < LM_NACC; ++i) tr[i][tid] = acc[i];
   __syncthreads();
+  double part = 0.0;
+  if (tid < LM_NACC * SEG) {
+    const int a = tid / SEG, q = tid % SEG;
+#pragma unroll 8
+    for (int k = 0; k < PER; ++k) part += tr[a][q * PER + k];
+  }
+  part += __shfl_xor(part, 4, 64);
+  part += __shfl_xor(part, 2, 64);
+  part += __shfl_xor(part, 1, 64);
+  if (tid < LM_NACC * SEG && (tid % SEG) == 0) sum[tid / SEG] = part;
+  __syncthreads();
+  if (prof && tid == 0) atomicAdd(&prof[1], __builtin_readcyclecounter() - tp1);
 }
 
 template <int kThreads>
@@ -650,7 +665,7 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
     // LDS word written in such a region and read through readfirstlane, so the control flow
     // around barriers is uniform whatever the compiler does with the regions.  A share's
     // completion (release) and the next claim are one thread-0 region.
-    lm_eval_sum<kThreads>(J.R, J.nrec, X, 0, G, bsum0);
+    lm_eval_sum<kThreads>(J.R, J.nrec, X, 0, G, bsum0, J.prof ? J.prof + 5 : nullptr);
     if (G > 1) {
       if (tid == 0) sshare = 1 + (int)__hip_atomic_fetch_add(&sync[4 + pass], 1u, RLX_AGENT);
       __syncthreads();
@@ -716,9 +731,11 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       if (lane == 0) {
+        const unsigned long long ts = J.prof ? __builtin_readcyclecounter() : 0ull;
         LmState L = ls;  // registers for the dependent chain
         lm_step(L, sred);
         ls = L;
+        if (J.prof) atomicAdd(&J.prof[-2], __builtin_readcyclecounter() - ts);  // [15]: the step alone
       }
     }
     __syncthreads();
