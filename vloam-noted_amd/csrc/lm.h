@@ -21,6 +21,7 @@
 // cost AND its normal equations (used only if the step is accepted), so an iteration costs
 // exactly one pass over the correspondences.
 #pragma once
+#include <type_traits>
 #include "common.h"
 #include "device_math.h"
 
@@ -438,10 +439,22 @@ __device__ inline void lm_eval_sum(const LmRecView& R, int nrec, const double* X
   // the 8 segment sums combine in a fixed butterfly (29 wave butterflies of 6 dependent
   // shuffles each took ~15k cycles per block, the transpose ~2k)
   static_assert(kThreads % 64 == 0 && LM_NACC * 8 <= kThreads, "transpose reduction layout");
-  constexpr int SEG = 8, PER = kThreads / SEG;
-  __shared__ double tr[LM_NACC][kThreads + 1];
+  // first the four lanes of each quad combine in registers (DPP quad permutes: lane pairs, then
+  // pairs of pairs), so a quarter of the rows go through LDS
+  constexpr int SEG = 8, ROWS = kThreads / 4, PER = ROWS / SEG;
+  __shared__ double tr[LM_NACC][ROWS + 1];
+  auto dpp_add = [](double v, auto ctrl) {
+    const uint64_t u = __double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, decltype(ctrl)::value, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), decltype(ctrl)::value, 0xF, 0xF, false);
+    return v + __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+  };
 #pragma unroll
-  for (int i = 0; i < LM_NACC; ++i) tr[i][tid] = acc[i];
+  for (int i = 0; i < LM_NACC; ++i) {
+    double v = dpp_add(acc[i], std::integral_constant<int, 0xB1>{});  // quad_perm [1, 0, 3, 2]
+    v = dpp_add(v, std::integral_constant<int, 0x4E>{});              // quad_perm [2, 3, 0, 1]
+    if ((tid & 3) == 0) tr[i][tid >> 2] = v;
+  }
   __syncthreads();
   double part = 0.0;
   if (tid < LM_NACC * SEG) {
