@@ -376,6 +376,44 @@ __host__ __device__ inline void lm_step(LmState& S, const double* red) {
 // Keeping the trust-region logic out of the evaluation kernel keeps its register budget (and
 // occupancy) that of the residual arithmetic alone.
 // ---------------------------------------------------------------------------------------
+// Block sum of LM_NACC per-thread accumulators -> sum[0 .. LM_NACC) (LDS, valid after the
+// trailing barrier; all kThreads threads call it).  The four lanes of each quad combine in
+// registers first (DPP quad permutes: lane pairs, then pairs of pairs), a quarter of the rows go
+// through an LDS transpose, thread 8a + q sums segment q of accumulator a in row order, and the
+// 8 segment sums combine in a fixed butterfly: a fixed summation order.  (29 wave butterflies
+// of 6 dependent fp64 shuffles took ~15k cycles per 256-thread block, this ~3k.)
+template <int kThreads>
+__device__ inline void lm_block_sum(const double* acc, double* sum) {
+  static_assert(kThreads % 64 == 0 && LM_NACC * 8 <= kThreads, "transpose reduction layout");
+  constexpr int SEG = 8, ROWS = kThreads / 4, PER = ROWS / SEG;
+  __shared__ double tr[LM_NACC][ROWS + 1];
+  const int tid = threadIdx.x;
+  auto dpp_add = [](double v, auto ctrl) {
+    const uint64_t u = __double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, decltype(ctrl)::value, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), decltype(ctrl)::value, 0xF, 0xF, false);
+    return v + __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+  };
+#pragma unroll
+  for (int i = 0; i < LM_NACC; ++i) {
+    double v = dpp_add(acc[i], std::integral_constant<int, 0xB1>{});  // quad_perm [1, 0, 3, 2]
+    v = dpp_add(v, std::integral_constant<int, 0x4E>{});              // quad_perm [2, 3, 0, 1]
+    if ((tid & 3) == 0) tr[i][tid >> 2] = v;
+  }
+  __syncthreads();
+  double part = 0.0;
+  if (tid < LM_NACC * SEG) {
+    const int a = tid / SEG, q = tid % SEG;
+#pragma unroll 8
+    for (int k = 0; k < PER; ++k) part += tr[a][q * PER + k];
+  }
+  part += __shfl_xor(part, 4, 64);
+  part += __shfl_xor(part, 2, 64);
+  part += __shfl_xor(part, 1, 64);
+  if (tid < LM_NACC * SEG && (tid % SEG) == 0) sum[tid / SEG] = part;
+  __syncthreads();
+}
+
 struct LmRecView {
   const int* type;
   const float *px, *py, *pz;
@@ -434,39 +472,7 @@ __device__ inline void lm_eval_sum(const LmRecView& R, int nrec, const double* X
     tp1 = __builtin_readcyclecounter();
     if (tid == 0) atomicAdd(&prof[0], tp1 - tp0);
   }
-  // block sum of the 29 accumulators through an LDS transpose: every thread stores its row,
-  // then thread 8a + q sums the 32 values of segment q of accumulator a in thread order and
-  // the 8 segment sums combine in a fixed butterfly (29 wave butterflies of 6 dependent
-  // shuffles each took ~15k cycles per block, the transpose ~2k)
-  static_assert(kThreads % 64 == 0 && LM_NACC * 8 <= kThreads, "transpose reduction layout");
-  // first the four lanes of each quad combine in registers (DPP quad permutes: lane pairs, then
-  // pairs of pairs), so a quarter of the rows go through LDS
-  constexpr int SEG = 8, ROWS = kThreads / 4, PER = ROWS / SEG;
-  __shared__ double tr[LM_NACC][ROWS + 1];
-  auto dpp_add = [](double v, auto ctrl) {
-    const uint64_t u = __double_as_longlong(v);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, decltype(ctrl)::value, 0xF, 0xF, false);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), decltype(ctrl)::value, 0xF, 0xF, false);
-    return v + __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-  };
-#pragma unroll
-  for (int i = 0; i < LM_NACC; ++i) {
-    double v = dpp_add(acc[i], std::integral_constant<int, 0xB1>{});  // quad_perm [1, 0, 3, 2]
-    v = dpp_add(v, std::integral_constant<int, 0x4E>{});              // quad_perm [2, 3, 0, 1]
-    if ((tid & 3) == 0) tr[i][tid >> 2] = v;
-  }
-  __syncthreads();
-  double part = 0.0;
-  if (tid < LM_NACC * SEG) {
-    const int a = tid / SEG, q = tid % SEG;
-#pragma unroll 8
-    for (int k = 0; k < PER; ++k) part += tr[a][q * PER + k];
-  }
-  part += __shfl_xor(part, 4, 64);
-  part += __shfl_xor(part, 2, 64);
-  part += __shfl_xor(part, 1, 64);
-  if (tid < LM_NACC * SEG && (tid % SEG) == 0) sum[tid / SEG] = part;
-  __syncthreads();
+  lm_block_sum<kThreads>(acc, sum);
   if (prof && tid == 0) atomicAdd(&prof[1], __builtin_readcyclecounter() - tp1);
 }
 

@@ -157,7 +157,6 @@ __device__ inline void vo_accum(int type, const double* rec, const VoRot& V, con
 __global__ void __launch_bounds__(VO_THREADS) k_vo_solve(const double* factors, const int* off, double* xs,
                                                           int max_iter, LmState* states) {
   __shared__ LmState S;
-  __shared__ double red[VO_THREADS / 64][LM_NACC];
   __shared__ double sum[LM_NACC];
   __shared__ double X[7];
   const int p = blockIdx.x, tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
@@ -183,17 +182,7 @@ __global__ void __launch_bounds__(VO_THREADS) k_vo_solve(const double* factors, 
       const int type = (int)rec[0];
       if (type == 4 || type == 5) vo_accum(type, rec, V, x, acc);
     }
-    for (int i = 0; i < LM_NACC; ++i) {
-      const double v = wave_sum_d(acc[i]);
-      if (lane == 0) red[wid][i] = v;
-    }
-    __syncthreads();
-    if (tid < LM_NACC) {
-      double v = 0.0;
-      for (int w = 0; w < VO_THREADS / 64; ++w) v += red[w][tid];
-      sum[tid] = v;
-    }
-    __syncthreads();
+    lm_block_sum<VO_THREADS>(acc, sum);
     if (tid == 0) {
       LmState L = S;
       lm_step(L, sum);
