@@ -11,12 +11,20 @@ from loam_amd.scanreg import ScanRegistration  # noqa: E402
 
 sr = ScanRegistration()
 frames = [synth.frame(1, f, 2000)[0] for f in range(20)]
-for xyz in frames[:3]:
-    sr.input(xyz)
+device = len(sys.argv) > 1 and sys.argv[1] == "device"  # inputs resident in HBM (input_device)
+if device:
+    import torch
+    dframes = [torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in frames]
+    feed = lambda k: sr.input_device(dframes[k].data_ptr(), len(frames[k]), 3)
+else:
+    feed = lambda k: sr.input(frames[k])
+for k in range(3):
+    feed(k)
 sr.debug_counters(reset=True)
 ms = []
-for xyz in frames:
-    sr.input(xyz)
+for k in range(len(frames)):
+    feed(k)
+    sr.counts()  # completes the frame
     ms.append(sr.ms)
 c = sr.debug_counters()
 rings = 64 * len(frames)

@@ -67,6 +67,7 @@ struct SrDev {
   int* ring_of;          // [cap] scanID per raw point (-1 dropped)
   int* blk_hist;         // [SR_MAX_RINGS][nblocks]
   int* blk_off;          // [SR_MAX_RINGS][nblocks]
+  int* blk_aux;          // [3][nblocks]: per block first / last valid index, first latch index
   float4* cloud;         // [cap] laserCloud
   float* curv;           // [cap]
   int* sort_ind;         // [cap] debug: label per point
@@ -107,18 +108,35 @@ __device__ inline int sr_scan_id(float x, float y, float z, int n_scans) {
   return scanID;
 }
 
-__global__ void k_sr_valid(SrDev D) {
+// one point per thread; every block leaves its first / last valid index in blk_aux (one
+// contended device-scope atomic per block or wave cost ~100 us per frame)
+__global__ void __launch_bounds__(SR_BLOCK) k_sr_valid(SrDev D, int nblocks) {
+  __shared__ int wf[SR_BLOCK / 64], wl[SR_BLOCK / 64];
   SrFrame& F = *D.fr;
   const float thr2 = D.min_range * D.min_range;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < F.n_in; i += gridDim.x * blockDim.x) {
+  const int i = blockIdx.x * SR_BLOCK + threadIdx.x, w = threadIdx.x >> 6;
+  bool ok = false;
+  if (i < F.n_in) {
     const float x = D.xyz[(size_t)i * D.stride], y = D.xyz[(size_t)i * D.stride + 1],
                 z = D.xyz[(size_t)i * D.stride + 2];
-    const bool ok = isfinite(x) && isfinite(y) && isfinite(z) && !(x * x + y * y + z * z < thr2);
+    ok = isfinite(x) && isfinite(y) && isfinite(z) && !(x * x + y * y + z * z < thr2);
     D.ring_of[i] = ok ? 0 : -2;  // -2: removed before the ring rule
-    if (ok) {
-      atomicMin(&F.first, i);
-      atomicMax(&F.last, i);
+  }
+  const uint64_t b = __ballot(ok);
+  const int i0 = i - (threadIdx.x & 63);
+  if ((threadIdx.x & 63) == 0) {
+    wf[w] = b ? i0 + __ffsll((unsigned long long)b) - 1 : 0x7FFFFFFF;
+    wl[w] = b ? i0 + 63 - __clzll((unsigned long long)b) : -1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int f = 0x7FFFFFFF, l = -1;
+    for (int k = 0; k < SR_BLOCK / 64; ++k) {
+      f = min(f, wf[k]);
+      l = max(l, wl[k]);
     }
+    D.blk_aux[blockIdx.x] = f;
+    D.blk_aux[nblocks + blockIdx.x] = l;
   }
 }
 
@@ -135,6 +153,7 @@ __global__ void __launch_bounds__(SR_BLOCK) k_sr_ring(SrDev D, int nblocks) {
   for (int r = threadIdx.x; r < SR_MAX_RINGS; r += SR_BLOCK) hist[r] = 0;
   __syncthreads();
   const int i = blockIdx.x * SR_BLOCK + threadIdx.x;
+  bool past = false;  // past the halfPassed latch candidate
   if (i < F.n_in && D.ring_of[i] == 0) {
     const float x = D.xyz[(size_t)i * D.stride], y = D.xyz[(size_t)i * D.stride + 1],
                 z = D.xyz[(size_t)i * D.stride + 2];
@@ -143,16 +162,50 @@ __global__ void __launch_bounds__(SR_BLOCK) k_sr_ring(SrDev D, int nblocks) {
     if (sid >= 0) {
       atomicAdd(&hist[sid], 1);
       const float ori = sr_ori_branch1(-glibc_atan2f(y, x), F.start_ori);
-      if (ori - F.start_ori > M_PI) atomicMin(&F.latch, i);
+      past = ori - F.start_ori > M_PI;
     }
   }
+  // the latch is the lowest such index: per block (lanes hold consecutive indices), reduced
+  // over the blocks in k_sr_ring_scan
+  __shared__ int wlat[SR_BLOCK / 64];
+  const uint64_t pb = __ballot(past);
+  if ((threadIdx.x & 63) == 0)
+    wlat[threadIdx.x >> 6] = pb ? i - (threadIdx.x & 63) + __ffsll((unsigned long long)pb) - 1 : 0x7FFFFFFF;
   __syncthreads();
+  if (threadIdx.x == 0) {
+    int lt = 0x7FFFFFFF;
+    for (int k = 0; k < SR_BLOCK / 64; ++k) lt = min(lt, wlat[k]);
+    D.blk_aux[2 * nblocks + blockIdx.x] = lt;
+  }
   for (int r = threadIdx.x; r < SR_MAX_RINGS; r += SR_BLOCK) D.blk_hist[r * nblocks + blockIdx.x] = hist[r];
 }
 
-__global__ void k_sr_oris(SrDev D) {
-  // startOri / endOri (scan_registration.cpp:185-197)
+__global__ void __launch_bounds__(1024) k_sr_oris(SrDev D, int nblocks) {
+  __shared__ int wf[16], wl[16];
   SrFrame& F = *D.fr;
+  int f = 0x7FFFFFFF, l = -1;
+  for (int k = threadIdx.x; k < nblocks; k += 1024) {
+    f = min(f, D.blk_aux[k]);
+    l = max(l, D.blk_aux[nblocks + k]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    f = min(f, __shfl_xor(f, o, 64));
+    l = max(l, __shfl_xor(l, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    wf[threadIdx.x >> 6] = f;
+    wl[threadIdx.x >> 6] = l;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  for (int k = 0; k < 16; ++k) {
+    f = min(f, wf[k]);
+    l = max(l, wl[k]);
+  }
+  F.first = f;
+  F.last = l;
+  // startOri / endOri (scan_registration.cpp:185-197)
   if (F.first > F.last) return;
   const float* p0 = D.xyz + (size_t)F.first * D.stride;
   const float* p1 = D.xyz + (size_t)F.last * D.stride;
@@ -172,34 +225,67 @@ __global__ void __launch_bounds__(1024) k_sr_ring_scan(SrDev D, int nblocks) {
   const int total = SR_MAX_RINGS * nblocks;
   const int per = (total + 1023) / 1024;
   const int b0 = threadIdx.x * per;
-  uint32_t sum = 0;
-  for (int k = 0; k < per; ++k)
-    if (b0 + k < total) sum += D.blk_hist[b0 + k];
-  uint32_t tot;
-  uint32_t pre = vx_block_scan(sum, ws, &tot);
-  for (int k = 0; k < per; ++k) {
-    int e = b0 + k;
-    if (e < total) {
-      D.blk_off[e] = pre;
-      pre += D.blk_hist[e];
+  {  // the halfPassed latch: the lowest of the blocks' first indices past startOri + pi
+    int lt = 0x7FFFFFFF;
+    for (int k = threadIdx.x; k < nblocks; k += 1024) lt = min(lt, D.blk_aux[2 * nblocks + k]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) lt = min(lt, __shfl_xor(lt, o, 64));
+    if ((threadIdx.x & 63) == 0 && lt != 0x7FFFFFFF) atomicMin(&F.latch, lt);
+  }
+  // exclusive scan of the flattened [ring][block] histogram: wave w owns a contiguous chunk and
+  // reads it 64 consecutive entries at a time (coalesced), wave totals -> chunk offsets -> the
+  // scan; a ring starts at the prefix of its block 0
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int chunk = ((total + 16 * 256 - 1) / (16 * 256)) * 256;
+  const int c0 = wid * chunk, c1 = min(total, c0 + chunk);
+  uint32_t wsum = 0;
+  for (int e0 = c0; e0 < c1; e0 += 256) {  // four loads in flight
+    uint32_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = e0 + 64 * j + lane;
+      v[j] = e < c1 ? (uint32_t)D.blk_hist[e] : 0u;
+    }
+    wsum += v[0] + v[1] + v[2] + v[3];
+  }
+  wsum = wave_sum_u(wsum);
+  if (lane == 0) ws[wid] = wsum;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t v = ws[k];
+    base += k < wid ? v : 0u;
+    tot += v;
+  }
+  for (int e0 = c0; e0 < c1; e0 += 256) {
+    uint32_t vv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = e0 + 64 * j + lane;
+      vv[j] = e < c1 ? (uint32_t)D.blk_hist[e] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = e0 + 64 * j + lane;
+      const uint32_t v = vv[j];
+      const uint32_t inc = wave_incl_scan_u(v);
+      const uint32_t pre = base + inc - v;
+      if (e < c1) {
+        D.blk_off[e] = (int)pre;
+        if (e % nblocks == 0) ring_tot[e / nblocks] = (int)pre;
+      }
+      base += __shfl(inc, 63, 64);
     }
   }
+  (void)per;
+  (void)b0;
   __syncthreads();
-  if (threadIdx.x < SR_MAX_RINGS) {
-    int r = threadIdx.x, c = 0;
-    for (int b = 0; b < nblocks; ++b) c += D.blk_hist[r * nblocks + b];
-    ring_tot[r] = c;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int r = 0; r < SR_MAX_RINGS; ++r) {
-      F.ring_off[r] = acc;
-      F.ring_cnt[r] = ring_tot[r];
-      acc += ring_tot[r];
-    }
-    F.ring_off[SR_MAX_RINGS] = acc;
-    F.n_cloud = acc;
+  if (threadIdx.x <= SR_MAX_RINGS) {
+    const int r = threadIdx.x;
+    const int start = r < SR_MAX_RINGS ? ring_tot[r] : (int)tot;
+    F.ring_off[r] = start;
+    if (r < SR_MAX_RINGS) F.ring_cnt[r] = (r + 1 < SR_MAX_RINGS ? ring_tot[r + 1] : (int)tot) - start;
+    if (r == SR_MAX_RINGS) F.n_cloud = (int)tot;
   }
 }
 
@@ -716,6 +802,7 @@ int32_t loam_scanreg_create(const loam_params* p, int32_t device, loam_scanreg**
   SRA(D.ring_of, cap);
   SRA(D.blk_hist, (size_t)SR_MAX_RINGS * nblocks);
   SRA(D.blk_off, (size_t)SR_MAX_RINGS * nblocks);
+  SRA(D.blk_aux, (size_t)3 * nblocks);
   SRA(D.cloud, cap);
   SRA(D.curv, cap);
   SRA(D.label, cap);
@@ -785,8 +872,8 @@ static int32_t sr_launch(loam_scanreg* h, const float* xyz, int32_t n, int32_t s
   LOAM_HIP(hipMemcpyAsync(D.fr, &f, sizeof(SrFrame), hipMemcpyHostToDevice, st));
   const int nblocks = std::max(1, (n + SR_BLOCK - 1) / SR_BLOCK);
   if (n > 0) {
-    k_sr_valid<<<std::min(nblocks, 1024), SR_BLOCK, 0, st>>>(D);
-    k_sr_oris<<<1, 1, 0, st>>>(D);
+    k_sr_valid<<<nblocks, SR_BLOCK, 0, st>>>(D, nblocks);
+    k_sr_oris<<<1, 1024, 0, st>>>(D, nblocks);
     k_sr_ring<<<nblocks, SR_BLOCK, 0, st>>>(D, nblocks);
     k_sr_ring_scan<<<1, 1024, 0, st>>>(D, nblocks);
     k_sr_scatter<<<nblocks, SR_BLOCK, 0, st>>>(D, nblocks);
