@@ -64,6 +64,7 @@ struct OdomFrame {
 };
 
 struct OdomDev {
+  int* corr_part;  // [B][2 rounds][OD_QBLK_MAX][2] per-workgroup correspondence counts of k_od_corr
   int B, cap;
   OdomFrame* fr;
   float4* stage[4];    // [B][cap] host-input staging
@@ -422,24 +423,42 @@ __global__ void __launch_bounds__(OD_QTHREADS) k_od_corr(OdomDev D, int round, i
       }
     }
   }
+  // the workgroup's counts go to its own slot (k_od_lm adds the slots): thousands of atomics on
+  // the stream's two counters serialise in the memory system
+  __shared__ uint32_t wsum[OD_QWAVES][2];
   uint32_t we = n_edge, wp = n_plane;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     we += __shfl_xor(we, o, 64);
     wp += __shfl_xor(wp, o, 64);
   }
-  if ((threadIdx.x & 63) == 0) {
-    if (we) atomicAdd(&F.corr[round * 2], (int)we);
-    if (wp) atomicAdd(&F.corr[round * 2 + 1], (int)wp);
+  if (lane == 0) {
+    wsum[wid][0] = we;
+    wsum[wid][1] = wp;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    uint32_t t = 0;
+    for (int w = 0; w < OD_QWAVES; ++w) t += wsum[w][threadIdx.x];
+    D.corr_part[(((size_t)s * 2 + round) * OD_QBLK_MAX + blk) * 2 + threadIdx.x] = (int)t;
   }
 }
 
-__global__ void __launch_bounds__(OD_LM_THREADS) k_od_lm(OdomDev D, int round, int G) {
+__global__ void __launch_bounds__(OD_LM_THREADS) k_od_lm(OdomDev D, int round, int G, int qblk) {
   // block b -> stream b % Bp, member b / Bp: a stream's blocks share an XCD (lm.h lm_padded)
   const int Bp = lm_padded(D.B), s = blockIdx.x % Bp, g = blockIdx.x / Bp;
   if (s >= D.B) return;
   OdomFrame& F = D.fr[s];
   if (!F.active || !F.inited) return;
+  if (g == 0 && threadIdx.x < 64) {  // the round's correspondence counts (k_od_corr slots)
+    const int c = threadIdx.x & 1;
+    uint32_t t = 0;
+    for (int b = threadIdx.x >> 1; b < qblk; b += 32)
+      t += (uint32_t)D.corr_part[(((size_t)s * 2 + round) * OD_QBLK_MAX + b) * 2 + c];
+#pragma unroll
+    for (int o = 2; o < 64; o <<= 1) t += __shfl_xor(t, o, 64);
+    if (threadIdx.x < 2) F.corr[round * 2 + c] = (int)t;
+  }
   const size_t rb = (size_t)s * OD_MAXQ;
   LmJob J;
   J.S = &F.lm[round];
@@ -563,6 +582,7 @@ int32_t loam_odometry_create(const loam_params* p, int32_t device, int32_t n_str
     OA(D.r_b[k], B * (size_t)OD_MAXQ);
   }
   OA(D.partials, B * (size_t)OD_PBLK * LM_NACC);
+  OA(D.corr_part, B * 2 * (size_t)OD_QBLK_MAX * 2);
   OA(D.lm_sync, B * 2 * LM_SYNC_WORDS);
   OA(D.lm_xpub, B * 2 * 8);
 #undef OA
@@ -690,7 +710,7 @@ int32_t loam_odometry_solve(loam_odometry* h) {
     const int qblk = std::min(OD_QBLK_MAX, (maxq + OD_QWAVES - 1) / OD_QWAVES);
     for (int round = 0; round < 2; ++round) {
       k_od_corr<<<B * qblk, OD_QTHREADS, 0, st>>>(D, round, qblk);
-      k_od_lm<<<lm_padded(B) * h->G, OD_LM_THREADS, 0, st>>>(D, round, h->G);
+      k_od_lm<<<lm_padded(B) * h->G, OD_LM_THREADS, 0, st>>>(D, round, h->G, qblk);
     }
   }
   k_od_build<<<B * 2, OD_BUILD_THREADS, 0, st>>>(D);
