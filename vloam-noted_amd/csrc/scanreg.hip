@@ -657,7 +657,7 @@ __global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(SrDev D) {
 
 // PCL VoxelGrid of one ring's lessFlat candidates in PCL's summation order (voxel_pcl.h): the
 // std::sort emulation in LDS up to SRV_LDS points, else in the global scratch
-constexpr int SRV_THREADS = 512;
+constexpr int SRV_THREADS = 1024;
 constexpr int SRV_LDS = 4096;
 constexpr int SRV_SEG = SR_RING_CAP / 17 + 2;  // level list (<= n / 17 + 1 segments per level)
 
