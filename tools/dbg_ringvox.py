@@ -9,11 +9,13 @@ import numpy as np  # noqa: E402
 from loam_amd import synth  # noqa: E402
 from loam_amd.scanreg import ScanRegistration  # noqa: E402
 
+device = len(sys.argv) > 1 and sys.argv[1] == "device"  # inputs resident in HBM (input_device)
+if device:  # torch's HIP runtime initialises before the library's
+    import torch
+    torch.cuda.init()
 sr = ScanRegistration()
 frames = [synth.frame(1, f, 2000)[0] for f in range(20)]
-device = len(sys.argv) > 1 and sys.argv[1] == "device"  # inputs resident in HBM (input_device)
 if device:
-    import torch
     dframes = [torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in frames]
     feed = lambda k: sr.input_device(dframes[k].data_ptr(), len(frames[k]), 3)
 else:
