@@ -1,4 +1,4 @@
 #!/bin/bash
 cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
-timeout -k 10 300 python -u tools/dbg_revox.py > gpurun_out/dbg_revox.log 2>&1
+LOAM_STACK_K=0 timeout -k 10 300 python -u tools/dbg_revox.py > gpurun_out/dbg_revox.log 2>&1
