@@ -435,6 +435,7 @@ def pipeline_stage(seed, device, n_frames=160, timed=80, n_az=2000):
     # pcl::PointXYZ layout (x, y, z, pad): 16 B per point like the reference's input cloud
     scans = [np.ascontiguousarray(np.concatenate([c, np.zeros((len(c), 1), np.float32)], axis=1)) for c in scans]
     out = {}
+    poses = {"sequential": [], "overlapped": []}
     for mode in ("sequential", "overlapped"):
         sr, od, mp = ScanRegistration(device=device), BatchOdometry(1, device=device), BatchMapper(1, device=device)
         t0 = None
@@ -456,12 +457,88 @@ def pipeline_stage(seed, device, n_frames=160, timed=80, n_az=2000):
             if mode == "overlapped" and f + 1 < n_frames:
                 sr.input_async(scans[f + 1])
             mp.solve()
+            poses[mode].append(mp.pose(0))
         dt = time.perf_counter() - t0
         out[mode] = {"ms_per_frame": round(1e3 * dt / timed, 4), "frames_per_s": round(timed / dt, 1)}
         for h in (sr, od, mp):
             h.close()
+    pl = pipelined_chain(scans, device, n_frames, timed)
+    same = all(np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+               for a, b in zip(pl.pop("poses"), poses["sequential"]))
+    out["pipelined"] = {**pl, "poses_identical_to_sequential": bool(same)}
     out["frames"] = f"{timed} timed after {n_frames - timed}, {n_az} azimuths x 64 rings, one stream"
     return out
+
+
+def pipelined_chain(scans, device, n_frames, timed):
+    """The same chain as a three-stage frame pipeline, the way the reference's ROS nodes run
+    (scanRegistration / laserOdometry / laserMapping as concurrent nodes): frame f + 1's scan
+    registration (queued asynchronously) and frame f's odometry on one host thread, frame
+    f - 1's mapping solve on another; the three handles' HIP streams overlap on the GPU.  Each
+    stage's input is copied (device to device, on a non-blocking stream) out of the producing
+    handle's buffers, which its next frame rewrites, into a two-deep ring.  Every frame's inputs and results are those of the
+    sequential chain; only the order in time changes.  Returns ms per frame over the last
+    `timed` frames and the mapping poses (checked against the sequential chain by the caller)."""
+    import ctypes
+
+    import torch
+
+    from loam_amd.mapping import BatchMapper
+    from loam_amd.odometry import BatchOdometry
+    from loam_amd.scanreg import ScanRegistration
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+    cap = 1 << 19  # points per ring slot and cloud
+    ring = torch.empty((2, 2, cap, 4), dtype=torch.float32, device=f"cuda:{device}")
+    feat = torch.empty((2, 4, cap, 4), dtype=torch.float32, device=f"cuda:{device}")
+    cs = torch.cuda.Stream(device=device)
+    sr, od, mp = ScanRegistration(device=device), BatchOdometry(1, device=device), BatchMapper(1, device=device)
+
+    def stash(dst, src):  # device-to-device copy of one cloud into a ring slot
+        p, n = src
+        assert n <= cap, n
+        if n:
+            rc = hip.hipMemcpyAsync(dst.data_ptr(), p, 16 * n, 3, cs.cuda_stream)
+            assert rc == 0, rc
+        return dst.data_ptr(), n
+
+    def front(f):  # odometry of frame f; scan registration of f + 1 queued beside it
+        sr.wait()
+        feats = [stash(feat[f % 2, w - 1], sr.device_ptr(w)) for w in (1, 2, 3, 4)]
+        cs.synchronize()
+        if f + 1 < n_frames:
+            sr.input_async(scans[f + 1])
+        ptrs, counts = zip(*feats)
+        od.input_device(0, ptrs, counts)
+        od.solve()
+        q, t, _, _, _ = od.output(0)
+        clouds = [stash(ring[f % 2, w], od.last_cloud_device(0, w)) for w in (0, 1)]
+        cs.synchronize()
+        return clouds, q, t
+
+    def back(job):  # mapping of the frame front() returned
+        (pc, nc), (ps, ns) = job[0]
+        mp.input_device(0, pc, nc, ps, ns, job[1], job[2])
+        mp.solve()
+        return mp.pose(0)
+
+    poses = []
+    sr.input_async(scans[0])
+    with ThreadPoolExecutor(max_workers=1) as ex:
+        prev = front(0)
+        t0 = None
+        for f in range(1, n_frames):  # the last `timed` of these iterations are timed
+            if f == n_frames - timed:
+                t0 = time.perf_counter()
+            fut = ex.submit(back, prev)
+            prev = front(f)
+            poses.append(fut.result())
+        dt = time.perf_counter() - t0
+        poses.append(back(prev))
+    for h in (sr, od, mp):
+        h.close()
+    return {"ms_per_frame": round(1e3 * dt / timed, 4), "frames_per_s": round(timed / dt, 1),
+            "poses": poses}
 
 
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r2_pmc_traffic.json")
