@@ -85,3 +85,39 @@ def test_cxx_shim_frames(tmp_path):
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "frame 3" in r.stdout
+
+
+def test_pipelined_chain_matches_sequential():
+    """bench.pipelined_chain (scan registration f + 1 | odometry f | mapping f - 1 on two host
+    threads, inputs copied into device rings) gives every mapping pose of the sequential chain
+    bit for bit"""
+    import sys
+
+    from conftest import ROOT
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+
+    seed, n_frames = 23, 10
+    scans = []
+    for f in range(n_frames):
+        xyz, _ = synth.frame(seed, f)
+        scans.append(np.ascontiguousarray(np.concatenate([xyz, np.zeros((len(xyz), 1), np.float32)], axis=1)))
+    sr, od, mp = ScanRegistration(), BatchOdometry(1), BatchMapper(1)
+    ref = []
+    for f in range(n_frames):
+        sr.input(scans[f])
+        ptrs, counts = zip(*(sr.device_ptr(w) for w in (1, 2, 3, 4)))
+        od.input_device(0, ptrs, counts)
+        od.solve()
+        q, t, _, _, _ = od.output(0)
+        (pc, nc), (ps, ns) = od.last_cloud_device(0, 0), od.last_cloud_device(0, 1)
+        mp.input_device(0, pc, nc, ps, ns, q, t)
+        mp.solve()
+        ref.append(mp.pose(0))
+    for h in (sr, od, mp):
+        h.close()
+    out = bench.pipelined_chain(scans, 0, n_frames, 4)
+    assert len(out["poses"]) == n_frames
+    for f, ((q, t), (qr, tr)) in enumerate(zip(out["poses"], ref)):
+        assert np.array_equal(q, qr) and np.array_equal(t, tr), f
