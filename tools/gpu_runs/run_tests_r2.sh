@@ -1,6 +1,5 @@
 #!/bin/bash
-# all GPU tests (no -x: every failure listed), each test under its own time limit
+# every GPU test, one process, each test time-limited
 cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
-timeout -k 10 1100 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider ${TEST_ARGS} > gpurun_out/gpu_tests.log 2>&1
-echo "pytest rc $?" >> gpurun_out/gpu_tests.log
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
