@@ -862,7 +862,14 @@ def main():
         if not args.no_depth and world == 1:
             stages["depth_association"] = depth_stage(args.seed, local, with_cpu=not args.no_cpu)
             stages["vo_solve"] = vo_stage(args.seed, local, with_cpu=not args.no_cpu)
-            stages["pipeline_one_stream"] = pipeline_stage(args.seed, local)
+            stages["pipeline_one_stream"] = pl = pipeline_stage(args.seed, local)
+            if cpu_st is not None:  # the oracle's three stages back to back, one core
+                c = (cpu_st["scan_registration"] + cpu_st["odometry"]) / K + cpu["ms_per_frame"]
+                pl["cpu_ms_per_frame"] = round(c, 3)
+                pl["cpu_sample"] = ("oracle scan registration + odometry + mapping per frame, one core, on the "
+                                    "cpu_baseline frames (same sequence shape, steady-state map)")
+                for mode in ("sequential", "overlapped", "pipelined"):
+                    pl[mode]["speedup_vs_cpu"] = round(c / pl[mode]["ms_per_frame"], 2)
         out["stages"] = stages
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(out["value"] / cpu["value"], 2)
