@@ -1,5 +1,7 @@
 """exact-mode phase counters: one mapping stream over a synthetic sequence (device-side
 voxel_grid_pcl phase cycles of the stack [42..45] and cube [11..14] filters)"""
+import os
+os.environ.setdefault("LOAM_PHASE_COUNTERS", "1")  # the handles below count phase cycles
 import sys, time
 import numpy as np
 sys.path[:0] = ['vloam-noted_amd', 'oracle', 'tests']

@@ -1,6 +1,7 @@
 """LM round phase cycles of a one-stream mapper (debug counters 15, 17..23) over 40 frames
 after 120 map-building frames of the synthetic street (GPU scan registration + odometry)."""
 import os
+os.environ.setdefault("LOAM_PHASE_COUNTERS", "1")  # the handles below count phase cycles
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

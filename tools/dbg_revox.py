@@ -2,6 +2,7 @@
 frames after 120 map-building frames of the synthetic street (GPU scan registration +
 odometry)."""
 import os
+os.environ.setdefault("LOAM_PHASE_COUNTERS", "1")  # the handles below count phase cycles
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

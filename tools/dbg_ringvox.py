@@ -1,5 +1,6 @@
 """Phase cycles of the per-ring PCL-order VoxelGrid (k_sr_ringvox) over 20 frames."""
 import os
+os.environ.setdefault("LOAM_PHASE_COUNTERS", "1")  # the handles below count phase cycles
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

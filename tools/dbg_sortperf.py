@@ -1,4 +1,6 @@
 """k_sort_perm timing (std::sort emulation alone) for several sizes / key spreads"""
+import os
+os.environ.setdefault("LOAM_PHASE_COUNTERS", "1")  # the handles below count phase cycles
 import sys, time
 import numpy as np
 import os; R = os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys.path[:0] = [os.path.join(R, 'vloam-noted_amd'), os.path.join(R, 'oracle')]

@@ -1,5 +1,6 @@
 """Diagnostic: repeat GPU ScanRegistration on one frame and compare counts with the oracle."""
 import os
+os.environ.setdefault("LOAM_PHASE_COUNTERS", "1")  # the handles below count phase cycles
 import sys
 
 import numpy as np
