@@ -45,8 +45,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "vloam-noted_amd"))
 
-HBM_PEAK_GBS = 8000.0
-SHARD_LEG_LIMIT_S = 240.0  # watchdog of the sharded leg (its RCCL collectives are the only exchange)  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+SHARD_LEG_LIMIT_S = 240.0  # watchdog of the sharded leg (its RCCL collectives are the only exchange)
 
 
 def parse():
@@ -883,10 +883,14 @@ def main():
         import threading
 
         def on_timeout():
+            # a hung collective is a failure: the line is printed (the headline stands, the
+            # sharded leg carries the error) and every rank exits non-zero
             if rank == 0:
                 out["sharded"] = {"error": f"sharded leg did not finish within {SHARD_LEG_LIMIT_S} s"}
                 print(json.dumps(out), flush=True)
-            os._exit(0)
+            sys.stderr.write(f"bench.py: sharded leg hung (> {SHARD_LEG_LIMIT_S} s), exiting 3\n")
+            sys.stderr.flush()
+            os._exit(3)
 
         dog = threading.Timer(SHARD_LEG_LIMIT_S, on_timeout)
         dog.daemon = True

@@ -126,7 +126,8 @@ int32_t loam_scanreg_curvature(loam_scanreg* h, float* curv, int32_t* label, int
 double loam_scanreg_ms(loam_scanreg* h);
 /* cumulative device cycle counters of the per-ring PCL-order VoxelGrid (k_sr_ringvox), summed
  * over rings and frames: [0] bounding box + keys, [1] sort levels, [2] final sort pass,
- * [3] centroids; reset = 1 zeroes them after the copy */
+ * [3] centroids; reset = 1 zeroes them after the copy.  Counted only in a handle created with
+ * LOAM_PHASE_COUNTERS=1 in the environment. */
 #define LOAM_SR_DEBUG_COUNTERS 8
 int32_t loam_scanreg_debug_counters(loam_scanreg* h, uint64_t* out, int32_t n, int32_t reset);
 
@@ -225,8 +226,11 @@ int32_t loam_mapper_stats(loam_mapper* h, int32_t stream, loam_map_stats* st);
  * [32..39] their cycles (filter + index), [40] sharded: pose values that differed from rank 0's
  * after the LM (0 when the all-reduce is bit-identical on every rank), [41] arena compactions
  * ((stream, map) pairs), [42..45] stack VoxelGrid cycles: bounding box, hash, sort + scan,
- * member lists + centroids, [46..47] of the latter: member lists, per-voxel sort + sums */
-#define LOAM_DEBUG_COUNTERS 48
+ * member lists + centroids, [46..47] of the latter: member lists, per-voxel sort + sums,
+ * [48..49] arena compactions of the corner / surf maps (summed over streams).
+ * The cycle counters (all but [40], [41], [48], [49]) run only in a handle created with the
+ * environment variable LOAM_PHASE_COUNTERS=1 (they cost atomics in the kernels); else they stay 0. */
+#define LOAM_DEBUG_COUNTERS 50
 int32_t loam_mapper_debug_counters(loam_mapper* h, uint64_t* out, int32_t n, int32_t reset);
 /* sum over the streams solved by the last loam_mapper_solve of their LM iterations (both rounds) */
 int64_t loam_mapper_total_iterations(loam_mapper* h);

@@ -82,6 +82,16 @@ def test_scanreg_long_tied_sectors(n_az):
     assert sizes.max() > 6 * (1024 if n_az == 5000 else 512)
 
 
+def test_scanreg_many_long_tied_rings():
+    """7000 azimuths, 1 cm quantization: every ring's sectors exceed 1024 points, so all rings'
+    workgroups run the long-sector path (block bitonic, then the tie re-sort with its level
+    lists in global memory) at the same time; each ring has its own list area"""
+    xyz, _ = synth.frame(6, 9, 7000, flags=synth.QUANTIZE)
+    ref = _check_frame(xyz, ScanRegistration(max_input_points=480000))
+    ids = np.floor(ref.cloud(0)[:, 3]).astype(int)
+    assert (np.bincount(ids) > 6 * 1024 + 11).sum() >= 20
+
+
 def test_scanreg_stride_and_nan():
     """(n, 4) input with NaN rows and points inside minimum_range (removeNaN + removeClosed)"""
     xyz, _ = synth.frame(4, 3)

@@ -8,9 +8,11 @@ One oracle pipeline run (scan registration -> odometry -> mapping, seed 11, 392 
     correspondence counts and LM iterations identical, the updated map within 1e-5 m;
   - the first recentering frame after 380 (grid shift, wrapped slabs cleared), teacher-forced;
   - a free-running GPU pipeline (HIP scan registration -> HIP odometry -> HIP mapping on the raw
-    scans) over 300 frames against the oracle trajectory: per-scan pose deltas and RMSE.
-The oracle sums VoxelGrid voxels in PCL's order, the mapper's kernels in input order (their
-stacks and cubes differ within the summation-order bound): the pose bar holds.
+    scans) over 300 frames against the oracle trajectory, in both VoxelGrid summation orders:
+    exact_voxel_order = 1 against the oracle in PCL's order, the default input order against the
+    oracle in input order (oracle_set_voxel_order) -- every per-scan pose within 1e-4.
+The teacher-forced frames load the PCL-order oracle's state; with the input-order mapper its
+stacks and cubes differ within the summation-order bound and the pose bar holds.
 """
 import numpy as np
 import pytest
@@ -81,18 +83,34 @@ def test_full_density_recentering(seq):
     m.close()
 
 
+def _oracle_input_order_poses(seq, n):
+    """the oracle mapper in input order (the default mode's summation order) on the features and
+    priors of the PCL-order run (scan registration and odometry do not depend on the mapper)"""
+    import loam_oracle as O
+    with O.voxel_order(1):
+        m = O.LaserMapping()
+        out = []
+        for rec in seq[:n]:
+            m.input(rec["corner"], rec["surf"], None, rec["q_wodom"], rec["t_wodom"])
+            m.solve()
+            out.append((m.pose(), m.stats()))
+    return out
+
+
 @pytest.mark.parametrize("exact", [1, 0])
 def test_free_running_300_frames(seq, exact):
-    """the whole GPU chain on the raw scans, free-running, against the oracle chain.  PCL's
-    VoxelGrid order (default): every per-scan pose within 1e-4 of the oracle's.  Input order
-    (exact_voxel_order = 0): the maps differ from the oracle's by summation-order ulps, which a
-    free-running chain amplifies through threshold decisions; reported, bounded loosely"""
+    """the whole GPU chain on the raw scans, free-running, against the oracle chain in the same
+    VoxelGrid summation order: PCL's (exact_voxel_order = 1) or input order (0, the library
+    default).  Every per-scan pose within 1e-4 m / 1e-4 rad, correspondence counts and LM
+    iterations equal every frame"""
     from loam_amd import synth
     from loam_amd.odometry import BatchOdometry
     from loam_amd.scanreg import ScanRegistration
+    n = 300
+    ref = [(r["pose"], r["stats"]) for r in seq[:n]] if exact else _oracle_input_order_poses(seq, n)
     sr, od, mp = ScanRegistration(), BatchOdometry(1), BatchMapper(1, exact_voxel_order=exact)
-    dt, dr = [], []
-    for f in range(300):
+    dt, dr, counts_bad = [], [], []
+    for f in range(n):
         xyz, _ = synth.frame(SEED, f, N_AZ)
         sr.input(xyz)
         ptrs, counts = zip(*(sr.device_ptr(w) for w in (1, 2, 3, 4)))
@@ -103,15 +121,17 @@ def test_free_running_300_frames(seq, exact):
         mp.input_device(0, pc, nc, ps, ns, q, t)
         mp.solve()
         qm, tm = mp.pose(0)
-        qr, tr = seq[f]["pose"]
+        (qr, tr), sr_ = ref[f]
+        st = mp.stats(0)
+        if (list(st.corner_num), list(st.surf_num), st.lm[0].iterations, st.lm[1].iterations) != \
+                (list(sr_.corner_num), list(sr_.surf_num), sr_.lm[0].iterations, sr_.lm[1].iterations):
+            counts_bad.append(f)
         dt.append(float(np.linalg.norm(tm - tr)))
         dr.append(quat_angle(qm, qr))
     dt, dr = np.array(dt), np.array(dr)
-    print(f"free-running 300 frames (exact_voxel_order={exact}): trans rms {np.sqrt(np.mean(dt ** 2)):.3e} "
+    print(f"free-running {n} frames (exact_voxel_order={exact}): trans rms {np.sqrt(np.mean(dt ** 2)):.3e} "
           f"max {dt.max():.3e} m, rot rms {np.sqrt(np.mean(dr ** 2)):.3e} max {dr.max():.3e} rad")
-    if exact:
-        assert dt.max() < 1e-4 and dr.max() < 1e-4
-    else:
-        assert dt.max() < 0.1 and dr.max() < 0.01
+    assert counts_bad == []
+    assert dt.max() < 1e-4 and dr.max() < 1e-4
     for h in (sr, od, mp):
         h.close()

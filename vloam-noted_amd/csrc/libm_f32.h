@@ -10,7 +10,7 @@
 // rule (:243-246) or at the halfPassed knife edge (:276,:288), moves a point to another ring
 // or by a whole revolution in relTime.  These restatements use only IEEE single-precision
 // + - * / (correctly rounded on gfx950, compiled with -ffp-contract=off) and integer tests on
-// the bit patterns, so they return glibc's bits.  tests/test_libm_f32.py checks them against
+// the bit patterns, so they return glibc's bits.  tests/test_host_models.py (tests/cxx/libm_f32_check.cpp) checks them against
 // the host's glibc on ~10^7 inputs, the special values included.
 //
 // Constants are the decimal literals of the glibc sources, converted double -> float exactly

@@ -50,7 +50,8 @@ constexpr int LM_EBLK = 32;     // LM evaluation workgroups per stream (grid-str
 constexpr int SUBMAP_BLOCKS = 64;
 constexpr int INS_SLOTS = WIN_VALID_MAX + EXTRA_CAP;
 constexpr int MAP_ERR_SUBMAP = 4, MAP_ERR_EXTRA = 8, MAP_ERR_HASH = 16, MAP_ERR_LM_SYNC = 32,
-              MAP_ERR_INDEX = 64, MAP_ERR_LIVE = 128, MAP_ERR_SORT = 256;
+              MAP_ERR_INDEX = 64, MAP_ERR_LIVE = 128, MAP_ERR_SORT = 256,
+              MAP_ERR_STACK = 512;
 
 struct StreamFrame {
   double pose[7];  // in: initial guess (transformAssociateToMap); out: optimised pose
@@ -111,7 +112,8 @@ struct MapperDev {
   int* ins_tag;
   float4* ins_sorted;    // [B][2][max_in] inserted points grouped by target cube (input order kept)
   uint32_t* ins_off;     // [B][2][INS_SLOTS + 1] group offsets: window slots, then extra cubes
-  unsigned long long* dbg;  // [LOAM_DEBUG_COUNTERS] phase cycle counters (loam_mapper_debug_counters)
+  unsigned long long* dbg;  // [LOAM_DEBUG_COUNTERS] counters (loam_mapper_debug_counters)
+  unsigned long long* pdbg;  // dbg when the phase cycle counters are on (LOAM_PHASE_COUNTERS=1), else null
   uint32_t* stable_tok;  // [B][2][NCUBE] arena offset + 1 of content known to be a VoxelGrid
                          // fixed point (re-filtering it is the identity), else 0
   float4* vx_pts;  // [B][2][scratch_cap]
@@ -230,13 +232,13 @@ __device__ inline bool map_voxel_pcl(const MapperDev& D, size_t sm, uint32_t so,
     uint32_t* B = A + MP_LDS_N;
     int* seg0 = reinterpret_cast<int*>(B + MP_LDS_N);
     const VxPclScratch X{E, A, B, D.ps + b, lev, {seg0, seg0 + 3 * MP_SEG_LDS}, MP_SEG_LDS, nullptr,
-                         so == 0 ? D.dbg + 42 : D.dbg + 11};
+                         D.pdbg ? (so == 0 ? D.pdbg + 42 : D.pdbg + 11) : nullptr};
     voxel_grid_pcl<VX_THREADS>(P, n, leaf, O, X, M, ws, err);
   } else {  // level lists in global memory, the LDS holds the waves' subtree sorts
     const int cap = (int)((n + MP_SLACK) / 16);
     int* seg0 = D.pseg + sm * (6 * (ps / 16) + 6) + 6 * (so / 16);
     const VxPclScratch X{D.pe + b, D.pa + b, D.pb + b, D.ps + b, lev, {seg0, seg0 + 3 * cap}, cap, lds,
-                         so == 0 ? D.dbg + 42 : D.dbg + 11};
+                         D.pdbg ? (so == 0 ? D.pdbg + 42 : D.pdbg + 11) : nullptr};
     voxel_grid_pcl<VX_THREADS>(P, n, leaf, O, X, M, ws, err);
   }
   return true;
@@ -271,7 +273,7 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
   S.res_off = nullptr;
   S.scratch_tail = nullptr;
   S.err = &F.err;
-  S.prof_seg = D.dbg + 42;  // stack VoxelGrid phases: dbg[42..45]
+  S.prof_seg = D.pdbg ? D.pdbg + 42 : nullptr;  // stack VoxelGrid phases: dbg[42..45]
   S.src0 = F.in_ptr[m];
   S.n0 = m == 0 ? F.nc_in : F.ns_in;
   S.out = D.stack[m] + (size_t)s * D.max_in;
@@ -381,7 +383,7 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_part(MapperDev D) {
   const uint32_t U = vx_group(S, g, P, N, D.vx_idx + sm * D.scratch_cap + base, klo, khi, base,
                               VX_LDS_WORDS - 256, lds, ws, M, &moved);
   if (tid == 0) {
-    if (U == VX_OVERFLOW) atomicOr(&F.err, MAP_ERR_SORT);
+    if (U == VX_OVERFLOW) atomicOr(&F.err, MAP_ERR_STACK);
     part[j] = make_uint2(base, U == VX_OVERFLOW ? 0u : U);
   }
 }
@@ -850,7 +852,7 @@ __global__ void __launch_bounds__(LM_THREADS) k_lm_round(MapperDev D, int round,
   J.best_out = F.pose;
   J.err = &F.err;
   J.err_code = MAP_ERR_LM_SYNC;
-  J.prof = D.dbg + 17;
+  J.prof = D.pdbg ? D.pdbg + 17 : nullptr;
   lm_round_device<LM_THREADS>(J, g, G);
 }
 
@@ -1049,12 +1051,14 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
   S.scratch_tail = &F.scratch_tail[m];
   S.scratch_cap = D.scratch_cap;
   S.err = &F.err;
-  S.prof = D.dbg + 11;  // merge phases: dbg[11..14]
+  S.prof = D.pdbg ? D.pdbg + 11 : nullptr;  // merge phases: dbg[11..14]
   bool merged = false;
   const unsigned long long t0 = __builtin_readcyclecounter();
-  if (D.pcl_order && !append && n_new > 0) {
+  if (D.pcl_order && !append) {
     // PCL's summation order: the sort of old content ++ new points (voxel_pcl.h); the merge
-    // path (input order) does not apply
+    // path (input order) does not apply.  Also a window cube that received nothing but is not
+    // a VoxelGrid fixed point (raw appended content, content set through the API): the
+    // reference re-filters every window cube (:795-808) in PCL's order
     uint32_t* sb = lds + LW - 3;
     const uint32_t n = cv.y + n_new;
     if (threadIdx.x == 0) *sb = atomicAdd(&F.scratch_tail[m], n + MP_SLACK);
@@ -1093,13 +1097,14 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
   int corner[3];
   cube_corner(cube, F.cen, corner);
   if (!cube_index_build<VX_THREADS, CI_LDS_MAX_T>(ar + off, n, corner, carena_base(D, s, m, F.arena_active[m]) + off,
-                                  ctab_base(D, s, m, F.arena_active[m]) + 4 * (size_t)off, lds, D.dbg + 16) &&
+                                  ctab_base(D, s, m, F.arena_active[m]) + 4 * (size_t)off, lds, D.pdbg ? D.pdbg + 16 : nullptr) &&
       threadIdx.x == 0)
     atomicOr(&F.err, MAP_ERR_INDEX);
   // read old content + new points, write the filtered cube, then its index (read it, write
   // the cell-sorted copy and the table)
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0)
     atomicAdd(&F.vx_bytes, 16ull * (cv.y + n_new) + 16ull * 3 * n + (n ? 8ull * ci_table_size(n) : 0ull));
+  if (threadIdx.x == 0 && D.pdbg) {
     const unsigned long long t2 = __builtin_readcyclecounter();
     const int k = merged ? 0 : (append ? 2 : 1);
     atomicAdd(&D.dbg[k], t1 - t0);       // filter cycles: merge / full / append
@@ -1231,6 +1236,7 @@ __global__ void k_compact_commit(MapperDev D, const uint32_t* new_off) {
     F.arena_active[m] = 1 - F.arena_active[m];
     if (no[NCUBE] > D.compact_at) atomicOr(&F.err, MAP_ERR_LIVE);  // the live map itself
     atomicAdd(&D.dbg[41], 1ull);
+    atomicAdd(&D.dbg[48 + m], 1ull);  // per map
   }
 }
 
@@ -1335,6 +1341,7 @@ inline std::string map_err_text(int e) {
   add(MAP_ERR_INDEX, "cube cell index capacity");
   add(MAP_ERR_LIVE, "live map larger than the arena's compaction bound");
   add(MAP_ERR_SORT, "PCL-order VoxelGrid input larger than its sort lists / scratch");
+  add(MAP_ERR_STACK, "split stack VoxelGrid: a range has more voxels than its LDS groups");
   return m + " (flags " + std::to_string(e) + ")";
 }
 
@@ -1578,6 +1585,10 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   ALLOC(D.stable_tok, B * 2 * (size_t)NCUBE);
   ALLOC(h->tok_tmp, B * 2 * (size_t)NCUBE);
   ALLOC(D.dbg, LOAM_DEBUG_COUNTERS);
+  {  // phase cycle counters (readcyclecounter + device-scope atomics in the kernels): diagnostics only
+    const char* penv = std::getenv("LOAM_PHASE_COUNTERS");
+    D.pdbg = (penv && std::atoi(penv) > 0) ? D.dbg : nullptr;
+  }
   ALLOC(D.vx_pts, B * 2 * (size_t)D.scratch_cap);
   if (D.pcl_order) {
     const size_t ps = mp_scratch(D);

@@ -25,6 +25,7 @@
 // the reference's bits.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "common.h"
@@ -85,8 +86,10 @@ struct SrDev {
   uint32_t* ss_a;
   uint32_t* ss_b;
   uint64_t* ss_s;
-  int* ss_seg;  // [2][3 * SR_SS_GSEG] level lists of the long-sector path (one sector at a time)
+  int* ss_seg;  // [ring][2][3 * SR_SS_GSEG] level lists of the long-sector path (one sector of a ring at a time;
+               // every ring's workgroup has its own area: k_sr_select runs the rings concurrently)
   unsigned long long* dbg;  // [LOAM_SR_DEBUG_COUNTERS] (loam_scanreg_debug_counters)
+  unsigned long long* pdbg;  // dbg when LOAM_PHASE_COUNTERS=1 at create, else null (no cycle counting)
 };
 
 // scan_registration.cpp:217-259 (float atan/sqrt like the reference's float overloads)
@@ -619,8 +622,8 @@ __global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(SrDev D) {
         }
       }
       if (wid == 0)
-        sr_exact_sector(D, sp[j], len[j], keys, nullptr, nullptr, nullptr, &ssLev[0], D.ss_seg, D.ss_seg + 3 * SR_SS_GSEG,
-                        SR_SS_GSEG);
+        sr_exact_sector(D, sp[j], len[j], keys, nullptr, nullptr, nullptr, &ssLev[0], D.ss_seg + r * 6 * SR_SS_GSEG,
+                        D.ss_seg + r * 6 * SR_SS_GSEG + 3 * SR_SS_GSEG, SR_SS_GSEG);
       __syncthreads();
     }
     if (wid == 0) sr_greedy(D, r, base, K, len[j], picked, lab, gapok, nsh, nls, nfl);
@@ -681,11 +684,11 @@ __global__ void __launch_bounds__(SRV_THREADS) k_sr_ringvox(SrDev D) {
   // memory would be generic (flat_*, slower)
   if (lds) {
     VxPclScratch X{sE, sA, sB, sS, &lev, {seg[0], seg[1]}, SRV_SEG};
-    X.prof = D.dbg;  // ring VoxelGrid phase cycles, summed over the rings
+    X.prof = D.pdbg;  // ring VoxelGrid phase cycles, summed over the rings (or null)
     voxel_grid_pcl<SRV_THREADS>(VxPtrSrc{D.less_flat_scan + base}, n, 0.2f, O, X, M, ws, &F.err);
   } else {
     VxPclScratch X{D.ss_e + base, D.ss_a + base, D.ss_b + base, D.ss_s + base, &lev, {seg[0], seg[1]}, SRV_SEG};
-    X.prof = D.dbg;
+    X.prof = D.pdbg;
     voxel_grid_pcl<SRV_THREADS>(VxPtrSrc{D.less_flat_scan + base}, n, 0.2f, O, X, M, ws, &F.err);
   }
 }
@@ -818,8 +821,12 @@ int32_t loam_scanreg_create(const loam_params* p, int32_t device, loam_scanreg**
   SRA(D.ss_a, cap);
   SRA(D.ss_b, cap);
   SRA(D.ss_s, cap);
-  SRA(D.ss_seg, 6 * SR_SS_GSEG);
+  SRA(D.ss_seg, (size_t)SR_MAX_RINGS * 6 * SR_SS_GSEG);
   SRA(D.dbg, LOAM_SR_DEBUG_COUNTERS);
+  {
+    const char* penv = std::getenv("LOAM_PHASE_COUNTERS");
+    D.pdbg = (penv && std::atoi(penv) > 0) ? D.dbg : nullptr;
+  }
 #undef SRA
   D.out[0] = D.cloud;
   D.sort_ind = nullptr;
