@@ -227,10 +227,12 @@ int32_t loam_mapper_stats(loam_mapper* h, int32_t stream, loam_map_stats* st);
  * after the LM (0 when the all-reduce is bit-identical on every rank), [41] arena compactions
  * ((stream, map) pairs), [42..45] stack VoxelGrid cycles: bounding box, hash, sort + scan,
  * member lists + centroids, [46..47] of the latter: member lists, per-voxel sort + sums,
- * [48..49] arena compactions of the corner / surf maps (summed over streams).
+ * [48..49] arena compactions of the corner / surf maps (summed over streams), [50..57] tile kNN
+ * (k_knn_tile, summed over waves): cycles of the tile record + query loads, the cell probes +
+ * cell starts, staging, the search, the results; then tiles, queries, staged points.
  * The cycle counters (all but [40], [41], [48], [49]) run only in a handle created with the
  * environment variable LOAM_PHASE_COUNTERS=1 (they cost atomics in the kernels); else they stay 0. */
-#define LOAM_DEBUG_COUNTERS 50
+#define LOAM_DEBUG_COUNTERS 64
 int32_t loam_mapper_debug_counters(loam_mapper* h, uint64_t* out, int32_t n, int32_t reset);
 /* sum over the streams solved by the last loam_mapper_solve of their LM iterations (both rounds) */
 int64_t loam_mapper_total_iterations(loam_mapper* h);

@@ -10,7 +10,8 @@ Scan registration always uses PCL's order (scan_registration.cpp:497-501 on the 
 Per frame it records what the GPU test (tests/test_gpu_long_stream.py) compares: the feature
 counts, the odometry pose / correspondences / LM iterations, and for both mapper modes the pose
 and every count of LaserMapping::solveMapping (stack, submap, correspondences per round, LM
-iterations per round, cube-grid centre, valid cubes).  At 1 m per frame the window recentres
+iterations per round, cube-grid centre, valid cubes, the grid's cen after recentering).  At 1 m
+per frame the window recentres
 (laser_mapping.cpp:252-444) about every 50 frames and map coordinates reach 10^4 m, where the
 insert / re-filter path (:741-808) has not been exercised before.
 
@@ -83,7 +84,7 @@ def mapper(order, qu, res):
     import loam_oracle as O
     O.set_voxel_order(order)
     m = O.LaserMapping()
-    q_all, t_all, rows = [], [], []
+    q_all, t_all, rows, cens = [], [], [], []
     t0 = time.time()
     while True:
         item = qu.get()
@@ -96,9 +97,10 @@ def mapper(order, qu, res):
         q_all.append(qm)
         t_all.append(tm)
         rows.append(map_row(m.stats()))
+        cens.append(m.get_state()[0])  # laserCloudCenWidth / Height / Depth (moves on recentering)
         if len(rows) % 500 == 0:
             print(f"mapper order {order}: {len(rows)} frames, {time.time() - t0:.0f} s", flush=True)
-    res.put((order, np.asarray(q_all), np.asarray(t_all), np.asarray(rows, np.int32)))
+    res.put((order, np.asarray(q_all), np.asarray(t_all), np.asarray(rows, np.int32), np.asarray(cens, np.int32)))
 
 
 def main():
@@ -116,17 +118,17 @@ def main():
     fr = front(a.frames, qs)
     got = {}
     for _ in procs:
-        order, q, t, rows = res.get()
-        got[order] = (q, t, rows)
+        order, q, t, rows, cens = res.get()
+        got[order] = (q, t, rows, cens)
     for p in procs:
         p.join()
     out = dict(seed=np.int64(SEED), n_az=np.int64(N_AZ), frames=np.int64(a.frames),
                map_cols=np.array(MAP_COLS), **fr)
     for order, name in ((0, "pcl"), (1, "input")):
-        q, t, rows = got[order]
-        out[f"{name}_q"], out[f"{name}_t"], out[f"{name}_stats"] = q, t, rows
+        q, t, rows, cens = got[order]
+        out[f"{name}_q"], out[f"{name}_t"], out[f"{name}_stats"], out[f"{name}_cen"] = q, t, rows, cens
     np.savez_compressed(a.out, **out)
-    cen = got[0][2][:, 11:14]
+    cen = got[0][3]
     shifts = int(np.sum(np.any(np.diff(cen, axis=0) != 0, axis=1)))
     print(f"{a.frames} frames in {time.time() - t0:.0f} s -> {a.out}; window recenterings {shifts}; "
           f"final t {got[0][1][-1]}")

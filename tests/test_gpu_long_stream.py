@@ -82,10 +82,11 @@ def test_long_stream_10k_frames_both_orders():
                     st = m.stats(0)
                     e = (float(np.linalg.norm(tm - G[f"{name}_t"][f])), quat_angle(qm, G[f"{name}_q"][f]))
                     err[name][f] = e
-                    if _row(st) != list(G[f"{name}_stats"][f]) or e[0] >= TOL or e[1] >= TOL:
+                    cen = tuple(m.get_state(0)[0])
+                    if (_row(st) != list(G[f"{name}_stats"][f]) or cen != tuple(G[f"{name}_cen"][f])
+                            or e[0] >= TOL or e[1] >= TOL):
                         bad[name].append(f)
-                cen = tuple(st.center)
-                shifts += cen_prev is not None and cen != cen_prev
+                shifts += cen_prev is not None and cen != cen_prev  # a recentering (laser_mapping.cpp:252-444)
                 cen_prev = cen
             if c0 % 2048 == 0:
                 print(f"frame {c0}: {time.time() - t0:.0f} s", flush=True)
