@@ -27,6 +27,39 @@ def synth_frame(seed, frame, n_az):
 
 
 # ---------------------------------------------------------------- CPU: oracle reproduces
+def test_oracle_long_stream_fixture_prefix():
+    """tests/golden/long_stream.npz (the 10k-frame configs[3] record of the GPU long-stream test):
+    the oracle chain reproduces its first 40 frames bit for bit, in both VoxelGrid orders"""
+    g = load("long_stream")
+    n = 40
+    seed, n_az = int(g["seed"]), int(g["n_az"])
+    old = O.set_voxel_order(0)
+    try:
+        sr, od = O.ScanRegistration(), O.LaserOdometry()
+        mps = {0: O.LaserMapping(), 1: O.LaserMapping()}
+        for f in range(n):
+            O.set_voxel_order(0)  # scan registration sums in PCL's order
+            sr.input(synth_frame(seed, f, n_az)[0])
+            clouds = sr.output()
+            assert [len(c) for c in clouds] == list(g["sr_counts"][f])
+            od.input(*clouds)
+            od.solve()
+            q, t, _, _, _ = od.output()
+            assert np.array_equal(q, g["od_q"][f]) and np.array_equal(t, g["od_t"][f])
+            for order, name in ((0, "pcl"), (1, "input")):
+                O.set_voxel_order(order)
+                m = mps[order]
+                m.input(od.cloud(0), od.cloud(1), None, q, t)
+                m.solve()
+                qm, tm = m.pose()
+                assert np.array_equal(qm, g[f"{name}_q"][f]) and np.array_equal(tm, g[f"{name}_t"][f]), (f, name)
+                assert np.array_equal(m.get_state()[0], g[f"{name}_cen"][f])
+    finally:
+        O.set_voxel_order(old)
+    cen = g["pcl_cen"]
+    assert int(g["frames"]) >= 10000 and int(np.sum(np.any(np.diff(cen, axis=0) != 0, axis=1))) >= 100
+
+
 def test_oracle_knn_fixture():
     g = load("knn")
     idx, d2 = O.knn(g["pts"], g["q"], 5)
