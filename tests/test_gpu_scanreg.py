@@ -92,6 +92,16 @@ def test_scanreg_many_long_tied_rings():
     assert (np.bincount(ids) > 6 * 1024 + 11).sum() >= 20
 
 
+def test_scanreg_curvature_exactly_threshold():
+    """frame 2417 of the long stream (seed 23) has a curvature of exactly 0.1f at a sector's edge
+    candidate: the reference compares the float with the double literal 0.1 (scan_registration.cpp
+    :381, :443), so 0.1f > 0.1 makes it lessSharp (a float compare with 0.1f would not)"""
+    xyz, _ = synth.frame(23, 2417, 2000)
+    ref = _check_frame(xyz)
+    c, lab = ref.curvature()
+    assert np.any((c == np.float32(0.1)) & (lab == 1))
+
+
 def test_scanreg_stride_and_nan():
     """(n, 4) input with NaN rows and points inside minimum_range (removeNaN + removeClosed)"""
     xyz, _ = synth.frame(4, 3)

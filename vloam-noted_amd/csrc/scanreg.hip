@@ -465,8 +465,10 @@ __device__ inline void sr_greedy(SrDev& D, int r, int base, const uint64_t* K, i
       const uint64_t key = K[k];
       ind = (int)(key & 0xFFFFFFFFu);
       const float c = __uint_as_float((uint32_t)(key >> 32));
-      cond = picked[ind - base] == 0 && c > 0.1f;
-      low = !(c > 0.1f);
+      // the reference compares the float curvature with the double literal 0.1 (:381): a
+      // curvature of exactly 0.1f (> 0.1) is an edge candidate
+      cond = picked[ind - base] == 0 && (double)c > 0.1;
+      low = !((double)c > 0.1);
     }
     const uint64_t bc = __ballot(cond);
     const uint64_t bl = __ballot(low);
@@ -508,8 +510,8 @@ __device__ inline void sr_greedy(SrDev& D, int r, int base, const uint64_t* K, i
       const uint64_t key = K[k];
       ind = (int)(key & 0xFFFFFFFFu);
       const float c = __uint_as_float((uint32_t)(key >> 32));
-      cond = picked[ind - base] == 0 && c < 0.1f;
-      high = !(c < 0.1f);
+      cond = picked[ind - base] == 0 && (double)c < 0.1;  // :443, double literal
+      high = !((double)c < 0.1);
     }
     const uint64_t bc = __ballot(cond);
     const uint64_t bh = __ballot(high);
