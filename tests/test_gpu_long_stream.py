@@ -41,7 +41,7 @@ def test_long_stream_10k_frames_both_orders():
     from loam_amd.odometry import BatchOdometry
     from loam_amd.scanreg import ScanRegistration
 
-    G = np.load(FIXTURE)
+    G = dict(np.load(FIXTURE))  # materialised once (NpzFile decompresses on every access)
     seed, n_az, N = int(G["seed"]), int(G["n_az"]), int(G["frames"])
     assert N >= 10000
     sr, od = ScanRegistration(), BatchOdometry(1)
