@@ -65,7 +65,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--n-az", type=int, default=2000)
     ap.add_argument("--cpu-cores", type=int, default=0,
-                    help="oracle replicas of the all-cores CPU figure (0: min(16, usable cores))")
+                    help="oracle replicas of the all-cores CPU figure (0: min(16, usable cores): the GPU pool "
+                         "allots 16 host CPUs to one GPU, whatever the affinity mask shows)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-prof", action="store_true", help="no per-launch HIP events")
     ap.add_argument("--prior", choices=["odometry", "drift"], default="odometry",
@@ -559,16 +560,45 @@ def pipelined_chain(scans, device, n_frames, timed):
             "poses": poses}
 
 
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r2_pmc_traffic.json")
+def _pmc_file():
+    """the newest committed PMC traffic summary (tools/pmc_traffic.py -> profiles/rN_pmc_traffic.json)"""
+    for r in (3, 2):
+        path = os.path.join(ROOT, "profiles", f"r{r}_pmc_traffic.json")
+        if os.path.exists(path):
+            return path
+    return None
+
+
+PMC_TRAFFIC = _pmc_file()
 
 
 def pmc_traffic(family):
     """HBM bytes per launch of a kernel family measured by the rocprofv3 PMC passes of this
-    bench configuration (tools/pmc_traffic.py -> profiles/r1_pmc_traffic.json), or None"""
+    bench configuration (tools/pmc_traffic.py), or None"""
     try:
         return json.load(open(PMC_TRAFFIC))["families"][family]["bytes_per_launch"]
-    except (OSError, KeyError, ValueError):
+    except (OSError, KeyError, ValueError, TypeError):
         return None
+
+
+def family_rooflines(kt, with_traffic):
+    """every kernel family of the mapper step against the HBM roofline: algorithmic bytes per
+    launch (counted by the library) / mean launch time (HIP events on the
+    library's streams over the timed steps), and the PMC-measured memory-side bytes per launch
+    of the same family with their ratio to the algorithmic bytes (wasted traffic when > 1)"""
+    out = {}
+    for name, v in kt.items():
+        if v["ms"] <= 0 or v["launches"] <= 0:
+            continue
+        alg = v["bytes"] / v["launches"]
+        us = 1e3 * v["ms"] / v["launches"]
+        ach = alg / (us * 1e-6) / 1e9
+        tr = pmc_traffic(name) if with_traffic else None
+        out[name] = {"algorithmic_bytes_per_launch": round(alg, 1), "avg_launch_us": round(us, 3),
+                     "achieved": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 5), "launches": v["launches"],
+                     "traffic": round(tr, 1) if tr is not None else None,
+                     "traffic_over_algorithmic": round(tr / alg, 3) if tr is not None and alg > 0 else None}
+    return out
 
 
 def aggregate(iters, dt, world, device):
@@ -739,9 +769,9 @@ def main():
                 "mode": "every stream split over all ranks (block-owned map shards, per-round 5-NN all-gather, "
                         "per-LM-iteration normal-equation all-reduce); iterations counted once per stream"}
 
-    single = None
-    if not args.no_single_stream and rank == 0 and world == 1 and not args.shard:
-        m1 = BatchMapper(1, device=local, exact_voxel_order=args.exact_voxel_order)
+    def single_stream(exact):
+        """B = 1 on stream 0's frames (the latency view): map building untimed, then K frames"""
+        m1 = BatchMapper(1, device=local, exact_voxel_order=exact)
         plan1 = [step_inputs(frames, 1, args.stride, k) for k in range(pre + K)]
         run_steps(m1, plan1, 0, pre)
         torch.cuda.synchronize(local)
@@ -749,8 +779,14 @@ def main():
         it1 = run_steps(m1, plan1, pre, K)
         torch.cuda.synchronize(local)
         d1 = time.perf_counter() - t1
-        single = {"value": it1 / d1, "ms_per_frame": 1e3 * d1 / K, "iterations": it1}
         m1.close()
+        return {"value": it1 / d1, "ms_per_frame": 1e3 * d1 / K, "iterations": it1}
+
+    single = single_exact = None
+    if not args.no_single_stream and rank == 0 and world == 1 and not args.shard:
+        single = single_stream(args.exact_voxel_order)
+        if not args.no_exact_leg and not args.exact_voxel_order:
+            single_exact = single_stream(1)
 
     if rank == 0:
         dom = max(kt, key=lambda k: kt[k]["ms"])
@@ -762,7 +798,8 @@ def main():
                     "traffic": round(traffic, 1) if traffic is not None else None,
                     "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) if traffic is not None else None,
                     "launches": d["launches"], "avg_launch_us": round(1e3 * d["ms"] / max(1, d["launches"]), 3),
-                    "algorithmic_bytes_per_launch": round(d["bytes"] / max(1, d["launches"]), 1)}
+                    "algorithmic_bytes_per_launch": round(d["bytes"] / max(1, d["launches"]), 1),
+                    "families": family_rooflines(kt, not args.shard)}
         cpu = cpu_st = rmse = allc = None
         if with_cpu:
             ci, cms, cposes = cpu_baseline(frames, pre, K)
@@ -792,8 +829,16 @@ def main():
                 "mode": "oracle with input-order VoxelGrid sums vs oracle with PCL's order, free-running"}
             cpu_st = cpu_stages(frames, pre, K)
             ai, adt = cpu_all_cores(frames, cores, args.stride, pre, K)
+            visible = len(os.sched_getaffinity(0))
             allc = {"value": round(ai / adt, 3), "unit": "LM iters/s", "cores": cores, "kind": "port",
-                    "nproc": os.cpu_count(), "usable_cores": len(os.sched_getaffinity(0)),
+                    "nproc": os.cpu_count(), "visible_cores": visible,
+                    "core_cap": ("replicas capped at 16: the GPU pool allots 16 host CPUs to one GPU (its "
+                                 "process guard and OMP_NUM_THREADS=16), although the affinity mask shows "
+                                 f"{visible}; the figure is {cores} cores, not the whole host"),
+                    "per_core": round(ai / adt / cores, 3),
+                    "whole_host_estimate": {
+                        "value": round(ai / adt / cores * visible, 1), "cores": visible,
+                        "how": "per-replica rate x visible cores (an extrapolation, not a measurement)"},
                     "sample": f"{cores} oracle replicas, one thread each, replica c on stream c's inputs: "
                               f"{pre} untimed map-building frames, then its {K} timed frames between two "
                               f"barriers; {ai} LM iterations in {adt:.3f} s"}
@@ -831,6 +876,8 @@ def main():
         }
         if single is not None:
             out["single_stream"] = {k: round(v, 4) for k, v in single.items()}
+        if single_exact is not None:
+            out["single_stream_exact_voxel_order"] = {k: round(v, 4) for k, v in single_exact.items()}
         if exact_leg is not None:
             exact_leg.pop("poses")
             exact_leg["value"] = round(exact_leg["value"], 3)
@@ -876,6 +923,9 @@ def main():
             out["speedup_vs_cpu_all_cores"] = round(out["value"] / allc["value"], 2)
             if single is not None:
                 out["single_stream"]["speedup_vs_cpu_baseline"] = round(single["value"] / cpu["value"], 2)
+            if single_exact is not None:
+                out["single_stream_exact_voxel_order"]["speedup_vs_cpu_baseline"] = round(
+                    single_exact["value"] / cpu["value"], 2)
     # the sharded leg last, so that it cannot cost the headline line: it is the one place where
     # ranks exchange data (RCCL), so a failure there is recorded in the line, and a hang ends at
     # a watchdog that prints the line without it
