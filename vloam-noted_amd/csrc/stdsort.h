@@ -56,6 +56,10 @@ struct SsLevels {
   uint32_t ws[17];  // block-scan scratch of the cooperative partition
   int sh[2];
   uint32_t* loc;  // optional LDS for wave-local subtree sorts (SS_LOC_WORDS per wave), else nullptr
+  // deferral (ss_levels<..., true>, a sort whose elements live in global memory): segments of at
+  // most `defer` elements are not partitioned level by level but listed in the caller's
+  // dseg[dcap][3] (lo, hi, depth budget), each then sorted whole in LDS (ss_sort_deferred)
+  int dcnt, dcap, defer;
 };
 
 // Wave-local subtree sort: a segment of at most SS_LOCAL elements whose array lives in global
@@ -356,15 +360,17 @@ __device__ inline void ss_local_sort(T* E, uint32_t* A, uint32_t* B, int lo, int
 }
 
 // Init with the root segment [0, n) (one thread; a barrier / wave fence before ss_levels).
-__device__ inline void ss_levels_init(SsLevels* L, int n, int* seg0, int* seg1, int cap) {
+// depth: the root's depth budget (< 0: 2 * __lg(n), std::sort's; a deferred subtree's own).
+__device__ inline void ss_levels_init(SsLevels* L, int n, int* seg0, int* seg1, int cap, int depth = -1) {
   L->seg[0] = seg0;
   L->seg[1] = seg1;
   L->cap = cap;
   L->err = 0;
   L->cnt[0] = L->cnt[1] = L->nbig[0] = L->nbig[1] = 0;
   L->loc = nullptr;
+  L->dcnt = L->dcap = L->defer = 0;
   if (n > SS_THRESHOLD) {
-    const int d = 2 * (31 - __clz(n));  // 2 * __lg(n)
+    const int d = depth >= 0 ? depth : 2 * (31 - __clz(n));  // 2 * __lg(n)
     const bool big = n > SS_BIG && d > 0;
     int* o = seg0 + 3 * (big ? cap - 1 : 0);
     o[0] = 0;
@@ -382,9 +388,9 @@ __device__ inline void ss_levels_init(SsLevels* L, int n, int* seg0, int* seg1, 
 // The list / buffer pointers are arguments (not read back from L, which lives in LDS): named
 // directly from __shared__ arrays at the call site they keep their LDS address space, so the
 // compiler emits ds_* instead of flat_* accesses.
-template <bool WG, int NT = 64, typename T, typename Less>
+template <bool WG, int NT = 64, bool DEFER = false, typename T, typename Less>
 __device__ inline void ss_levels(T* E, uint32_t* A, uint32_t* B, SsLevels* L, int wave, int nw, const Less& less,
-                                 int* seg0, int* seg1, uint32_t* loc) {
+                                 int* seg0, int* seg1, uint32_t* loc, int* dseg = nullptr) {
   const int lane = threadIdx.x & 63;
   int* const segs[2] = {seg0, seg1};
   auto barrier = [] {
@@ -392,6 +398,18 @@ __device__ inline void ss_levels(T* E, uint32_t* A, uint32_t* B, SsLevels* L, in
     else ss_wave_fence();
   };
   auto push = [&](int nxt, int a, int b, int d) {  // one lane
+    if (DEFER && b - a <= L->defer && d > 0) {  // sorted whole later (ss_sort_deferred)
+      const int t = atomicAdd(&L->dcnt, 1);
+      if (t < L->dcap) {
+        int* o = dseg + 3 * t;
+        o[0] = a;
+        o[1] = b;
+        o[2] = d;
+      } else {
+        atomicOr(&L->err, 2);
+      }
+      return;
+    }
     const bool big = b - a > SS_BIG && d > 0;
     const int t = atomicAdd(big ? &L->nbig[nxt] : &L->cnt[nxt], 1);
     const int slot = big ? L->cap - 1 - t : t;
@@ -486,6 +504,37 @@ __device__ inline void ss_final(const T* E, const uint32_t* A, const uint32_t* B
       r += (less(ej, ei) || (j < i && !less(ei, ej))) ? 1 : 0;
     }
     out[lo + r] = ei;
+  }
+}
+
+// The deferred segments of a sort in global memory (ss_levels with L->defer), one after the
+// other by the whole workgroup: the segment is copied into LDS (lE / lA / lB, level lists
+// lseg0 / lseg1 of lcap entries, state LL), its whole introsort subtree runs there with the
+// depth budget it was deferred with, and the final stable pass writes it back sorted; its
+// bounds become the identity (sorted in place, like ss_local_sort).  Segments are disjoint and
+// independent, so this order gives std::sort's permutation.
+template <int NT, typename T, typename Less>
+__device__ inline void ss_sort_deferred(T* E, uint32_t* A, uint32_t* B, SsLevels* L, const int* dseg, const Less& less,
+                                        T* lE, uint32_t* lA, uint32_t* lB, int* lseg0, int* lseg1, int lcap,
+                                        SsLevels* LL) {
+  const int tid = threadIdx.x;
+  __syncthreads();
+  const int nd = min(L->dcnt, L->dcap);
+  for (int k = 0; k < nd; ++k) {
+    const int lo = dseg[3 * k], hi = dseg[3 * k + 1], d = dseg[3 * k + 2];
+    const int m = hi - lo;
+    for (int i = tid; i < m; i += NT) lE[i] = E[lo + i];
+    if (tid == 0) ss_levels_init(LL, m, lseg0, lseg1, lcap, d);
+    __syncthreads();
+    ss_levels<true, NT>(lE, lA, lB, LL, tid >> 6, NT / 64, less, lseg0, lseg1, nullptr);
+    __syncthreads();
+    if (tid == 0 && LL->err) atomicOr(&L->err, LL->err);
+    ss_final(lE, lA, lB, m, E + lo, tid, NT, less);
+    for (int i = tid; i < m; i += NT) {
+      A[lo + i] = (uint32_t)(lo + i);
+      B[lo + i] = (uint32_t)(lo + i + 1);
+    }
+    __syncthreads();
   }
 }
 

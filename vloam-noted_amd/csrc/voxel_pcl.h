@@ -17,6 +17,21 @@
 
 namespace loam {
 
+// A sort too large for the LDS (E in global memory): segments of at most `defer` elements are
+// sorted whole in LDS (ss_sort_deferred) instead of level by level in global memory.
+struct VxPclDefer {
+  int defer;
+  int* dseg;  // [dcap][3], global
+  int dcap;
+  uint64_t* lE;
+  uint32_t* lA;
+  uint32_t* lB;
+  int* lseg0;
+  int* lseg1;
+  int lcap;
+  SsLevels* LL;  // LDS
+};
+
 struct VxPclScratch {
   uint64_t* E;   // n: (idx << 32 | point), permuted by the sort
   uint32_t* A;   // n
@@ -54,9 +69,10 @@ struct VxPclOut {
 
 // All NT threads call it.  P(i): the i-th input point (i < n).  ws: >= NT / 64 + 1 words of
 // LDS; M: LDS misc.  err |= 4: level list overflow, |= 2 (VX_ERR_OUTPUT): output block past cap.
-template <int NT, typename PF>
+// DEFER (a sort in global memory): segments that fit the LDS are sorted there whole (dfr).
+template <int NT, bool DEFER = false, typename PF>
 __device__ inline void voxel_grid_pcl(const PF& P, int n, float leaf, const VxPclOut& O, const VxPclScratch& X,
-                                      VxMisc& M, uint32_t* ws, int* err) {
+                                      VxMisc& M, uint32_t* ws, int* err, const VxPclDefer* dfr = nullptr) {
   const int tid = threadIdx.x;
   auto finish = [&](uint32_t base, uint32_t cnt, bool fixed) {
     if (O.res_off) *O.res_off = base;
@@ -91,12 +107,22 @@ __device__ inline void voxel_grid_pcl(const PF& P, int n, float leaf, const VxPc
   if (tid == 0) {
     ss_levels_init(X.lev, n, X.seg[0], X.seg[1], X.cap);
     X.lev->loc = X.loc;
+    if (DEFER) {
+      X.lev->defer = dfr->defer;
+      X.lev->dcap = dfr->dcap;
+    }
     M.moved = 0;
   }
   const VxIdxLess less;
   __syncthreads();
   vx_phase(X.prof, 0, &tp);
-  ss_levels<true, NT>(X.E, X.A, X.B, X.lev, tid >> 6, NT / 64, less, X.seg[0], X.seg[1], X.loc);
+  if constexpr (DEFER) {
+    ss_levels<true, NT, true>(X.E, X.A, X.B, X.lev, tid >> 6, NT / 64, less, X.seg[0], X.seg[1], X.loc, dfr->dseg);
+    ss_sort_deferred<NT>(X.E, X.A, X.B, X.lev, dfr->dseg, less, dfr->lE, dfr->lA, dfr->lB, dfr->lseg0, dfr->lseg1,
+                         dfr->lcap, dfr->LL);
+  } else {
+    ss_levels<true, NT>(X.E, X.A, X.B, X.lev, tid >> 6, NT / 64, less, X.seg[0], X.seg[1], X.loc);
+  }
   __syncthreads();
   vx_phase(X.prof, 1, &tp);
   if (tid == 0 && X.lev->err) atomicOr(err, 4);
