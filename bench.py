@@ -176,6 +176,24 @@ def run_steps(mapper, plan, first, count, poses=None):
     return iters
 
 
+def run_steps_pipelined(mapper, plan, first, count):
+    """count solveMapping steps with the next step's input given, and its stack VoxelGrid queued
+    (loam_mapper_prefetch), while the current step is in flight (loam_mapper_solve_async /
+    loam_mapper_wait): the same results as run_steps, frame after frame"""
+    iters = 0
+    mapper.input_device_batch(*plan[first])
+    mapper.solve_async()
+    for k in range(first + 1, first + count + 1):
+        if k < first + count:
+            mapper.input_device_batch(*plan[k])
+            mapper.prefetch()
+        mapper.wait()
+        iters += mapper.total_iterations()
+        if k < first + count:
+            mapper.solve_async()
+    return iters
+
+
 def run_handles(mappers, plans, first, count, poses=None):
     """run_steps on every handle, one host thread each (ctypes releases the GIL in the
     library calls): one handle's host work overlaps the others' kernels"""
@@ -770,17 +788,24 @@ def main():
                         "per-LM-iteration normal-equation all-reduce); iterations counted once per stream"}
 
     def single_stream(exact):
-        """B = 1 on stream 0's frames (the latency view): map building untimed, then K frames"""
-        m1 = BatchMapper(1, device=local, exact_voxel_order=exact)
-        plan1 = [step_inputs(frames, 1, args.stride, k) for k in range(pre + K)]
-        run_steps(m1, plan1, 0, pre)
-        torch.cuda.synchronize(local)
-        t1 = time.perf_counter()
-        it1 = run_steps(m1, plan1, pre, K)
-        torch.cuda.synchronize(local)
-        d1 = time.perf_counter() - t1
-        m1.close()
-        return {"value": it1 / d1, "ms_per_frame": 1e3 * d1 / K, "iterations": it1}
+        """B = 1 on stream 0's frames (the latency view): map building untimed, then K frames,
+        frame after frame.  Pipelined: frame f + 1's input and stack VoxelGrid are queued while
+        frame f is in flight (loam_mapper_solve_async / _prefetch / _wait, the same results);
+        the blocking loam_mapper_solve beside it"""
+        out = {}
+        for mode in ("pipelined", "blocking"):
+            m1 = BatchMapper(1, device=local, exact_voxel_order=exact)
+            plan1 = [step_inputs(frames, 1, args.stride, k) for k in range(pre + K)]
+            run_steps(m1, plan1, 0, pre)
+            torch.cuda.synchronize(local)
+            t1 = time.perf_counter()
+            it1 = run_steps_pipelined(m1, plan1, pre, K) if mode == "pipelined" else run_steps(m1, plan1, pre, K)
+            torch.cuda.synchronize(local)
+            d1 = time.perf_counter() - t1
+            m1.close()
+            out[mode] = {"value": it1 / d1, "ms_per_frame": 1e3 * d1 / K, "iterations": it1}
+        return {**out["pipelined"], "blocking_value": out["blocking"]["value"],
+                "blocking_ms_per_frame": out["blocking"]["ms_per_frame"]}
 
     single = single_exact = None
     if not args.no_single_stream and rank == 0 and world == 1 and not args.shard:

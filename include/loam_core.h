@@ -212,6 +212,18 @@ int32_t loam_mapper_input_device_batch(loam_mapper* h, int32_t n, const int32_t*
  * timed out; loam_last_error names the stream and the cause) still leaves the frame committed
  * as computed (pose, insertion, re-VoxelGrid): reset the failed stream before relying on it. */
 int32_t loam_mapper_solve(loam_mapper* h);
+/* loam_mapper_solve in two halves: _async enqueues the frame on the handle's HIP streams and
+ * returns; _wait blocks until it is done and then does the host side (transformUpdate,
+ * laser_mapping.cpp:147-151, stats, status).  Every other call on the handle waits first.  While
+ * a frame is in flight the next frame's inputs may be given (loam_mapper_input*) and their stack
+ * VoxelGrids (:492-500, which read only the body-frame input) queued with loam_mapper_prefetch:
+ * they run beside the frame in flight, into the other of two stack buffers.  The results are
+ * those of the sequential loam_mapper_solve; only the order in time changes.  Device inputs must
+ * stay valid until the frame that takes them is waited for. */
+int32_t loam_mapper_solve_async(loam_mapper* h);
+int32_t loam_mapper_wait(loam_mapper* h);
+/* queue the stack VoxelGrids of every stream's pending input now (no-op with profiling on) */
+int32_t loam_mapper_prefetch(loam_mapper* h);
 /* pose after solveMapping: q_w_curr (xyzw), t_w_curr (laser_mapping.cpp:826-832) */
 int32_t loam_mapper_pose(loam_mapper* h, int32_t stream, double* q_w, double* t_w);
 int32_t loam_mapper_stats(loam_mapper* h, int32_t stream, loam_map_stats* st);

@@ -399,3 +399,44 @@ def test_cube_edge_filing():
         m.solve()
         _check_frame(m, 0, want)
         m.close()
+
+
+@pytest.mark.parametrize("n_streams,exact", [(1, 0), (1, 1), (6, 0)])
+def test_async_solve_with_prefetched_stacks(seq, n_streams, exact):
+    """loam_mapper_solve_async / _prefetch / _wait (include/loam_core.h): frame f + 1's input is
+    given and its stack VoxelGrid queued while frame f is in flight (double-buffered stacks);
+    every pose and count equals the blocking loam_mapper_solve, bit for bit.  One stream takes
+    the hipGraph path, six the kernel-by-kernel path; host inputs copy on the stack stream"""
+    def row(m, s):
+        st = m.stats(s)
+        q, t = m.pose(s)
+        return (q.tobytes(), t.tobytes(), st.corner_stack, st.surf_stack, tuple(st.corner_num), tuple(st.surf_num),
+                st.lm[0].iterations, st.lm[1].iterations)
+
+    def feed(m, f):
+        for s in range(n_streams):
+            rec = seq[f + s]  # stream s runs the sequence s frames ahead
+            m.input(s, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+
+    n = len(seq) - n_streams + 1
+    ref = BatchMapper(n_streams, exact_voxel_order=exact)
+    want = []
+    for f in range(n):
+        feed(ref, f)
+        ref.solve()
+        want.append([row(ref, s) for s in range(n_streams)])
+    ref.close()
+    m = BatchMapper(n_streams, exact_voxel_order=exact)
+    got = []
+    feed(m, 0)
+    m.solve_async()
+    for f in range(1, n + 1):
+        if f < n:
+            feed(m, f)  # while frame f - 1 is in flight
+            m.prefetch()
+        m.wait()
+        got.append([row(m, s) for s in range(n_streams)])
+        if f < n:
+            m.solve_async()
+    m.close()
+    assert got == want

@@ -82,6 +82,16 @@ struct StreamFrame {
   LmState lm[2];
 };
 
+// the stack VoxelGrid inputs of a stream (laser_mapping.cpp:492-500): set when its stack is
+// launched (loam_mapper_prefetch or the solve), double-buffered by stack parity so that the next
+// frame's stack can run beside a frame in flight
+struct StackIn {
+  const float4* p[2];
+  int n[2];
+  int active;
+  int pad;
+};
+
 struct MapPose {  // by-value kernel argument: q (xyzw) + t
   double x[7];
 };
@@ -147,6 +157,13 @@ struct MapperDev {
   // idx range (k_stack_part + k_stack_cat), else one workgroup (k_stack_ds)
   int stack_k = 0;
   uint2* stk_part;       // [B][2][STACK_K_MAX] (staging offset, centroids) of each range
+  // the stack kernels' inputs, outputs and scratch (one stack parity: the frame's, or the next
+  // frame's while this one is in flight; D.stack[m] is that parity's stack)
+  const StackIn* sin;    // [B]
+  int* stk_n;            // [B][2] stack sizes (copied into the frame records by k_stack_counts)
+  int* stk_err;          // [B] error flags of the stack kernels (merged by k_stack_counts)
+  float4* stk_pts;       // [B][2][max_in] scratch of the input-order stack filter
+  int* stk_idx;          // [B][2][max_in]
   // tile kNN (k_tile_bin / k_knn_tile): per (stream, map) the queries grouped by 2 m tile
   uint2* tile_r;         // [B][2][max_in] a query's (tile table slot, rank in its tile), slot empty if none
   uint2* tiles;          // [B][2][max_in] occupied 4 m tiles: (key | count << 18, first position in tile_q)
@@ -213,20 +230,32 @@ __global__ void k_shift_cubes(MapperDev D, const uint2* __restrict__ old_tab, ui
 // else at offset `so` of the (stream, map) sort scratch, where the sorted copy S always goes.
 // Returns false (MAP_ERR_SORT) when the input is too large for the lists.
 constexpr int MP_LDS_N = 8192;                                    // E 64 KiB + A, B 32 KiB each
-constexpr int MP_LEV_W = 32;  // SsLevels words
+constexpr int MP_LEV_W = 40;  // SsLevels words
 static_assert(sizeof(SsLevels) <= 4 * MP_LEV_W, "SsLevels area");
-constexpr int MP_SEG_LDS = (VX_LDS_WORDS - 256 - MP_LEV_W - 4 * MP_LDS_N) / 6;  // level lists beside them
+constexpr int MP_SEG_LDS = (VX_LDS_WORDS - 256 - 2 * MP_LEV_W - 4 * MP_LDS_N) / 6;  // level lists beside them
 static_assert(MP_SEG_LDS >= MP_LDS_N / (SS_THRESHOLD + 1) + 2, "level lists of an LDS-resident sort");
-static_assert(VX_THREADS / 64 * SS_LOC_WORDS + 256 + MP_LEV_W <= VX_LDS_WORDS, "wave-local sort buffers");
+static_assert(VX_THREADS / 64 * SS_LOC_WORDS + 256 + 2 * MP_LEV_W <= VX_LDS_WORDS, "wave-local sort buffers");
+// global-memory sorts: segments of at most MP_LDS_N elements are sorted whole in LDS
+// (ss_sort_deferred: E, A, B and the level lists of one segment at a time)
+constexpr int MP_DEF_SEG = MP_LDS_N / (SS_THRESHOLD + 1) + 2;
+static_assert(4 * MP_LDS_N + 6 * MP_DEF_SEG + 256 + 2 * MP_LEV_W <= VX_LDS_WORDS, "deferred segment sort in LDS");
 // sort scratch of a (stream, map): the stack at 0, the cubes' blocks of n + MP_SLACK from the
-// frame's scratch_tail; the level lists of a global-memory sort at 6 (offset / 16) ints
+// frame's scratch_tail; the level lists and the deferred list of a global-memory sort at
+// 9 (offset / 16) ints
 constexpr uint32_t MP_SLACK = 64;
-inline size_t mp_scratch(const MapperDev& D) { return (size_t)D.scratch_cap + MP_SLACK * (INS_SLOTS + 1); }
+// cubes from 0, the stack (its own region: it may run beside the previous frame's re-filter)
+// at mp_stack_offset
+__host__ __device__ inline size_t mp_cube_scratch(const MapperDev& D) {
+  return (size_t)D.scratch_cap + MP_SLACK * (INS_SLOTS + 1);
+}
+__host__ __device__ inline uint32_t mp_stack_offset(const MapperDev& D) { return (uint32_t)mp_cube_scratch(D); }
+inline size_t mp_scratch(const MapperDev& D) { return mp_cube_scratch(D) + (size_t)D.max_in + MP_SLACK; }
 template <typename PF>
 __device__ inline bool map_voxel_pcl(const MapperDev& D, size_t sm, uint32_t so, const PF& P, int n, float leaf,
                                      const VxPclOut& O, uint32_t* lds, int* err) {
-  const size_t ps = (size_t)D.scratch_cap + MP_SLACK * (INS_SLOTS + 1);
-  if ((size_t)so + (uint32_t)n + MP_SLACK > ps) {
+  const size_t ps = (size_t)D.scratch_cap + MP_SLACK * (INS_SLOTS + 1) + (size_t)D.max_in + MP_SLACK;
+  const size_t lim = so == mp_stack_offset(D) ? ps : mp_cube_scratch(D);  // cubes stay below the stack
+  if ((size_t)so + (uint32_t)n + MP_SLACK > lim) {
     if (threadIdx.x == 0) atomicOr(err, MAP_ERR_SORT);
     return false;
   }
@@ -242,12 +271,22 @@ __device__ inline bool map_voxel_pcl(const MapperDev& D, size_t sm, uint32_t so,
     const VxPclScratch X{E, A, B, D.ps + b, lev, {seg0, seg0 + 3 * MP_SEG_LDS}, MP_SEG_LDS, nullptr,
                          D.pdbg ? (so == 0 ? D.pdbg + 42 : D.pdbg + 11) : nullptr};
     voxel_grid_pcl<VX_THREADS>(P, n, leaf, O, X, M, ws, err);
-  } else {  // level lists in global memory, the LDS holds the waves' subtree sorts
+  } else {  // level lists in global memory; segments that fit the LDS are sorted there whole
     const int cap = (int)((n + MP_SLACK) / 16);
-    int* seg0 = D.pseg + sm * (6 * (ps / 16) + 6) + 6 * (so / 16);
+    int* seg0 = D.pseg + sm * (9 * (ps / 16) + 9) + 9 * (so / 16);
+    const VxPclDefer dfr{MP_LDS_N,
+                         seg0 + 6 * cap,
+                         cap,
+                         reinterpret_cast<uint64_t*>(lds),
+                         lds + 2 * MP_LDS_N,
+                         lds + 3 * MP_LDS_N,
+                         reinterpret_cast<int*>(lds + 4 * MP_LDS_N),
+                         reinterpret_cast<int*>(lds + 4 * MP_LDS_N) + 3 * MP_DEF_SEG,
+                         MP_DEF_SEG,
+                         reinterpret_cast<SsLevels*>(lds + VX_LDS_WORDS - 256 - 2 * MP_LEV_W)};
     const VxPclScratch X{D.pe + b, D.pa + b, D.pb + b, D.ps + b, lev, {seg0, seg0 + 3 * cap}, cap, lds,
                          D.pdbg ? (so == 0 ? D.pdbg + 42 : D.pdbg + 11) : nullptr};
-    voxel_grid_pcl<VX_THREADS>(P, n, leaf, O, X, M, ws, err);
+    voxel_grid_pcl<VX_THREADS, true>(P, n, leaf, O, X, M, ws, err, &dfr);
   }
   return true;
 }
@@ -259,15 +298,16 @@ __device__ inline bool map_voxel_pcl(const MapperDev& D, size_t sm, uint32_t so,
 __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
   const int s = D.s0 + (blockIdx.x >> 1), m = blockIdx.x & 1;
-  StreamFrame& F = D.fr[s];
-  if (!F.active) return;
+  const StackIn& I = D.sin[s];
+  if (!I.active) return;
   const size_t sm = sm_index(s, m);
+  int* err = &D.stk_err[s];
   if (D.pcl_order) {
     VxPclOut O;
     O.out = D.stack[m] + (size_t)s * D.max_in;
     O.cap = D.max_in;
-    O.res_cnt = reinterpret_cast<uint32_t*>(m == 0 ? &F.nc_stack : &F.ns_stack);
-    map_voxel_pcl(D, sm, 0u, VxPtrSrc{F.in_ptr[m]}, m == 0 ? F.nc_in : F.ns_in, D.leaf[m], O, lds, &F.err);
+    O.res_cnt = reinterpret_cast<uint32_t*>(&D.stk_n[2 * s + m]);
+    map_voxel_pcl(D, sm, mp_stack_offset(D), VxPtrSrc{I.p[m]}, I.n[m], D.leaf[m], O, lds, err);
     return;
   }
   VoxSeg S;
@@ -280,16 +320,16 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
   S.tail = nullptr;
   S.res_off = nullptr;
   S.scratch_tail = nullptr;
-  S.err = &F.err;
+  S.err = err;
   S.prof_seg = D.pdbg ? D.pdbg + 42 : nullptr;  // stack VoxelGrid phases: dbg[42..45]
-  S.src0 = F.in_ptr[m];
-  S.n0 = m == 0 ? F.nc_in : F.ns_in;
+  S.src0 = I.p[m];
+  S.n0 = I.n[m];
   S.out = D.stack[m] + (size_t)s * D.max_in;
   S.cap = D.max_in;
-  S.res_cnt = reinterpret_cast<uint32_t*>(m == 0 ? &F.nc_stack : &F.ns_stack);
-  S.scratch_pts = D.vx_pts + sm * D.scratch_cap;
-  S.scratch_idx = D.vx_idx + sm * D.scratch_cap;
-  S.scratch_cap = D.scratch_cap;
+  S.res_cnt = reinterpret_cast<uint32_t*>(&D.stk_n[2 * s + m]);
+  S.scratch_pts = D.stk_pts + sm * D.max_in;
+  S.scratch_idx = D.stk_idx + sm * D.max_in;
+  S.scratch_cap = D.max_in;
   voxel_segment(S, lds);
 }
 
@@ -306,13 +346,13 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_part(MapperDev D) {
   const int K = D.stack_k;
   const int j = blockIdx.x % K, pm = blockIdx.x / K;
   const int s = D.s0 + (pm >> 1), m = pm & 1;
-  StreamFrame& F = D.fr[s];
-  if (!F.active) return;
+  const StackIn& I = D.sin[s];
+  if (!I.active) return;
   const size_t sm = sm_index(s, m);
   uint2* part = D.stk_part + sm * STACK_K_MAX;
-  const uint32_t N = (uint32_t)(m == 0 ? F.nc_in : F.ns_in);
-  const VxSrc P{F.in_ptr[m], (int)N, nullptr};
-  float4* stage = D.vx_pts + sm * D.scratch_cap;
+  const uint32_t N = (uint32_t)I.n[m];
+  const VxSrc P{I.p[m], (int)N, nullptr};
+  float4* stage = D.stk_pts + sm * D.max_in;
   uint32_t* ws = lds + VX_LDS_WORDS - 256;
   VxMisc& M = *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192);
   const int tid = threadIdx.x;
@@ -368,7 +408,7 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_part(MapperDev D) {
     return;
   }
   VoxSeg S;
-  S.src0 = F.in_ptr[m];
+  S.src0 = I.p[m];
   S.n0 = (int)N;
   S.src1 = nullptr;
   S.tag1 = nullptr;
@@ -378,20 +418,20 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_part(MapperDev D) {
   S.append_only = 0;
   S.out = stage;
   S.tail = nullptr;
-  S.cap = (uint32_t)D.scratch_cap;
+  S.cap = (uint32_t)D.max_in;
   S.res_off = nullptr;
   S.res_cnt = nullptr;
   S.scratch_pts = nullptr;
-  S.scratch_idx = D.vx_idx + sm * D.scratch_cap;
+  S.scratch_idx = D.stk_idx + sm * D.max_in;
   S.scratch_tail = nullptr;
-  S.scratch_cap = (uint32_t)D.scratch_cap;
-  S.err = &F.err;
+  S.scratch_cap = (uint32_t)D.max_in;
+  S.err = &D.stk_err[s];
   int moved = 0;
   const uint32_t klo = blo(b0), khi = b1 >= (uint32_t)VX_NB ? 0xFFFFFFFFu : blo(b1);
-  const uint32_t U = vx_group(S, g, P, N, D.vx_idx + sm * D.scratch_cap + base, klo, khi, base,
+  const uint32_t U = vx_group(S, g, P, N, D.stk_idx + sm * D.max_in + base, klo, khi, base,
                               VX_LDS_WORDS - 256, lds, ws, M, &moved);
   if (tid == 0) {
-    if (U == VX_OVERFLOW) atomicOr(&F.err, MAP_ERR_STACK);
+    if (U == VX_OVERFLOW) atomicOr(&D.stk_err[s], MAP_ERR_STACK);
     part[j] = make_uint2(base, U == VX_OVERFLOW ? 0u : U);
   }
 }
@@ -399,11 +439,10 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_part(MapperDev D) {
 // the ranges of k_stack_part in idx order -> the stack and its count
 __global__ void __launch_bounds__(VX_THREADS) k_stack_cat(MapperDev D) {
   const int s = D.s0 + (blockIdx.x >> 1), m = blockIdx.x & 1;
-  StreamFrame& F = D.fr[s];
-  if (!F.active) return;
+  if (!D.sin[s].active) return;
   const size_t sm = sm_index(s, m);
   const uint2* part = D.stk_part + sm * STACK_K_MAX;
-  const float4* stage = D.vx_pts + sm * D.scratch_cap;
+  const float4* stage = D.stk_pts + sm * D.max_in;
   float4* out = D.stack[m] + (size_t)s * D.max_in;
   uint32_t o = 0;
   for (int j = 0; j < D.stack_k; ++j) {
@@ -411,9 +450,21 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_cat(MapperDev D) {
     for (uint32_t i = threadIdx.x; i < pj.y; i += VX_THREADS) out[o + i] = stage[pj.x + i];
     o += pj.y;
   }
-  if (threadIdx.x == 0) {
-    if (m == 0) F.nc_stack = (int)o;
-    else F.ns_stack = (int)o;
+  if (threadIdx.x == 0) D.stk_n[2 * s + m] = (int)o;
+}
+
+// the frame's stack sizes and stack-filter errors into its stream records (after the stack
+// kernels, which may have run while the previous frame was in flight)
+__global__ void k_stack_counts(MapperDev D) {
+  const int s = D.s0 + blockIdx.x;
+  StreamFrame& F = D.fr[s];
+  if (threadIdx.x != 0 || !F.active) return;
+  F.nc_stack = D.stk_n[2 * s];
+  F.ns_stack = D.stk_n[2 * s + 1];
+  const int e = D.stk_err[s];
+  if (e) {
+    F.err |= e;
+    D.stk_err[s] = 0;
   }
 }
 
@@ -1868,6 +1919,13 @@ struct HostStream {
   double q_hf[4] = {0, 0, 0, 1}, t_hf[3] = {0, 0, 0};
   bool pending = false, skip = false;
   bool solved_last = false;  // solved by the last loam_mapper_solve (loam_mapper_total_iterations)
+  // the input of the next solve (LaserMapping::input, laser_mapping.cpp:178-209), kept apart from
+  // the frame in flight (loam_mapper_solve_async) until that solve takes it
+  bool in_ready = false;
+  bool stk_launched = false;  // its stack VoxelGrid already queued (loam_mapper_prefetch)
+  const float4* in_p[2] = {nullptr, nullptr};
+  int in_n[2] = {0, 0};
+  double in_q[4] = {0, 0, 0, 1}, in_t[3] = {0, 0, 0};
   int frame = 0;
   loam_map_stats st{};
 };
@@ -1933,7 +1991,19 @@ struct loam_mapper {
   // hipGraph of the whole per-frame sequence (handles of <= 4 streams): one per cube-table
   // parity, used for frames without recentering, compaction, profiling or sharding
   int use_graph = 0;
-  hipGraphExec_t gexec[2] = {nullptr, nullptr};
+  hipGraphExec_t gexec[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [cube parity][stack parity]
+  // stack VoxelGrids ahead of their frame (loam_mapper_prefetch / loam_mapper_solve_async):
+  // stacks, their inputs and counts double-buffered by stack parity; spar: the next frame's
+  int spar = 0, last_spar = 0;
+  bool inflight = false;       // a frame enqueued by loam_mapper_solve_async, not yet waited for
+  bool last_graph = false;     // that frame ran as a graph
+  hipEvent_t ev_stack = nullptr;   // after the last stack launch (on st2)
+  hipEvent_t ev_sin[2] = {nullptr, nullptr};  // the H2D of hsin[parity] done
+  float4* stack_buf[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [parity][map]
+  int* stk_n_buf[2] = {nullptr, nullptr};
+  int* stk_err_buf[2] = {nullptr, nullptr};
+  StackIn* sin_buf[2] = {nullptr, nullptr};
+  PinnedArray<StackIn> hsin[2];
   // publish-side buffers (grown on demand)
   uint32_t* d_map_off = nullptr;  // [2 * NCUBE + 1]
   float4* d_pub = nullptr;
@@ -1967,9 +2037,13 @@ void free_all(loam_mapper* h) {
   if (h->d_pub) (void)hipFree(h->d_pub);
   h->d_pub = nullptr;
   h->pub_cap = 0;
-  for (auto& g : h->gexec)
-    if (g) (void)hipGraphExecDestroy(g);
+  for (auto& gp : h->gexec)
+    for (auto& g : gp)
+      if (g) (void)hipGraphExecDestroy(g);
   for (auto& e : h->ev_pool) (void)hipEventDestroy(e);
+  if (h->ev_stack) (void)hipEventDestroy(h->ev_stack);
+  for (auto& e : h->ev_sin)
+    if (e) (void)hipEventDestroy(e);
   h->ev_pool.clear();
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
@@ -2099,6 +2173,10 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     return fail(LOAM_ERR_HIP);
   for (auto& e : h->ev)
     if (hipEventCreate(&e) != hipSuccess) return fail(LOAM_ERR_HIP);
+  if (hipEventCreateWithFlags(&h->ev_stack, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_sin[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_sin[1], hipEventDisableTiming) != hipSuccess)
+    return fail(LOAM_ERR_HIP);
   // graphs pay off where launch gaps are the cost (B = 1: 0.750 -> 0.733 ms per frame); with
   // two handles of 64 streams, graph launches measured 20% slower (375k vs 470k iterations/s)
   h->use_graph = n_streams <= 4 ? 1 : 0;
@@ -2117,7 +2195,8 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   ALLOC(D.fr, B);
   for (int m = 0; m < 2; ++m) {
     ALLOC(D.in_pts[m], B * D.max_in);
-    ALLOC(D.stack[m], B * D.max_in);
+    for (int p = 0; p < 2; ++p) ALLOC(h->stack_buf[p][m], B * D.max_in);
+    D.stack[m] = h->stack_buf[0][m];
   }
   ALLOC(D.arena, B * 2 * 2 * (size_t)D.map_cap);
   ALLOC(D.carena, B * 2 * 2 * (size_t)D.map_cap);
@@ -2153,10 +2232,21 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     ALLOC(D.pa, B * 2 * ps);
     ALLOC(D.pb, B * 2 * ps);
     ALLOC(D.ps, B * 2 * ps);
-    ALLOC(D.pseg, B * 2 * (6 * (ps / 16) + 6));
+    ALLOC(D.pseg, B * 2 * (9 * (ps / 16) + 9));
   }
   ALLOC(D.vx_idx, B * 2 * (size_t)D.scratch_cap);
   ALLOC(D.stk_part, B * 2 * (size_t)STACK_K_MAX);
+  for (int p = 0; p < 2; ++p) {
+    ALLOC(h->stk_n_buf[p], B * 2);
+    ALLOC(h->stk_err_buf[p], B);
+    ALLOC(h->sin_buf[p], B);
+    if (!h->hsin[p].assign(B, StackIn{})) return fail(LOAM_ERR_HIP);
+  }
+  D.sin = h->sin_buf[0];
+  D.stk_n = h->stk_n_buf[0];
+  D.stk_err = h->stk_err_buf[0];
+  ALLOC(D.stk_pts, B * 2 * (size_t)D.max_in);
+  ALLOC(D.stk_idx, B * 2 * (size_t)D.max_in);
   ALLOC(D.tile_r, B * 2 * (size_t)D.max_in);
   ALLOC(D.tiles, B * 2 * (size_t)D.max_in);
   ALLOC(D.tile_q, B * 2 * (size_t)D.max_in);
@@ -2225,9 +2315,22 @@ int32_t loam_shard_owner(const float* xyz, float leaf, int32_t nrank) {
   return shard_owner(xyz[0], xyz[1], xyz[2], 1.0f / leaf, shard_block_voxels(leaf), nrank);
 }
 
+static int32_t mapper_finish(loam_mapper* h);
+// a frame enqueued by loam_mapper_solve_async is finished before anything reads or changes the
+// handle's state
+#define SETTLE(h)                                \
+  do {                                           \
+    if ((h) && (h)->inflight) {                  \
+      LOAM_HIP(hipSetDevice((h)->dev));          \
+      TRY(mapper_finish(h));                     \
+    }                                            \
+  } while (0)
+
 int32_t loam_mapper_destroy(loam_mapper* h) {
   if (!h) return LOAM_ERR_ARG;
   (void)hipSetDevice(h->dev);
+  if (h->inflight) (void)mapper_finish(h);
+  (void)hipStreamSynchronize(h->st2);
   free_all(h);
   delete h;
   return LOAM_OK;
@@ -2235,7 +2338,9 @@ int32_t loam_mapper_destroy(loam_mapper* h) {
 
 int32_t loam_mapper_reset(loam_mapper* h) {
   if (!h) return LOAM_ERR_ARG;
+  SETTLE(h);
   LOAM_HIP(hipSetDevice(h->dev));
+  LOAM_HIP(hipStreamSynchronize(h->st2));  // stacks queued ahead are dropped with their inputs
   for (int p = 0; p < 2; ++p)
     LOAM_HIP(hipMemsetAsync(h->cube_tab[p], 0, sizeof(uint2) * h->B * 2 * NCUBE, h->st));
   LOAM_HIP(hipMemsetAsync(h->D.stable_tok, 0, sizeof(uint32_t) * h->B * 2 * NCUBE, h->st));
@@ -2249,6 +2354,9 @@ int32_t loam_mapper_reset(loam_mapper* h) {
   return LOAM_OK;
 }
 
+// LaserMapping::input (laser_mapping.cpp:178-209): the clouds and odometry pose of the next
+// solve.  Kept apart from a frame in flight (loam_mapper_solve_async): the solve that takes it
+// computes the initial guess (:206-207) once the previous frame's transformUpdate is known.
 static int32_t mapper_input_common(loam_mapper* h, int32_t s, const float* corner, int32_t nc,
                                    const float* surf, int32_t ns, const double* q_wodom,
                                    const double* t_wodom, int32_t skip, hipMemcpyKind kind) {
@@ -2263,34 +2371,39 @@ static int32_t mapper_input_common(loam_mapper* h, int32_t s, const float* corne
   }
   LOAM_HIP(hipSetDevice(h->dev));
   HostStream& H = h->hs[s];
-  for (int i = 0; i < 4; ++i) H.q_wodom[i] = q_wodom[i];
-  for (int i = 0; i < 3; ++i) H.t_wodom[i] = t_wodom[i];
-  H.skip = skip != 0;
-  if (H.skip) {  // laser_mapping.cpp:197-201: high-frequency pose only
+  if (skip) {  // laser_mapping.cpp:197-201: high-frequency pose only (needs the last transformUpdate)
+    if (h->inflight) TRY(mapper_finish(h));
+    for (int i = 0; i < 4; ++i) H.q_wodom[i] = q_wodom[i];
+    for (int i = 0; i < 3; ++i) H.t_wodom[i] = t_wodom[i];
+    H.skip = true;
     double pose[7];
     host_initial_guess(H, pose);
     for (int i = 0; i < 4; ++i) H.q_hf[i] = pose[i];
     for (int i = 0; i < 3; ++i) H.t_hf[i] = pose[4 + i];
-    H.pending = false;
+    H.in_ready = false;
+    H.stk_launched = false;
     return LOAM_OK;
   }
-  StreamFrame& F = h->hf[s];
-  F.nc_in = nc;
-  F.ns_in = ns;
   if (kind == hipMemcpyHostToDevice) {
-    // LaserMapping::input deep-copies the clouds (laser_mapping.cpp:188-190)
-    F.in_ptr[0] = h->D.in_pts[0] + (size_t)s * h->D.max_in;
-    F.in_ptr[1] = h->D.in_pts[1] + (size_t)s * h->D.max_in;
-    if (nc) LOAM_HIP(hipMemcpyAsync((void*)F.in_ptr[0], corner, sizeof(float4) * nc, kind, h->st));
-    if (ns) LOAM_HIP(hipMemcpyAsync((void*)F.in_ptr[1], surf, sizeof(float4) * ns, kind, h->st));
+    // LaserMapping::input deep-copies the clouds (:188-190); on the stack stream, after any
+    // stack still reading the staging buffer
+    H.in_p[0] = h->D.in_pts[0] + (size_t)s * h->D.max_in;
+    H.in_p[1] = h->D.in_pts[1] + (size_t)s * h->D.max_in;
+    if (nc) LOAM_HIP(hipMemcpyAsync((void*)H.in_p[0], corner, sizeof(float4) * nc, kind, h->st2));
+    if (ns) LOAM_HIP(hipMemcpyAsync((void*)H.in_p[1], surf, sizeof(float4) * ns, kind, h->st2));
   } else {
-    // HBM-resident clouds are read in place: they must stay valid until loam_mapper_solve
-    // returns (no copy, like the output() aliasing of scan_registration.cpp:572-576)
-    F.in_ptr[0] = reinterpret_cast<const float4*>(corner);
-    F.in_ptr[1] = reinterpret_cast<const float4*>(surf);
+    // HBM-resident clouds are read in place: they must stay valid until the stack VoxelGrid has
+    // read them (loam_mapper_solve returns, or the wait after loam_mapper_solve_async)
+    H.in_p[0] = reinterpret_cast<const float4*>(corner);
+    H.in_p[1] = reinterpret_cast<const float4*>(surf);
   }
-  host_initial_guess(H, H.pose);
-  H.pending = true;
+  H.in_n[0] = nc;
+  H.in_n[1] = ns;
+  for (int i = 0; i < 4; ++i) H.in_q[i] = q_wodom[i];
+  for (int i = 0; i < 3; ++i) H.in_t[i] = t_wodom[i];
+  H.skip = false;
+  H.in_ready = true;
+  H.stk_launched = false;
   return LOAM_OK;
 }
 
@@ -2351,6 +2464,7 @@ int32_t loam_mapper_input_device_batch(loam_mapper* h, int32_t n, const int32_t*
 
 int64_t loam_mapper_total_iterations(loam_mapper* h) {
   if (!h) return LOAM_ERR_ARG;
+  SETTLE(h);
   int64_t it = 0;
   for (int s = 0; s < h->B; ++s)
     if (h->hs[s].solved_last) it += h->hs[s].st.lm[0].iterations + h->hs[s].st.lm[1].iterations;
@@ -2358,17 +2472,86 @@ int64_t loam_mapper_total_iterations(loam_mapper* h) {
 }
 
 int32_t loam_mapper_stats_all(loam_mapper* h, loam_map_stats* out, int32_t n) {
+  SETTLE(h);
   if (!h || !out || n < 0 || n > h->B) return LOAM_ERR_ARG;
   for (int s = 0; s < n; ++s) out[s] = h->hs[s].st;
   return LOAM_OK;
 }
 
-int32_t loam_mapper_solve(loam_mapper* h) {
+// The stack VoxelGrids (laser_mapping.cpp:492-500) of every stream whose input has none queued
+// yet, in one launch on the stack stream, into the stack buffers of the next frame's parity.
+// They read only the frame's body-frame input, so they may run beside a frame in flight.
+static int32_t launch_stacks(loam_mapper* h) {
+  const int par = h->spar, B = h->B;
+  bool any = false;
+  LOAM_HIP(hipEventSynchronize(h->ev_sin[par]));  // the last copy out of hsin[par] is done
+  StackIn* in = h->hsin[par].data();
+  for (int s = 0; s < B; ++s) {
+    HostStream& H = h->hs[s];
+    const bool go = H.in_ready && !H.stk_launched;
+    in[s].active = go ? 1 : 0;
+    if (!go) continue;
+    any = true;
+    H.stk_launched = true;
+    for (int m = 0; m < 2; ++m) {
+      in[s].p[m] = H.in_p[m];
+      in[s].n[m] = H.in_n[m];
+    }
+  }
+  if (!any) return LOAM_OK;
+  MapperDev D = h->D;
+  D.sin = h->sin_buf[par];
+  D.stk_n = h->stk_n_buf[par];
+  D.stk_err = h->stk_err_buf[par];
+  for (int m = 0; m < 2; ++m) D.stack[m] = h->stack_buf[par][m];
+  hipStream_t s2 = h->st2;
+  LOAM_HIP(hipMemcpyAsync(h->sin_buf[par], in, sizeof(StackIn) * B, hipMemcpyHostToDevice, s2));
+  LOAM_HIP(hipEventRecord(h->ev_sin[par], s2));
+  if (D.stack_k) {
+    LAUNCH_ON(s2, FAM_STACK, k_stack_part<<<B * 2 * D.stack_k, VX_THREADS, 0, s2>>>(D));
+    LAUNCH_ON(s2, FAM_STACK, k_stack_cat<<<B * 2, VX_THREADS, 0, s2>>>(D));
+  } else {
+    LAUNCH_ON(s2, FAM_STACK, k_stack_ds<<<B * 2, VX_THREADS, 0, s2>>>(D));
+  }
+  LOAM_HIP(hipGetLastError());
+  LOAM_HIP(hipEventRecord(h->ev_stack, s2));
+  return LOAM_OK;
+}
+
+int32_t loam_mapper_prefetch(loam_mapper* h) {
   if (!h) return LOAM_ERR_ARG;
-  h->ev_fam.clear();
   LOAM_HIP(hipSetDevice(h->dev));
+  if (h->prof) return LOAM_OK;  // with profiling, stacks are timed inside their frame
+  return launch_stacks(h);
+}
+
+// Enqueue one solveMapping of every stream with an input (the work of loam_mapper_solve up to
+// the host bookkeeping, which mapper_finish does)
+static int32_t mapper_enqueue(loam_mapper* h) {
+  h->ev_fam.clear();
   MapperDev& D = h->D;
   const int B = h->B;
+  TRY(launch_stacks(h));  // inputs not prefetched
+  const int fpar = h->spar;  // the stack parity of this frame
+  D.sin = h->sin_buf[fpar];
+  D.stk_n = h->stk_n_buf[fpar];
+  D.stk_err = h->stk_err_buf[fpar];
+  for (int m = 0; m < 2; ++m) D.stack[m] = h->stack_buf[fpar][m];
+  for (int s = 0; s < B; ++s) {  // the inputs become the frame; initial guess (:206-207)
+    HostStream& H = h->hs[s];
+    StreamFrame& F = h->hf[s];
+    H.pending = H.in_ready;
+    if (!H.in_ready) continue;
+    for (int i = 0; i < 4; ++i) H.q_wodom[i] = H.in_q[i];
+    for (int i = 0; i < 3; ++i) H.t_wodom[i] = H.in_t[i];
+    F.in_ptr[0] = H.in_p[0];
+    F.in_ptr[1] = H.in_p[1];
+    F.nc_in = H.in_n[0];
+    F.ns_in = H.in_n[1];
+    host_initial_guess(H, H.pose);
+    H.in_ready = false;
+    H.stk_launched = false;
+  }
   bool any = false, any_shift = false;
   for (int s = 0; s < B; ++s) {
     StreamFrame& F = h->hf[s];
@@ -2408,11 +2591,8 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   if (!any) return LOAM_OK;
   h->frame_counter++;
   D.epoch = h->frame_counter;
-  for (int s = 0; s < B; ++s) h->hf[s].epoch = h->frame_counter;
-  std::vector<uint32_t> tail0(2 * B);
   for (int s = 0; s < B; ++s) {
-    tail0[2 * s] = h->hf[s].arena_tail[0];
-    tail0[2 * s + 1] = h->hf[s].arena_tail[1];
+    h->hf[s].epoch = h->frame_counter;
     h->hf[s].cand[0] = h->hf[s].cand[1] = 0;
   }
   D.cube_tab = h->cube_tab[h->parity];
@@ -2426,23 +2606,13 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     // stream) beside the submap prep, 2 x (kNN, geometry, LM round), insertion, re-VoxelGrid,
     // records D2H.  Every kernel argument is fixed per (handle, parity): the frame's values
     // travel in the stream records.
-    hipGraphExec_t& ge = h->gexec[h->parity];
+    hipGraphExec_t& ge = h->gexec[h->parity][fpar];
     if (!ge) {
-      hipStream_t s2 = h->st2;
       hipGraph_t gr = nullptr;
       LOAM_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
       LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(StreamFrame) * B, hipMemcpyHostToDevice, st));
-      LOAM_HIP(hipEventRecord(h->ev_fork, st));
-      LOAM_HIP(hipStreamWaitEvent(s2, h->ev_fork, 0));
-      if (D.stack_k) {
-        k_stack_part<<<B * 2 * D.stack_k, VX_THREADS, 0, s2>>>(D);
-        k_stack_cat<<<B * 2, VX_THREADS, 0, s2>>>(D);
-      } else {
-        k_stack_ds<<<B * 2, VX_THREADS, 0, s2>>>(D);
-      }
-      LOAM_HIP(hipEventRecord(h->ev_join, s2));
       k_submap_prep<<<B, 128, 0, st>>>(D);
-      LOAM_HIP(hipStreamWaitEvent(st, h->ev_join, 0));
+      k_stack_counts<<<B, 64, 0, st>>>(D);
       for (int round = 0; round < 2; ++round) {
         if (h->knn_tile) {
           k_tile_bin<<<B * 2, TB_THREADS, 0, st>>>(D, round);
@@ -2464,10 +2634,10 @@ int32_t loam_mapper_solve(loam_mapper* h) {
       (void)hipGraphDestroy(gr);
       LOAM_HIP(ie);
     }
+    LOAM_HIP(hipStreamWaitEvent(st, h->ev_stack, 0));  // the frame's stacks
     LOAM_HIP(hipEventRecord(h->ev[0], st));
     LOAM_HIP(hipGraphLaunch(ge, st));
     LOAM_HIP(hipEventRecord(h->ev[3], st));
-    LOAM_HIP(hipStreamSynchronize(st));
   }
   if (!graph) {
   LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(StreamFrame) * B, hipMemcpyHostToDevice, st));
@@ -2480,18 +2650,9 @@ int32_t loam_mapper_solve(loam_mapper* h) {
     k_compact_commit<<<B * 2, 256, 0, st>>>(D, h->d_new_off);
     LOAM_HIP(hipGetLastError());
   }
-  // stack VoxelGrid (reads only this frame's inputs) on the second stream, overlapping the cube
-  // shift and submap preparation; joined before the correspondences
-  hipStream_t s2 = h->st2;
-  LOAM_HIP(hipEventRecord(h->ev_fork, st));
-  LOAM_HIP(hipStreamWaitEvent(s2, h->ev_fork, 0));
-  if (D.stack_k) {
-    LAUNCH_ON(s2, FAM_STACK, k_stack_part<<<B * 2 * D.stack_k, VX_THREADS, 0, s2>>>(D));
-    LAUNCH_ON(s2, FAM_STACK, k_stack_cat<<<B * 2, VX_THREADS, 0, s2>>>(D));
-  } else {
-    LAUNCH_ON(s2, FAM_STACK, k_stack_ds<<<B * 2, VX_THREADS, 0, s2>>>(D));
-  }
-  LOAM_HIP(hipEventRecord(h->ev_join, s2));
+  // the stack VoxelGrids run on the second stream (launch_stacks: at prefetch, or at the start
+  // of this solve), overlapping the cube shift and submap preparation; joined before the
+  // correspondences
   if (any_shift) {
     LAUNCH(FAM_OTHER, k_shift_cubes<<<dim3(16, B), 256, 0, st>>>(D, h->cube_tab[h->parity],
                                                                  h->cube_tab[1 - h->parity], h->tok_tmp));
@@ -2506,7 +2667,8 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   }
   LAUNCH(FAM_OTHER, k_submap_prep<<<B, 128, 0, st>>>(D));
   LOAM_HIP(hipEventRecord(h->ev[1], st));
-  LOAM_HIP(hipStreamWaitEvent(st, h->ev_join, 0));
+  LOAM_HIP(hipStreamWaitEvent(st, h->ev_stack, 0));
+  LAUNCH(FAM_OTHER, k_stack_counts<<<B, 64, 0, st>>>(D));
   size_t q_tot = 0;
   if (multi) {
     // the stack sizes (identical on every rank) place each stream's queries in the exchange
@@ -2561,8 +2723,22 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   LOAM_HIP(hipGetLastError());
   LOAM_HIP(hipEventRecord(h->ev[3], st));
   LOAM_HIP(hipMemcpyAsync(h->hf.data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
-  LOAM_HIP(hipStreamSynchronize(st));
   }  // !graph
+  h->inflight = true;
+  h->last_graph = graph;
+  h->last_spar = fpar;
+  h->spar ^= 1;  // the next frame's stacks go to the other buffers
+  return LOAM_OK;
+}
+
+// wait for the frame in flight, then the host side of solveMapping: transformUpdate (:147-151),
+// stats, errors, timing
+static int32_t mapper_finish(loam_mapper* h) {
+  h->inflight = false;
+  MapperDev& D = h->D;
+  const int B = h->B;
+  const bool graph = h->last_graph;
+  LOAM_HIP(hipStreamSynchronize(h->st));
   float ms_total = 0, ms_opt = 0;
   LOAM_HIP(hipEventElapsedTime(&ms_total, h->ev[0], h->ev[3]));
   if (graph) ms_opt = ms_total;  // no event inside the graph (the optimisation block is most of it)
@@ -2635,7 +2811,27 @@ int32_t loam_mapper_solve(loam_mapper* h) {
   return status;
 }
 
+int32_t loam_mapper_solve_async(loam_mapper* h) {
+  if (!h) return LOAM_ERR_ARG;
+  LOAM_HIP(hipSetDevice(h->dev));
+  if (h->inflight) TRY(mapper_finish(h));
+  return mapper_enqueue(h);
+}
+
+int32_t loam_mapper_wait(loam_mapper* h) {
+  if (!h) return LOAM_ERR_ARG;
+  if (!h->inflight) return LOAM_OK;
+  LOAM_HIP(hipSetDevice(h->dev));
+  return mapper_finish(h);
+}
+
+int32_t loam_mapper_solve(loam_mapper* h) {
+  TRY(loam_mapper_solve_async(h));
+  return loam_mapper_wait(h);
+}
+
 int32_t loam_mapper_debug_counters(loam_mapper* h, uint64_t* out, int32_t n, int32_t reset) {
+  SETTLE(h);
   if (!h || !out || n < 0 || n > LOAM_DEBUG_COUNTERS) return LOAM_ERR_ARG;
   LOAM_HIP(hipSetDevice(h->dev));
   LOAM_HIP(hipStreamSynchronize(h->st));
@@ -2645,12 +2841,14 @@ int32_t loam_mapper_debug_counters(loam_mapper* h, uint64_t* out, int32_t n, int
 }
 
 int32_t loam_mapper_set_profiling(loam_mapper* h, int32_t enable) {
+  SETTLE(h);
   if (!h) return LOAM_ERR_ARG;
   h->prof = enable != 0;
   return LOAM_OK;
 }
 
 int32_t loam_mapper_kernel_times(loam_mapper* h, loam_kernel_times* out) {
+  SETTLE(h);
   if (!h || !out) return LOAM_ERR_ARG;
   for (int f = 0; f < LOAM_KFAM_COUNT; ++f) {
     out->ms[f] = f < NFAM ? h->fam_ms[f] : 0.0;
@@ -2661,6 +2859,7 @@ int32_t loam_mapper_kernel_times(loam_mapper* h, loam_kernel_times* out) {
 }
 
 int32_t loam_mapper_reset_kernel_times(loam_mapper* h) {
+  SETTLE(h);
   if (!h) return LOAM_ERR_ARG;
   for (int f = 0; f < NFAM; ++f) {
     h->fam_ms[f] = h->fam_bytes[f] = 0.0;
@@ -2670,6 +2869,7 @@ int32_t loam_mapper_reset_kernel_times(loam_mapper* h) {
 }
 
 int32_t loam_mapper_pose(loam_mapper* h, int32_t s, double* q_w, double* t_w) {
+  SETTLE(h);
   TRY(check_stream(h, s));
   if (!q_w || !t_w) return LOAM_ERR_ARG;
   const HostStream& H = h->hs[s];
@@ -2684,6 +2884,7 @@ int32_t loam_mapper_pose(loam_mapper* h, int32_t s, double* q_w, double* t_w) {
 }
 
 int32_t loam_mapper_stats(loam_mapper* h, int32_t s, loam_map_stats* st) {
+  SETTLE(h);
   TRY(check_stream(h, s));
   if (!st) return LOAM_ERR_ARG;
   *st = h->hs[s].st;
@@ -2691,6 +2892,7 @@ int32_t loam_mapper_stats(loam_mapper* h, int32_t s, loam_map_stats* st) {
 }
 
 int32_t loam_mapper_get_state(loam_mapper* h, int32_t s, int32_t* cen, double* q, double* t) {
+  SETTLE(h);
   TRY(check_stream(h, s));
   if (!cen || !q || !t) return LOAM_ERR_ARG;
   for (int a = 0; a < 3; ++a) cen[a] = h->hf[s].cen[a];
@@ -2714,6 +2916,7 @@ static int32_t build_cube_index(loam_mapper* h, int32_t s, int32_t m, int32_t c0
 }
 
 int32_t loam_mapper_set_state(loam_mapper* h, int32_t s, const int32_t* cen, const double* q, const double* t) {
+  SETTLE(h);
   TRY(check_stream(h, s));
   if (!cen || !q || !t) return LOAM_ERR_ARG;
   bool moved = false;
@@ -2729,6 +2932,7 @@ int32_t loam_mapper_set_state(loam_mapper* h, int32_t s, const int32_t* cen, con
 }
 
 int32_t loam_mapper_cube_count(loam_mapper* h, int32_t s, int32_t which, int32_t cube) {
+  SETTLE(h);
   TRY(check_stream(h, s));
   if (which < 0 || which > 1 || cube < 0 || cube >= NCUBE) return LOAM_ERR_ARG;
   LOAM_HIP(hipSetDevice(h->dev));
@@ -2738,6 +2942,7 @@ int32_t loam_mapper_cube_count(loam_mapper* h, int32_t s, int32_t which, int32_t
 }
 
 int32_t loam_mapper_cube_copy(loam_mapper* h, int32_t s, int32_t which, int32_t cube, float* out) {
+  SETTLE(h);
   TRY(check_stream(h, s));
   if (which < 0 || which > 1 || cube < 0 || cube >= NCUBE || !out) return LOAM_ERR_ARG;
   LOAM_HIP(hipSetDevice(h->dev));
@@ -2749,18 +2954,21 @@ int32_t loam_mapper_cube_copy(loam_mapper* h, int32_t s, int32_t which, int32_t 
 }
 
 int32_t loam_mapper_stack_copy(loam_mapper* h, int32_t s, int32_t which, float* out, int32_t cap) {
+  SETTLE(h);
   TRY(check_stream(h, s));
   if (which < 0 || which > 1 || (cap > 0 && !out)) return LOAM_ERR_ARG;
   LOAM_HIP(hipSetDevice(h->dev));
   const int32_t n = which == 0 ? h->hf[s].nc_stack : h->hf[s].ns_stack;
   if (n > cap) return n;  // the count only
   if (n) {
-    LOAM_HIP(hipMemcpy(out, h->D.stack[which] + (size_t)s * h->D.max_in, sizeof(float4) * n, hipMemcpyDeviceToHost));
+    LOAM_HIP(hipMemcpy(out, h->stack_buf[h->last_spar][which] + (size_t)s * h->D.max_in, sizeof(float4) * n,
+                       hipMemcpyDeviceToHost));
   }
   return n;
 }
 
 int32_t loam_mapper_cube_set(loam_mapper* h, int32_t s, int32_t which, int32_t cube, const float* pts, int32_t n) {
+  SETTLE(h);
   TRY(check_stream(h, s));
   if (which < 0 || which > 1 || cube < 0 || cube >= NCUBE || n < 0 || (n > 0 && !pts)) return LOAM_ERR_ARG;
   LOAM_HIP(hipSetDevice(h->dev));
@@ -2792,14 +3000,13 @@ static int32_t pub_reserve(loam_mapper* h, size_t n) {
   if (h->d_pub) (void)hipFree(h->d_pub);
   h->d_pub = nullptr;
   h->pub_cap = 0;
-  for (auto& g : h->gexec)
-    if (g) (void)hipGraphExecDestroy(g);
   LOAM_HIP(hipMalloc(&h->d_pub, sizeof(float4) * std::max<size_t>(n, 1)));
   h->pub_cap = n;
   return LOAM_OK;
 }
 
 int32_t loam_mapper_map_copy(loam_mapper* h, int32_t s, float* out, int64_t cap) {
+  SETTLE(h);
   TRY(check_stream(h, s));
   if (cap < 0 || (cap > 0 && !out)) return LOAM_ERR_ARG;
   LOAM_HIP(hipSetDevice(h->dev));
@@ -2844,10 +3051,12 @@ static int32_t register_common(loam_mapper* h, int32_t s, const float* in, int32
 }
 
 int32_t loam_mapper_register_cloud(loam_mapper* h, int32_t s, const float* in, int32_t n, float* out) {
+  SETTLE(h);
   return register_common(h, s, in, n, out, false);
 }
 
 int32_t loam_mapper_register_cloud_device(loam_mapper* h, int32_t s, const float* d_in, int32_t n, float* d_out) {
+  SETTLE(h);
   return register_common(h, s, d_in, n, d_out, true);
 }
 

@@ -108,6 +108,18 @@ class BatchMapper:
     def solve(self):
         check(lib().loam_mapper_solve(self.h))
 
+    def solve_async(self):
+        """enqueue solveMapping for the streams with an input and return (include/loam_core.h);
+        results after wait() (every other call waits first)"""
+        check(lib().loam_mapper_solve_async(self.h))
+
+    def wait(self):
+        check(lib().loam_mapper_wait(self.h))
+
+    def prefetch(self):
+        """queue the stack VoxelGrids of the pending inputs now, beside a frame in flight"""
+        check(lib().loam_mapper_prefetch(self.h))
+
     def set_profiling(self, enable=True):
         check(lib().loam_mapper_set_profiling(self.h, int(enable)))
 
