@@ -79,6 +79,9 @@ def parse():
                          "library default; maps differ by summation-order ulps)")
     ap.add_argument("--shard-streams", type=int, default=32,
                     help="streams of the sharded leg (every stream split over all ranks; 0: skip the leg)")
+    ap.add_argument("--pipelined", action="store_true",
+                    help="one handle: the timed steps queue step k + 1's input and stack VoxelGrid while step k is "
+                         "in flight (loam_mapper_solve_async; for kernel traces of the single-stream mode)")
     ap.add_argument("--no-exact-leg", action="store_true",
                     help="skip the second (exact_voxel_order = 1) measurement of the same workload")
     ap.add_argument("--shard", action="store_true",
@@ -699,7 +702,10 @@ def main():
             m.reset_kernel_times()
         barrier()
         t0 = time.perf_counter()
-        it = run_handles(mappers, plans, pre, K, poses)
+        if args.pipelined and H == 1:
+            it = run_steps_pipelined(mappers[0], plans[0], pre, K)
+        else:
+            it = run_handles(mappers, plans, pre, K, poses)
         barrier()
         secs = time.perf_counter() - t0
         fam = {}

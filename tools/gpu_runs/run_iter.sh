@@ -12,4 +12,4 @@ cd /tmp && export TMPDIR=/tmp && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- \
   python3 "$R/bench.py" $A > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof_bench.err" && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof1" -o run --output-format csv -- \
-  python3 "$R/bench.py" $A --streams 1 --handles 1 --steps 30 > "$R/gpurun_out/prof1_bench.json" 2> "$R/gpurun_out/prof1_bench.err"
+  python3 "$R/bench.py" $A --streams 1 --handles 1 --steps 30 --pipelined --no-prof > "$R/gpurun_out/prof1_bench.json" 2> "$R/gpurun_out/prof1_bench.err"

@@ -1,4 +1,8 @@
-"""Print one step of a rocprofv3 kernel trace (between the last k_revox launches) with gaps."""
+"""Print one step of a rocprofv3 kernel trace (between the last k_revox launches) with gaps.
+
+    python tools/timeline.py [kernel_trace.csv] [steps back]
+
+Overlapping kernels (the stack VoxelGrid of the next frame beside this one) show a negative gap."""
 import csv
 import sys
 

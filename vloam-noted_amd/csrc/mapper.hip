@@ -171,6 +171,7 @@ struct MapperDev {
   uint32_t* tile_tab;    // [B][2][tile_tab_n] the tile hash of stacks too large for the LDS table
   uint32_t tile_tab_n = 0;
   int tk_blk = 32;       // k_knn_tile workgroups per stream
+  int knn_blk = CORR_BLK;  // k_knn workgroups per stream of the cell-split variant
 };
 
 // one query's 5 nearest candidates on one rank (d: FLANN L2_Simple float distance, id: global
@@ -564,7 +565,12 @@ __device__ inline void corr_block(const MapperDev& D, int* s, int* blk) {
 #ifndef KNN_WAVES
 #define KNN_WAVES 7  // 72 VGPRs, 20 B spill outside the cell loop: 6 -> 7 waves, correspondence -8%
 #endif
-template <int L>
+// CS (cell split): the L lanes of a query take different cells, lane g the cells g, g + L, ...
+// of the nearest-first order, each scanning all of its cell's points, with the group minimum of
+// their 5th distances as the shared pruning bound: a query's chain of dependent probes is 27 / L
+// steps long instead of 27 (few streams leave the chip mostly idle: latency, not issue, bounds
+// the search).  Without CS the lanes share each cell and split its points.
+template <int L, bool CS = false>
 __global__ void __launch_bounds__(CORR_THREADS) __attribute__((amdgpu_waves_per_eu(KNN_WAVES, 8))) k_knn(MapperDev D, int round) {
   __shared__ WinMap W[2];
   __shared__ int slot_of[75];  // 5 x 5 x 3 window position -> slot (laserCloudValidInd order)
@@ -600,7 +606,8 @@ __global__ void __launch_bounds__(CORR_THREADS) __attribute__((amdgpu_waves_per_
   const size_t rb = (size_t)s * 2 * D.max_in;
   uint32_t ncand = 0;
   const int gsub = tid % L;
-  for (int ridx = blk * (CORR_THREADS / L) + tid / L; ridx < nc + ns; ridx += CORR_BLK * (CORR_THREADS / L)) {
+  const int nblk = CS ? D.knn_blk : CORR_BLK;
+  for (int ridx = blk * (CORR_THREADS / L) + tid / L; ridx < nc + ns; ridx += nblk * (CORR_THREADS / L)) {
     const int m = ridx < nc ? 0 : 1;  // corners [0, nc), surfs [nc, nc + ns)
     const int qi = m == 0 ? ridx : ridx - nc;
     const float4 q = to_map(X, D.stack[m][(size_t)s * D.max_in + qi]);
@@ -632,7 +639,7 @@ __global__ void __launch_bounds__(CORR_THREADS) __attribute__((amdgpu_waves_per_
                               (uint32_t)ax | ((uint32_t)ay << 6) | ((uint32_t)az << 12));
       ncand += e.y;
       const int sub = WM.sub[sl];
-      for (uint32_t k = gsub; k < e.y; k += L) {
+      for (uint32_t k = CS ? 0 : gsub; k < e.y; k += CS ? 1 : L) {
         const uint32_t pos = off + e.x + k;
         const float4 p = cp[pos];
         // sharded: submap position x ranks + rank keeps the key unique (and equal to the
@@ -641,16 +648,17 @@ __global__ void __launch_bounds__(CORR_THREADS) __attribute__((amdgpu_waves_per_
         near5_offer(T, fdist2(q.x, q.y, q.z, p.x, p.y, p.z), key, (int)pos);
       }
     };
-    for (int o = 0; o < 27; ++o) {
-      const uint32_t code = cell_order_code(o);
+    for (int ob = 0; ob < 27; ob += CS ? L : 1) {
+      const int o = CS ? ob + gsub : ob;
+      const uint32_t code = cell_order_code(o < 27 ? o : 0);
       const int dx = (int)(code & 3u) - 1, dy = (int)((code >> 2) & 3u) - 1, dz = (int)(code >> 4) - 1;
       const float gx = dx < 0 ? lx : (dx > 0 ? hx : 0.f);
       const float gy = dy < 0 ? ly : (dy > 0 ? hy : 0.f);
       const float gz = dz < 0 ? lz : (dz > 0 ? hz : 0.f);
       float bound = fminf(T.d[4], 1.0f) * 1.01f + 1e-6f;  // rounding margin
 #pragma unroll
-      for (int o = 1; o < L; o <<= 1) bound = fminf(bound, __shfl_xor(bound, o, 64));
-      if (gx * gx + gy * gy + gz * gz > bound) continue;
+      for (int o2 = 1; o2 < L; o2 <<= 1) bound = fminf(bound, __shfl_xor(bound, o2, 64));
+      if (o >= 27 || gx * gx + gy * gy + gz * gz > bound) continue;
       const int x = qx + dx, y = qy + dy, z = qz + dz;
       const int bi = floor_div50(x + 25) + F.cen[0], bj = floor_div50(y + 25) + F.cen[1],
                 bk = floor_div50(z + 25) + F.cen[2];
@@ -1985,6 +1993,7 @@ struct loam_mapper {
   int lm_G = 0;  // workgroups per stream of k_lm_round (0: two-kernel path k_lm_eval / k_lm_step)
   int knn_lanes = 1;  // lanes per query of k_knn (1, or 2 for handles of <= 4 streams)
   int knn_tile = 0;   // LOAM_KNN_TILE=1: the tile kNN (k_tile_bin + k_knn_tile) instead of k_knn
+  int knn_cs = 0;     // lanes per query of k_knn's cell split (8 for <= 4 streams; LOAM_KNN_CS)
   loam_comm* comm = nullptr;  // sharded mode (loam_mapper_create_sharded)
   PinnedArray<int> q_off;     // [B + 1] query offsets of the sharded kNN exchange
   int* d_q_off = nullptr;
@@ -2191,6 +2200,14 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     D.tk_blk = n_streams <= 4 ? 256 : 16;  // few streams: about one tile per wave
     const char* benv = std::getenv("LOAM_TK_BLK");  // measurement override
     if (benv && std::atoi(benv) > 0) D.tk_blk = std::atoi(benv);
+    // cell split at few streams: B = 1 correspondence search 67.8 -> 35.6 us per round (8 lanes;
+    // 4 lanes 43.4, 16 lanes 41.3); at B = 128 it costs 1.2x (more lanes idle on pruned cells)
+    const char* cenv = std::getenv("LOAM_KNN_CS");  // measurement override (0: point split)
+    const int cs = cenv ? std::atoi(cenv) : (n_streams <= 4 ? 8 : 0);
+    h->knn_cs = (cs == 4 || cs == 8 || cs == 16) ? cs : 0;
+    D.knn_blk = n_streams <= 4 ? 4 * CORR_BLK : CORR_BLK;
+    const char* kenv = std::getenv("LOAM_KNN_BLK");  // measurement override
+    if (kenv && std::atoi(kenv) > 0) D.knn_blk = std::atoi(kenv);
   }
   ALLOC(D.fr, B);
   for (int m = 0; m < 2; ++m) {
@@ -2617,6 +2634,12 @@ static int32_t mapper_enqueue(loam_mapper* h) {
         if (h->knn_tile) {
           k_tile_bin<<<B * 2, TB_THREADS, 0, st>>>(D, round);
           k_knn_tile<<<B * D.tk_blk, TK_THREADS, 0, st>>>(D, round);
+        } else if (h->knn_cs == 4) {
+          k_knn<4, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round);
+        } else if (h->knn_cs == 8) {
+          k_knn<8, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round);
+        } else if (h->knn_cs == 16) {
+          k_knn<16, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round);
         } else if (h->knn_lanes == 2) {
           k_knn<2><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
         } else {
@@ -2686,6 +2709,12 @@ static int32_t mapper_enqueue(loam_mapper* h) {
     if (h->knn_tile) {
       LAUNCH(FAM_CORR, k_tile_bin<<<B * 2, TB_THREADS, 0, st>>>(D, round));
       LAUNCH(FAM_CORR, k_knn_tile<<<B * D.tk_blk, TK_THREADS, 0, st>>>(D, round));
+    } else if (h->knn_cs == 4) {
+      LAUNCH(FAM_CORR, (k_knn<4, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round)));
+    } else if (h->knn_cs == 8) {
+      LAUNCH(FAM_CORR, (k_knn<8, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round)));
+    } else if (h->knn_cs == 16) {
+      LAUNCH(FAM_CORR, (k_knn<16, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round)));
     } else if (h->knn_lanes == 2) {
       LAUNCH(FAM_CORR, k_knn<2><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round));
     } else {
