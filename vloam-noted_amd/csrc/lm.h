@@ -218,6 +218,10 @@ __host__ __device__ inline double lm_norm7(const double* x) {
 }
 
 // LM step: (S J^T J S + diag(D^2)) y = S J^T r, step = -y.  Returns false if not solvable.
+// LDL^T of the 6x6 system: one reciprocal per column on the dependent chain and no square roots
+// (a Cholesky took 6 square roots and 27 divisions in sequence, 5.7k cycles on one lane of
+// gfx950; this ~2k).  D^2 = diag / radius enters directly (Ceres' D = sqrt(diag / radius)
+// appears only squared in the normal equations of [J S; D]).
 __host__ __device__ inline bool lm_solve_step(LmState& S, double* step) {
   double A[6][6], b[6];
   for (int i = 0; i < 6; ++i) {
@@ -226,40 +230,38 @@ __host__ __device__ inline bool lm_solve_step(LmState& S, double* step) {
       S.diag[i] = fmin(fmax(d, 1e-6), 1e32);
     }
   }
+  const double rinv = 1.0 / S.radius;
   for (int i = 0; i < 6; ++i) {
-    for (int j = 0; j < 6; ++j) {
-      int r = i < j ? i : j, c = i < j ? j : i;
-      A[i][j] = S.scaling[i] * S.jtj[ut_index(r, c)] * S.scaling[j];
-    }
-    double D = sqrt(S.diag[i] / S.radius);
-    A[i][i] += D * D;
+    for (int j = 0; j <= i; ++j) A[i][j] = S.scaling[i] * S.jtj[ut_index(j, i)] * S.scaling[j];
+    A[i][i] += S.diag[i] * rinv;
     b[i] = S.scaling[i] * S.g[i];
   }
   S.reuse_diag = 1;
-  // Cholesky A = L L^T, L in A's lower triangle (the upper triangle is not read again)
-  double (&L)[6][6] = A;
+  // A = L diag(dv) L^T: unit L in the strict lower triangle, w = L[i][j] dv[j] in the upper
+  // (A[j][i]) for the rows below
+  double rd[6];
   for (int j = 0; j < 6; ++j) {
-    double s = A[j][j];
-    for (int k = 0; k < j; ++k) s -= L[j][k] * L[j][k];
-    if (!(s > 0.0)) return false;
-    double d = sqrt(s);
-    L[j][j] = d;
+    double d = A[j][j];
+    for (int k = 0; k < j; ++k) d -= A[j][k] * A[k][j];
+    if (!(d > 0.0)) return false;
+    rd[j] = 1.0 / d;
     for (int i = j + 1; i < 6; ++i) {
       double t = A[i][j];
-      for (int k = 0; k < j; ++k) t -= L[i][k] * L[j][k];
-      L[i][j] = t / d;
+      for (int k = 0; k < j; ++k) t -= A[i][k] * A[k][j];
+      A[j][i] = t;
+      A[i][j] = t * rd[j];
     }
   }
   double z[6], y[6];
   for (int i = 0; i < 6; ++i) {
     double t = b[i];
-    for (int k = 0; k < i; ++k) t -= L[i][k] * z[k];
-    z[i] = t / L[i][i];
+    for (int k = 0; k < i; ++k) t -= A[i][k] * z[k];
+    z[i] = t;
   }
   for (int i = 5; i >= 0; --i) {
-    double t = z[i];
-    for (int k = i + 1; k < 6; ++k) t -= L[k][i] * y[k];
-    y[i] = t / L[i][i];
+    double t = z[i] * rd[i];
+    for (int k = i + 1; k < 6; ++k) t -= A[k][i] * y[k];
+    y[i] = t;
   }
   for (int i = 0; i < 6; ++i) {
     step[i] = -y[i];
@@ -333,13 +335,14 @@ __host__ __device__ inline void lm_step(LmState& S, const double* red) {
     bool valid = lm_solve_step(S, step);
     if (valid) {
       // model_cost_change = -(step^T S g + 1/2 step^T (S JtJ S) step)
-      double lin = 0, quad = 0;
+      // (six independent row sums, then one of six: a short dependent chain)
+      double v[6], lin = 0, quad = 0;
+      for (int i = 0; i < 6; ++i) v[i] = step[i] * S.scaling[i];
       for (int i = 0; i < 6; ++i) {
-        lin += step[i] * S.scaling[i] * S.g[i];
-        for (int j = 0; j < 6; ++j) {
-          int r = i < j ? i : j, c = i < j ? j : i;
-          quad += step[i] * S.scaling[i] * S.jtj[ut_index(r, c)] * S.scaling[j] * step[j];
-        }
+        double w = 0;
+        for (int j = 0; j < 6; ++j) w += S.jtj[ut_index(i < j ? i : j, i < j ? j : i)] * v[j];
+        lin += v[i] * S.g[i];
+        quad += v[i] * w;
       }
       S.mcc = -(lin + 0.5 * quad);
       valid = S.mcc > 0.0;

@@ -571,7 +571,7 @@ __device__ inline void corr_block(const MapperDev& D, int* s, int* blk) {
 // steps long instead of 27 (few streams leave the chip mostly idle: latency, not issue, bounds
 // the search).  Without CS the lanes share each cell and split its points.
 template <int L, bool CS = false>
-__global__ void __launch_bounds__(CORR_THREADS) __attribute__((amdgpu_waves_per_eu(KNN_WAVES, 8))) k_knn(MapperDev D, int round) {
+__global__ void __launch_bounds__(CORR_THREADS) __attribute__((amdgpu_waves_per_eu(CS ? 4 : KNN_WAVES, 8))) k_knn(MapperDev D, int round) {
   __shared__ WinMap W[2];
   __shared__ int slot_of[75];  // 5 x 5 x 3 window position -> slot (laserCloudValidInd order)
   int s, blk;
