@@ -180,20 +180,19 @@ def run_steps(mapper, plan, first, count, poses=None):
 
 
 def run_steps_pipelined(mapper, plan, first, count):
-    """count solveMapping steps with the next step's input given, and its stack VoxelGrid queued
-    (loam_mapper_prefetch), while the current step is in flight (loam_mapper_solve_async /
-    loam_mapper_wait): the same results as run_steps, frame after frame"""
+    """count solveMapping steps, each enqueued behind the one in flight (loam_mapper_solve_async
+    queues it on the device, its records prepared there: include/loam_core.h) before that one is
+    waited for: the same results as run_steps, frame after frame, without the host round trip
+    between frames"""
     iters = 0
     mapper.input_device_batch(*plan[first])
     mapper.solve_async()
     for k in range(first + 1, first + count + 1):
         if k < first + count:
             mapper.input_device_batch(*plan[k])
-            mapper.prefetch()
-        mapper.wait()
+            mapper.solve_async()  # queued behind frame k - 1
+        mapper.wait()  # frame k - 1
         iters += mapper.total_iterations()
-        if k < first + count:
-            mapper.solve_async()
     return iters
 
 

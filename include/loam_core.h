@@ -86,8 +86,12 @@ typedef struct loam_map_stats {
   loam_lm_stats lm[2];
   int32_t center[3];             /* centerCubeI/J/K after recentering */
   int32_t valid_num;             /* laserCloudValidNum */
-  double ms_total;               /* device time of the whole solveMapping */
+  double ms_total;               /* device time of the whole solveMapping (0 when queued) */
   double ms_opt;                 /* device time of the optimisation block (:516-729) */
+  int32_t queued;                /* 1: ran queued behind another frame, records prepared on the
+                                  * device (loam_mapper_solve_async) */
+  int32_t rerun;                 /* 1: deferred by the device (recentering / compaction due) and
+                                  * run again on the host-prepared path */
 } loam_map_stats;
 
 /* --------------------------------------------------------------------------------------
@@ -213,13 +217,23 @@ int32_t loam_mapper_input_device_batch(loam_mapper* h, int32_t n, const int32_t*
  * as computed (pose, insertion, re-VoxelGrid): reset the failed stream before relying on it. */
 int32_t loam_mapper_solve(loam_mapper* h);
 /* loam_mapper_solve in two halves: _async enqueues the frame on the handle's HIP streams and
- * returns; _wait blocks until it is done and then does the host side (transformUpdate,
- * laser_mapping.cpp:147-151, stats, status).  Every other call on the handle waits first.  While
- * a frame is in flight the next frame's inputs may be given (loam_mapper_input*) and their stack
- * VoxelGrids (:492-500, which read only the body-frame input) queued with loam_mapper_prefetch:
- * they run beside the frame in flight, into the other of two stack buffers.  The results are
- * those of the sequential loam_mapper_solve; only the order in time changes.  Device inputs must
- * stay valid until the frame that takes them is waited for. */
+ * returns; _wait blocks until the OLDEST frame not yet waited for is done and then does its host
+ * side (transformUpdate, laser_mapping.cpp:147-151, stats, status).
+ * Up to two frames can be in the queue: while frame f is in flight, frame f + 1's inputs may be
+ * given (loam_mapper_input*) and _async called again.  On a handle that runs frames as one
+ * hipGraph (<= 4 streams, not sharded, profiling off) frame f + 1 is then queued behind f on the
+ * device: its stream records (the initial guess :206-207 from f's transformUpdate, the cube
+ * window :228-251) are prepared by the device, so the GPU goes from f to f + 1 without a host
+ * round trip.  A frame the host foresees recentering (:252-444) waits, pending, for f to be
+ * waited for; one the device finds recentering or due for an arena compaction is deferred and
+ * run again on the host-prepared path (loam_map_stats.queued / .rerun say which happened).
+ * Otherwise (other handles) frame f + 1's stack VoxelGrids (:492-500) run beside f and the rest
+ * after it.  loam_mapper_prefetch queues the stack VoxelGrids of given inputs early.
+ * The results are those of the sequential loam_mapper_solve, bit for bit; only the order in time
+ * changes.  loam_mapper_pose / _stats / _stats_all / _total_iterations / _get_state report the
+ * newest frame waited for (a frame enqueued with nothing before it in the queue is waited for by
+ * them first); every other call waits for every frame in the queue.  Device inputs must stay
+ * valid until the frame that takes them is waited for. */
 int32_t loam_mapper_solve_async(loam_mapper* h);
 int32_t loam_mapper_wait(loam_mapper* h);
 /* queue the stack VoxelGrids of every stream's pending input now (no-op with profiling on) */
@@ -241,7 +255,9 @@ int32_t loam_mapper_stats(loam_mapper* h, int32_t stream, loam_map_stats* st);
  * member lists + centroids, [46..47] of the latter: member lists, per-voxel sort + sums,
  * [48..49] arena compactions of the corner / surf maps (summed over streams), [50..57] tile kNN
  * (k_knn_tile, summed over waves): cycles of the tile record + query loads, the cell probes +
- * cell starts, staging, the search, the results; then tiles, queries, staged points.
+ * cell starts, staging, the search, the results; then tiles, queries, staged points,
+ * [58..61] k_frame_prep cycles: FrameIn load, device preparation, stack sizes, submap offsets,
+ * [62] its launches, [63] of them frames prepared on the device.
  * The cycle counters (all but [40], [41], [48], [49]) run only in a handle created with the
  * environment variable LOAM_PHASE_COUNTERS=1 (they cost atomics in the kernels); else they stay 0. */
 #define LOAM_DEBUG_COUNTERS 64

@@ -6,6 +6,10 @@ The whole HIP chain runs on the raw scans (ScanRegistration -> LaserOdometry -> 
 device pointers between the stages) with two mappers fed the same features and priors:
   exact_voxel_order = 1 (PCL's VoxelGrid summation order) against the oracle in PCL's order,
   exact_voxel_order = 0 (input order, the library default) against the oracle in input order.
+The PCL-order mapper solves frame by frame (loam_mapper_solve, device inputs); the input-order
+mapper queues every frame behind the one in flight (loam_mapper_solve_async, host inputs): the
+device prepares its stream records from the frame before, and frames the host foresees (or the
+device finds) recentering or compacting run on the host-prepared path.
 Every frame: the scan-registration feature counts equal, the odometry correspondences and LM
 iterations equal and its pose within 1e-4, and for both mappers every solveMapping count equal
 (stacks, submaps, correspondences and LM iterations per round, grid centre, valid cubes) and the
@@ -51,6 +55,17 @@ def test_long_stream_10k_frames_both_orders():
     bad = {k: [] for k in ("sr", "od", "pcl", "input")}
     err = {k: np.zeros((N, 2)) for k in mp}
     cen_prev, shifts = None, 0
+
+    def check(name, m, f):
+        qm, tm = m.pose(0)
+        st = m.stats(0)
+        e = (float(np.linalg.norm(tm - G[f"{name}_t"][f])), quat_angle(qm, G[f"{name}_q"][f]))
+        err[name][f] = e
+        cen = tuple(m.get_state(0)[0])
+        if (_row(st) != list(G[f"{name}_stats"][f]) or cen != tuple(G[f"{name}_cen"][f])
+                or e[0] >= TOL or e[1] >= TOL):
+            bad[name].append(f)
+        return cen
     t0 = time.time()
     chunk = 64
     workers = min(16, os.cpu_count() or 4)
@@ -75,21 +90,22 @@ def test_long_stream_10k_frames_both_orders():
                         or np.linalg.norm(t - G["od_t"][f]) >= TOL or quat_angle(q, G["od_q"][f]) >= TOL):
                     bad["od"].append(f)
                 (pc, nc), (ps, ns) = od.last_cloud_device(0, 0), od.last_cloud_device(0, 1)
-                for name, m in mp.items():
-                    m.input_device(0, pc, nc, ps, ns, q, t)
-                    m.solve()
-                    qm, tm = m.pose(0)
-                    st = m.stats(0)
-                    e = (float(np.linalg.norm(tm - G[f"{name}_t"][f])), quat_angle(qm, G[f"{name}_q"][f]))
-                    err[name][f] = e
-                    cen = tuple(m.get_state(0)[0])
-                    if (_row(st) != list(G[f"{name}_stats"][f]) or cen != tuple(G[f"{name}_cen"][f])
-                            or e[0] >= TOL or e[1] >= TOL):
-                        bad[name].append(f)
+                mp["pcl"].input_device(0, pc, nc, ps, ns, q, t)
+                mp["pcl"].solve()
+                cen = check("pcl", mp["pcl"], f)
                 shifts += cen_prev is not None and cen != cen_prev  # a recentering (laser_mapping.cpp:252-444)
                 cen_prev = cen
+                # host inputs: copied on the mapper's stack stream before the odometry moves on
+                mi = mp["input"]
+                mi.input(0, od.last_cloud(0, 0), od.last_cloud(0, 1), q, t)
+                mi.solve_async()  # queued behind frame f - 1
+                if f:
+                    mi.wait()  # frame f - 1
+                    check("input", mi, f - 1)
             if c0 % 2048 == 0:
                 print(f"frame {c0}: {time.time() - t0:.0f} s", flush=True)
+    mp["input"].wait()
+    check("input", mp["input"], N - 1)
     compactions = {name: m.debug_counters()[48:50].tolist() for name, m in mp.items()}
     for h in (sr, od, *mp.values()):
         h.close()

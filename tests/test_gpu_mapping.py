@@ -440,3 +440,53 @@ def test_async_solve_with_prefetched_stacks(seq, n_streams, exact):
             m.solve_async()
     m.close()
     assert got == want
+
+
+@pytest.mark.parametrize("n_streams,exact,defer_every", [(1, 0, 0), (1, 1, 0), (2, 0, 0), (1, 0, 3), (2, 0, 2)])
+def test_chained_solve_matches_blocking(seq, n_streams, exact, defer_every, monkeypatch):
+    """frames queued behind the one in flight (loam_mapper_solve_async on a graph-path handle,
+    include/loam_core.h): frame f + 1 is enqueued before frame f is waited for, its stream records
+    prepared on the device (k_frame_prep: transformUpdate, initial guess, window); every pose and
+    count equals the blocking loam_mapper_solve, bit for bit.  defer_every > 0 forces the
+    deferral path (LOAM_DEFER_EVERY: queued frames whose frame number is a multiple are left to
+    the host, which runs them again with their own inputs and stacks)"""
+    def row(m, s):
+        st = m.stats(s)
+        q, t = m.pose(s)
+        return (q.tobytes(), t.tobytes(), st.corner_stack, st.surf_stack, tuple(st.corner_num), tuple(st.surf_num),
+                st.lm[0].iterations, st.lm[1].iterations, tuple(st.center), st.valid_num)
+
+    def feed(m, f):
+        for s in range(n_streams):
+            rec = seq[f + s]
+            m.input(s, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+
+    n = len(seq) - n_streams + 1
+    ref = BatchMapper(n_streams, exact_voxel_order=exact)
+    want = []
+    for f in range(n):
+        feed(ref, f)
+        ref.solve()
+        want.append([row(ref, s) for s in range(n_streams)])
+    ref.close()
+    if defer_every:
+        monkeypatch.setenv("LOAM_DEFER_EVERY", str(defer_every))
+    m = BatchMapper(n_streams, exact_voxel_order=exact)
+    monkeypatch.delenv("LOAM_DEFER_EVERY", raising=False)
+    got, queued, rerun = [], 0, 0
+    feed(m, 0)
+    m.solve_async()
+    for f in range(1, n + 1):
+        if f < n:
+            feed(m, f)
+            m.solve_async()  # queued behind frame f - 1
+        m.wait()             # frame f - 1
+        got.append([row(m, s) for s in range(n_streams)])
+        queued += m.stats(0).queued
+        rerun += m.stats(0).rerun
+    m.close()
+    assert got == want
+    if defer_every:
+        assert queued > 0 and rerun > 0, (queued, rerun)
+    else:
+        assert queued >= n - 2, queued  # every frame but the first ran queued behind another

@@ -22,7 +22,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <array>
 #include <cstring>
+#include <deque>
 #include <vector>
 
 #include "common.h"
@@ -79,7 +81,25 @@ struct StreamFrame {
   unsigned long long cand[2];     // map points in the queries' 27-cell neighbourhoods, per round
   int ntile[2];                   // occupied 2 m query tiles of this round (k_tile_bin)
   unsigned long long vx_bytes;    // algorithmic bytes of this frame's re-VoxelGrid + cell index
+  double wodom[7];  // the frame's odometry pose q_wodom (xyzw), t_wodom
+  // q_wmap_wodom, t_wmap_wodom: the frame's initial guess (:206-207) is taken with it, and k_insert
+  // advances it by the frame's transformUpdate (:147-151) as the host does after the frame
+  double wmap[7];
+  int deferred;     // a queued frame found a recentering or compaction due: left to the host
   LmState lm[2];
+};
+
+// per-stream input of a frame in the graph path (k_frame_prep), read from page-locked host
+// memory: mode 0, the host uploaded the stream records; mode 1, a frame queued behind the one
+// in flight (loam_mapper_solve_async) whose records the device prepares from the frame before
+struct FrameIn {
+  double wodom[7];
+  const float4* in_ptr[2];
+  int n[2];
+  int active;
+  int mode;
+  uint32_t epoch;
+  int pad;
 };
 
 // the stack VoxelGrid inputs of a stream (laser_mapping.cpp:492-500): set when its stack is
@@ -136,6 +156,7 @@ struct MapperDev {
   // sharded mode (loam_mapper_create_sharded): this rank of nrank; map points are stored by
   // the rank owning their 4 m block (comm.h, shard_owner); blk_v: voxels per block edge
   uint32_t compact_at = 0;  // an arena whose tail passed this is compacted
+  uint32_t compact_due_at = 0;  // the compaction kernels' test (compact_at, or earlier: mapper_enqueue)
   // exact_voxel_order: the stack and cube VoxelGrids in PCL's summation order (voxel_pcl.h);
   // sort scratch [B][2][scratch_cap] (the stack at offset 0, the cubes from scratch_tail)
   int pcl_order = 0;
@@ -172,6 +193,8 @@ struct MapperDev {
   uint32_t tile_tab_n = 0;
   int tk_blk = 32;       // k_knn_tile workgroups per stream
   int knn_blk = CORR_BLK;  // k_knn workgroups per stream of the cell-split variant
+  const FrameIn* fin = nullptr;  // [B] (page-locked host memory) the graph path's frame inputs
+  int defer_every = 0;    // tests: queued frames with epoch % defer_every == 0 are deferred
 };
 
 // one query's 5 nearest candidates on one rank (d: FLANN L2_Simple float distance, id: global
@@ -454,12 +477,75 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_cat(MapperDev D) {
   if (threadIdx.x == 0) D.stk_n[2 * s + m] = (int)o;
 }
 
+// LaserMapping::input's initial guess (laser_mapping.cpp:206-207): pose = wmap (x) wodom
+__host__ __device__ inline void pose_initial_guess(const double* wmap, const double* wodom, double* pose) {
+  const dq qm{wmap[0], wmap[1], wmap[2], wmap[3]};
+  const dq qo{wodom[0], wodom[1], wodom[2], wodom[3]};
+  const dq q = qmul(qm, qo);
+  const d3 r = qrot(qm, d3{wodom[4], wodom[5], wodom[6]});
+  pose[0] = q.x; pose[1] = q.y; pose[2] = q.z; pose[3] = q.w;
+  pose[4] = r.x + wmap[4];
+  pose[5] = r.y + wmap[5];
+  pose[6] = r.z + wmap[6];
+}
+
+// LaserMapping::transformUpdate (laser_mapping.cpp:147-151): wmap = pose (x) wodom^-1
+__host__ __device__ inline void pose_transform_update(const double* pose, const double* wodom, double* wmap) {
+  const dq qw{pose[0], pose[1], pose[2], pose[3]};
+  const dq qo{wodom[0], wodom[1], wodom[2], wodom[3]};
+  const dq qm = qmul(qw, qinv(qo));
+  const d3 r = qrot(qm, d3{wodom[4], wodom[5], wodom[6]});
+  wmap[0] = qm.x; wmap[1] = qm.y; wmap[2] = qm.z; wmap[3] = qm.w;
+  wmap[4] = pose[4] - r.x;
+  wmap[5] = pose[5] - r.y;
+  wmap[6] = pose[6] - r.z;
+}
+
+// centerCube and the recentering count (laser_mapping.cpp:228-251): the window centre of a pose
+// and how far the grid must shift (cen follows the shift); true if it shifts
+__host__ __device__ inline bool frame_center(const double* pose, int* cen, int* center, int* shift) {
+  const int dims[3] = {CW, CH, CD};
+  bool any = false;
+  for (int a = 0; a < 3; ++a) {
+    int c = cube_of(pose[4 + a], cen[a]);
+    shift[a] = 0;
+    while (c < 3) { c++; cen[a]++; shift[a]++; }
+    while (c >= dims[a] - 3) { c--; cen[a]--; shift[a]--; }
+    center[a] = c;
+    any |= shift[a] != 0;
+  }
+  return any;
+}
+
+// the window cubes (laserCloudValidInd, :455-472) and the cell-hash origin of F.center / F.cen
+__host__ __device__ inline void frame_window(StreamFrame& F) {
+  const int* c3 = F.center;
+  int vn = 0;
+  for (int i = c3[0] - 2; i <= c3[0] + 2; i++)
+    for (int j = c3[1] - 2; j <= c3[1] + 2; j++)
+      for (int k = c3[2] - 1; k <= c3[2] + 1; k++)
+        if (i >= 0 && i < CW && j >= 0 && j < CH && k >= 0 && k < CD) F.window[vn++] = i + CW * j + CW * CH * k;
+  F.valid_num = vn;
+  // hash cell origin: world metres of the window's low corner, minus a 2-cell margin
+  F.origin[0] = (c3[0] - 2 - F.cen[0]) * 50 - 25 - 2;
+  F.origin[1] = (c3[1] - 2 - F.cen[1]) * 50 - 25 - 2;
+  F.origin[2] = (c3[2] - 1 - F.cen[2]) * 50 - 25 - 2;
+}
+
+// per-frame resets of a stream record (the host's, or k_frame_prep's for a queued frame)
+__host__ __device__ inline void frame_reset(StreamFrame& F) {
+  F.shift[0] = F.shift[1] = F.shift[2] = 0;
+  F.err = 0;
+  F.nc_stack = F.ns_stack = 0;
+  F.corner_num[0] = F.corner_num[1] = F.surf_num[0] = F.surf_num[1] = 0;
+  F.sub_n[0] = F.sub_n[1] = 0;
+  F.optimize = 0;
+  F.cand[0] = F.cand[1] = 0;
+}
+
 // the frame's stack sizes and stack-filter errors into its stream records (after the stack
 // kernels, which may have run while the previous frame was in flight)
-__global__ void k_stack_counts(MapperDev D) {
-  const int s = D.s0 + blockIdx.x;
-  StreamFrame& F = D.fr[s];
-  if (threadIdx.x != 0 || !F.active) return;
+__device__ inline void stack_counts(const MapperDev& D, int s, StreamFrame& F) {
   F.nc_stack = D.stk_n[2 * s];
   F.ns_stack = D.stk_n[2 * s + 1];
   const int e = D.stk_err[s];
@@ -469,14 +555,95 @@ __global__ void k_stack_counts(MapperDev D) {
   }
 }
 
+__global__ void k_stack_counts(MapperDev D) {
+  const int s = D.s0 + blockIdx.x;
+  StreamFrame& F = D.fr[s];
+  if (threadIdx.x != 0 || !F.active) return;
+  stack_counts(D, s, F);
+}
+
+// a queued frame's stream record, prepared on the device from what the frames before left (what
+// the host does in mapper_enqueue): the initial guess (:206-207) with the transform of the
+// stream's last solve, the window (:228-251, :455-472).  A frame that needs a recentering or an
+// arena compaction, or follows a deferred one, is deferred: the stream stays inactive and the
+// host runs it again on its own path (the device state is left as the frames before left it).
+// All threads of the block: thread 0 decides from registers (one round of loads of the record),
+// the window list is built one slot per thread (i, j, k order: :455-472).
+__device__ inline void frame_prep_device(const MapperDev& D, StreamFrame& F, const FrameIn& I) {
+  __shared__ int ok, c3s[3], cens[3];
+  __shared__ uint64_t vmask[2];
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    const int prev_deferred = F.deferred;
+    double wmap[7];
+    for (int i = 0; i < 7; ++i) wmap[i] = F.wmap[i];
+    int cen[3] = {F.cen[0], F.cen[1], F.cen[2]};
+    const uint32_t t0 = F.arena_tail[0], t1 = F.arena_tail[1];
+    F.active = 0;
+    ok = 0;
+    if (I.active) {
+      double pose[7];
+      pose_initial_guess(wmap, I.wodom, pose);
+      int center[3], shift[3];
+      const bool shifted = frame_center(pose, cen, center, shift);
+      const bool compact = t0 > D.compact_at || t1 > D.compact_at;
+      const bool forced = D.defer_every > 0 && I.epoch % (uint32_t)D.defer_every == 0;
+      for (int i = 0; i < 7; ++i) F.wodom[i] = I.wodom[i];
+      if (prev_deferred || shifted || compact || forced) {
+        F.deferred = 1;
+      } else {
+        frame_reset(F);
+        F.active = 1;
+        for (int i = 0; i < 7; ++i) F.pose[i] = pose[i];
+        for (int a = 0; a < 3; ++a) {
+          F.center[a] = c3s[a] = center[a];
+          cens[a] = cen[a];
+        }
+        F.origin[0] = (center[0] - 2 - cen[0]) * 50 - 25 - 2;  // as frame_window
+        F.origin[1] = (center[1] - 2 - cen[1]) * 50 - 25 - 2;
+        F.origin[2] = (center[2] - 1 - cen[2]) * 50 - 25 - 2;
+        F.epoch = I.epoch;
+        F.in_ptr[0] = I.in_ptr[0];
+        F.in_ptr[1] = I.in_ptr[1];
+        F.nc_in = I.n[0];
+        F.ns_in = I.n[1];
+        ok = 1;
+      }
+    }
+  }
+  __syncthreads();
+  if (!ok) return;
+  // window slot t = (i * 5 + j) * 3 + k of the 5 x 5 x 3 cubes around the centre, kept if inside
+  // the grid, in that order (frame_window)
+  const int t = tid;
+  const int i = c3s[0] - 2 + t / 15, j = c3s[1] - 2 + (t / 3) % 5, k = c3s[2] - 1 + t % 3;
+  const bool in = t < 75 && i >= 0 && i < CW && j >= 0 && j < CH && k >= 0 && k < CD;
+  const uint64_t b = __ballot(in);
+  const int w = tid >> 6, lane = tid & 63;
+  if (lane == 0 && w < 2) vmask[w] = b;
+  __syncthreads();
+  const int pos = (w == 1 ? __popcll(vmask[0]) : 0) + __popcll(b & ((1ull << lane) - 1));
+  if (in) F.window[pos] = i + CW * j + CW * CH * k;
+  if (tid == 0) F.valid_num = __popcll(vmask[0]) + __popcll(vmask[1]);
+  __syncthreads();
+}
+
+// FrameIn from page-locked host memory into LDS: one system-scope load per lane, all in flight
+// together (the host wrote it before the launch; each read crosses the host link)
+constexpr int FRAME_IN_WORDS = (int)(sizeof(FrameIn) / 8);
+static_assert(sizeof(FrameIn) % 8 == 0 && FRAME_IN_WORDS <= 64, "FrameIn copy granularity");
+__device__ inline void load_frame_in(const FrameIn* p, FrameIn* lds) {
+  const int w = threadIdx.x;
+  if (w < FRAME_IN_WORDS)
+    reinterpret_cast<unsigned long long*>(lds)[w] =
+        __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p) + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ---------------------------------------------------------------------------------------
 // submap: offsets of the window cubes (laserCloudCornerFromMap concatenation order)
 // ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(128) k_submap_prep(MapperDev D) {
+__device__ inline void submap_prep(const MapperDev& D, int s, StreamFrame& F) {
   // one wave per map; window slots 2*lane, 2*lane+1 (valid_num <= 75 <= 128)
-  const int s = D.s0 + blockIdx.x;
-  StreamFrame& F = D.fr[s];
-  if (!F.active) return;
   const int m = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint2* tab = D.cube_tab + sm_index(s, m) * NCUBE;
   const int vn = F.valid_num;
@@ -504,6 +671,45 @@ __global__ void __launch_bounds__(128) k_submap_prep(MapperDev D) {
   __syncthreads();
   // laser_mapping.cpp:514
   if (threadIdx.x == 0) F.optimize = (F.sub_n[0] > 10 && F.sub_n[1] > 50) ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(128) k_submap_prep(MapperDev D) {
+  const int s = D.s0 + blockIdx.x;
+  StreamFrame& F = D.fr[s];
+  if (!F.active) return;
+  submap_prep(D, s, F);
+}
+
+// the graph path's first kernel: a queued frame's records (frame_prep_device), the stack sizes
+// (k_stack_counts) and the submap offsets (k_submap_prep) in one launch
+__global__ void __launch_bounds__(128) k_frame_prep(MapperDev D) {
+  const int s = D.s0 + blockIdx.x;
+  StreamFrame& F = D.fr[s];
+  __shared__ int go;
+  __shared__ FrameIn I;
+  const unsigned long long t0 = __builtin_readcyclecounter();
+  load_frame_in(D.fin + s, &I);
+  __syncthreads();
+  const unsigned long long t1 = __builtin_readcyclecounter();
+  if (I.mode == 1) frame_prep_device(D, F, I);  // (block-uniform branch)
+  const unsigned long long t2 = __builtin_readcyclecounter();
+  if (threadIdx.x == 0) {
+    if (F.active) stack_counts(D, s, F);
+    go = F.active;
+  }
+  __syncthreads();
+  if (!go) return;
+  const unsigned long long t3 = __builtin_readcyclecounter();
+  submap_prep(D, s, F);
+  if (D.pdbg && threadIdx.x == 0) {  // cycles: [58] FrameIn load, [59] device prep, [60] stack counts, [61] submap
+    const unsigned long long t4 = __builtin_readcyclecounter();
+    atomicAdd(&D.pdbg[58], t1 - t0);
+    atomicAdd(&D.pdbg[59], t2 - t1);
+    atomicAdd(&D.pdbg[60], t3 - t2);
+    atomicAdd(&D.pdbg[61], t4 - t3);
+    atomicAdd(&D.pdbg[62], 1ull);
+    if (I.mode == 1) atomicAdd(&D.pdbg[63], 1ull);  // frames prepared on the device
+  }
 }
 
 // sharded: this rank's point count of every window cube, all-reduced before k_submap_prep so
@@ -1488,6 +1694,9 @@ __global__ void k_insert(MapperDev D) {
   const int nc = F.nc_stack, ns = F.ns_stack;
   double X[7];
   for (int i = 0; i < 7; ++i) X[i] = F.pose[i];
+  // transformUpdate (:147-151) for a frame queued behind this one (k_frame_prep); the host
+  // computes the same at the end of the frame
+  if (blockIdx.x == 0 && threadIdx.x == 0) pose_transform_update(X, F.wodom, F.wmap);
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nc + ns; t += gridDim.x * blockDim.x) {
     const int m = t < nc ? 0 : 1;
     const int i = m == 0 ? t : t - nc;
@@ -1731,6 +1940,7 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
 // one workgroup per (stream, map, slot): block = slot item
 __global__ void __launch_bounds__(VX_THREADS) k_revox(MapperDev D) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
+
   const uint32_t item = 2 * (uint32_t)D.s0 * INS_SLOTS + blockIdx.x;
   const int slot = (int)(item % INS_SLOTS), sm = (int)(item / INS_SLOTS);
   int cube = 0, append = 0;
@@ -1764,7 +1974,7 @@ __global__ void __launch_bounds__(VX_THREADS) k_cube_index(MapperDev D, int s, i
 // Launched over every (stream, map) pair sm = 2 s0 + b of the handle; a pair whose tail is at
 // or below compact_at exits at once (the decision is taken on the device, from the records)
 __device__ inline bool compact_due(const MapperDev& D, int sm) {
-  return D.fr[sm >> 1].arena_tail[sm & 1] > D.compact_at;
+  return D.fr[sm >> 1].arena_tail[sm & 1] > D.compact_due_at;
 }
 
 __global__ void k_compact_scan(MapperDev D, uint32_t* new_off) {
@@ -1903,10 +2113,9 @@ struct PinnedArray {
     p = nullptr;
     n = 0;
   }
-  bool assign(size_t count, const T& v) {
+  bool assign(size_t count, const T& v, unsigned flags = hipHostMallocDefault) {
     release();
-    if (hipHostMalloc(reinterpret_cast<void**>(&p), sizeof(T) * std::max<size_t>(count, 1), hipHostMallocDefault) !=
-        hipSuccess) {
+    if (hipHostMalloc(reinterpret_cast<void**>(&p), sizeof(T) * std::max<size_t>(count, 1), flags) != hipSuccess) {
       p = nullptr;
       return false;
     }
@@ -1935,6 +2144,7 @@ struct HostStream {
   int in_n[2] = {0, 0};
   double in_q[4] = {0, 0, 0, 1}, in_t[3] = {0, 0, 0};
   int frame = 0;
+  int cen[3] = {10, 10, 5};  // laserCloudCen* after the stream's last finished frame
   loam_map_stats st{};
 };
 
@@ -1963,6 +2173,22 @@ inline std::string map_err_text(int e) {
 using namespace loam;
 
 enum : int { FAM_STACK = 0, FAM_HASH, FAM_CORR, FAM_LM, FAM_INSERT, FAM_REVOX, FAM_OTHER, NFAM };
+
+// a frame in flight (loam_mapper_solve_async): what its streams were given, where its records
+// come back (the D2H buffer of its stack parity), and whether it was queued behind another
+// frame with its records prepared on the device (chained)
+struct FrameRec {
+  bool chained = false, graph = false;
+  bool has_deferred = false;  // known (its records are back) to have deferred streams
+  bool pending = false;       // not enqueued yet: inputs and stack taken, run on the host path later
+  bool behind = false;        // solve_async was called with another frame in the queue
+  int fpar = 0;
+  uint64_t seq = 0;  // enqueue order (0: nothing was enqueued)
+  std::vector<int> active;
+  std::vector<std::array<double, 7>> wodom;
+  std::vector<std::array<const float4*, 2>> in_p;
+  std::vector<std::array<int, 2>> in_n;
+};
 
 struct loam_mapper {
   loam_params P;
@@ -2004,8 +2230,20 @@ struct loam_mapper {
   // stack VoxelGrids ahead of their frame (loam_mapper_prefetch / loam_mapper_solve_async):
   // stacks, their inputs and counts double-buffered by stack parity; spar: the next frame's
   int spar = 0, last_spar = 0;
-  bool inflight = false;       // a frame enqueued by loam_mapper_solve_async, not yet waited for
-  bool last_graph = false;     // that frame ran as a graph
+  // frames in flight, oldest first: at most two, the second queued behind the first on the
+  // device (loam_mapper_solve_async on a graph-path handle, its records from k_frame_prep)
+  std::deque<FrameRec> q;
+  uint64_t seq = 0, mirror_seq = 0;  // hf mirrors the device records as of frame mirror_seq
+  PinnedArray<StreamFrame> hfo[2];   // [stack parity] the records after that parity's frame
+  PinnedArray<FrameIn> fin[2];       // [stack parity] the graph path's frame inputs (k_frame_prep)
+  const FrameIn* fin_dev[2] = {nullptr, nullptr};
+  FrameIn* d_fin[2] = {nullptr, nullptr};  // LOAM_FIN_DEVICE=1 (measurement): FrameIn uploaded to HBM
+  int fin_device = 0, rec_copy_out = 0;    // LOAM_REC_COPY_OUT=1 (measurement): records D2H after the graph
+  hipEvent_t ev_fr[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [parity] frame start / records back (timed)
+  hipEvent_t ev_done[2] = {nullptr, nullptr};  // [parity] records back (untimed: what a queued frame records)
+  int chain = 1;             // LOAM_CHAIN=0: never queue a frame behind another
+  uint32_t grow_max = 0;     // largest arena growth of one frame seen (compaction foresight)
+  std::vector<std::array<uint32_t, 2>> last_tail;
   hipEvent_t ev_stack = nullptr;   // after the last stack launch (on st2)
   hipEvent_t ev_sin[2] = {nullptr, nullptr};  // the H2D of hsin[parity] done
   float4* stack_buf[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [parity][map]
@@ -2052,6 +2290,11 @@ void free_all(loam_mapper* h) {
   for (auto& e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->ev_stack) (void)hipEventDestroy(h->ev_stack);
   for (auto& e : h->ev_sin)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& ep : h->ev_fr)
+    for (auto& e : ep)
+      if (e) (void)hipEventDestroy(e);
+  for (auto& e : h->ev_done)
     if (e) (void)hipEventDestroy(e);
   h->ev_pool.clear();
   for (auto& e : h->ev)
@@ -2131,6 +2374,7 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     const uint64_t cap = (uint64_t)D.map_cap, margin = (uint64_t)D.sub_cap + 2ull * D.max_in;
     h->compact_at = (uint32_t)std::max<uint64_t>(cap / 2, cap > margin ? cap - margin : 0);
     D.compact_at = h->compact_at;
+    D.compact_due_at = h->compact_at;
   }
   D.max_chunks = LM_EBLK;
   {
@@ -2186,6 +2430,17 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
       hipEventCreateWithFlags(&h->ev_sin[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_sin[1], hipEventDisableTiming) != hipSuccess)
     return fail(LOAM_ERR_HIP);
+  for (auto& ep : h->ev_fr)
+    for (auto& e : ep)
+      if (hipEventCreate(&e) != hipSuccess) return fail(LOAM_ERR_HIP);
+  for (auto& e : h->ev_done)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(LOAM_ERR_HIP);
+  {
+    const char* cenv = std::getenv("LOAM_CHAIN");
+    h->chain = (cenv && cenv[0] == '0') ? 0 : 1;
+    const char* denv = std::getenv("LOAM_DEFER_EVERY");  // tests: force the deferral path
+    D.defer_every = denv ? std::max(0, std::atoi(denv)) : 0;
+  }
   // graphs pay off where launch gaps are the cost (B = 1: 0.750 -> 0.733 ms per frame); with
   // two handles of 64 streams, graph launches measured 20% slower (375k vs 470k iterations/s)
   h->use_graph = n_streams <= 4 ? 1 : 0;
@@ -2303,11 +2558,30 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
 #undef ALLOC
   D.cube_tab = h->cube_tab[0];
   if (!h->hf.assign(B, StreamFrame{})) return fail(LOAM_ERR_HIP);
+  for (int p = 0; p < 2; ++p) {
+    void* dp = nullptr;
+    if (!h->hfo[p].assign(B, StreamFrame{}) ||
+        !h->fin[p].assign(B, FrameIn{}, hipHostMallocMapped | hipHostMallocCoherent) ||
+        hipHostGetDevicePointer(&dp, h->fin[p].data(), 0) != hipSuccess)
+      return fail(LOAM_ERR_HIP);
+    h->fin_dev[p] = reinterpret_cast<const FrameIn*>(dp);
+    void* q = nullptr;
+    if (hipMalloc(&q, sizeof(FrameIn) * B) != hipSuccess) return fail(LOAM_ERR_HIP);
+    h->allocs.push_back(q);
+    h->d_fin[p] = reinterpret_cast<FrameIn*>(q);
+  }
+  {
+    const char* e1 = std::getenv("LOAM_FIN_DEVICE");
+    const char* e2 = std::getenv("LOAM_REC_COPY_OUT");
+    h->fin_device = (e1 && e1[0] == '1') ? 1 : 0;
+    h->rec_copy_out = (e2 && e2[0] == '1') ? 1 : 0;
+  }
   h->hs.assign(B, HostStream{});
+  h->last_tail.assign(B, std::array<uint32_t, 2>{0u, 0u});
   for (size_t s = 0; s < B; ++s) {
     StreamFrame& F = h->hf[s];
     F.cen[0] = 10; F.cen[1] = 10; F.cen[2] = 5;
-    F.pose[3] = 1.0;
+    F.pose[3] = F.wodom[3] = F.wmap[3] = 1.0;
   }
   if (hipStreamSynchronize(h->st) != hipSuccess) return fail(LOAM_ERR_HIP);  // zero-fills done
   *out = h;
@@ -2332,21 +2606,31 @@ int32_t loam_shard_owner(const float* xyz, float leaf, int32_t nrank) {
   return shard_owner(xyz[0], xyz[1], xyz[2], 1.0f / leaf, shard_block_voxels(leaf), nrank);
 }
 
-static int32_t mapper_finish(loam_mapper* h);
-// a frame enqueued by loam_mapper_solve_async is finished before anything reads or changes the
-// handle's state
+static int32_t finish_oldest(loam_mapper* h);
+static int32_t settle_all(loam_mapper* h);
+static bool chain_capable(const loam_mapper* h);
+// every frame in flight is finished before anything reads or changes the handle's state
 #define SETTLE(h)                                \
   do {                                           \
-    if ((h) && (h)->inflight) {                  \
+    if ((h) && !(h)->q.empty()) {                \
       LOAM_HIP(hipSetDevice((h)->dev));          \
-      TRY(mapper_finish(h));                     \
+      TRY(settle_all(h));                        \
     }                                            \
+  } while (0)
+// the result calls (pose, stats, state, iterations) report the newest finished frame: they finish
+// the oldest frame in the queue unless it was given behind another (whose results they report)
+#define SETTLE_RESULTS(h)                                  \
+  do {                                                     \
+    if ((h) && !(h)->q.empty() && !(h)->q.front().behind) { \
+      LOAM_HIP(hipSetDevice((h)->dev));                    \
+      TRY(finish_oldest(h));                               \
+    }                                                      \
   } while (0)
 
 int32_t loam_mapper_destroy(loam_mapper* h) {
   if (!h) return LOAM_ERR_ARG;
   (void)hipSetDevice(h->dev);
-  if (h->inflight) (void)mapper_finish(h);
+  while (!h->q.empty()) (void)finish_oldest(h);
   (void)hipStreamSynchronize(h->st2);
   free_all(h);
   delete h;
@@ -2365,7 +2649,8 @@ int32_t loam_mapper_reset(loam_mapper* h) {
   for (int s = 0; s < h->B; ++s) {
     h->hf[s] = StreamFrame{};
     h->hf[s].cen[0] = 10; h->hf[s].cen[1] = 10; h->hf[s].cen[2] = 5;
-    h->hf[s].pose[3] = 1.0;
+    h->hf[s].pose[3] = h->hf[s].wodom[3] = h->hf[s].wmap[3] = 1.0;
+    h->last_tail[s] = {0u, 0u};
     h->hs[s] = HostStream{};
   }
   return LOAM_OK;
@@ -2389,7 +2674,7 @@ static int32_t mapper_input_common(loam_mapper* h, int32_t s, const float* corne
   LOAM_HIP(hipSetDevice(h->dev));
   HostStream& H = h->hs[s];
   if (skip) {  // laser_mapping.cpp:197-201: high-frequency pose only (needs the last transformUpdate)
-    if (h->inflight) TRY(mapper_finish(h));
+    SETTLE(h);
     for (int i = 0; i < 4; ++i) H.q_wodom[i] = q_wodom[i];
     for (int i = 0; i < 3; ++i) H.t_wodom[i] = t_wodom[i];
     H.skip = true;
@@ -2481,7 +2766,7 @@ int32_t loam_mapper_input_device_batch(loam_mapper* h, int32_t n, const int32_t*
 
 int64_t loam_mapper_total_iterations(loam_mapper* h) {
   if (!h) return LOAM_ERR_ARG;
-  SETTLE(h);
+  SETTLE_RESULTS(h);
   int64_t it = 0;
   for (int s = 0; s < h->B; ++s)
     if (h->hs[s].solved_last) it += h->hs[s].st.lm[0].iterations + h->hs[s].st.lm[1].iterations;
@@ -2489,7 +2774,7 @@ int64_t loam_mapper_total_iterations(loam_mapper* h) {
 }
 
 int32_t loam_mapper_stats_all(loam_mapper* h, loam_map_stats* out, int32_t n) {
-  SETTLE(h);
+  SETTLE_RESULTS(h);
   if (!h || !out || n < 0 || n > h->B) return LOAM_ERR_ARG;
   for (int s = 0; s < n; ++s) out[s] = h->hs[s].st;
   return LOAM_OK;
@@ -2500,6 +2785,8 @@ int32_t loam_mapper_stats_all(loam_mapper* h, loam_map_stats* out, int32_t n) {
 // They read only the frame's body-frame input, so they may run beside a frame in flight.
 static int32_t launch_stacks(loam_mapper* h) {
   const int par = h->spar, B = h->B;
+  for (const FrameRec& R : h->q)  // that parity's stack buffers still belong to a frame in flight
+    if (R.fpar == par) return LOAM_OK;
   bool any = false;
   LOAM_HIP(hipEventSynchronize(h->ev_sin[par]));  // the last copy out of hsin[par] is done
   StackIn* in = h->hsin[par].data();
@@ -2542,9 +2829,42 @@ int32_t loam_mapper_prefetch(loam_mapper* h) {
   return launch_stacks(h);
 }
 
+// the frame's kernel sequence for the hipGraph path: k_frame_prep (records of a queued frame,
+// stack sizes, submap offsets), 2 x (kNN, geometry, LM round), insertion, re-VoxelGrid, and the
+// records back to the D2H buffer of the frame's stack parity.  Every kernel argument is fixed per
+// (cube-table parity, stack parity): the frame's values travel in the records and FrameIn.
+static void capture_frame(loam_mapper* h, const MapperDev& D, int fpar, hipStream_t st) {
+  const int B = h->B;
+  k_frame_prep<<<B, 128, 0, st>>>(D);
+  for (int round = 0; round < 2; ++round) {
+    if (h->knn_tile) {
+      k_tile_bin<<<B * 2, TB_THREADS, 0, st>>>(D, round);
+      k_knn_tile<<<B * D.tk_blk, TK_THREADS, 0, st>>>(D, round);
+    } else if (h->knn_cs == 4) {
+      k_knn<4, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round);
+    } else if (h->knn_cs == 8) {
+      k_knn<8, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round);
+    } else if (h->knn_cs == 16) {
+      k_knn<16, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round);
+    } else if (h->knn_lanes == 2) {
+      k_knn<2><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
+    } else {
+      k_knn<1><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
+    }
+    k_geom<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
+    k_lm_round<<<lm_padded(B) * h->lm_G, LM_THREADS, 0, st>>>(D, round, h->lm_G);
+  }
+  k_insert<<<dim3(16, B), 256, 0, st>>>(D);
+  k_bucket<<<B * 2, VX_THREADS, 0, st>>>(D);
+  k_revox<<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D);
+  if (!h->rec_copy_out) (void)hipMemcpyAsync(h->hfo[fpar].data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st);
+}
+
 // Enqueue one solveMapping of every stream with an input (the work of loam_mapper_solve up to
-// the host bookkeeping, which mapper_finish does)
-static int32_t mapper_enqueue(loam_mapper* h) {
+// the host bookkeeping, which mapper_finish_rec does).  chained: queued behind the frame in
+// flight, whose results the host does not have yet: the device prepares the stream records
+// (k_frame_prep) from what that frame left, and only the graph path runs.
+static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
   h->ev_fam.clear();
   MapperDev& D = h->D;
   const int B = h->B;
@@ -2553,124 +2873,140 @@ static int32_t mapper_enqueue(loam_mapper* h) {
   D.sin = h->sin_buf[fpar];
   D.stk_n = h->stk_n_buf[fpar];
   D.stk_err = h->stk_err_buf[fpar];
+  D.fin = h->fin_device ? h->d_fin[fpar] : h->fin_dev[fpar];
   for (int m = 0; m < 2; ++m) D.stack[m] = h->stack_buf[fpar][m];
-  for (int s = 0; s < B; ++s) {  // the inputs become the frame; initial guess (:206-207)
+  R = FrameRec{};
+  R.chained = chained;
+  R.fpar = fpar;
+  R.active.assign(B, 0);
+  R.wodom.assign(B, std::array<double, 7>{0, 0, 0, 1, 0, 0, 0});
+  R.in_p.assign(B, std::array<const float4*, 2>{nullptr, nullptr});
+  R.in_n.assign(B, std::array<int, 2>{0, 0});
+  bool any = false;
+  for (int s = 0; s < B; ++s) {  // the inputs become the frame
     HostStream& H = h->hs[s];
-    StreamFrame& F = h->hf[s];
-    H.pending = H.in_ready;
     if (!H.in_ready) continue;
-    for (int i = 0; i < 4; ++i) H.q_wodom[i] = H.in_q[i];
-    for (int i = 0; i < 3; ++i) H.t_wodom[i] = H.in_t[i];
-    F.in_ptr[0] = H.in_p[0];
-    F.in_ptr[1] = H.in_p[1];
-    F.nc_in = H.in_n[0];
-    F.ns_in = H.in_n[1];
-    host_initial_guess(H, H.pose);
+    if (!H.stk_launched) {
+      set_error("loam_mapper: stack buffers of the frame's parity still in use");
+      return LOAM_ERR_ARG;
+    }
+    any = true;
+    R.active[s] = 1;
+    for (int i = 0; i < 4; ++i) R.wodom[s][i] = H.in_q[i];
+    for (int i = 0; i < 3; ++i) R.wodom[s][4 + i] = H.in_t[i];
+    R.in_p[s] = {H.in_p[0], H.in_p[1]};
+    R.in_n[s] = {H.in_n[0], H.in_n[1]};
     H.in_ready = false;
     H.stk_launched = false;
   }
-  bool any = false, any_shift = false;
-  for (int s = 0; s < B; ++s) {
-    StreamFrame& F = h->hf[s];
-    HostStream& H = h->hs[s];
-    F.active = H.pending ? 1 : 0;
-    F.shift[0] = F.shift[1] = F.shift[2] = 0;
-    F.err = 0;
-    F.nc_stack = F.ns_stack = 0;
-    F.corner_num[0] = F.corner_num[1] = F.surf_num[0] = F.surf_num[1] = 0;
-    F.sub_n[0] = F.sub_n[1] = 0;
-    F.optimize = 0;
-    if (F.active) {
-      any = true;
-      for (int i = 0; i < 7; ++i) F.pose[i] = H.pose[i];
-      // centerCube + recentering (laser_mapping.cpp:228-444)
-      int cI = cube_of(F.pose[4], F.cen[0]), cJ = cube_of(F.pose[5], F.cen[1]), cK = cube_of(F.pose[6], F.cen[2]);
-      const int dims[3] = {CW, CH, CD};
-      int c3[3] = {cI, cJ, cK};
-      for (int a = 0; a < 3; ++a) {
-        while (c3[a] < 3) { c3[a]++; F.cen[a]++; F.shift[a]++; }
-        while (c3[a] >= dims[a] - 3) { c3[a]--; F.cen[a]--; F.shift[a]--; }
-        if (F.shift[a]) any_shift = true;
-      }
-      F.center[0] = c3[0]; F.center[1] = c3[1]; F.center[2] = c3[2];
-      int vn = 0;
-      for (int i = c3[0] - 2; i <= c3[0] + 2; i++)
-        for (int j = c3[1] - 2; j <= c3[1] + 2; j++)
-          for (int k = c3[2] - 1; k <= c3[2] + 1; k++)
-            if (i >= 0 && i < CW && j >= 0 && j < CH && k >= 0 && k < CD) F.window[vn++] = i + CW * j + CW * CH * k;
-      F.valid_num = vn;
-      // hash cell origin: world metres of the window's low corner, minus a 2-cell margin
-      F.origin[0] = (c3[0] - 2 - F.cen[0]) * 50 - 25 - 2;
-      F.origin[1] = (c3[1] - 2 - F.cen[1]) * 50 - 25 - 2;
-      F.origin[2] = (c3[2] - 1 - F.cen[2]) * 50 - 25 - 2;
-    }
-  }
   if (!any) return LOAM_OK;
+  R.seq = ++h->seq;
   h->frame_counter++;
   D.epoch = h->frame_counter;
-  for (int s = 0; s < B; ++s) {
-    h->hf[s].epoch = h->frame_counter;
-    h->hf[s].cand[0] = h->hf[s].cand[1] = 0;
-  }
   D.cube_tab = h->cube_tab[h->parity];
   hipStream_t st = h->st;
-  bool compact_due = false;  // the graph path has no compaction step: such frames run without it
+  FrameIn* fin = h->fin[fpar].data();
+  if (chained) {
+    for (int s = 0; s < B; ++s) {
+      FrameIn& I = fin[s];
+      I = FrameIn{};
+      I.mode = 1;
+      I.active = R.active[s];
+      for (int i = 0; i < 7; ++i) I.wodom[i] = R.wodom[s][i];
+      I.in_ptr[0] = R.in_p[s][0];
+      I.in_ptr[1] = R.in_p[s][1];
+      I.n[0] = R.in_n[s][0];
+      I.n[1] = R.in_n[s][1];
+      I.epoch = h->frame_counter;
+    }
+  } else {
+    // the host prepares the records: initial guess (:206-207), centerCube + recentering
+    // (:228-444), window (:455-472)
+    for (int s = 0; s < B; ++s) {
+      StreamFrame& F = h->hf[s];
+      const HostStream& H = h->hs[s];
+      frame_reset(F);
+      F.active = R.active[s];
+      if (!F.active) continue;  // (a stream deferred in a frame still in flight stays deferred)
+      F.deferred = 0;
+      for (int i = 0; i < 4; ++i) F.wmap[i] = H.q_wmap_wodom[i];
+      for (int i = 0; i < 3; ++i) F.wmap[4 + i] = H.t_wmap_wodom[i];
+      for (int i = 0; i < 7; ++i) F.wodom[i] = R.wodom[s][i];
+      pose_initial_guess(F.wmap, F.wodom, F.pose);
+      frame_center(F.pose, F.cen, F.center, F.shift);
+      frame_window(F);
+      F.epoch = h->frame_counter;
+      F.in_ptr[0] = R.in_p[s][0];
+      F.in_ptr[1] = R.in_p[s][1];
+      F.nc_in = R.in_n[s][0];
+      F.ns_in = R.in_n[s][1];
+    }
+    for (int s = 0; s < B; ++s) fin[s] = FrameIn{};  // mode 0: the records as uploaded
+  }
+  bool any_shift = false;
+  for (int s = 0; s < B && !chained; ++s)
+    any_shift |= h->hf[s].active && (h->hf[s].shift[0] || h->hf[s].shift[1] || h->hf[s].shift[2]);
+  // arenas past the compaction threshold are compacted ahead of this frame.  With frames queued
+  // behind each other, a little early (the threshold less three frames' growth) so that queued
+  // frames rarely meet a due compaction (they would be deferred); the moves are verbatim, the
+  // results do not depend on when they happen.
+  uint32_t due_at = h->compact_at;
+  if (h->chain && chain_capable(h)) {
+    const uint64_t ahead = 3ull * h->grow_max + 4096ull;
+    due_at = (uint32_t)std::max<uint64_t>(h->compact_at / 2, h->compact_at > ahead ? h->compact_at - ahead : 0);
+  }
+  // (a queued frame: the tails known now are those before the frame in flight, which may add
+  // one frame's growth; the kernels test the tails as they are when they run)
+  bool compact_due = false;
+  const uint64_t unknown = chained ? (uint64_t)h->grow_max : 0ull;
   for (int s = 0; s < B && !compact_due; ++s)
-    compact_due = h->hf[s].arena_tail[0] > h->compact_at || h->hf[s].arena_tail[1] > h->compact_at;
-  const bool graph = h->use_graph && !h->prof && !any_shift && !compact_due && !D.sharded && h->lm_G > 0;
+    compact_due = h->hf[s].arena_tail[0] + unknown > due_at || h->hf[s].arena_tail[1] + unknown > due_at;
+  const bool graph = chained || (h->use_graph && !h->prof && !any_shift && !D.sharded && h->lm_G > 0);
+  R.graph = graph;
   if (graph) {
-    // the frame's whole sequence as one graph launch: records H2D, stack VoxelGrid (forked
-    // stream) beside the submap prep, 2 x (kNN, geometry, LM round), insertion, re-VoxelGrid,
-    // records D2H.  Every kernel argument is fixed per (handle, parity): the frame's values
-    // travel in the stream records.
     hipGraphExec_t& ge = h->gexec[h->parity][fpar];
     if (!ge) {
       hipGraph_t gr = nullptr;
       LOAM_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-      LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(StreamFrame) * B, hipMemcpyHostToDevice, st));
-      k_submap_prep<<<B, 128, 0, st>>>(D);
-      k_stack_counts<<<B, 64, 0, st>>>(D);
-      for (int round = 0; round < 2; ++round) {
-        if (h->knn_tile) {
-          k_tile_bin<<<B * 2, TB_THREADS, 0, st>>>(D, round);
-          k_knn_tile<<<B * D.tk_blk, TK_THREADS, 0, st>>>(D, round);
-        } else if (h->knn_cs == 4) {
-          k_knn<4, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round);
-        } else if (h->knn_cs == 8) {
-          k_knn<8, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round);
-        } else if (h->knn_cs == 16) {
-          k_knn<16, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round);
-        } else if (h->knn_lanes == 2) {
-          k_knn<2><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
-        } else {
-          k_knn<1><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
-        }
-        k_geom<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
-        k_lm_round<<<lm_padded(B) * h->lm_G, LM_THREADS, 0, st>>>(D, round, h->lm_G);
-      }
-      k_insert<<<dim3(16, B), 256, 0, st>>>(D);
-      k_bucket<<<B * 2, VX_THREADS, 0, st>>>(D);
-      k_revox<<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D);
-      LOAM_HIP(hipMemcpyAsync(h->hf.data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
+      capture_frame(h, D, fpar, st);
       LOAM_HIP(hipStreamEndCapture(st, &gr));
       const hipError_t ie = hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0);
       (void)hipGraphDestroy(gr);
       LOAM_HIP(ie);
     }
-    LOAM_HIP(hipStreamWaitEvent(st, h->ev_stack, 0));  // the frame's stacks
-    LOAM_HIP(hipEventRecord(h->ev[0], st));
+    if (!chained) LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(StreamFrame) * B, hipMemcpyHostToDevice, st));
+    if (compact_due) {  // compactions ahead of the graph (a queued frame's k_frame_prep defers if still due)
+      MapperDev Dc = D;
+      Dc.compact_due_at = due_at;
+      k_compact_scan<<<B * 2, VX_THREADS, 0, st>>>(Dc, h->d_new_off);
+      k_compact_copy<<<dim3(128, B * 2), 256, 0, st>>>(Dc, h->d_new_off);
+      k_compact_commit<<<B * 2, 256, 0, st>>>(Dc, h->d_new_off);
+      LOAM_HIP(hipGetLastError());
+    }
+    if (hipEventQuery(h->ev_stack) != hipSuccess)
+      LOAM_HIP(hipStreamWaitEvent(st, h->ev_stack, 0));  // the frame's stacks
+    // a queued frame is not timed: its start is its predecessor's end, and the timing markers
+    // between two graph launches would cost the device time
+    if (!chained) LOAM_HIP(hipEventRecord(h->ev_fr[fpar][0], st));
+    if (h->fin_device)
+      LOAM_HIP(hipMemcpyAsync(h->d_fin[fpar], h->fin[fpar].data(), sizeof(FrameIn) * B, hipMemcpyHostToDevice, st));
     LOAM_HIP(hipGraphLaunch(ge, st));
-    LOAM_HIP(hipEventRecord(h->ev[3], st));
+    if (h->rec_copy_out)
+      LOAM_HIP(hipMemcpyAsync(h->hfo[fpar].data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
+    LOAM_HIP(hipEventRecord(chained ? h->ev_done[fpar] : h->ev_fr[fpar][1], st));
+    h->spar ^= 1;  // the next frame's stacks go to the other buffers
+    return LOAM_OK;
   }
-  if (!graph) {
   LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(StreamFrame) * B, hipMemcpyHostToDevice, st));
-  LOAM_HIP(hipEventRecord(h->ev[0], st));
-  // arenas the last frame left past the compaction threshold are compacted here, queued ahead
-  // of this frame (each workgroup checks its own pair's tail), so the host never waits on them
+  LOAM_HIP(hipEventRecord(h->ev_fr[fpar][0], st));
+  // compaction queued ahead of this frame (each workgroup checks its own pair's tail against
+  // due_at), so the host never waits on it
   if (compact_due) {
-    k_compact_scan<<<B * 2, VX_THREADS, 0, st>>>(D, h->d_new_off);
-    k_compact_copy<<<dim3(128, B * 2), 256, 0, st>>>(D, h->d_new_off);
-    k_compact_commit<<<B * 2, 256, 0, st>>>(D, h->d_new_off);
+    MapperDev Dc = D;
+    Dc.compact_due_at = due_at;
+    k_compact_scan<<<B * 2, VX_THREADS, 0, st>>>(Dc, h->d_new_off);
+    k_compact_copy<<<dim3(128, B * 2), 256, 0, st>>>(Dc, h->d_new_off);
+    k_compact_commit<<<B * 2, 256, 0, st>>>(Dc, h->d_new_off);
     LOAM_HIP(hipGetLastError());
   }
   // the stack VoxelGrids run on the second stream (launch_stacks: at prefetch, or at the start
@@ -2695,10 +3031,10 @@ static int32_t mapper_enqueue(loam_mapper* h) {
   size_t q_tot = 0;
   if (multi) {
     // the stack sizes (identical on every rank) place each stream's queries in the exchange
-    LOAM_HIP(hipMemcpyAsync(h->hf.data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
+    LOAM_HIP(hipMemcpyAsync(h->hfo[fpar].data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
     LOAM_HIP(hipStreamSynchronize(st));
     for (int s = 0; s < B; ++s) {
-      const StreamFrame& F = h->hf[s];
+      const StreamFrame& F = h->hfo[fpar][s];
       h->q_off[s] = (int)q_tot;
       if (F.active) q_tot += (size_t)F.nc_stack + F.ns_stack;
     }
@@ -2750,28 +3086,32 @@ static int32_t mapper_enqueue(loam_mapper* h) {
   LAUNCH(FAM_INSERT, k_bucket<<<B * 2, VX_THREADS, 0, st>>>(D));
   LAUNCH(FAM_REVOX, k_revox<<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D));
   LOAM_HIP(hipGetLastError());
-  LOAM_HIP(hipEventRecord(h->ev[3], st));
-  LOAM_HIP(hipMemcpyAsync(h->hf.data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
-  }  // !graph
-  h->inflight = true;
-  h->last_graph = graph;
-  h->last_spar = fpar;
+  LOAM_HIP(hipMemcpyAsync(h->hfo[fpar].data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
+  LOAM_HIP(hipEventRecord(h->ev_fr[fpar][1], st));
   h->spar ^= 1;  // the next frame's stacks go to the other buffers
   return LOAM_OK;
 }
 
-// wait for the frame in flight, then the host side of solveMapping: transformUpdate (:147-151),
-// stats, errors, timing
-static int32_t mapper_finish(loam_mapper* h) {
-  h->inflight = false;
-  MapperDev& D = h->D;
+static int32_t mapper_replay(loam_mapper* h, const FrameRec& R, const std::vector<int>& redo);
+
+// the host side of one finished frame: transformUpdate (:147-151), stats, errors, timing.
+// replay: a deferred frame run again for some streams (the others keep what their frame gave).
+static int32_t mapper_finish_rec(loam_mapper* h, const FrameRec& R, bool replay) {
   const int B = h->B;
-  const bool graph = h->last_graph;
-  LOAM_HIP(hipStreamSynchronize(h->st));
-  float ms_total = 0, ms_opt = 0;
-  LOAM_HIP(hipEventElapsedTime(&ms_total, h->ev[0], h->ev[3]));
-  if (graph) ms_opt = ms_total;  // no event inside the graph (the optimisation block is most of it)
-  else LOAM_HIP(hipEventElapsedTime(&ms_opt, h->ev[1], h->ev[2]));
+  float ms_total = 0, ms_opt = 0;  // (0 for a queued frame: not timed)
+  if (R.chained) {
+    LOAM_HIP(hipEventSynchronize(h->ev_done[R.fpar]));
+  } else {
+    LOAM_HIP(hipEventSynchronize(h->ev_fr[R.fpar][1]));
+    LOAM_HIP(hipEventElapsedTime(&ms_total, h->ev_fr[R.fpar][0], h->ev_fr[R.fpar][1]));
+    if (R.graph) ms_opt = ms_total;  // no event inside the graph (the optimisation block is most of it)
+    else LOAM_HIP(hipEventElapsedTime(&ms_opt, h->ev[1], h->ev[2]));
+  }
+  const StreamFrame* FO = h->hfo[R.fpar].data();
+  if (R.seq > h->mirror_seq) {  // the newest records the host has seen
+    std::memcpy(h->hf.data(), FO, sizeof(StreamFrame) * B);
+    h->mirror_seq = R.seq;
+  }
   if (h->prof) {
     for (size_t k = 0; k < h->ev_fam.size(); ++k) {
       float ms = 0;
@@ -2781,7 +3121,7 @@ static int32_t mapper_finish(loam_mapper* h) {
     }
     // algorithmic bytes (DESIGN.md "Kernels"): what each family must read / write
     for (int s = 0; s < B; ++s) {
-      const StreamFrame& F = h->hf[s];
+      const StreamFrame& F = FO[s];
       if (!F.active) continue;
       const double nst = (double)F.nc_stack + F.ns_stack;
       h->fam_bytes[FAM_STACK] += 16.0 * ((double)F.nc_in + F.ns_in + nst);
@@ -2796,17 +3136,29 @@ static int32_t mapper_finish(loam_mapper* h) {
       }
     }
   }
-  // host bookkeeping + compaction decisions
+  h->last_spar = R.fpar;
+  // host bookkeeping
   int32_t status = LOAM_OK;
+  std::vector<int> redo;
   for (int s = 0; s < B; ++s) {
-    StreamFrame& F = h->hf[s];
+    const StreamFrame& F = FO[s];
     HostStream& H = h->hs[s];
-    H.solved_last = F.active != 0;
-    if (!F.active) continue;
+    if (R.active[s] && F.deferred) {  // left to the host (k_frame_prep): run again below
+      redo.push_back(s);
+      continue;
+    }
+    if (!replay || R.active[s]) H.solved_last = R.active[s] && F.active;
+    if (!R.active[s] || !F.active) continue;
     H.pending = false;
     for (int i = 0; i < 7; ++i) H.pose[i] = F.pose[i];
+    for (int i = 0; i < 4; ++i) H.q_wodom[i] = R.wodom[s][i];
+    for (int i = 0; i < 3; ++i) H.t_wodom[i] = R.wodom[s][4 + i];
     host_transform_update(H);
     H.frame++;
+    for (int m = 0; m < 2; ++m) {  // arena growth of one frame (compaction foresight)
+      if (F.arena_tail[m] >= h->last_tail[s][m]) h->grow_max = std::max(h->grow_max, F.arena_tail[m] - h->last_tail[s][m]);
+      h->last_tail[s][m] = F.arena_tail[m];
+    }
     loam_map_stats& S = H.st;
     S.optimized = F.optimize;
     S.corner_stack = F.nc_stack;
@@ -2824,10 +3176,15 @@ static int32_t mapper_finish(loam_mapper* h) {
       S.lm[r].initial_cost = L.initial_cost;
       S.lm[r].final_cost = L.min_cost;
     }
-    for (int a = 0; a < 3; ++a) S.center[a] = F.center[a];
+    for (int a = 0; a < 3; ++a) {
+      S.center[a] = F.center[a];
+      H.cen[a] = F.cen[a];
+    }
     S.valid_num = F.valid_num;
     S.ms_total = ms_total;
     S.ms_opt = ms_opt;
+    S.queued = R.chained ? 1 : 0;
+    S.rerun = replay ? 1 : 0;
     if (h->prof) h->fam_bytes[FAM_REVOX] += (double)F.vx_bytes;  // counted by k_revox
     if (F.err) {
       // the frame is committed as computed (pose, insertion, re-VoxelGrid ran on the device);
@@ -2837,26 +3194,205 @@ static int32_t mapper_finish(loam_mapper* h) {
       if (status == LOAM_OK || st == LOAM_ERR_SYNC) status = st;
     }
   }
+  if (!redo.empty()) {
+    const int32_t rc = mapper_replay(h, R, redo);
+    if (rc != LOAM_OK && (status == LOAM_OK || rc == LOAM_ERR_SYNC)) status = rc;
+  }
   return status;
 }
 
+// Enqueue, on the host-prepared path, the streams `run` of a frame whose inputs and stack were
+// taken earlier (R: a pending frame, or a deferred one to run again): the stack buffers of its
+// parity still hold them (no stack is launched into a parity a frame in the queue holds).
+static int32_t enqueue_saved(loam_mapper* h, const FrameRec& R, const std::vector<int>& run, FrameRec& out) {
+  const int B = h->B;
+  std::vector<HostStream> saved(h->hs.begin(), h->hs.end());  // the inputs given since
+  const int spar = h->spar;
+  for (int s = 0; s < B; ++s) h->hs[s].in_ready = false;
+  for (int s : run) {
+    HostStream& H = h->hs[s];
+    H.in_ready = true;
+    H.stk_launched = true;
+    H.in_p[0] = R.in_p[s][0];
+    H.in_p[1] = R.in_p[s][1];
+    H.in_n[0] = R.in_n[s][0];
+    H.in_n[1] = R.in_n[s][1];
+    for (int i = 0; i < 4; ++i) H.in_q[i] = R.wodom[s][i];
+    for (int i = 0; i < 3; ++i) H.in_t[i] = R.wodom[s][4 + i];
+  }
+  h->spar = R.fpar;
+  const int32_t rc = mapper_enqueue(h, false, out);
+  for (int s = 0; s < B; ++s) {  // restore the pending inputs
+    HostStream& H = h->hs[s];
+    const HostStream& O = saved[s];
+    H.in_ready = O.in_ready;
+    H.stk_launched = O.stk_launched;
+    for (int m = 0; m < 2; ++m) {
+      H.in_p[m] = O.in_p[m];
+      H.in_n[m] = O.in_n[m];
+    }
+    for (int i = 0; i < 4; ++i) H.in_q[i] = O.in_q[i];
+    for (int i = 0; i < 3; ++i) H.in_t[i] = O.in_t[i];
+  }
+  h->spar = spar;
+  return rc;
+}
+
+// A deferred frame (k_frame_prep found a recentering or compaction due, or followed a deferred
+// frame) runs again for its deferred streams on the host-prepared path, with the inputs and the
+// stack it was given.  The device work queued after it, if any, left those streams alone (they
+// were inactive).
+static int32_t mapper_replay(loam_mapper* h, const FrameRec& R, const std::vector<int>& redo) {
+  const int B = h->B;
+  LOAM_HIP(hipStreamSynchronize(h->st));
+  for (FrameRec& Q : h->q) {  // every frame in flight has finished on the device
+    if (Q.pending) continue;
+    if (Q.seq > h->mirror_seq) {  // the newest records
+      std::memcpy(h->hf.data(), h->hfo[Q.fpar].data(), sizeof(StreamFrame) * B);
+      h->mirror_seq = Q.seq;
+    }
+    // frames queued behind this one defer the same streams (k_frame_prep): no frame is queued
+    // behind them until they have run again (chain_ok), so the device's deferral flags, which the
+    // runs again clear, are never read meanwhile
+    for (int s = 0; s < B; ++s) Q.has_deferred |= Q.active[s] && h->hfo[Q.fpar][s].deferred;
+  }
+  FrameRec R2;
+  int32_t rc = enqueue_saved(h, R, redo, R2);
+  if (rc == LOAM_OK && R2.seq) rc = mapper_finish_rec(h, R2, true);
+  return rc;
+}
+
+// a pending frame at the front of the queue is enqueued (its predecessor has been waited for)
+static int32_t launch_front(loam_mapper* h) {
+  if (h->q.empty() || !h->q.front().pending) return LOAM_OK;
+  FrameRec P = std::move(h->q.front());
+  h->q.pop_front();
+  std::vector<int> run;
+  for (int s = 0; s < h->B; ++s)
+    if (P.active[s]) run.push_back(s);
+  FrameRec R;
+  TRY(enqueue_saved(h, P, run, R));
+  R.behind = P.behind;
+  if (R.seq) h->q.push_front(std::move(R));
+  return LOAM_OK;
+}
+
+static int32_t finish_oldest(loam_mapper* h) {
+  TRY(launch_front(h));
+  if (h->q.empty()) return LOAM_OK;
+  FrameRec R = std::move(h->q.front());
+  h->q.pop_front();
+  return mapper_finish_rec(h, R, false);
+}
+
+static int32_t settle_all(loam_mapper* h) {
+  int32_t status = LOAM_OK;
+  while (!h->q.empty()) {
+    const int32_t rc = finish_oldest(h);
+    if (rc != LOAM_OK && (status == LOAM_OK || rc == LOAM_ERR_SYNC)) status = rc;
+  }
+  return status;
+}
+
+// can the next frame be queued behind the one in flight?  Not when the host foresees a
+// recentering for it: the initial guess from the transform known now, with a 2 m margin for the
+// correction of the frame in flight.  (k_frame_prep checks exactly and defers the frame when the
+// foresight was wrong.)  Compactions are queued ahead of it instead (mapper_enqueue).
+static bool chain_capable(const loam_mapper* h) {
+  return h->use_graph && !h->prof && !h->D.sharded && h->lm_G > 0;
+}
+
+static bool chain_ok(const loam_mapper* h) {
+  if (!h->chain || !chain_capable(h)) return false;
+  for (const FrameRec& Q : h->q)
+    if (Q.has_deferred || Q.pending) return false;
+  const int dims[3] = {CW, CH, CD};
+  const double R = 2.0;
+  for (int s = 0; s < h->B; ++s) {
+    const HostStream& H = h->hs[s];
+    if (!H.in_ready) continue;
+    const StreamFrame& F = h->hf[s];
+    double wmap[7], wodom[7], pose[7];
+    for (int i = 0; i < 4; ++i) {
+      wmap[i] = H.q_wmap_wodom[i];
+      wodom[i] = H.in_q[i];
+    }
+    for (int i = 0; i < 3; ++i) {
+      wmap[4 + i] = H.t_wmap_wodom[i];
+      wodom[4 + i] = H.in_t[i];
+    }
+    pose_initial_guess(wmap, wodom, pose);
+    for (int a = 0; a < 3; ++a)
+      for (double d : {-R, R}) {
+        const int c = cube_of(pose[4 + a] + d, F.cen[a]);
+        if (c < 3 || c >= dims[a] - 3) return false;
+      }
+  }
+  return true;
+}
+
+// Frames in the queue, oldest first, at most two: a frame in flight may have one more behind
+// it, queued on the device (chained) or, when the host cannot queue it there (chain_ok), kept
+// pending with its inputs and stack taken, and enqueued once its predecessor has been waited for.
+// loam_mapper_wait always finishes the oldest frame, so frame f + 1 can be given before frame f
+// is waited for, whichever way it runs.
 int32_t loam_mapper_solve_async(loam_mapper* h) {
   if (!h) return LOAM_ERR_ARG;
   LOAM_HIP(hipSetDevice(h->dev));
-  if (h->inflight) TRY(mapper_finish(h));
-  return mapper_enqueue(h);
+  if (h->q.size() >= 2) TRY(finish_oldest(h));
+  TRY(launch_front(h));
+  FrameRec R;
+  const bool behind = !h->q.empty();
+  if (h->q.empty()) {
+    TRY(mapper_enqueue(h, false, R));
+  } else if (chain_ok(h)) {
+    TRY(mapper_enqueue(h, true, R));
+  } else {  // pending: its stack now, beside the frame in flight; the rest after that frame
+    TRY(launch_stacks(h));
+    R.fpar = h->spar;
+    R.pending = true;
+    const int B = h->B;
+    R.active.assign(B, 0);
+    R.wodom.assign(B, std::array<double, 7>{0, 0, 0, 1, 0, 0, 0});
+    R.in_p.assign(B, std::array<const float4*, 2>{nullptr, nullptr});
+    R.in_n.assign(B, std::array<int, 2>{0, 0});
+    bool any = false;
+    for (int s = 0; s < B; ++s) {
+      HostStream& H = h->hs[s];
+      if (!H.in_ready) continue;
+      if (!H.stk_launched) {
+        set_error("loam_mapper: stack buffers of the frame's parity still in use");
+        return LOAM_ERR_ARG;
+      }
+      any = true;
+      R.active[s] = 1;
+      for (int i = 0; i < 4; ++i) R.wodom[s][i] = H.in_q[i];
+      for (int i = 0; i < 3; ++i) R.wodom[s][4 + i] = H.in_t[i];
+      R.in_p[s] = {H.in_p[0], H.in_p[1]};
+      R.in_n[s] = {H.in_n[0], H.in_n[1]};
+      H.in_ready = false;
+      H.stk_launched = false;
+    }
+    if (!any) return LOAM_OK;
+    R.seq = 1;  // (a real sequence number when it is enqueued)
+    h->spar ^= 1;
+  }
+  R.behind = behind;
+  if (R.seq) h->q.push_back(std::move(R));
+  return LOAM_OK;
 }
 
 int32_t loam_mapper_wait(loam_mapper* h) {
   if (!h) return LOAM_ERR_ARG;
-  if (!h->inflight) return LOAM_OK;
+  if (h->q.empty()) return LOAM_OK;
   LOAM_HIP(hipSetDevice(h->dev));
-  return mapper_finish(h);
+  return finish_oldest(h);  // (a pending oldest frame is enqueued first)
 }
 
 int32_t loam_mapper_solve(loam_mapper* h) {
   TRY(loam_mapper_solve_async(h));
-  return loam_mapper_wait(h);
+  SETTLE(h);
+  return LOAM_OK;
 }
 
 int32_t loam_mapper_debug_counters(loam_mapper* h, uint64_t* out, int32_t n, int32_t reset) {
@@ -2898,7 +3434,7 @@ int32_t loam_mapper_reset_kernel_times(loam_mapper* h) {
 }
 
 int32_t loam_mapper_pose(loam_mapper* h, int32_t s, double* q_w, double* t_w) {
-  SETTLE(h);
+  SETTLE_RESULTS(h);
   TRY(check_stream(h, s));
   if (!q_w || !t_w) return LOAM_ERR_ARG;
   const HostStream& H = h->hs[s];
@@ -2913,7 +3449,7 @@ int32_t loam_mapper_pose(loam_mapper* h, int32_t s, double* q_w, double* t_w) {
 }
 
 int32_t loam_mapper_stats(loam_mapper* h, int32_t s, loam_map_stats* st) {
-  SETTLE(h);
+  SETTLE_RESULTS(h);
   TRY(check_stream(h, s));
   if (!st) return LOAM_ERR_ARG;
   *st = h->hs[s].st;
@@ -2921,10 +3457,10 @@ int32_t loam_mapper_stats(loam_mapper* h, int32_t s, loam_map_stats* st) {
 }
 
 int32_t loam_mapper_get_state(loam_mapper* h, int32_t s, int32_t* cen, double* q, double* t) {
-  SETTLE(h);
+  SETTLE_RESULTS(h);
   TRY(check_stream(h, s));
   if (!cen || !q || !t) return LOAM_ERR_ARG;
-  for (int a = 0; a < 3; ++a) cen[a] = h->hf[s].cen[a];
+  for (int a = 0; a < 3; ++a) cen[a] = h->hs[s].cen[a];
   for (int i = 0; i < 4; ++i) q[i] = h->hs[s].q_wmap_wodom[i];
   for (int i = 0; i < 3; ++i) t[i] = h->hs[s].t_wmap_wodom[i];
   return LOAM_OK;
@@ -2951,10 +3487,10 @@ int32_t loam_mapper_set_state(loam_mapper* h, int32_t s, const int32_t* cen, con
   bool moved = false;
   for (int a = 0; a < 3; ++a) {
     moved |= h->hf[s].cen[a] != cen[a];
-    h->hf[s].cen[a] = cen[a];
+    h->hf[s].cen[a] = h->hs[s].cen[a] = cen[a];
   }
-  for (int i = 0; i < 4; ++i) h->hs[s].q_wmap_wodom[i] = q[i];
-  for (int i = 0; i < 3; ++i) h->hs[s].t_wmap_wodom[i] = t[i];
+  for (int i = 0; i < 4; ++i) h->hs[s].q_wmap_wodom[i] = h->hf[s].wmap[i] = q[i];
+  for (int i = 0; i < 3; ++i) h->hs[s].t_wmap_wodom[i] = h->hf[s].wmap[4 + i] = t[i];
   if (moved)  // cube world positions changed: rebuild every cube's cell index
     for (int m = 0; m < 2; ++m) TRY(build_cube_index(h, s, m, 0, NCUBE));
   return LOAM_OK;

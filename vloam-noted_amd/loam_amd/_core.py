@@ -45,7 +45,8 @@ class MapStats(ctypes.Structure):
     _fields_ = [("optimized", c_i32), ("corner_stack", c_i32), ("surf_stack", c_i32),
                 ("corner_map", c_i32), ("surf_map", c_i32), ("corner_num", c_i32 * 2),
                 ("surf_num", c_i32 * 2), ("lm", LMStats * 2), ("center", c_i32 * 3),
-                ("valid_num", c_i32), ("ms_total", c_d), ("ms_opt", c_d)]
+                ("valid_num", c_i32), ("ms_total", c_d), ("ms_opt", c_d), ("queued", c_i32),
+                ("rerun", c_i32)]
 
 
 class OdomStats(ctypes.Structure):

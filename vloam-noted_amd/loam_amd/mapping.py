@@ -109,11 +109,13 @@ class BatchMapper:
         check(lib().loam_mapper_solve(self.h))
 
     def solve_async(self):
-        """enqueue solveMapping for the streams with an input and return (include/loam_core.h);
-        results after wait() (every other call waits first)"""
+        """enqueue solveMapping for the streams with an input and return (include/loam_core.h).
+        With a frame already in flight the new one is queued behind it (on the device for
+        graph-path handles): give frame f + 1 and call this before waiting for frame f."""
         check(lib().loam_mapper_solve_async(self.h))
 
     def wait(self):
+        """finish the oldest frame in the queue; pose / stats / get_state then report it"""
         check(lib().loam_mapper_wait(self.h))
 
     def prefetch(self):
