@@ -56,9 +56,15 @@ int main() {
   }
   const char* names[] = {"plain stream order", "D2H copy (4 KiB, page-locked) between", "untimed event record between",
                          "timed event record between", "graph -> graph", "graph with D2H node -> graph",
-                         "graph with D2H node + untimed event -> graph"};
+                         "graph with D2H node + untimed event -> graph",
+                         "graph -> wait (event of a 2nd stream, done) -> graph",
+                         "graph -> wait (2nd stream event, pending at enqueue) -> graph"};
+  hipStream_t st2;
+  check(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking), "stream2");
+  hipEvent_t ev2;
+  check(hipEventCreateWithFlags(&ev2, hipEventDisableTiming), "ev2");
   for (int clean = 0; clean < 2; ++clean) {
-    for (int v = 0; v < 7; ++v) {
+    for (int v = 0; v < 9; ++v) {
       double tot = 0;
       const int reps = 20;
       for (int r = 0; r < reps; ++r) {
@@ -75,8 +81,18 @@ int main() {
           if (clean) {  // (graphs hold the full size; the clean rows use the plain forms only)
             k_dirty<<<1024, 256, 0, st>>>(buf, w, stamp);
           } else {
-            hipGraphLaunch(v == 4 ? g_dirty : g_dirty_copy, st);
+            if (v == 7) {  // an event of stream 2, complete before anything is enqueued here
+              k_stamp<<<1, 64, 0, st2>>>(stamp + 4);
+              hipEventRecord(ev2, st2);
+              hipStreamSynchronize(st2);
+            }
+            if (v == 8) {  // pending at enqueue, done while the first graph runs
+              k_stamp<<<1, 64, 0, st2>>>(stamp + 4);
+              hipEventRecord(ev2, st2);
+            }
+            hipGraphLaunch(v == 4 || v >= 7 ? g_dirty : g_dirty_copy, st);
             if (v == 6) hipEventRecord(ev, st);
+            if (v >= 7) hipStreamWaitEvent(st, ev2, 0);
           }
           hipGraphLaunch(g_stamp, st);
         }

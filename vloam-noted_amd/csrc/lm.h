@@ -542,13 +542,51 @@ __device__ inline bool lm_step_wave(const double* partials, int nblk, LmState& S
 // that running workgroups hold.  No workgroup waits for one that may not be resident, so
 // handles sharing the GPU cannot deadlock (the leaders are the first blocks of every grid; a
 // member that starts after the round ended sees DONE and leaves).  The leader keeps the
-// trust-region state in its LDS and runs the step.  Hand-offs follow the agent-scope
-// release/acquire recipe (cdna_hip_programming.md §6 Guideline 16): partials are plain
-// stores + drain + release fence + relaxed counter; the eval point is published with sc1
-// (atomic) stores + drain + a relaxed generation; consumers poll relaxed and acquire once.
-// Every spin is bounded (err_code).
+// trust-region state in its LDS and runs the step.  Every word handed between workgroups is an
+// agent-scope atomic (sc1: written through / read past the XCD's L2): partials are stored so,
+// drained, then counted with a relaxed ticket; the eval point is published with sc1 stores +
+// drain + a relaxed generation; consumers poll relaxed and read the words with sc1 loads.  No
+// fence: on gfx950 an agent-scope release fence writes back the whole L2 of the XCD and an
+// acquire invalidates it (buffer_wbl2 / buffer_inv), whatever is dirty or cached from other
+// kernels (LM_HANDOFF_FENCES=1 builds the fence recipe of cdna_hip_programming.md §6 Guideline
+// 16 instead).  Every spin is bounded (err_code).
 // ---------------------------------------------------------------------------------------
 #define RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+#ifndef LM_HANDOFF_FENCES
+#define LM_HANDOFF_FENCES 0
+#endif
+
+__device__ inline void lm_part_store(double* p, double v) {
+#if LM_HANDOFF_FENCES
+  *p = v;
+#else
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v), RLX_AGENT);
+#endif
+}
+
+__device__ inline double lm_part_load(const double* p) {
+#if LM_HANDOFF_FENCES
+  return *p;
+#else
+  return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), RLX_AGENT));
+#endif
+}
+
+// the producer side of a hand-off: this thread's stores are complete before what follows
+__device__ inline void lm_release() {
+#if LM_HANDOFF_FENCES
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// the consumer side, after the polled word showed the hand-off
+__device__ inline void lm_acquire() {
+#if LM_HANDOFF_FENCES
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+}
 
 constexpr int LM_MAX_PASSES = 8;          // a round needs <= 1 + max_num_iterations = 5
 constexpr uint32_t LM_SPIN_LIMIT = 1u << 21;
@@ -589,12 +627,11 @@ template <int kThreads>
 __device__ inline void lm_share(const LmJob& J, const double* X, int c, int G, int pass, double* bsum) {
   const int tid = threadIdx.x;
   lm_eval_sum<kThreads>(J.R, J.nrec, X, c, G, bsum);
-  if (tid < LM_NACC) J.part[(size_t)c * LM_NACC + tid] = bsum[tid];
+  if (tid < LM_NACC) lm_part_store(&J.part[(size_t)c * LM_NACC + tid], bsum[tid]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lm_release();
     __hip_atomic_fetch_add(&J.sync[4 + LM_MAX_PASSES + pass], 1u, RLX_AGENT);
   }
 }
@@ -621,7 +658,7 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
         int st = LM_DONE, c = G, p = 0;
         if (lm_spin_ge(&sync[1], want)) {  // a member that waits too long just leaves
           const uint32_t gen = __hip_atomic_load(&sync[1], RLX_AGENT);
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          lm_acquire();
           st = (int)__hip_atomic_load(&sync[2], RLX_AGENT);
           p = (int)gen - 1;
           if (st != LM_DONE && p < LM_MAX_PASSES) {
@@ -695,12 +732,11 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
         const int c = __builtin_amdgcn_readfirstlane(sshare);
         if (c >= G) break;
         lm_eval_sum<kThreads>(J.R, J.nrec, X, c, G, bsum);
-        if (tid < LM_NACC) J.part[(size_t)c * LM_NACC + tid] = bsum[tid];
+        if (tid < LM_NACC) lm_part_store(&J.part[(size_t)c * LM_NACC + tid], bsum[tid]);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // every thread has read sshare and stored its part
         if (tid == 0) {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          lm_release();
           __hip_atomic_fetch_add(&sync[4 + LM_MAX_PASSES + pass], 1u, RLX_AGENT);
           sshare = 1 + (int)__hip_atomic_fetch_add(&sync[4 + pass], 1u, RLX_AGENT);
         }
@@ -716,8 +752,7 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
     // ---- every share complete (the others are held by running workgroups)
     if (tid == 0 && G > 1) {
       if (lm_spin_ge(&sync[4 + LM_MAX_PASSES + pass], (uint32_t)(G - 1))) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lm_acquire();
       } else {
         atomicOr(J.err, J.err_code);
         sstat = -1;
@@ -742,11 +777,11 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
         for (; c + 8 <= G; c += 8) {
           double q[8];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) q[u] = part[(size_t)(c + u) * LM_NACC + lane];
+          for (int u = 0; u < 8; ++u) q[u] = lm_part_load(&part[(size_t)(c + u) * LM_NACC + lane]);
 #pragma unroll
           for (int u = 0; u < 8; ++u) v += q[u];
         }
-        for (; c < G; ++c) v += part[(size_t)c * LM_NACC + lane];
+        for (; c < G; ++c) v += lm_part_load(&part[(size_t)c * LM_NACC + lane]);
         sred[lane] = v;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

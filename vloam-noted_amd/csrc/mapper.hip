@@ -1,20 +1,27 @@
 // mapper.hip — LaserMapping::solveMapping (laser_mapping.cpp:212-814) on MI355X.
 //
 // One handle = B independent mapping streams; every launch below covers all of them.
-// Per frame (all device resident, one host round-trip at the end for the poses):
+// Per frame (all device resident):
+//   k_stack_part/_cat  VoxelGrid of laserCloudCornerLast (0.4 m) / SurfLast (0.8 m) (:492-500),
+//                      on a second stream, ahead of the frame (loam_mapper_prefetch / the
+//                      solve), double-buffered by frame parity; k_stack_ds at many streams
 //   k_shift_cubes      ring-buffer recentering of the 21x21x11 cube grid (:252-444), rare
-//   k_stack_ds         VoxelGrid of laserCloudCornerLast (0.4 m) / SurfLast (0.8 m) (:492-500)
-//   k_submap_prep      offsets of the 5x5x3 window cubes in the submap order (:448-489);
+//   k_frame_prep       (graph path) a queued frame's records from the frame before (initial
+//                      guess :206-207, window :228-251), stack sizes, submap offsets (:448-489);
 //                      no per-frame index build: every cube keeps a persistent 1 m cell
 //                      index (cubeindex.h, replaces the KD-tree build :519-520), rebuilt
 //                      only when its content changes (k_revox); exact 5-NN because accepted
 //                      matches need all 5 neighbours within 1 m (:557, :642)
-//   2 x { k_knn         exact 5-NN of every query in the cell hash (:554, :633)
+//   2 x { k_knn         exact 5-NN of every query in the cell index (:554, :633)
 //         k_geom        PCA line / QR plane fit of the neighbours -> factor records (:557-699)
-//         5 x { k_lm_eval  candidate cost + J^T J + J^T r, per-workgroup partials (lm.h)
-//               k_lm_step  one wave per stream: reduce partials, Ceres TR-LM step } }
-//   k_insert           transform stacks with the final pose, assign cubes (:741-788)
-//   k_revox            re-VoxelGrid every window cube (:795-808) into the map arena
+//         k_lm_round    all <= 5 Ceres TR-LM passes, G workgroups per stream (lm.h) }
+//   k_insert_bucket    transform stacks with the final pose, assign cubes (:741-788), group
+//                      the points by target cube
+//   k_revox            re-VoxelGrid every changed window cube (:795-808) into the map arena,
+//                      and its cell index
+//   k_frame_out        (graph path) the records to the host and the frame's done word
+//                      (a last-workgroup hand-off inside k_revox measured 1.5x slower: every
+//                      workgroup's agent-scope release writes back L2)
 //
 // Map storage: per (stream, map) an append-only arena of float4 points + a cube table
 // (offset, count) for the 4851 cubes; window cubes are rewritten at the arena tail every
@@ -53,7 +60,7 @@ constexpr int SUBMAP_BLOCKS = 64;
 constexpr int INS_SLOTS = WIN_VALID_MAX + EXTRA_CAP;
 constexpr int MAP_ERR_SUBMAP = 4, MAP_ERR_EXTRA = 8, MAP_ERR_HASH = 16, MAP_ERR_LM_SYNC = 32,
               MAP_ERR_INDEX = 64, MAP_ERR_LIVE = 128, MAP_ERR_SORT = 256,
-              MAP_ERR_STACK = 512, MAP_ERR_TILE = 1024;
+              MAP_ERR_STACK = 512, MAP_ERR_TILE = 1024, MAP_ERR_STACK_WAIT = 2048;
 
 struct StreamFrame {
   double pose[7];  // in: initial guess (transformAssociateToMap); out: optimised pose
@@ -82,7 +89,7 @@ struct StreamFrame {
   int ntile[2];                   // occupied 2 m query tiles of this round (k_tile_bin)
   unsigned long long vx_bytes;    // algorithmic bytes of this frame's re-VoxelGrid + cell index
   double wodom[7];  // the frame's odometry pose q_wodom (xyzw), t_wodom
-  // q_wmap_wodom, t_wmap_wodom: the frame's initial guess (:206-207) is taken with it, and k_insert
+  // q_wmap_wodom, t_wmap_wodom: the frame's initial guess (:206-207) is taken with it, and k_insert_bucket
   // advances it by the frame's transformUpdate (:147-151) as the host does after the frame
   double wmap[7];
   int deferred;     // a queued frame found a recentering or compaction due: left to the host
@@ -100,6 +107,7 @@ struct FrameIn {
   int mode;
   uint32_t epoch;
   int pad;
+  unsigned long long stack_seq;  // the stack launch (launch_stacks) whose stacks the stream takes
 };
 
 // the stack VoxelGrid inputs of a stream (laser_mapping.cpp:492-500): set when its stack is
@@ -194,6 +202,7 @@ struct MapperDev {
   int tk_blk = 32;       // k_knn_tile workgroups per stream
   int knn_blk = CORR_BLK;  // k_knn workgroups per stream of the cell-split variant
   const FrameIn* fin = nullptr;  // [B] (page-locked host memory) the graph path's frame inputs
+  unsigned long long* stk_ready = nullptr;  // the last stack launch done into this parity (k_stack_done)
   int defer_every = 0;    // tests: queued frames with epoch % defer_every == 0 are deferred
 };
 
@@ -555,6 +564,13 @@ __device__ inline void stack_counts(const MapperDev& D, int s, StreamFrame& F) {
   }
 }
 
+// after a stack launch on the stack stream: its number, released at agent scope; k_frame_prep
+// waits for it on the device (a cross-stream event wait between two graph launches, pending when
+// enqueued, costs ~5 us of the device's time, tools/mb_flush.hip)
+__global__ void k_stack_done(unsigned long long* w, unsigned long long v) {
+  if (threadIdx.x == 0) __hip_atomic_store(w, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ void k_stack_counts(MapperDev D) {
   const int s = D.s0 + blockIdx.x;
   StreamFrame& F = D.fr[s];
@@ -628,6 +644,26 @@ __device__ inline void frame_prep_device(const MapperDev& D, StreamFrame& F, con
   __syncthreads();
 }
 
+// the graph path's last kernel: every stream record to page-locked host memory, then the frame's
+// number (FrameIn.epoch) to the host's done word, with system-scope release: the host waits on
+// that word instead of an event record and a D2H copy between frames
+__global__ void __launch_bounds__(256) k_frame_out(MapperDev D, StreamFrame* out, unsigned long long* done) {
+  constexpr int W = (int)(sizeof(StreamFrame) / 8);
+  static_assert(sizeof(StreamFrame) % 8 == 0, "record copy granularity");
+  const unsigned long long* src = reinterpret_cast<const unsigned long long*>(D.fr + D.s0);
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(out);
+  for (int w = threadIdx.x; w < D.B * W; w += blockDim.x)
+    __hip_atomic_store(dst + w, src[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __threadfence_system();  // every lane's stores complete before the done word
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long e = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(&D.fin[0].epoch),
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 0xFFFFFFFFull;
+    __hip_atomic_store(done, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+
 // FrameIn from page-locked host memory into LDS: one system-scope load per lane, all in flight
 // together (the host wrote it before the launch; each read crosses the host link)
 constexpr int FRAME_IN_WORDS = (int)(sizeof(FrameIn) / 8);
@@ -689,6 +725,17 @@ __global__ void __launch_bounds__(128) k_frame_prep(MapperDev D) {
   __shared__ FrameIn I;
   const unsigned long long t0 = __builtin_readcyclecounter();
   load_frame_in(D.fin + s, &I);
+  __syncthreads();
+  if (threadIdx.x == 0 && I.active && I.stack_seq) {  // the stream's stacks (launched on the stack stream)
+    uint32_t spins = 0;
+    while (__hip_atomic_load(D.stk_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < I.stack_seq) {
+      if (++spins > (1u << 24)) {
+        atomicOr(&F.err, MAP_ERR_STACK_WAIT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(4);
+    }
+  }
   __syncthreads();
   const unsigned long long t1 = __builtin_readcyclecounter();
   if (I.mode == 1) frame_prep_device(D, F, I);  // (block-uniform branch)
@@ -1684,47 +1731,6 @@ __global__ void k_pose_adopt(MapperDev D) {
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// insertion of the stacks into the cube grid with the final pose (laser_mapping.cpp:741-788)
-// ---------------------------------------------------------------------------------------
-__global__ void k_insert(MapperDev D) {
-  const int s = D.s0 + blockIdx.y;
-  StreamFrame& F = D.fr[s];
-  if (!F.active) return;
-  const int nc = F.nc_stack, ns = F.ns_stack;
-  double X[7];
-  for (int i = 0; i < 7; ++i) X[i] = F.pose[i];
-  // transformUpdate (:147-151) for a frame queued behind this one (k_frame_prep); the host
-  // computes the same at the end of the frame
-  if (blockIdx.x == 0 && threadIdx.x == 0) pose_transform_update(X, F.wodom, F.wmap);
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nc + ns; t += gridDim.x * blockDim.x) {
-    const int m = t < nc ? 0 : 1;
-    const int i = m == 0 ? t : t - nc;
-    const float4 sel = to_map(X, D.stack[m][(size_t)s * D.max_in + i]);
-    const int ci = cube_of(sel.x, F.cen[0]), cj = cube_of(sel.y, F.cen[1]), ck = cube_of(sel.z, F.cen[2]);
-    int tag = -1;
-    // sharded: only the owner of the point's 4 m block stores it (comm.h)
-    const bool mine = !D.sharded || shard_owner(sel.x, sel.y, sel.z, 1.0f / D.leaf[m], D.blk_v[m], D.nrank) == D.rank;
-    if (mine && ci >= 0 && ci < CW && cj >= 0 && cj < CH && ck >= 0 && ck < CD) {
-      tag = ci + CW * cj + CW * CH * ck;
-      const bool in_window = ci >= F.center[0] - 2 && ci <= F.center[0] + 2 &&
-                             cj >= F.center[1] - 2 && cj <= F.center[1] + 2 &&
-                             ck >= F.center[2] - 1 && ck <= F.center[2] + 1;
-      if (!in_window) {
-        uint32_t* fl = D.extra_flag + sm_index(s, m) * NCUBE + tag;
-        if (atomicExch(fl, F.epoch) != F.epoch) {
-          int e = atomicAdd(&F.extra_n[m], 1);
-          if (e < EXTRA_CAP) F.extra_list[m][e] = tag;
-          else atomicOr(&F.err, MAP_ERR_EXTRA);
-        }
-      }
-    }
-    const size_t o = sm_index(s, m) * D.max_in + i;
-    D.ins_pts[o] = sel;
-    D.ins_tag[o] = tag;
-  }
-}
-
 // which cube (if any) slot `slot` of (s, m) re-filters this frame; false: nothing to do.  A
 // window cube that received nothing and whose content is a VoxelGrid fixed point keeps it:
 // re-filtering it (laser_mapping.cpp:795-808) would reproduce it bit for bit.
@@ -1752,18 +1758,56 @@ __device__ inline bool revox_target(const MapperDev& D, int s, int m, int slot, 
 }
 
 // ---------------------------------------------------------------------------------------
-// group the inserted points by target cube (stable counting sort, one workgroup per (stream,
-// map)): each re-VoxelGrid workgroup then reads one contiguous run, in input order
+// insertion of the stacks into the cube grid with the final pose (laser_mapping.cpp:741-788),
+// then the inserted points grouped by target cube (stable counting sort); one workgroup per
+// (stream, map): each re-VoxelGrid workgroup then reads one contiguous run, in input order
 // ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(VX_THREADS) k_bucket(MapperDev D) {
+__global__ void __launch_bounds__(VX_THREADS) k_insert_bucket(MapperDev D) {
   __shared__ int cslot[NCUBE];
   __shared__ uint32_t base[INS_SLOTS];
   __shared__ uint32_t wcnt[VX_WAVES][INS_SLOTS];
   const int sm = 2 * D.s0 + blockIdx.x, s = sm >> 1, m = sm & 1;
-  const StreamFrame& F = D.fr[s];
+  StreamFrame& F = D.fr[s];
   if (!F.active) return;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int n = m == 0 ? F.nc_stack : F.ns_stack;
+  {
+    // insertion of the stack into the cube grid with the final pose (laser_mapping.cpp:741-788):
+    // the map-frame point and its cube; cubes outside the window that receive points are listed
+    double X[7];
+    for (int i = 0; i < 7; ++i) X[i] = F.pose[i];
+    // transformUpdate (:147-151) for a frame queued behind this one (k_frame_prep); the host
+    // computes the same at the end of the frame
+    if (m == 0 && tid == 0) pose_transform_update(X, F.wodom, F.wmap);
+    const int c0 = F.center[0], c1 = F.center[1], c2 = F.center[2];
+    const int e0 = F.cen[0], e1 = F.cen[1], e2 = F.cen[2];
+    const uint32_t epoch = F.epoch;
+    for (int i = tid; i < n; i += VX_THREADS) {
+      const float4 sel = to_map(X, D.stack[m][(size_t)s * D.max_in + i]);
+      const int ci = cube_of(sel.x, e0), cj = cube_of(sel.y, e1), ck = cube_of(sel.z, e2);
+      int tag = -1;
+      // sharded: only the owner of the point's 4 m block stores it (comm.h)
+      const bool mine = !D.sharded || shard_owner(sel.x, sel.y, sel.z, 1.0f / D.leaf[m], D.blk_v[m], D.nrank) == D.rank;
+      if (mine && ci >= 0 && ci < CW && cj >= 0 && cj < CH && ck >= 0 && ck < CD) {
+        tag = ci + CW * cj + CW * CH * ck;
+        const bool in_window = ci >= c0 - 2 && ci <= c0 + 2 && cj >= c1 - 2 && cj <= c1 + 2 && ck >= c2 - 1 && ck <= c2 + 1;
+        if (!in_window) {
+          uint32_t* fl = D.extra_flag + sm_index(s, m) * NCUBE + tag;
+          if (atomicExch(fl, epoch) != epoch) {
+            int e = atomicAdd(&F.extra_n[m], 1);
+            if (e < EXTRA_CAP) F.extra_list[m][e] = tag;
+            else atomicOr(&F.err, MAP_ERR_EXTRA);
+          }
+        }
+      }
+      const size_t o = sm_index(s, m) * D.max_in + i;
+      D.ins_pts[o] = sel;
+      D.ins_tag[o] = tag;
+    }
+    __syncthreads();  // the points, tags and the out-of-window list, for the grouping below
+  }
+  // group the inserted points by target cube (stable counting sort): each re-VoxelGrid
+  // workgroup then reads one contiguous run, in input order
   const int* tag = D.ins_tag + sm_index(s, m) * D.max_in;
   const float4* pts = D.ins_pts + sm_index(s, m) * D.max_in;
   float4* out = D.ins_sorted + sm_index(s, m) * D.max_in;
@@ -1940,7 +1984,6 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
 // one workgroup per (stream, map, slot): block = slot item
 __global__ void __launch_bounds__(VX_THREADS) k_revox(MapperDev D) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
-
   const uint32_t item = 2 * (uint32_t)D.s0 * INS_SLOTS + blockIdx.x;
   const int slot = (int)(item % INS_SLOTS), sm = (int)(item / INS_SLOTS);
   int cube = 0, append = 0;
@@ -2140,6 +2183,7 @@ struct HostStream {
   // the frame in flight (loam_mapper_solve_async) until that solve takes it
   bool in_ready = false;
   bool stk_launched = false;  // its stack VoxelGrid already queued (loam_mapper_prefetch)
+  unsigned long long stk_seq = 0;  // that stack launch (k_stack_done)
   const float4* in_p[2] = {nullptr, nullptr};
   int in_n[2] = {0, 0};
   double in_q[4] = {0, 0, 0, 1}, in_t[3] = {0, 0, 0};
@@ -2165,6 +2209,7 @@ inline std::string map_err_text(int e) {
   add(MAP_ERR_SORT, "PCL-order VoxelGrid input larger than its sort lists / scratch");
   add(MAP_ERR_STACK, "split stack VoxelGrid: a range has more voxels than its LDS groups");
   add(MAP_ERR_TILE, "more than 2046 queries in one 2 m tile (unfiltered stack)");
+  add(MAP_ERR_STACK_WAIT, "the frame's stack VoxelGrid did not finish in time (device wait)");
   return m + " (flags " + std::to_string(e) + ")";
 }
 
@@ -2182,12 +2227,14 @@ struct FrameRec {
   bool has_deferred = false;  // known (its records are back) to have deferred streams
   bool pending = false;       // not enqueued yet: inputs and stack taken, run on the host path later
   bool behind = false;        // solve_async was called with another frame in the queue
+  uint32_t epoch = 0;         // its frame number (the done word frame_out writes)
   int fpar = 0;
   uint64_t seq = 0;  // enqueue order (0: nothing was enqueued)
   std::vector<int> active;
   std::vector<std::array<double, 7>> wodom;
   std::vector<std::array<const float4*, 2>> in_p;
   std::vector<std::array<int, 2>> in_n;
+  std::vector<unsigned long long> stk_seq;
 };
 
 struct loam_mapper {
@@ -2241,6 +2288,15 @@ struct loam_mapper {
   int fin_device = 0, rec_copy_out = 0;    // LOAM_REC_COPY_OUT=1 (measurement): records D2H after the graph
   hipEvent_t ev_fr[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [parity] frame start / records back (timed)
   hipEvent_t ev_done[2] = {nullptr, nullptr};  // [parity] records back (untimed: what a queued frame records)
+  // the graph path's records and done word, written by k_revox's last workgroup (LOAM_FRAME_FLAG=0: a D2H
+  // copy and an event instead)
+  int frame_flag = 1;
+  int stack_event = 0;  // LOAM_STACK_EVENT=1: graph frames wait for their stacks with an event
+  unsigned long long stack_seq = 0;
+  unsigned long long* d_stk_ready = nullptr;  // [2 parities]
+  PinnedArray<unsigned long long> done;  // [2 parities]
+  unsigned long long* done_dev = nullptr;
+  StreamFrame* hfo_dev[2] = {nullptr, nullptr};
   int chain = 1;             // LOAM_CHAIN=0: never queue a frame behind another
   uint32_t grow_max = 0;     // largest arena growth of one frame seen (compaction foresight)
   std::vector<std::array<uint32_t, 2>> last_tail;
@@ -2517,6 +2573,7 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   D.sin = h->sin_buf[0];
   D.stk_n = h->stk_n_buf[0];
   D.stk_err = h->stk_err_buf[0];
+  ALLOC(h->d_stk_ready, 2);
   ALLOC(D.stk_pts, B * 2 * (size_t)D.max_in);
   ALLOC(D.stk_idx, B * 2 * (size_t)D.max_in);
   ALLOC(D.tile_r, B * 2 * (size_t)D.max_in);
@@ -2560,15 +2617,28 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   if (!h->hf.assign(B, StreamFrame{})) return fail(LOAM_ERR_HIP);
   for (int p = 0; p < 2; ++p) {
     void* dp = nullptr;
-    if (!h->hfo[p].assign(B, StreamFrame{}) ||
+    if (!h->hfo[p].assign(B, StreamFrame{}, hipHostMallocMapped | hipHostMallocCoherent) ||
         !h->fin[p].assign(B, FrameIn{}, hipHostMallocMapped | hipHostMallocCoherent) ||
         hipHostGetDevicePointer(&dp, h->fin[p].data(), 0) != hipSuccess)
       return fail(LOAM_ERR_HIP);
     h->fin_dev[p] = reinterpret_cast<const FrameIn*>(dp);
+    if (hipHostGetDevicePointer(&dp, h->hfo[p].data(), 0) != hipSuccess) return fail(LOAM_ERR_HIP);
+    h->hfo_dev[p] = reinterpret_cast<StreamFrame*>(dp);
     void* q = nullptr;
     if (hipMalloc(&q, sizeof(FrameIn) * B) != hipSuccess) return fail(LOAM_ERR_HIP);
     h->allocs.push_back(q);
     h->d_fin[p] = reinterpret_cast<FrameIn*>(q);
+  }
+  {
+    void* dp = nullptr;
+    if (!h->done.assign(2, 0ull, hipHostMallocMapped | hipHostMallocCoherent) ||
+        hipHostGetDevicePointer(&dp, h->done.data(), 0) != hipSuccess)
+      return fail(LOAM_ERR_HIP);
+    h->done_dev = reinterpret_cast<unsigned long long*>(dp);
+    const char* fenv = std::getenv("LOAM_FRAME_FLAG");
+    h->frame_flag = (fenv && fenv[0] == '0') ? 0 : 1;
+    const char* senv = std::getenv("LOAM_STACK_EVENT");
+    h->stack_event = (senv && senv[0] == '1') ? 1 : 0;
   }
   {
     const char* e1 = std::getenv("LOAM_FIN_DEVICE");
@@ -2797,12 +2867,14 @@ static int32_t launch_stacks(loam_mapper* h) {
     if (!go) continue;
     any = true;
     H.stk_launched = true;
+    H.stk_seq = h->stack_seq + 1;
     for (int m = 0; m < 2; ++m) {
       in[s].p[m] = H.in_p[m];
       in[s].n[m] = H.in_n[m];
     }
   }
   if (!any) return LOAM_OK;
+  const unsigned long long seq = ++h->stack_seq;
   MapperDev D = h->D;
   D.sin = h->sin_buf[par];
   D.stk_n = h->stk_n_buf[par];
@@ -2817,6 +2889,7 @@ static int32_t launch_stacks(loam_mapper* h) {
   } else {
     LAUNCH_ON(s2, FAM_STACK, k_stack_ds<<<B * 2, VX_THREADS, 0, s2>>>(D));
   }
+  k_stack_done<<<1, 64, 0, s2>>>(h->d_stk_ready + par, seq);
   LOAM_HIP(hipGetLastError());
   LOAM_HIP(hipEventRecord(h->ev_stack, s2));
   return LOAM_OK;
@@ -2854,10 +2927,10 @@ static void capture_frame(loam_mapper* h, const MapperDev& D, int fpar, hipStrea
     k_geom<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
     k_lm_round<<<lm_padded(B) * h->lm_G, LM_THREADS, 0, st>>>(D, round, h->lm_G);
   }
-  k_insert<<<dim3(16, B), 256, 0, st>>>(D);
-  k_bucket<<<B * 2, VX_THREADS, 0, st>>>(D);
+  k_insert_bucket<<<B * 2, VX_THREADS, 0, st>>>(D);
   k_revox<<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D);
-  if (!h->rec_copy_out) (void)hipMemcpyAsync(h->hfo[fpar].data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st);
+  if (h->frame_flag) k_frame_out<<<1, 256, 0, st>>>(D, h->hfo_dev[fpar], h->done_dev + fpar);
+  else if (!h->rec_copy_out) (void)hipMemcpyAsync(h->hfo[fpar].data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st);
 }
 
 // Enqueue one solveMapping of every stream with an input (the work of loam_mapper_solve up to
@@ -2874,6 +2947,7 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
   D.stk_n = h->stk_n_buf[fpar];
   D.stk_err = h->stk_err_buf[fpar];
   D.fin = h->fin_device ? h->d_fin[fpar] : h->fin_dev[fpar];
+  D.stk_ready = h->d_stk_ready + fpar;
   for (int m = 0; m < 2; ++m) D.stack[m] = h->stack_buf[fpar][m];
   R = FrameRec{};
   R.chained = chained;
@@ -2882,6 +2956,7 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
   R.wodom.assign(B, std::array<double, 7>{0, 0, 0, 1, 0, 0, 0});
   R.in_p.assign(B, std::array<const float4*, 2>{nullptr, nullptr});
   R.in_n.assign(B, std::array<int, 2>{0, 0});
+  R.stk_seq.assign(B, 0ull);
   bool any = false;
   for (int s = 0; s < B; ++s) {  // the inputs become the frame
     HostStream& H = h->hs[s];
@@ -2896,6 +2971,7 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
     for (int i = 0; i < 3; ++i) R.wodom[s][4 + i] = H.in_t[i];
     R.in_p[s] = {H.in_p[0], H.in_p[1]};
     R.in_n[s] = {H.in_n[0], H.in_n[1]};
+    R.stk_seq[s] = H.stk_seq;
     H.in_ready = false;
     H.stk_launched = false;
   }
@@ -2918,6 +2994,7 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
       I.n[0] = R.in_n[s][0];
       I.n[1] = R.in_n[s][1];
       I.epoch = h->frame_counter;
+      I.stack_seq = R.stk_seq[s];
     }
   } else {
     // the host prepares the records: initial guess (:206-207), centerCube + recentering
@@ -2941,7 +3018,12 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
       F.nc_in = R.in_n[s][0];
       F.ns_in = R.in_n[s][1];
     }
-    for (int s = 0; s < B; ++s) fin[s] = FrameIn{};  // mode 0: the records as uploaded
+    for (int s = 0; s < B; ++s) {  // mode 0: the records as uploaded
+      fin[s] = FrameIn{};
+      fin[s].epoch = h->frame_counter;
+      fin[s].active = R.active[s];
+      fin[s].stack_seq = R.stk_seq[s];
+    }
   }
   bool any_shift = false;
   for (int s = 0; s < B && !chained; ++s)
@@ -2983,8 +3065,8 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
       k_compact_commit<<<B * 2, 256, 0, st>>>(Dc, h->d_new_off);
       LOAM_HIP(hipGetLastError());
     }
-    if (hipEventQuery(h->ev_stack) != hipSuccess)
-      LOAM_HIP(hipStreamWaitEvent(st, h->ev_stack, 0));  // the frame's stacks
+    // the frame's stacks: waited for by k_frame_prep on the device (stack_seq)
+    if (h->stack_event && hipEventQuery(h->ev_stack) != hipSuccess) LOAM_HIP(hipStreamWaitEvent(st, h->ev_stack, 0));
     // a queued frame is not timed: its start is its predecessor's end, and the timing markers
     // between two graph launches would cost the device time
     if (!chained) LOAM_HIP(hipEventRecord(h->ev_fr[fpar][0], st));
@@ -2993,7 +3075,9 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
     LOAM_HIP(hipGraphLaunch(ge, st));
     if (h->rec_copy_out)
       LOAM_HIP(hipMemcpyAsync(h->hfo[fpar].data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
-    LOAM_HIP(hipEventRecord(chained ? h->ev_done[fpar] : h->ev_fr[fpar][1], st));
+    if (!chained) LOAM_HIP(hipEventRecord(h->ev_fr[fpar][1], st));
+    else if (!h->frame_flag) LOAM_HIP(hipEventRecord(h->ev_done[fpar], st));
+    R.epoch = h->frame_counter;
     h->spar ^= 1;  // the next frame's stacks go to the other buffers
     return LOAM_OK;
   }
@@ -3082,8 +3166,7 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
     LAUNCH(FAM_OTHER, k_pose_adopt<<<B, 64, 0, st>>>(D));
   }
   LOAM_HIP(hipEventRecord(h->ev[2], st));
-  LAUNCH(FAM_INSERT, k_insert<<<dim3(16, B), 256, 0, st>>>(D));
-  LAUNCH(FAM_INSERT, k_bucket<<<B * 2, VX_THREADS, 0, st>>>(D));
+  LAUNCH(FAM_INSERT, k_insert_bucket<<<B * 2, VX_THREADS, 0, st>>>(D));
   LAUNCH(FAM_REVOX, k_revox<<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D));
   LOAM_HIP(hipGetLastError());
   LOAM_HIP(hipMemcpyAsync(h->hfo[fpar].data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
@@ -3094,12 +3177,33 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
 
 static int32_t mapper_replay(loam_mapper* h, const FrameRec& R, const std::vector<int>& redo);
 
+// a queued frame is done when frame_out has written its number to the done word of its parity
+// (the words only grow: a later frame of the same parity is not enqueued before this one is
+// finished).  The stream is polled for errors while waiting.
+static int32_t wait_done(loam_mapper* h, const FrameRec& R) {
+  const volatile unsigned long long* w = h->done.data() + R.fpar;
+  for (uint64_t spins = 0;; ++spins) {
+    if (__atomic_load_n(const_cast<const unsigned long long*>(w), __ATOMIC_ACQUIRE) >= R.epoch) return LOAM_OK;
+    if ((spins & 1023) == 1023) {
+      const hipError_t e = hipStreamQuery(h->st);
+      if (e == hipSuccess) {  // the stream drained: the word must be there now
+        if (__atomic_load_n(const_cast<const unsigned long long*>(w), __ATOMIC_ACQUIRE) >= R.epoch) return LOAM_OK;
+        set_error("loam_mapper: frame finished without its done word");
+        return LOAM_ERR_HIP;
+      }
+      if (e != hipErrorNotReady) LOAM_HIP(e);
+    }
+  }
+}
+
 // the host side of one finished frame: transformUpdate (:147-151), stats, errors, timing.
 // replay: a deferred frame run again for some streams (the others keep what their frame gave).
 static int32_t mapper_finish_rec(loam_mapper* h, const FrameRec& R, bool replay) {
   const int B = h->B;
   float ms_total = 0, ms_opt = 0;  // (0 for a queued frame: not timed)
-  if (R.chained) {
+  if (R.chained && h->frame_flag) {
+    TRY(wait_done(h, R));
+  } else if (R.chained) {
     LOAM_HIP(hipEventSynchronize(h->ev_done[R.fpar]));
   } else {
     LOAM_HIP(hipEventSynchronize(h->ev_fr[R.fpar][1]));
@@ -3190,7 +3294,7 @@ static int32_t mapper_finish_rec(loam_mapper* h, const FrameRec& R, bool replay)
       // the frame is committed as computed (pose, insertion, re-VoxelGrid ran on the device);
       // the status says it is not trustworthy: the caller resets the stream (include/loam_core.h)
       set_error("loam_mapper_solve: stream " + std::to_string(s) + ": " + map_err_text(F.err));
-      const int32_t st = (F.err & MAP_ERR_LM_SYNC) ? LOAM_ERR_SYNC : LOAM_ERR_CAPACITY;
+      const int32_t st = (F.err & (MAP_ERR_LM_SYNC | MAP_ERR_STACK_WAIT)) ? LOAM_ERR_SYNC : LOAM_ERR_CAPACITY;
       if (status == LOAM_OK || st == LOAM_ERR_SYNC) status = st;
     }
   }
@@ -3213,6 +3317,7 @@ static int32_t enqueue_saved(loam_mapper* h, const FrameRec& R, const std::vecto
     HostStream& H = h->hs[s];
     H.in_ready = true;
     H.stk_launched = true;
+    H.stk_seq = R.stk_seq[s];
     H.in_p[0] = R.in_p[s][0];
     H.in_p[1] = R.in_p[s][1];
     H.in_n[0] = R.in_n[s][0];
@@ -3227,6 +3332,7 @@ static int32_t enqueue_saved(loam_mapper* h, const FrameRec& R, const std::vecto
     const HostStream& O = saved[s];
     H.in_ready = O.in_ready;
     H.stk_launched = O.stk_launched;
+    H.stk_seq = O.stk_seq;
     for (int m = 0; m < 2; ++m) {
       H.in_p[m] = O.in_p[m];
       H.in_n[m] = O.in_n[m];
@@ -3356,6 +3462,7 @@ int32_t loam_mapper_solve_async(loam_mapper* h) {
     R.wodom.assign(B, std::array<double, 7>{0, 0, 0, 1, 0, 0, 0});
     R.in_p.assign(B, std::array<const float4*, 2>{nullptr, nullptr});
     R.in_n.assign(B, std::array<int, 2>{0, 0});
+    R.stk_seq.assign(B, 0ull);
     bool any = false;
     for (int s = 0; s < B; ++s) {
       HostStream& H = h->hs[s];
@@ -3370,6 +3477,7 @@ int32_t loam_mapper_solve_async(loam_mapper* h) {
       for (int i = 0; i < 3; ++i) R.wodom[s][4 + i] = H.in_t[i];
       R.in_p[s] = {H.in_p[0], H.in_p[1]};
       R.in_n[s] = {H.in_n[0], H.in_n[1]};
+      R.stk_seq[s] = H.stk_seq;
       H.in_ready = false;
       H.stk_launched = false;
     }
