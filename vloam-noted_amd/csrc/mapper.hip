@@ -564,11 +564,13 @@ __device__ inline void stack_counts(const MapperDev& D, int s, StreamFrame& F) {
   }
 }
 
-// after a stack launch on the stack stream: its number, released at agent scope; k_frame_prep
+// after a stack launch on the stack stream: its number (agent scope); k_frame_prep
 // waits for it on the device (a cross-stream event wait between two graph launches, pending when
 // enqueued, costs ~5 us of the device's time, tools/mb_flush.hip)
 __global__ void k_stack_done(unsigned long long* w, unsigned long long v) {
-  if (threadIdx.x == 0) __hip_atomic_store(w, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  // (the stack kernels before it on this stream ended with their own release: a relaxed store,
+  // no L2 write-back here)
+  if (threadIdx.x == 0) __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void k_stack_counts(MapperDev D) {
@@ -644,8 +646,8 @@ __device__ inline void frame_prep_device(const MapperDev& D, StreamFrame& F, con
   __syncthreads();
 }
 
-// the graph path's last kernel: every stream record to page-locked host memory, then the frame's
-// number (FrameIn.epoch) to the host's done word, with system-scope release: the host waits on
+// the graph path's last kernel: every stream record to page-locked host memory (write-through
+// stores), then the frame's number (FrameIn.epoch) to the host's done word: the host waits on
 // that word instead of an event record and a D2H copy between frames
 __global__ void __launch_bounds__(256) k_frame_out(MapperDev D, StreamFrame* out, unsigned long long* done) {
   constexpr int W = (int)(sizeof(StreamFrame) / 8);
@@ -654,12 +656,14 @@ __global__ void __launch_bounds__(256) k_frame_out(MapperDev D, StreamFrame* out
   unsigned long long* dst = reinterpret_cast<unsigned long long*>(out);
   for (int w = threadIdx.x; w < D.B * W; w += blockDim.x)
     __hip_atomic_store(dst + w, src[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __threadfence_system();  // every lane's stores complete before the done word
+  // every lane's write-through stores complete before the done word (no fence: a system-scope
+  // release writes back the whole L2, dirty with the frame's map; ~5 us, tools/mb_flush.hip)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned long long e = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(&D.fin[0].epoch),
                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 0xFFFFFFFFull;
-    __hip_atomic_store(done, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(done, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -728,7 +732,9 @@ __global__ void __launch_bounds__(128) k_frame_prep(MapperDev D) {
   __syncthreads();
   if (threadIdx.x == 0 && I.active && I.stack_seq) {  // the stream's stacks (launched on the stack stream)
     uint32_t spins = 0;
-    while (__hip_atomic_load(D.stk_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < I.stack_seq) {
+    // relaxed: the stack sizes read next are not in this XCD's L2 (invalidated at this kernel's
+    // start, not read since) and the stacks themselves are read by later kernels
+    while (__hip_atomic_load(D.stk_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < I.stack_seq) {
       if (++spins > (1u << 24)) {
         atomicOr(&F.err, MAP_ERR_STACK_WAIT);
         break;
