@@ -2610,7 +2610,7 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     ALLOC(D.pose_x, (size_t)D.nrank * B * 8);
     ALLOC(h->d_q_off, B + 1);
     D.q_off = h->d_q_off;
-    if (!h->q_off.assign(B + 1, 0)) return fail(LOAM_ERR_HIP);
+    if (!h->q_off.assign(2 * (B + 1), 0)) return fail(LOAM_ERR_HIP);  // [parity][B + 1]
     if (D.nrank == 1) {  // fixed query slots: no per-frame host read of the stack sizes
       for (size_t s = 0; s <= B; ++s) h->q_off[s] = (int)(s * 2 * (size_t)D.max_in);
       if (hipMemcpyAsync(h->d_q_off, h->q_off.data(), sizeof(int) * (B + 1), hipMemcpyHostToDevice, h->st) !=
@@ -3120,16 +3120,18 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
   LAUNCH(FAM_OTHER, k_stack_counts<<<B, 64, 0, st>>>(D));
   size_t q_tot = 0;
   if (multi) {
-    // the stack sizes (identical on every rank) place each stream's queries in the exchange
-    LOAM_HIP(hipMemcpyAsync(h->hfo[fpar].data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
-    LOAM_HIP(hipStreamSynchronize(st));
+    // each stream's queries in the exchange: slots sized by the frame's input counts, which the
+    // host has without waiting (a VoxelGrid never outputs more points than it reads, :492-500),
+    // identical on every rank.  The host array is double-buffered by the frame parity: its copy
+    // may still be queued when the next frame is enqueued.
+    int* qo = h->q_off.data() + (size_t)fpar * (B + 1);
     for (int s = 0; s < B; ++s) {
-      const StreamFrame& F = h->hfo[fpar][s];
-      h->q_off[s] = (int)q_tot;
-      if (F.active) q_tot += (size_t)F.nc_stack + F.ns_stack;
+      const StreamFrame& F = h->hf[s];
+      qo[s] = (int)q_tot;
+      if (F.active) q_tot += (size_t)F.nc_in + F.ns_in;
     }
-    h->q_off[B] = (int)q_tot;
-    LOAM_HIP(hipMemcpyAsync(h->d_q_off, h->q_off.data(), sizeof(int) * (B + 1), hipMemcpyHostToDevice, st));
+    qo[B] = (int)q_tot;
+    LOAM_HIP(hipMemcpyAsync(h->d_q_off, qo, sizeof(int) * (B + 1), hipMemcpyHostToDevice, st));
   }
   for (int round = 0; round < 2; ++round) {
     if (h->knn_tile) {
