@@ -61,12 +61,24 @@ def test_sort_perm_matches_std_sort(n, kv):
         assert np.array_equal(prims.sort_perm(keys, waves), O.std_sort_perm(keys)), waves
 
 
-@pytest.mark.parametrize("pattern", range(5))
+@pytest.mark.parametrize("pattern", range(8))
 def test_sort_perm_adversarial(pattern):
     """sorted, reversed, organ-pipe and median-of-3-killer inputs: the depth-limit heap sort
-    (__partial_sort) and unbalanced partitions"""
+    (__partial_sort) and unbalanced partitions.  Patterns 5-7 are the exact mode's cube
+    re-filter: distinct sorted keys (old content) with a few random keys appended (new points),
+    which drives introsort into the depth limit on segments of distinct keys (placed by rank,
+    stdsort.h ss_depth_limit) and, with ties to the old keys, of tied keys (the heap itself)"""
     n = 4096
     i = np.arange(n)
+    if pattern >= 5:
+        rng = np.random.default_rng(pattern)
+        n_old, n_new = (14000, 60) if pattern == 5 else (4300, 180)
+        old = np.sort(rng.choice(1 << 22, n_old, replace=False))
+        new = rng.integers(0, 1 << 22, n_new) if pattern != 7 else rng.choice(old, n_new)
+        keys = np.concatenate([old, new]).astype(np.uint32)
+        for waves in (1, 16):
+            assert np.array_equal(prims.sort_perm(keys, waves), O.std_sort_perm(keys)), waves
+        return
     if pattern == 0:
         k = i
     elif pattern == 1:
@@ -95,6 +107,33 @@ def test_voxel_grid_pcl_order_large_and_tied():
         with O.voxel_order(1):
             assert np.array_equal(gpu_voxel(pts, leaf).view(np.uint32), O.voxel_grid(pts, leaf).view(np.uint32))
         assert_centroids_within_order_bound(pts, leaf, gpu_voxel(pts, leaf), ref)
+
+
+def _cube_cloud(n_old, n_single, n_pair, seed, leaf):
+    """a map cube as the exact mode re-filters it: VoxelGrid output (one point per voxel, in voxel
+    order) ++ new points, n_single of them in voxels of their own old point (2-member voxels) and
+    n_pair pairs sharing an old point's voxel (3-member voxels)"""
+    rng = np.random.default_rng(seed)
+    side = int(round(n_old ** (1 / 3) * 1.6))
+    xyz = rng.uniform(0, side * leaf, (n_old * 3, 3)).astype(np.float32)
+    old = O.voxel_grid(np.concatenate([xyz, rng.uniform(0, 50, (len(xyz), 1)).astype(np.float32)], 1), leaf)
+    pick = rng.choice(len(old), n_single + n_pair, replace=False)
+    jitter = lambda: np.float32(0.01 * leaf) * rng.uniform(-1, 1, 4).astype(np.float32)  # noqa: E731
+    new = [old[i] + jitter() for i in pick[:n_single]]
+    new += [old[i] + jitter() for i in pick[n_single:] for _ in range(2)]
+    return np.concatenate([old, np.asarray(new, np.float32)]).astype(np.float32)
+
+
+@pytest.mark.parametrize("n_old,n_single,n_pair", [(13500, 50, 1), (4300, 100, 3), (2000, 5, 0), (2000, 40, 6)])
+def test_voxel_grid_pcl_depth_limit(n_old, n_single, n_pair):
+    """sorted content with a few points appended drives introsort into its depth limit on long
+    segments (tools/introsort_stats.py: the exact mode's cube re-filters); those segments are
+    sorted by (key, element) when the heap's tie order cannot show in a centroid and heap-sorted
+    otherwise (stdsort.h ss_depth_limit): PCL's bits either way, LDS and global scratch paths"""
+    for leaf in (0.4, 0.8):
+        pts = _cube_cloud(n_old, n_single, n_pair, n_old + n_pair, leaf)
+        ref = O.voxel_grid(pts, leaf)
+        assert np.array_equal(prims.voxel_grid_pcl(pts, leaf).view(np.uint32), ref.view(np.uint32)), leaf
 
 
 def test_voxel_grid_edge_cases():

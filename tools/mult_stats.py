@@ -4,7 +4,7 @@ inserted points)?  A voxel of 1 or 2 members sums the same in any order, so a cu
 
     python tools/mult_stats.py [frames]      (CPU only: the oracle pipeline)
 
-New points: the frame's features downsampled with the mapper's leaves (0.2 / 0.4 m) and moved to
+New points: the frame's features downsampled with the mapper's leaves (0.4 / 0.8 m, laser_mapping.cpp:99-105) and moved to
 the map with the frame's final pose; cubes by laser_mapping.cpp:747-756."""
 import collections
 import os
@@ -42,7 +42,7 @@ def main():
         q, t = rec["pose"]
         rot = R.from_quat(q)
         cen = rec["before"]["cen"]
-        for key, leaf in (("corner", 0.2), ("surf", 0.4)):
+        for key, leaf in (("corner", 0.4), ("surf", 0.8)):
             new = rot.apply(downsample(rec[key][:, :3].astype(np.float64), leaf)) + t
             nc = cube_of(new, cen)
             per_cube = collections.defaultdict(list)

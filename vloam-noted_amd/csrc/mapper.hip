@@ -287,7 +287,8 @@ template <typename PF>
 __device__ inline bool map_voxel_pcl(const MapperDev& D, size_t sm, uint32_t so, const PF& P, int n, float leaf,
                                      const VxPclOut& O, uint32_t* lds, int* err) {
   const size_t ps = (size_t)D.scratch_cap + MP_SLACK * (INS_SLOTS + 1) + (size_t)D.max_in + MP_SLACK;
-  const size_t lim = so == mp_stack_offset(D) ? ps : mp_cube_scratch(D);  // cubes stay below the stack
+  const bool stk = so == mp_stack_offset(D);
+  const size_t lim = stk ? ps : mp_cube_scratch(D);  // cubes stay below the stack
   if ((size_t)so + (uint32_t)n + MP_SLACK > lim) {
     if (threadIdx.x == 0) atomicOr(err, MAP_ERR_SORT);
     return false;
@@ -302,7 +303,7 @@ __device__ inline bool map_voxel_pcl(const MapperDev& D, size_t sm, uint32_t so,
     uint32_t* B = A + MP_LDS_N;
     int* seg0 = reinterpret_cast<int*>(B + MP_LDS_N);
     const VxPclScratch X{E, A, B, D.ps + b, lev, {seg0, seg0 + 3 * MP_SEG_LDS}, MP_SEG_LDS, nullptr,
-                         D.pdbg ? (so == 0 ? D.pdbg + 42 : D.pdbg + 11) : nullptr};
+                         D.pdbg ? (stk ? D.pdbg + 42 : D.pdbg + 11) : nullptr, D.pdbg ? (stk ? D.pdbg + 18 : D.pdbg + 48) : nullptr};
     voxel_grid_pcl<VX_THREADS>(P, n, leaf, O, X, M, ws, err);
   } else {  // level lists in global memory; segments that fit the LDS are sorted there whole
     const int cap = (int)((n + MP_SLACK) / 16);
@@ -318,7 +319,7 @@ __device__ inline bool map_voxel_pcl(const MapperDev& D, size_t sm, uint32_t so,
                          MP_DEF_SEG,
                          reinterpret_cast<SsLevels*>(lds + VX_LDS_WORDS - 256 - 2 * MP_LEV_W)};
     const VxPclScratch X{D.pe + b, D.pa + b, D.pb + b, D.ps + b, lev, {seg0, seg0 + 3 * cap}, cap, lds,
-                         D.pdbg ? (so == 0 ? D.pdbg + 42 : D.pdbg + 11) : nullptr};
+                         D.pdbg ? (stk ? D.pdbg + 42 : D.pdbg + 11) : nullptr, D.pdbg ? (stk ? D.pdbg + 18 : D.pdbg + 48) : nullptr};
     voxel_grid_pcl<VX_THREADS, true>(P, n, leaf, O, X, M, ws, err, &dfr);
   }
   return true;
@@ -1918,11 +1919,17 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
   S.prof = D.pdbg ? D.pdbg + 11 : nullptr;  // merge phases: dbg[11..14]
   bool merged = false;
   const unsigned long long t0 = __builtin_readcyclecounter();
-  if (D.pcl_order && !append) {
-    // PCL's summation order: the sort of old content ++ new points (voxel_pcl.h); the merge
-    // path (input order) does not apply.  Also a window cube that received nothing but is not
-    // a VoxelGrid fixed point (raw appended content, content set through the API): the
-    // reference re-filters every window cube (:795-808) in PCL's order
+  if (D.pcl_order && !append && n_new > 0 && n_new <= VX_MERGE_CAP && cv.y > 0 && *tok == cv.x + 1) {
+    // a fixed-point cube whose voxels all end with at most 2 members: the merge's sums are
+    // PCL's whatever the order (vx_merge_fixed_point ORDER_FREE); else the PCL-order filter
+    merged = vx_merge_fixed_point<VX_THREADS, (int)VX_MERGE_CAP, VX_LDS_WORDS, true>(S, lds);
+    __syncthreads();
+  }
+  if (D.pcl_order && !append && !merged) {
+    // PCL's summation order: the sort of old content ++ new points (voxel_pcl.h).  Also a
+    // window cube that received nothing but is not a VoxelGrid fixed point (raw appended
+    // content, content set through the API): the reference re-filters every window cube
+    // (:795-808) in PCL's order
     uint32_t* sb = lds + LW - 3;
     const uint32_t n = cv.y + n_new;
     if (threadIdx.x == 0) *sb = atomicAdd(&F.scratch_tail[m], n + MP_SLACK);
@@ -1939,7 +1946,7 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
     map_voxel_pcl(D, sm_index(s, m), so, VxSrc{ar + cv.x, (int)cv.y, D.ins_sorted + sm_index(s, m) * D.max_in + i0},
                   (int)n, D.leaf[m], O, lds, &F.err);
     __syncthreads();
-  } else {
+  } else if (!D.pcl_order || append) {
     if (!append && n_new > 0 && n_new <= VX_MERGE_CAP && cv.y > 0 && *tok == cv.x + 1) {
       merged = vx_merge_fixed_point(S, lds);
       __syncthreads();  // false: grid overflow, full filter below
@@ -2298,6 +2305,10 @@ struct loam_mapper {
   // copy and an event instead)
   int frame_flag = 1;
   int stack_event = 0;  // LOAM_STACK_EVENT=1: graph frames wait for their stacks with an event
+  // the graph path's kernel sequence launched directly instead of as a hipGraph: frames queued
+  // behind the one in flight (-1, the default; the graph launch costs 14 against 6 us between
+  // two frames at one stream, rocprofv3 trace), always (LOAM_GRAPH_DIRECT=1) or never (0)
+  int graph_direct = -1;
   unsigned long long stack_seq = 0;
   unsigned long long* d_stk_ready = nullptr;  // [2 parities]
   PinnedArray<unsigned long long> done;  // [2 parities]
@@ -2645,6 +2656,8 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     h->frame_flag = (fenv && fenv[0] == '0') ? 0 : 1;
     const char* senv = std::getenv("LOAM_STACK_EVENT");
     h->stack_event = (senv && senv[0] == '1') ? 1 : 0;
+    const char* genv2 = std::getenv("LOAM_GRAPH_DIRECT");
+    if (genv2 && (genv2[0] == '0' || genv2[0] == '1')) h->graph_direct = genv2[0] - '0';
   }
   {
     const char* e1 = std::getenv("LOAM_FIN_DEVICE");
@@ -3053,7 +3066,8 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
   R.graph = graph;
   if (graph) {
     hipGraphExec_t& ge = h->gexec[h->parity][fpar];
-    if (!ge) {
+    const bool direct = h->graph_direct < 0 ? chained : h->graph_direct == 1;
+    if (!ge && !direct) {
       hipGraph_t gr = nullptr;
       LOAM_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
       capture_frame(h, D, fpar, st);
@@ -3078,7 +3092,12 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
     if (!chained) LOAM_HIP(hipEventRecord(h->ev_fr[fpar][0], st));
     if (h->fin_device)
       LOAM_HIP(hipMemcpyAsync(h->d_fin[fpar], h->fin[fpar].data(), sizeof(FrameIn) * B, hipMemcpyHostToDevice, st));
-    LOAM_HIP(hipGraphLaunch(ge, st));
+    if (direct) {
+      capture_frame(h, D, fpar, st);
+      LOAM_HIP(hipGetLastError());
+    } else {
+      LOAM_HIP(hipGraphLaunch(ge, st));
+    }
     if (h->rec_copy_out)
       LOAM_HIP(hipMemcpyAsync(h->hfo[fpar].data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
     if (!chained) LOAM_HIP(hipEventRecord(h->ev_fr[fpar][1], st));

@@ -88,6 +88,7 @@ __global__ void __launch_bounds__(P_PCL_THREADS) k_voxel_pcl_one(const float4* s
 }
 
 struct PKeyLess {
+  static constexpr int free_run = 1;  // the permutation itself: every tie order is visible
   __device__ bool operator()(uint64_t a, uint64_t b) const { return (uint32_t)(a >> 32) < (uint32_t)(b >> 32); }
 };
 

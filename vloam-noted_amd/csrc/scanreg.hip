@@ -419,6 +419,7 @@ constexpr int SR_SS_SEG = SR_WSORT_MAX / 17 + 2;  // level list of one wave-sort
 constexpr int SR_SS_GSEG = 6 * SR_WSORT_MAX / 17 + 2;  // long sectors: global level lists
 
 struct SrCurvLess {  // the reference's comparator: cloudCurvature[i] < cloudCurvature[j]
+  static constexpr int free_run = 1;  // tied curvatures: the order picks the features
   __device__ bool operator()(uint64_t a, uint64_t b) const {
     return __uint_as_float((uint32_t)(a >> 32)) < __uint_as_float((uint32_t)(b >> 32));
   }

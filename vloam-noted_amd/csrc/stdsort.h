@@ -60,6 +60,7 @@ struct SsLevels {
   // most `defer` elements are not partitioned level by level but listed in the caller's
   // dseg[dcap][3] (lo, hi, depth budget), each then sorted whole in LDS (ss_sort_deferred)
   int dcnt, dcap, defer;
+  unsigned long long* hctr;  // optional: [0] depth-limit heap sorts, [1] their elements (diagnostics)
 };
 
 // Wave-local subtree sort: a segment of at most SS_LOCAL elements whose array lives in global
@@ -108,6 +109,13 @@ __device__ inline void ss_adjust_heap(T* E, int first, int hole, int len, T valu
   E[first + hole] = value;
 }
 
+__device__ inline void ss_heap_count(unsigned long long* hctr, int m) {
+  if (hctr) {
+    atomicAdd(hctr, 1ull);
+    atomicAdd(hctr + 1, (unsigned long long)m);
+  }
+}
+
 // __partial_sort(first, last, last): __make_heap then __sort_heap, one lane
 template <typename T, typename Less>
 __device__ inline void ss_heap_sort(T* E, int lo, int hi, const Less& less) {
@@ -128,6 +136,89 @@ __device__ inline void ss_heap_sort(T* E, int lo, int hi, const Less& less) {
     E[last] = E[lo];
     ss_adjust_heap(E, lo, 0, last - lo, v, less);
   }
+}
+
+// The depth-limit fallback (__partial_sort) of one segment by a wave.  Its result only matters
+// where it orders equal keys, and often not even there, so the wave first sorts the segment by
+// (key, element) -- by rank up to SS_RANK_MAX elements, else a bitonic network -- and keeps that
+// order when it is indistinguishable from the heap's:
+//   * Less::free_run is the longest run of equal keys whose internal order cannot show: 1 for
+//     sorts whose tie order is visible (scan registration's sector sort, the plain permutation),
+//     2 for VoxelGrid (a centroid sums its voxel's points from 0: (0 + a) + b == (0 + b) + a);
+//   * a run longer than that inside the segment needs the heap's order;
+//   * keys strictly between the segment's smallest and largest have all their elements inside
+//     it (the partitions above it cut by pivot values), but the smallest and largest key may
+//     have elements in neighbouring segments, so with free_run 2 a pair at either end counts
+//     as a longer run.
+// Otherwise the segment is restored (A / B hold a copy) and heap-sorted literally on one lane.
+// (The exact mode's cube re-filters reach the depth limit on old, already sorted content with a
+// few new points appended, where median-of-3 degenerates: segments of thousands of points.)
+constexpr int SS_RANK_PER = 4;
+constexpr int SS_RANK_MAX = 64 * SS_RANK_PER;
+
+template <typename Less>
+__device__ inline bool ss_full_less(uint64_t a, uint64_t b, const Less& less) {
+  return less(a, b) || (!less(b, a) && (uint32_t)a < (uint32_t)b);
+}
+
+template <typename Less>
+__device__ inline void ss_depth_limit(uint64_t* E, uint32_t* A, uint32_t* B, int lo, int hi, const Less& less) {
+  const int lane = threadIdx.x & 63;
+  const int m = hi - lo;
+  for (int i = lane; i < m; i += 64) {  // the copy the heap sort restarts from
+    const uint64_t e = E[lo + i];
+    A[lo + i] = (uint32_t)e;
+    B[lo + i] = (uint32_t)(e >> 32);
+  }
+  if (m <= SS_RANK_MAX) {
+    uint64_t e[SS_RANK_PER];
+    int r[SS_RANK_PER];
+#pragma unroll
+    for (int u = 0; u < SS_RANK_PER; ++u) {
+      r[u] = 0;
+      if (lane + 64 * u < m) e[u] = E[lo + lane + 64 * u];
+    }
+    for (int j = 0; j < m; ++j) {
+      const uint64_t x = E[lo + j];
+#pragma unroll
+      for (int u = 0; u < SS_RANK_PER; ++u)
+        if (lane + 64 * u < m && ss_full_less(x, e[u], less)) ++r[u];
+    }
+    ss_wave_fence();  // every read of the segment before the writes
+#pragma unroll
+    for (int u = 0; u < SS_RANK_PER; ++u)
+      if (lane + 64 * u < m) E[lo + r[u]] = e[u];
+  } else {  // bitonic network over the next power of two; positions >= m act as +inf
+    int K = 1;
+    while (K < m) K <<= 1;
+    for (int k = 2; k <= K; k <<= 1) {
+      for (int j = k >> 1; j >= 1; j >>= 1) {
+        ss_wave_fence();
+        for (int t = lane; t < (K >> 1); t += 64) {
+          const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));  // bit log2(j) of i is 0
+          const int l = j == (k >> 1) ? (i ^ (k - 1)) : (i + j);
+          if (l < m) {
+            const uint64_t a = E[lo + i], b = E[lo + l];
+            if (ss_full_less(b, a, less)) {
+              E[lo + i] = b;
+              E[lo + l] = a;
+            }
+          }
+        }
+      }
+    }
+  }
+  ss_wave_fence();
+  constexpr int FR = Less::free_run;
+  bool keep = true;
+  for (int i = lane + FR; i < m; i += 64) keep &= less(E[lo + i - FR], E[lo + i]);
+  if (FR >= 2 && m >= 2) keep &= less(E[lo], E[lo + 1]) && less(E[lo + m - 2], E[lo + m - 1]);
+  if (__ballot(!keep) == 0ull) return;
+  ss_wave_fence();
+  for (int i = lane; i < m; i += 64) E[lo + i] = ((uint64_t)B[lo + i] << 32) | A[lo + i];
+  ss_wave_fence();
+  if (lane == 0) ss_heap_sort(E, lo, hi, less);
+  ss_wave_fence();
 }
 
 // One segment [lo, hi) with depth budget d: partition and return the cut (wave-uniform)
@@ -293,7 +384,7 @@ __device__ inline void ss_mark(uint32_t* A, uint32_t* B, int lo, int hi, bool so
 
 template <typename T, typename Less>
 __device__ inline void ss_local_sort(T* E, uint32_t* A, uint32_t* B, int lo, int hi, int d, uint32_t* loc,
-                                     const Less& less) {
+                                     const Less& less, unsigned long long* hctr = nullptr) {
   const int lane = threadIdx.x & 63;
   const int m = hi - lo;
   T* lE = reinterpret_cast<T*>(loc);
@@ -319,8 +410,8 @@ __device__ inline void ss_local_sort(T* E, uint32_t* A, uint32_t* B, int lo, int
         break;
       }
       if (dd == 0) {
-        if (lane == 0) ss_heap_sort(lE, a, b, less);
-        ss_wave_fence();
+        if (lane == 0) ss_heap_count(hctr, b - a);
+        ss_depth_limit(lE, lA, lB, a, b, less);
         ss_mark(lA, lB, a, b, true);
         break;
       }
@@ -369,6 +460,7 @@ __device__ inline void ss_levels_init(SsLevels* L, int n, int* seg0, int* seg1, 
   L->cnt[0] = L->cnt[1] = L->nbig[0] = L->nbig[1] = 0;
   L->loc = nullptr;
   L->dcnt = L->dcap = L->defer = 0;
+  L->hctr = nullptr;
   if (n > SS_THRESHOLD) {
     const int d = depth >= 0 ? depth : 2 * (31 - __clz(n));  // 2 * __lg(n)
     const bool big = n > SS_BIG && d > 0;
@@ -398,7 +490,7 @@ __device__ inline void ss_levels(T* E, uint32_t* A, uint32_t* B, SsLevels* L, in
     else ss_wave_fence();
   };
   auto push = [&](int nxt, int a, int b, int d) {  // one lane
-    if (DEFER && b - a <= L->defer && d > 0) {  // sorted whole later (ss_sort_deferred)
+    if (DEFER && b - a <= L->defer && (d > 0 || b - a > SS_RANK_MAX)) {  // sorted whole later in LDS (ss_sort_deferred)
       const int t = atomicAdd(&L->dcnt, 1);
       if (t < L->dcap) {
         int* o = dseg + 3 * t;
@@ -458,12 +550,12 @@ __device__ inline void ss_levels(T* E, uint32_t* A, uint32_t* B, SsLevels* L, in
       const int* e = sg + 3 * (k < cnt ? k : L->cap - 1 - (k - cnt));
       const int lo = e[0], hi = e[1], d = e[2];
       if (loc && hi - lo <= SS_LOCAL) {
-        ss_local_sort(E, A, B, lo, hi, d, loc + wave * SS_LOC_WORDS, less);
+        ss_local_sort(E, A, B, lo, hi, d, loc + wave * SS_LOC_WORDS, less, L->hctr);
         continue;
       }
       if (d == 0) {  // depth limit: __partial_sort(first, last, last)
-        if (lane == 0) ss_heap_sort(E, lo, hi, less);
-        ss_wave_fence();
+        if (lane == 0) ss_heap_count(L->hctr, hi - lo);
+        ss_depth_limit(E, A, B, lo, hi, less);
         ss_mark(A, B, lo, hi, true);
         continue;
       }
@@ -524,7 +616,10 @@ __device__ inline void ss_sort_deferred(T* E, uint32_t* A, uint32_t* B, SsLevels
     const int lo = dseg[3 * k], hi = dseg[3 * k + 1], d = dseg[3 * k + 2];
     const int m = hi - lo;
     for (int i = tid; i < m; i += NT) lE[i] = E[lo + i];
-    if (tid == 0) ss_levels_init(LL, m, lseg0, lseg1, lcap, d);
+    if (tid == 0) {
+      ss_levels_init(LL, m, lseg0, lseg1, lcap, d);
+      LL->hctr = L->hctr;
+    }
     __syncthreads();
     ss_levels<true, NT>(lE, lA, lB, LL, tid >> 6, NT / 64, less, lseg0, lseg1, nullptr);
     __syncthreads();

@@ -801,11 +801,17 @@ __device__ inline void vx_copy_through(const VoxSeg& S, uint32_t* sbase) {
 // the voxels holding A points alone need sorting, and there are few: the map is dense where
 // new points land.  Returns false, with nothing written, when the grid overflows (the caller
 // then runs the full filter).
+// ORDER_FREE (PCL's summation order wanted, exact_voxel_order = 1): the merge is used only when
+// every voxel ends up with at most 2 members.  (0 + a) + b == (0 + b) + a in IEEE arithmetic
+// (commutative; the leading 0 + x turns a -0 into +0 either way), so such a voxel's centroid
+// does not depend on the order PCL's std::sort leaves its members in, and the merge gives
+// PCL's bits.  A voxel with 3 or more members returns false, nothing written, before anything
+// is allocated: the caller runs the PCL-order filter.
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t VX_MERGE_CAP = 4096;
 
 // NT threads, up to CAP new points, LW LDS words (scan scratch and misc in the last 256)
-template <int NT = VX_THREADS, int CAP = (int)VX_MERGE_CAP, int LW = VX_LDS_WORDS>
+template <int NT = VX_THREADS, int CAP = (int)VX_MERGE_CAP, int LW = VX_LDS_WORDS, bool ORDER_FREE = false>
 __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
   constexpr int TMAX = 2 * CAP;       // hash slots (load factor <= 1/2)
   constexpr int RX = 2 * TMAX + CAP;  // start of the shared region: C hits, then the sort
@@ -923,6 +929,21 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
     if (h != NONE) hit[h] = (int)k;
   }
   __syncthreads();
+  if constexpr (ORDER_FREE) {  // a voxel of 3+ members: its sum depends on PCL's order
+    int many = 0;
+#pragma unroll
+    for (int q = 0; q < SPT; ++q) {
+      const uint32_t h = tid + q * NT;
+      if (h < T && (hcnt[h] & 0x1FFFu) + (hit[h] >= 0 ? 1u : 0u) >= 3u) many = 1;
+    }
+    if (tid == 0) M.moved = 0;
+    __syncthreads();
+    if (many) M.moved = 1;
+    __syncthreads();
+    const bool any_many = M.moved != 0;
+    __syncthreads();
+    if (any_many) return false;
+  }
   vx_phase(S.prof, 1, &tp);
   // 4. the voxels holding A points only, listed then sorted by key
   uint32_t fmask = 0, cnt = 0;

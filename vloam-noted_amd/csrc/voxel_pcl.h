@@ -43,6 +43,7 @@ struct VxPclScratch {
   uint32_t* loc = nullptr;  // LDS for the waves' subtree sorts (SS_LOC_WORDS each) when E is global
   unsigned long long* prof = nullptr;  // optional phase cycles: [0] bbox + keys, [1] sort levels,
                                        // [2] final pass, [3] centroids
+  unsigned long long* heap = nullptr;  // optional: depth-limit heap sorts [0] and their elements [1]
 };
 
 struct VxPtrSrc {
@@ -51,6 +52,7 @@ struct VxPtrSrc {
 };
 
 struct VxIdxLess {
+  static constexpr int free_run = 2;  // a voxel's centroid: 2 members sum alike in either order
   __device__ bool operator()(uint64_t a, uint64_t b) const { return (uint32_t)(a >> 32) < (uint32_t)(b >> 32); }
 };
 
@@ -107,6 +109,7 @@ __device__ inline void voxel_grid_pcl(const PF& P, int n, float leaf, const VxPc
   if (tid == 0) {
     ss_levels_init(X.lev, n, X.seg[0], X.seg[1], X.cap);
     X.lev->loc = X.loc;
+    X.lev->hctr = X.heap;
     if (DEFER) {
       X.lev->defer = dfr->defer;
       X.lev->dcap = dfr->dcap;
