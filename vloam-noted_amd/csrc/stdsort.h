@@ -72,6 +72,7 @@ constexpr int SS_LOC_STK = SS_LOCAL / (SS_THRESHOLD + 1) + 2;
 constexpr int SS_LOC_WORDS = 2 * SS_LOCAL + 2 * SS_LOCAL + 3 * SS_LOC_STK;
 
 constexpr int SS_BIG = 1024;  // longer segments are partitioned by the whole workgroup
+constexpr int SS_WG_CHUNK = 16;  // positions per thread of a workgroup partition in one pass
 
 // Elements are 64-bit; Less compares two elements (the reference's comparator).  Per sort:
 //   E[n]    the elements, permuted in place by the partitions (LDS or global)
@@ -321,29 +322,71 @@ __device__ inline int ss_partition_wg(T* E, uint32_t* A, uint32_t* B, int lo, in
   __syncthreads();
   const T p = E[lo];
   uint32_t nl = 0, nr = 1;
-  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-  for (int c0 = lo + 1; c0 < hi; c0 += NT) {
-    const int i = c0 + tid;
-    bool isl = false, isr = false;
-    if (i < hi) {
-      const T e = E[i];
-      isl = !less(e, p);
-      isr = !less(p, e);
+  const int len = hi - lo - 1;  // the scanned positions lo + 1 .. hi - 1
+  if (len <= NT * SS_WG_CHUNK) {
+    // each thread classifies a contiguous chunk (its loads all in flight at once), and one block
+    // scan of the per-thread stop counts places every stop: no barrier per tile
+    const int c = (len + NT - 1) / NT;
+    const int b0 = lo + 1 + tid * c;
+    uint32_t ml = 0, mr = 0;  // bit u: position b0 + u is a left / right stop
+#pragma unroll
+    for (int u = 0; u < SS_WG_CHUNK; ++u) {
+      const int i = b0 + u;
+      if (u < c && i < hi) {
+        const T e = E[i];
+        if (!less(e, p)) ml |= 1u << u;
+        if (!less(p, e)) mr |= 1u << u;
+      }
     }
-    const uint64_t bl = __ballot(isl), br = __ballot(isr);
-    if (lane == 0) L->ws[wid] = (uint32_t)__popcll(bl) | ((uint32_t)__popcll(br) << 16);
+    const uint32_t v = (uint32_t)__popc(ml) | ((uint32_t)__popc(mr) << 16);  // totals < 2^16
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) L->ws[wid] = x;
     __syncthreads();
-    uint32_t off = 0, tot = 0;
+    uint32_t off = x - v, tot = 0;
     for (int w = 0; w < NW; ++w) {
-      const uint32_t v = L->ws[w];
-      off += w < wid ? v : 0u;
-      tot += v;
+      const uint32_t t = L->ws[w];
+      off += w < wid ? t : 0u;
+      tot += t;
     }
-    if (isl) A[lo + 1 + nl + (off & 0xFFFFu) + __popcll(bl & lt)] = (uint32_t)i;
-    if (isr) B[lo + nr + (off >> 16) + __popcll(br & lt)] = (uint32_t)i;
-    nl += tot & 0xFFFFu;
-    nr += tot >> 16;
-    __syncthreads();  // ws is rewritten by the next tile
+    uint32_t ol = (uint32_t)lo + 1u + (off & 0xFFFFu), orr = (uint32_t)lo + 1u + (off >> 16);
+#pragma unroll
+    for (int u = 0; u < SS_WG_CHUNK; ++u) {
+      if (ml & (1u << u)) A[ol++] = (uint32_t)(b0 + u);
+      if (mr & (1u << u)) B[orr++] = (uint32_t)(b0 + u);
+    }
+    nl = tot & 0xFFFFu;
+    nr = 1u + (tot >> 16);
+    __syncthreads();  // the stop lists complete, ws free
+  } else {
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (int c0 = lo + 1; c0 < hi; c0 += NT) {
+      const int i = c0 + tid;
+      bool isl = false, isr = false;
+      if (i < hi) {
+        const T e = E[i];
+        isl = !less(e, p);
+        isr = !less(p, e);
+      }
+      const uint64_t bl = __ballot(isl), br = __ballot(isr);
+      if (lane == 0) L->ws[wid] = (uint32_t)__popcll(bl) | ((uint32_t)__popcll(br) << 16);
+      __syncthreads();
+      uint32_t off = 0, tot = 0;
+      for (int w = 0; w < NW; ++w) {
+        const uint32_t v = L->ws[w];
+        off += w < wid ? v : 0u;
+        tot += v;
+      }
+      if (isl) A[lo + 1 + nl + (off & 0xFFFFu) + __popcll(bl & lt)] = (uint32_t)i;
+      if (isr) B[lo + nr + (off >> 16) + __popcll(br & lt)] = (uint32_t)i;
+      nl += tot & 0xFFFFu;
+      nr += tot >> 16;
+      __syncthreads();  // ws is rewritten by the next tile
+    }
   }
   const int kmax = min((int)nl, (int)nr);
   if (tid == 0) L->sh[0] = kmax + 1;  // first k with !(l_k < r_k)

@@ -42,7 +42,8 @@ struct VxPclScratch {
   int cap;        // >= n / 17 + 1
   uint32_t* loc = nullptr;  // LDS for the waves' subtree sorts (SS_LOC_WORDS each) when E is global
   unsigned long long* prof = nullptr;  // optional phase cycles: [0] bbox + keys, [1] sort levels,
-                                       // [2] final pass, [3] centroids
+                                       // [2] final pass, [3] centroids, [4] (a sort in global
+                                       // memory) its levels there, [1] then its deferred segments
   unsigned long long* heap = nullptr;  // optional: depth-limit heap sorts [0] and their elements [1]
 };
 
@@ -121,6 +122,8 @@ __device__ inline void voxel_grid_pcl(const PF& P, int n, float leaf, const VxPc
   vx_phase(X.prof, 0, &tp);
   if constexpr (DEFER) {
     ss_levels<true, NT, true>(X.E, X.A, X.B, X.lev, tid >> 6, NT / 64, less, X.seg[0], X.seg[1], X.loc, dfr->dseg);
+    __syncthreads();
+    vx_phase(X.prof, 4, &tp);  // [4]: the global-memory levels, [1]: the deferred LDS sorts
     ss_sort_deferred<NT>(X.E, X.A, X.B, X.lev, dfr->dseg, less, dfr->lE, dfr->lA, dfr->lB, dfr->lseg0, dfr->lseg1,
                          dfr->lcap, dfr->LL);
   } else {
