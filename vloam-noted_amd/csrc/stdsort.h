@@ -72,10 +72,7 @@ constexpr int SS_LOC_STK = SS_LOCAL / (SS_THRESHOLD + 1) + 2;
 constexpr int SS_LOC_WORDS = 2 * SS_LOCAL + 2 * SS_LOCAL + 3 * SS_LOC_STK;
 
 constexpr int SS_BIG = 1024;  // longer segments are partitioned by the whole workgroup
-constexpr int SS_WG_CHUNK = 16;
-#ifndef SS_REG_MAX
-#define SS_REG_MAX 64  // segments up to this long are sorted whole in registers (ss_reg_sort64; at most 64)
-#endif  // positions per thread of a workgroup partition in one pass
+constexpr int SS_WG_CHUNK = 16;  // positions per thread of a workgroup partition in one pass
 
 // Elements are 64-bit; Less compares two elements (the reference's comparator).  Per sort:
 //   E[n]    the elements, permuted in place by the partitions (LDS or global)
@@ -428,120 +425,6 @@ __device__ inline void ss_mark(uint32_t* A, uint32_t* B, int lo, int hi, bool so
   }
 }
 
-// bits below i / above i / in [a, b) of a wave mask (0 <= i < 64, 0 <= a <= b <= 64)
-__device__ inline uint64_t ss_bits_below(int i) { return i <= 0 ? 0ull : (~0ull >> (64 - i)); }
-__device__ inline uint64_t ss_bits_above(int i) { return i >= 63 ? 0ull : (~0ull << (i + 1)); }
-__device__ inline uint64_t ss_bits_range(int a, int b) { return ss_bits_below(b) & ~ss_bits_below(a); }
-// position of the k-th (1-based) set bit of x counted from bit 0 / from bit 63 (k <= popc(x))
-__device__ inline int ss_sel_asc(uint64_t x, int k) {
-  int pos = 0;  // the largest q with popc(x & bits below q) < k
-#pragma unroll
-  for (int w = 32; w >= 1; w >>= 1)
-    if (__popcll(x & ss_bits_below(pos + w)) < k) pos += w;
-  return pos;
-}
-__device__ inline int ss_sel_desc(uint64_t x, int k) { return ss_sel_asc(x, __popcll(x) - k + 1); }
-
-// The whole introsort subtree of a segment of at most 64 elements in one wave's registers: lane
-// i holds position lo + i, every pending segment of the subtree is partitioned at once per round
-// (segment masks over the wave's ballots), with no memory traffic until the final stable pass.
-// The partition is the stop-list formulation of ss_partition: left stops (positions after the
-// pivot with !(e < p)) ranked upwards, right stops (from the pivot on, with !(p < e)) ranked
-// downwards; S = #{k : l_k < r_k} (a left stop with k right stops above it), the pairs (l_k, r_k),
-// k <= S, swapped by a lane shuffle, cut = min(l_{S+1}, r_S).  Segments at the depth limit go
-// through ss_depth_limit in memory.  E / A / B as for ss_levels; the segment ends sorted in place.
-template <typename Less>
-__device__ inline void ss_reg_sort64(uint64_t* E, uint32_t* A, uint32_t* B, int lo, int hi, int d, const Less& less,
-                                     unsigned long long* hctr) {
-  const int lane = threadIdx.x & 63;
-  const int m = hi - lo;
-  const bool in = lane < m;
-  uint64_t v = in ? E[lo + lane] : 0ull;
-  int sa = 0, sb = m, dd = d;  // this lane's pending segment [sa, sb) and its depth budget
-  auto shf = [](uint64_t x, int src) -> uint64_t {
-    const uint32_t l = (uint32_t)__shfl((int)(uint32_t)x, src, 64);
-    const uint32_t h = (uint32_t)__shfl((int)(uint32_t)(x >> 32), src, 64);
-    return ((uint64_t)h << 32) | l;
-  };
-  while (true) {
-    const bool act = in && sb - sa > SS_THRESHOLD && dd > 0;
-    if (__ballot(act) == 0ull) break;
-    // __move_median_to_first(lo, lo + 1, mid, hi - 1) of every active segment
-    const int pa = sa + 1, pb = sa + (sb - sa) / 2, pc = sb - 1;
-    const uint64_t ea = shf(v, in ? pa : lane), eb = shf(v, in ? pb : lane), ec = shf(v, in ? pc : lane);
-    int mm;
-    if (less(ea, eb)) {
-      if (less(eb, ec)) mm = pb;
-      else if (less(ea, ec)) mm = pc;
-      else mm = pa;
-    } else if (less(ea, ec)) {
-      mm = pa;
-    } else if (less(eb, ec)) {
-      mm = pc;
-    } else {
-      mm = pb;
-    }
-    int src = lane;
-    if (act && lane == sa) src = mm;
-    else if (act && lane == mm) src = sa;
-    v = shf(v, src);
-    const uint64_t p = shf(v, in ? sa : lane);
-    const bool isl = act && lane > sa && !less(v, p);
-    const bool isr = act && !less(p, v);
-    const uint64_t sm = ss_bits_range(sa, sb);
-    const uint64_t Lm = __ballot(isl) & sm, Rm = __ballot(isr) & sm;
-    const int nl = __popcll(Lm);
-    const int kl = __popcll(Lm & ss_bits_below(lane)) + 1;  // rank among the left stops (isl)
-    const int ra = __popcll(Rm & ss_bits_above(lane));      // right stops above this lane
-    const int S = __popcll(__ballot(isl && ra >= kl) & sm);
-    const int lK = S + 1 <= nl ? ss_sel_asc(Lm, S + 1) : 64;
-    const int rS = S >= 1 ? ss_sel_desc(Rm, S) : sb;
-    const int cut = min(lK, rS);
-    int partner = lane;
-    if (isl && kl <= S) partner = ss_sel_desc(Rm, kl);
-    else if (isr && ra + 1 <= S) partner = ss_sel_asc(Lm, ra + 1);
-    v = shf(v, partner);
-    if (act) {
-      if (lane < cut) sb = cut;
-      else sa = cut;
-      --dd;
-    }
-  }
-  // segments stopped by the depth limit: __partial_sort in memory, one after the other
-  const bool hp = in && sb - sa > SS_THRESHOLD;
-  uint64_t hs = __ballot(hp && lane == sa);
-  if (hs) {
-    if (in) E[lo + lane] = v;
-    ss_wave_fence();
-    while (hs) {
-      const int a = __ffsll((long long)hs) - 1;
-      hs &= hs - 1;
-      const int b = __builtin_amdgcn_readfirstlane(__shfl(sb, a, 64));
-      if (lane == 0) ss_heap_count(hctr, b - a);
-      ss_depth_limit(E, A, B, lo + a, lo + b, less);
-    }
-    if (hp) v = E[lo + lane];
-    ss_wave_fence();
-  }
-  // the final insertion sort: stable within each segment of at most 16
-  int r = lane - sa;
-  if (in && !hp) {
-    r = 0;
-#pragma unroll
-    for (int t = 0; t < SS_THRESHOLD; ++t) {
-      const int j = sa + t;
-      const uint64_t ej = shf(v, j < sb ? j : lane);
-      if (j < sb) r += (less(ej, v) || (j < lane && !less(v, ej))) ? 1 : 0;
-    }
-  }
-  if (in) {
-    E[lo + sa + r] = v;
-    A[lo + lane] = (uint32_t)(lo + lane);
-    B[lo + lane] = (uint32_t)(lo + lane + 1);
-  }
-  ss_wave_fence();
-}
-
 template <typename T, typename Less>
 __device__ inline void ss_local_sort(T* E, uint32_t* A, uint32_t* B, int lo, int hi, int d, uint32_t* loc,
                                      const Less& less, unsigned long long* hctr = nullptr) {
@@ -567,10 +450,6 @@ __device__ inline void ss_local_sort(T* E, uint32_t* A, uint32_t* B, int lo, int
     while (true) {
       if (b - a <= SS_THRESHOLD) {
         ss_mark(lA, lB, a, b, false);
-        break;
-      }
-      if (b - a <= SS_REG_MAX) {  // the rest of this subtree in registers
-        ss_reg_sort64(lE, lA, lB, a, b, dd, less, hctr);
         break;
       }
       if (dd == 0) {
@@ -713,10 +592,6 @@ __device__ inline void ss_levels(T* E, uint32_t* A, uint32_t* B, SsLevels* L, in
     for (int k = wave; wave < nw && k < tot; k += nw) {
       const int* e = sg + 3 * (k < cnt ? k : L->cap - 1 - (k - cnt));
       const int lo = e[0], hi = e[1], d = e[2];
-      if (hi - lo <= SS_REG_MAX) {  // the whole subtree in registers
-        ss_reg_sort64(E, A, B, lo, hi, d, less, L->hctr);
-        continue;
-      }
       if (loc && hi - lo <= SS_LOCAL) {
         ss_local_sort(E, A, B, lo, hi, d, loc + wave * SS_LOC_WORDS, less, L->hctr);
         continue;
