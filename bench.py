@@ -784,13 +784,68 @@ def main():
         torch.cuda.synchronize(local)
         udt = time.perf_counter() - t0
         um.close()
+        thread_ranks = thread_rank_overhead(splan, pre) if world == 1 else None
         return {"value": round(sit_all / world / sdt_max, 3), "unit": "LM iters/s",
                 "ms_per_step": round(1e3 * sdt_max / K, 4), "streams": Bs, "ranks": world, "scaling": "strong",
                 "frames_per_step": Bs, "unsharded_same_streams": round(uit / udt, 3),
                 "sharded_over_unsharded": round((sit_all / world / sdt_max) / (uit / udt), 4),
                 "transport": "RCCL" if world > 1 else "one rank: every collective is the identity",
                 "mode": "every stream split over all ranks (block-owned map shards, per-round 5-NN all-gather, "
-                        "per-LM-iteration normal-equation all-reduce); iterations counted once per stream"}
+                        "per-LM-iteration normal-equation all-reduce); iterations counted once per stream",
+                "thread_ranks": thread_ranks}
+
+    def thread_rank_overhead(splan, pre, n_streams=8, steps=10):
+        """the multi-rank schedule on this one GPU: R = 2, 3 ranks as host threads,
+        each a sharded handle of the first n_streams streams, exchanging through host-buffer
+        callbacks (loam_amd.comm.ThreadGroup); every rank's kernels share the GPU, so the time
+        includes R times the redundant per-rank work plus the exchanges, against the unsharded
+        handle on the same streams and frames"""
+        import threading
+        from loam_amd.comm import ThreadGroup
+        plan = [tuple(a[:n_streams] for a in step) for step in splan[:pre + steps]]
+        um = BatchMapper(n_streams, device=local, max_map_points=args.map_points)
+        run_steps(um, plan, 0, pre)
+        torch.cuda.synchronize(local)
+        t0 = time.perf_counter()
+        uit = run_steps(um, plan, pre, steps)
+        torch.cuda.synchronize(local)
+        u_rate = uit / (time.perf_counter() - t0)
+        um.close()
+        res = {"streams": n_streams, "steps": steps, "unsharded": round(u_rate, 1),
+               "transport": "host-buffer callbacks between threads (ThreadGroup), one GPU"}
+        for R in (2, 3):
+            group = ThreadGroup(R)
+            times, iters, errs = [0.0] * R, [0] * R, []
+            start = threading.Barrier(R)
+
+            def work(r):
+                try:
+                    m = BatchMapper(n_streams, device=local, max_map_points=args.map_points, comm=group.comm(r))
+                    run_steps(m, plan, 0, pre)
+                    torch.cuda.synchronize(local)
+                    start.wait()
+                    t1 = time.perf_counter()
+                    iters[r] = run_steps(m, plan, pre, steps)
+                    torch.cuda.synchronize(local)
+                    times[r] = time.perf_counter() - t1
+                    m.close()
+                except BaseException as e:  # noqa: BLE001 - recorded below
+                    errs.append(repr(e))
+                    group.barrier.abort()
+                    start.abort()
+
+            th = [threading.Thread(target=work, args=(r,)) for r in range(R)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join(timeout=120)
+            if errs or any(t.is_alive() for t in th):
+                res[f"ranks_{R}"] = {"error": errs[0] if errs else "timeout"}
+                continue
+            rate = iters[0] / max(times)
+            res[f"ranks_{R}"] = {"value": round(rate, 1), "over_unsharded": round(rate / u_rate, 4),
+                                 "ms_per_step": round(1e3 * max(times) / steps, 3)}
+        return res
 
     def single_stream(exact):
         """B = 1 on stream 0's frames (the latency view): map building untimed, then K frames,

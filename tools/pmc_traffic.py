@@ -16,7 +16,9 @@ import sys
 FAMILY = {  # kernel -> bench.py family (vloam-noted_amd/loam_amd/_core.py KFAM)
     "k_stack_ds": "stack_voxelgrid", "k_knn": "correspondence", "k_geom": "correspondence",
     "k_lm_round": "lm_pass", "k_lm_eval": "lm_pass", "k_lm_step": "lm_pass", "k_insert": "insert",
-    "k_bucket": "insert", "k_revox": "cube_revoxel", "k_submap_prep": "other", "k_shift_cubes": "other",
+    "k_bucket": "insert", "k_insert_bucket": "insert", "k_revox": "cube_revoxel", "k_submap_prep": "other",
+    "k_shift_cubes": "other", "k_stack_part": "stack_voxelgrid", "k_stack_cat": "stack_voxelgrid",
+    "k_frame_prep": "other",
 }
 
 
