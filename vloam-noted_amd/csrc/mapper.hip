@@ -1832,15 +1832,32 @@ __global__ void __launch_bounds__(VX_THREADS) k_insert_bucket(MapperDev D) {
     if (sl >= 0) atomicAdd(&base[sl], 1u);
   }
   __syncthreads();
-  if (tid == 0) {
-    uint32_t acc = 0;
-    for (int k = 0; k < INS_SLOTS; ++k) {
-      const uint32_t c = base[k];
-      base[k] = acc;
-      off[k] = acc;
-      acc += c;
+  if (wid == 0) {  // exclusive scan of the slot counts by one wave: lane l owns slots l*PL ..
+    constexpr int PL = (INS_SLOTS + 63) / 64;
+    uint32_t c[PL], sum = 0;
+#pragma unroll
+    for (int u = 0; u < PL; ++u) {
+      const int k = lane * PL + u;
+      c[u] = k < INS_SLOTS ? base[k] : 0u;
+      sum += c[u];
     }
-    off[INS_SLOTS] = acc;
+    uint32_t x = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    uint32_t acc = x - sum;
+#pragma unroll
+    for (int u = 0; u < PL; ++u) {
+      const int k = lane * PL + u;
+      if (k < INS_SLOTS) {
+        base[k] = acc;
+        off[k] = acc;
+      }
+      acc += c[u];
+    }
+    if (lane == 63) off[INS_SLOTS] = x;
   }
   __syncthreads();
   for (int c0 = 0; c0 < n; c0 += VX_THREADS) {
