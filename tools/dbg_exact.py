@@ -32,7 +32,7 @@ for exact in (1, 0):
     cnt, cyc = dc[24:32], dc[32:40]
     per = [round(c / max(n, 1) / 1e3, 1) for n, c in zip(cnt, cyc)]
     print(f"exact={exact}: {1e3 * t_all / 20:.3f} ms/frame; stack phases (Mcycles/frame) {[round(v / 20e6, 3) for v in dc[42:46]]}; "
-          f"cube phases {[round(v / 20e6, 3) for v in dc[11:16]]}; revox items merge/full/append {dc[4:7]} "
+          f"cube phases {[round(v / 20e6, 3) for v in dc[11:15] + [dc[64]]]}; revox items merge/full/append {dc[4:7]} "
           f"filter Mcycles {[round(v / 20e6, 2) for v in dc[0:3]]} index {round(dc[8] / 20e6, 2)}; "
-          f"cubes per size bucket (<1k,<2k,..) {cnt}; kcycles per cube {per}; heap sorts cubes {dc[48]} of {dc[49]} elements, stacks {dc[18]} of {dc[19]}; "
+          f"cubes per size bucket (<1k,<2k,..) {cnt}; kcycles per cube {per}; depth-limit segments cubes {dc[66]} of {dc[67]} elements, stacks {dc[68]} of {dc[69]}; "
           f"stacks {st.corner_stack},{st.surf_stack}", flush=True)

@@ -303,7 +303,8 @@ __device__ inline bool map_voxel_pcl(const MapperDev& D, size_t sm, uint32_t so,
     uint32_t* B = A + MP_LDS_N;
     int* seg0 = reinterpret_cast<int*>(B + MP_LDS_N);
     const VxPclScratch X{E, A, B, D.ps + b, lev, {seg0, seg0 + 3 * MP_SEG_LDS}, MP_SEG_LDS, nullptr,
-                         D.pdbg ? (stk ? D.pdbg + 42 : D.pdbg + 11) : nullptr, D.pdbg ? (stk ? D.pdbg + 18 : D.pdbg + 48) : nullptr};
+                         D.pdbg ? (stk ? D.pdbg + 42 : D.pdbg + 11) : nullptr, D.pdbg ? (stk ? D.pdbg + 68 : D.pdbg + 66) : nullptr,
+                         D.pdbg ? (stk ? D.pdbg + 65 : D.pdbg + 64) : nullptr};
     voxel_grid_pcl<VX_THREADS>(P, n, leaf, O, X, M, ws, err);
   } else {  // level lists in global memory; segments that fit the LDS are sorted there whole
     const int cap = (int)((n + MP_SLACK) / 16);
@@ -319,7 +320,8 @@ __device__ inline bool map_voxel_pcl(const MapperDev& D, size_t sm, uint32_t so,
                          MP_DEF_SEG,
                          reinterpret_cast<SsLevels*>(lds + VX_LDS_WORDS - 256 - 2 * MP_LEV_W)};
     const VxPclScratch X{D.pe + b, D.pa + b, D.pb + b, D.ps + b, lev, {seg0, seg0 + 3 * cap}, cap, lds,
-                         D.pdbg ? (stk ? D.pdbg + 42 : D.pdbg + 11) : nullptr, D.pdbg ? (stk ? D.pdbg + 18 : D.pdbg + 48) : nullptr};
+                         D.pdbg ? (stk ? D.pdbg + 42 : D.pdbg + 11) : nullptr, D.pdbg ? (stk ? D.pdbg + 68 : D.pdbg + 66) : nullptr,
+                         D.pdbg ? (stk ? D.pdbg + 65 : D.pdbg + 64) : nullptr};
     voxel_grid_pcl<VX_THREADS, true>(P, n, leaf, O, X, M, ws, err, &dfr);
   }
   return true;

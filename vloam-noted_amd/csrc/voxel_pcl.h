@@ -42,9 +42,10 @@ struct VxPclScratch {
   int cap;        // >= n / 17 + 1
   uint32_t* loc = nullptr;  // LDS for the waves' subtree sorts (SS_LOC_WORDS each) when E is global
   unsigned long long* prof = nullptr;  // optional phase cycles: [0] bbox + keys, [1] sort levels,
-                                       // [2] final pass, [3] centroids, [4] (a sort in global
-                                       // memory) its levels there, [1] then its deferred segments
-  unsigned long long* heap = nullptr;  // optional: depth-limit heap sorts [0] and their elements [1]
+                                       // [2] final pass, [3] centroids (a sort in global memory:
+                                       // [1] its deferred segments, its own levels in glob)
+  unsigned long long* heap = nullptr;  // optional: depth-limit segments [0] and their elements [1]
+  unsigned long long* glob = nullptr;  // optional: cycles of a global-memory sort's own levels
 };
 
 struct VxPtrSrc {
@@ -123,7 +124,7 @@ __device__ inline void voxel_grid_pcl(const PF& P, int n, float leaf, const VxPc
   if constexpr (DEFER) {
     ss_levels<true, NT, true>(X.E, X.A, X.B, X.lev, tid >> 6, NT / 64, less, X.seg[0], X.seg[1], X.loc, dfr->dseg);
     __syncthreads();
-    vx_phase(X.prof, 4, &tp);  // [4]: the global-memory levels, [1]: the deferred LDS sorts
+    vx_phase(X.glob, 0, &tp);  // the global-memory levels; prof[1]: the deferred LDS sorts
     ss_sort_deferred<NT>(X.E, X.A, X.B, X.lev, dfr->dseg, less, dfr->lE, dfr->lA, dfr->lB, dfr->lseg0, dfr->lseg1,
                          dfr->lcap, dfr->LL);
   } else {
