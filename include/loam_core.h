@@ -233,7 +233,11 @@ int32_t loam_mapper_solve(loam_mapper* h);
  * changes.  loam_mapper_pose / _stats / _stats_all / _total_iterations / _get_state report the
  * newest frame waited for (a frame enqueued with nothing before it in the queue is waited for by
  * them first); every other call waits for every frame in the queue.  Device inputs must stay
- * valid until the frame that takes them is waited for. */
+ * valid until the frame that takes them is waited for.
+ * Status: _wait returns the status of the frame it finishes.  _async called with two frames in
+ * the queue first finishes the oldest; a LOAM_ERR_CAPACITY / LOAM_ERR_SYNC it returns is that
+ * older frame's (its pose and stats are readable as after _wait), and the new frame IS enqueued;
+ * LOAM_ERR_HIP / _ARG / _STATE mean the new frame was not enqueued. */
 int32_t loam_mapper_solve_async(loam_mapper* h);
 int32_t loam_mapper_wait(loam_mapper* h);
 /* queue the stack VoxelGrids of every stream's pending input now (no-op with profiling on) */

@@ -490,3 +490,47 @@ def test_chained_solve_matches_blocking(seq, n_streams, exact, defer_every, monk
         assert queued > 0 and rerun > 0, (queued, rerun)
     else:
         assert queued >= n - 2, queued  # every frame but the first ran queued behind another
+
+
+@pytest.mark.parametrize("exact", [0, 1])
+def test_split_prefetch_matches_blocking(seq, exact):
+    """streams of one frame taking their stacks from two different stack launches of the same
+    parity: stream 0's input is given and its stack VoxelGrid launched (loam_mapper_prefetch),
+    then stream 1's input, whose stack the solve launches; the frames queue behind each other
+    (graph path, k_frame_prep waits for each stream's own launch and then acquires before it reads
+    the stack sizes, which share one cache line).  Every pose and count equals the blocking solve"""
+    n_streams = 2
+
+    def row(m, s):
+        st = m.stats(s)
+        q, t = m.pose(s)
+        return (q.tobytes(), t.tobytes(), st.corner_stack, st.surf_stack, tuple(st.corner_num), tuple(st.surf_num),
+                st.lm[0].iterations, st.lm[1].iterations)
+
+    def give(m, f, s):
+        rec = seq[f + s]
+        m.input(s, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+
+    n = len(seq) - n_streams + 1
+    ref = BatchMapper(n_streams, exact_voxel_order=exact)
+    want = []
+    for f in range(n):
+        for s in range(n_streams):
+            give(ref, f, s)
+        ref.solve()
+        want.append([row(ref, s) for s in range(n_streams)])
+    ref.close()
+    m = BatchMapper(n_streams, exact_voxel_order=exact)
+    got = []
+    for f in range(n):
+        give(m, f, 0)
+        m.prefetch()  # stream 0's stack: its own launch
+        give(m, f, 1)
+        m.solve_async()  # stream 1's stack launched here; queued behind frame f - 1
+        if f:
+            m.wait()
+            got.append([row(m, s) for s in range(n_streams)])
+    m.wait()
+    got.append([row(m, s) for s in range(n_streams)])
+    m.close()
+    assert got == want

@@ -270,3 +270,17 @@ def test_voxel_merge_bit_exact(frame_clouds, leaf, n_new):
     assert merged == (n_new <= 4096)
     assert got.shape == ref.shape
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("kind,n,m,seed", [("cube", 13500, 400, 11), ("cube", 4300, 300, 1), ("cube", 1500, 600, 4),
+                                           ("cube", 9000, 3000, 12), ("stack", 6000, 3000, 5),
+                                           ("stack", 28000, 3400, 13), ("stack", 800, 790, 8)])
+def test_voxel_grid_pcl_hot_voxels(kind, n, m, seed):
+    """voxels of 3+ members (the ones whose centroid shows std::sort's order) on cube-shaped
+    clouds (sorted content ++ new points, introsort at its depth limit, literal heap sorts) and on
+    raw-feature-shaped clouds (most voxels hot): the pruned emulation of voxel_hot.h, PCL's bits"""
+    from test_sort_rule import _stack_cloud, _triples_cloud
+    for leaf in (0.4, 0.8):
+        pts = _triples_cloud(n, m, seed, leaf) if kind == "cube" else _stack_cloud(n, m, seed, leaf)
+        ref = O.voxel_grid(pts, leaf)
+        assert np.array_equal(prims.voxel_grid_pcl(pts, leaf).view(np.uint32), ref.view(np.uint32)), leaf

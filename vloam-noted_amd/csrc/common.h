@@ -59,6 +59,16 @@ __device__ inline uint32_t wave_sum_u(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+__device__ inline int wave_sum_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ inline int wave_min_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
 // inclusive prefix sum across the wave
 __device__ inline uint32_t wave_incl_scan_u(uint32_t v) {
   int l = wave_lane();

@@ -41,6 +41,7 @@
 #include "cubeindex.h"
 #include "lm.h"
 #include "voxel.h"
+#include "voxel_hot.h"
 #include "voxel_pcl.h"
 
 namespace loam {
@@ -81,6 +82,7 @@ struct StreamFrame {
   uint32_t arena_tail[2];
   int arena_active[2];
   uint32_t scratch_tail[2];
+  uint32_t hot_tail[2];   // exact order: the cubes' blocks of the sort scratch (pe / pa / pb / ps)
   int extra_n[2];
   int extra_list[2][EXTRA_CAP];
   int err;
@@ -327,10 +329,25 @@ __device__ inline bool map_voxel_pcl(const MapperDev& D, size_t sm, uint32_t so,
   return true;
 }
 
+// exact order (voxel_hot.h): the hot records of a filter of n points in the (stream, map) sort
+// scratch at offset so (a block of n + MP_SLACK): rk in pa, fpos in pb, the member lists and the
+// per-voxel records in pe (2 (n + MP_SLACK) words)
+__device__ inline VxHot map_hot(const MapperDev& D, size_t sm, uint32_t so, uint32_t n) {
+  const size_t b = sm * (mp_cube_scratch(D) + (size_t)D.max_in + MP_SLACK) + so;
+  VxHot H;
+  H.rk = D.pa + b;
+  H.fpos = D.pb + b;
+  H.hl = reinterpret_cast<uint32_t*>(D.pe + b);
+  H.hv = H.hl + n;
+  H.cap_h = n / 3 + 1;
+  return H;
+}
+
 // ---------------------------------------------------------------------------------------
 // VoxelGrid of the incoming feature clouds -> CornerStack / SurfStack (:492-500)
 // ---------------------------------------------------------------------------------------
 // one 1024-thread workgroup per (stream, map): grid B * 2
+template <bool PCL>
 __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
   const int s = D.s0 + (blockIdx.x >> 1), m = blockIdx.x & 1;
@@ -338,7 +355,7 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
   if (!I.active) return;
   const size_t sm = sm_index(s, m);
   int* err = &D.stk_err[s];
-  if (D.pcl_order) {
+  if (PCL && I.n[m] > VH_MAX_N) {  // PCL's order, the sort in global memory
     VxPclOut O;
     O.out = D.stack[m] + (size_t)s * D.max_in;
     O.cap = D.max_in;
@@ -366,7 +383,11 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
   S.scratch_pts = D.stk_pts + sm * D.max_in;
   S.scratch_idx = D.stk_idx + sm * D.max_in;
   S.scratch_cap = D.max_in;
+  if (PCL) S.hot = map_hot(D, sm, mp_stack_offset(D), (uint32_t)I.n[m]);
   voxel_segment(S, lds);
+  if (PCL)  // PCL's summation order for the voxels of 3+ members (voxel_hot.h)
+    vh_fixup<VX_THREADS>(VxSrc{I.p[m], I.n[m], nullptr}, I.n[m], S.out, S.hot, lds, VX_LDS_WORDS - 256,
+                         *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192), nullptr, err);
 }
 
 // Few streams: the input-order stack VoxelGrid of a (stream, map) over stack_k workgroups.
@@ -708,6 +729,7 @@ __device__ inline void submap_prep(const MapperDev& D, int s, StreamFrame& F) {
     F.sub_off[m][vn] = total;
     F.sub_n[m] = total;
     F.scratch_tail[m] = 0;  // re-VoxelGrid scratch (bounded by max_submap_points + stacks)
+    F.hot_tail[m] = 0;
     F.extra_n[m] = 0;
     if (m == 0) F.vx_bytes = 0;
   }
@@ -735,8 +757,6 @@ __global__ void __launch_bounds__(128) k_frame_prep(MapperDev D) {
   __syncthreads();
   if (threadIdx.x == 0 && I.active && I.stack_seq) {  // the stream's stacks (launched on the stack stream)
     uint32_t spins = 0;
-    // relaxed: the stack sizes read next are not in this XCD's L2 (invalidated at this kernel's
-    // start, not read since) and the stacks themselves are read by later kernels
     while (__hip_atomic_load(D.stk_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < I.stack_seq) {
       if (++spins > (1u << 24)) {
         atomicOr(&F.err, MAP_ERR_STACK_WAIT);
@@ -744,6 +764,11 @@ __global__ void __launch_bounds__(128) k_frame_prep(MapperDev D) {
       }
       __builtin_amdgcn_s_sleep(4);
     }
+    // acquire: the stack sizes this thread reads next (stack_counts) may share a line that
+    // another stream's block of this XCD pulled into the L2 before the stack kernel wrote it
+    // (streams of one frame can take stacks from different launches: loam_mapper_prefetch for
+    // some, the solve for the others); once per block per frame
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
   const unsigned long long t1 = __builtin_readcyclecounter();
@@ -1906,6 +1931,7 @@ __global__ void __launch_bounds__(VX_THREADS) k_insert_bucket(MapperDev D) {
 // the merge path (a fixed-point cube plus a few new points, voxel.h vx_merge_fixed_point) or
 // the full filter in a VX_THREADS workgroup with the whole LDS, then the cube's cell index.
 // ---------------------------------------------------------------------------------------
+template <bool PCL>
 __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube, int append, uint32_t* lds) {
   constexpr int LW = VX_LDS_WORDS;
   StreamFrame& F = D.fr[s];
@@ -1938,35 +1964,46 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
   S.prof = D.pdbg ? D.pdbg + 11 : nullptr;  // merge phases: dbg[11..14]
   bool merged = false;
   const unsigned long long t0 = __builtin_readcyclecounter();
-  if (D.pcl_order && !append && n_new > 0 && n_new <= VX_MERGE_CAP && cv.y > 0 && *tok == cv.x + 1) {
-    // a fixed-point cube whose voxels all end with at most 2 members: the merge's sums are
-    // PCL's whatever the order (vx_merge_fixed_point ORDER_FREE); else the PCL-order filter
-    merged = vx_merge_fixed_point<VX_THREADS, (int)VX_MERGE_CAP, VX_LDS_WORDS, true>(S, lds);
-    __syncthreads();
-  }
-  if (D.pcl_order && !append && !merged) {
-    // PCL's summation order: the sort of old content ++ new points (voxel_pcl.h).  Also a
-    // window cube that received nothing but is not a VoxelGrid fixed point (raw appended
-    // content, content set through the API): the reference re-filters every window cube
-    // (:795-808) in PCL's order
+  const bool fixed = n_new > 0 && n_new <= VX_MERGE_CAP && cv.y > 0 && *tok == cv.x + 1;
+  if (PCL && !append) {
+    // PCL's summation order (exact_voxel_order): also a window cube that received nothing but
+    // is not a VoxelGrid fixed point (raw appended content, content set through the API), as the
+    // reference re-filters every window cube (:795-808)
     uint32_t* sb = lds + LW - 3;
     const uint32_t n = cv.y + n_new;
-    if (threadIdx.x == 0) *sb = atomicAdd(&F.scratch_tail[m], n + MP_SLACK);
+    if (threadIdx.x == 0) *sb = atomicAdd(&F.hot_tail[m], n + MP_SLACK);
     __syncthreads();
     const uint32_t so = *sb;
     __syncthreads();
-    VxPclOut O;
-    O.out = ar;
-    O.tail = &F.arena_tail[m];
-    O.cap = D.map_cap;
-    O.res_off = &tab[cube].x;
-    O.res_cnt = &tab[cube].y;
-    O.stable_out = tok;
-    map_voxel_pcl(D, sm_index(s, m), so, VxSrc{ar + cv.x, (int)cv.y, D.ins_sorted + sm_index(s, m) * D.max_in + i0},
-                  (int)n, D.leaf[m], O, lds, &F.err);
+    if (n <= (uint32_t)VH_MAX_N) {
+      // the input-order filter sums every voxel of at most 2 members (order-free) and records the
+      // others, then voxel_hot.h sums those in std::sort's order
+      if ((size_t)so + n + MP_SLACK > mp_cube_scratch(D)) {
+        if (threadIdx.x == 0) atomicOr(&F.err, MAP_ERR_SORT);
+      } else {
+        S.hot = map_hot(D, sm_index(s, m), so, n);
+        if (fixed) {
+          merged = vx_merge_fixed_point<VX_THREADS, (int)VX_MERGE_CAP, VX_LDS_WORDS, true>(S, lds);
+          __syncthreads();  // false: grid overflow, full filter below
+        }
+        if (!merged) voxel_segment(S, lds);
+        vh_fixup<VX_THREADS>(VxSrc{ar + cv.x, (int)cv.y, D.ins_sorted + sm_index(s, m) * D.max_in + i0}, (int)n, ar,
+                             S.hot, lds, LW - 256, *reinterpret_cast<VxMisc*>(lds + LW - 192), tok, &F.err);
+      }
+    } else {  // the whole std::sort emulated in global memory (voxel_pcl.h)
+      VxPclOut O;
+      O.out = ar;
+      O.tail = &F.arena_tail[m];
+      O.cap = D.map_cap;
+      O.res_off = &tab[cube].x;
+      O.res_cnt = &tab[cube].y;
+      O.stable_out = tok;
+      map_voxel_pcl(D, sm_index(s, m), so, VxSrc{ar + cv.x, (int)cv.y, D.ins_sorted + sm_index(s, m) * D.max_in + i0},
+                    (int)n, D.leaf[m], O, lds, &F.err);
+    }
     __syncthreads();
-  } else if (!D.pcl_order || append) {
-    if (!append && n_new > 0 && n_new <= VX_MERGE_CAP && cv.y > 0 && *tok == cv.x + 1) {
+  } else {
+    if (!append && fixed) {
       merged = vx_merge_fixed_point(S, lds);
       __syncthreads();  // false: grid overflow, full filter below
     }
@@ -2013,14 +2050,16 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
   }
 }
 
-// one workgroup per (stream, map, slot): block = slot item
+// one workgroup per (stream, map, slot): block = slot item.  PCL: exact_voxel_order (its own
+// instantiation, so that the sort's registers do not weigh on the input-order kernel)
+template <bool PCL>
 __global__ void __launch_bounds__(VX_THREADS) k_revox(MapperDev D) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
   const uint32_t item = 2 * (uint32_t)D.s0 * INS_SLOTS + blockIdx.x;
   const int slot = (int)(item % INS_SLOTS), sm = (int)(item / INS_SLOTS);
   int cube = 0, append = 0;
   if (!revox_target(D, sm >> 1, sm & 1, slot, &cube, &append)) return;
-  revox_item(D, sm >> 1, sm & 1, slot, cube, append, lds);
+  revox_item<PCL>(D, sm >> 1, sm & 1, slot, cube, append, lds);
 }
 
 // cell index of one cube whose content was set through the API (cen: the host's grid centre)
@@ -2925,7 +2964,8 @@ static int32_t launch_stacks(loam_mapper* h) {
     LAUNCH_ON(s2, FAM_STACK, k_stack_part<<<B * 2 * D.stack_k, VX_THREADS, 0, s2>>>(D));
     LAUNCH_ON(s2, FAM_STACK, k_stack_cat<<<B * 2, VX_THREADS, 0, s2>>>(D));
   } else {
-    LAUNCH_ON(s2, FAM_STACK, k_stack_ds<<<B * 2, VX_THREADS, 0, s2>>>(D));
+    if (D.pcl_order) LAUNCH_ON(s2, FAM_STACK, k_stack_ds<true><<<B * 2, VX_THREADS, 0, s2>>>(D));
+    else LAUNCH_ON(s2, FAM_STACK, k_stack_ds<false><<<B * 2, VX_THREADS, 0, s2>>>(D));
   }
   k_stack_done<<<1, 64, 0, s2>>>(h->d_stk_ready + par, seq);
   LOAM_HIP(hipGetLastError());
@@ -2966,7 +3006,8 @@ static void capture_frame(loam_mapper* h, const MapperDev& D, int fpar, hipStrea
     k_lm_round<<<lm_padded(B) * h->lm_G, LM_THREADS, 0, st>>>(D, round, h->lm_G);
   }
   k_insert_bucket<<<B * 2, VX_THREADS, 0, st>>>(D);
-  k_revox<<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D);
+  if (D.pcl_order) k_revox<true><<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D);
+  else k_revox<false><<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D);
   if (h->frame_flag) k_frame_out<<<1, 256, 0, st>>>(D, h->hfo_dev[fpar], h->done_dev + fpar);
   else if (!h->rec_copy_out) (void)hipMemcpyAsync(h->hfo[fpar].data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st);
 }
@@ -3213,7 +3254,8 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
   }
   LOAM_HIP(hipEventRecord(h->ev[2], st));
   LAUNCH(FAM_INSERT, k_insert_bucket<<<B * 2, VX_THREADS, 0, st>>>(D));
-  LAUNCH(FAM_REVOX, k_revox<<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D));
+  if (D.pcl_order) LAUNCH(FAM_REVOX, k_revox<true><<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D));
+  else LAUNCH(FAM_REVOX, k_revox<false><<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D));
   LOAM_HIP(hipGetLastError());
   LOAM_HIP(hipMemcpyAsync(h->hfo[fpar].data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
   LOAM_HIP(hipEventRecord(h->ev_fr[fpar][1], st));
@@ -3491,7 +3533,14 @@ static bool chain_ok(const loam_mapper* h) {
 int32_t loam_mapper_solve_async(loam_mapper* h) {
   if (!h) return LOAM_ERR_ARG;
   LOAM_HIP(hipSetDevice(h->dev));
-  if (h->q.size() >= 2) TRY(finish_oldest(h));
+  // a third frame first finishes the oldest; that frame's own status (a capacity or hand-off
+  // error, committed as computed) is returned after the new frame is enqueued, so the caller's
+  // input is never left behind.  A HIP or argument error stops here.
+  int32_t older = LOAM_OK;
+  if (h->q.size() >= 2) {
+    older = finish_oldest(h);
+    if (older == LOAM_ERR_HIP || older == LOAM_ERR_ARG || older == LOAM_ERR_STATE) return older;
+  }
   TRY(launch_front(h));
   FrameRec R;
   const bool behind = !h->q.empty();
@@ -3527,13 +3576,13 @@ int32_t loam_mapper_solve_async(loam_mapper* h) {
       H.in_ready = false;
       H.stk_launched = false;
     }
-    if (!any) return LOAM_OK;
+    if (!any) return older;
     R.seq = 1;  // (a real sequence number when it is enqueued)
     h->spar ^= 1;
   }
   R.behind = behind;
   if (R.seq) h->q.push_back(std::move(R));
-  return LOAM_OK;
+  return older;
 }
 
 int32_t loam_mapper_wait(loam_mapper* h) {

@@ -9,6 +9,7 @@
 #include "common.h"
 #include "lm.h"
 #include "voxel.h"
+#include "voxel_hot.h"
 #include "voxel_pcl.h"
 
 namespace loam {
@@ -85,6 +86,16 @@ __global__ void __launch_bounds__(P_PCL_THREADS) k_voxel_pcl_one(const float4* s
   O.out = out;
   O.res_cnt = out_n;
   voxel_grid_pcl<P_PCL_THREADS>(VxPtrSrc{src}, n, leaf, O, X, M, ws, err);
+}
+
+// PCL-order VoxelGrid of one cloud of at most VH_MAX_N points the way the mapper runs it
+// (exact_voxel_order): the input-order filter for the voxels of at most 2 members, the pruned
+// std::sort emulation for the others (voxel_hot.h)
+__global__ void __launch_bounds__(VX_THREADS) k_voxel_hot_one(VoxSeg S, int* err) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
+  voxel_segment(S, lds);
+  vh_fixup<VX_THREADS>(VxSrc{S.src0, S.n0, nullptr}, S.n0, S.out, S.hot, lds, VX_LDS_WORDS - 256,
+                       *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192), nullptr, err);
 }
 
 struct PKeyLess {
@@ -375,6 +386,50 @@ int32_t loam_voxel_grid_pcl(int32_t device, const float* in, int32_t n, float le
   int32_t rc = ensure_device(device);
   if (rc != LOAM_OK) return rc;
   LOAM_HIP(hipSetDevice(device));
+  if (n <= VH_MAX_N) {
+    DevBuf din, dout, drk, dhl, dhv, dfp, didx, dcnt, derr;
+    const size_t m = std::max(n, 1);
+    LOAM_HIP(dmalloc<float4>(din, m));
+    LOAM_HIP(dmalloc<float4>(dout, m));
+    LOAM_HIP(dmalloc<uint32_t>(drk, m));
+    LOAM_HIP(dmalloc<uint32_t>(dhl, m));
+    LOAM_HIP(dmalloc<uint32_t>(dhv, m + 3));
+    LOAM_HIP(dmalloc<uint32_t>(dfp, m));
+    LOAM_HIP(dmalloc<int>(didx, m));
+    LOAM_HIP(dmalloc<uint32_t>(dcnt, 1));
+    LOAM_HIP(dmalloc<int>(derr, 1));
+    LOAM_HIP(hipMemset(dcnt.p, 0, sizeof(uint32_t)));
+    LOAM_HIP(hipMemset(derr.p, 0, sizeof(int)));
+    if (n) LOAM_HIP(hipMemcpy(din.p, in, sizeof(float4) * n, hipMemcpyHostToDevice));
+    VoxSeg S{};
+    S.src0 = (const float4*)din.p;
+    S.n0 = n;
+    S.leaf = leaf;
+    S.out = (float4*)dout.p;
+    S.cap = (uint32_t)m;
+    S.res_cnt = (uint32_t*)dcnt.p;
+    S.scratch_idx = (int*)didx.p;
+    S.scratch_cap = (uint32_t)m;
+    S.err = (int*)derr.p;
+    S.hot.rk = (uint32_t*)drk.p;
+    S.hot.hl = (uint32_t*)dhl.p;
+    S.hot.hv = (uint32_t*)dhv.p;
+    S.hot.fpos = (uint32_t*)dfp.p;
+    S.hot.cap_h = (uint32_t)(n / 3 + 1);
+    k_voxel_hot_one<<<1, VX_THREADS>>>(S, (int*)derr.p);
+    LOAM_HIP(hipGetLastError());
+    uint32_t cnt = 0;
+    int err = 0;
+    LOAM_HIP(hipMemcpy(&cnt, dcnt.p, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    LOAM_HIP(hipMemcpy(&err, derr.p, sizeof(int), hipMemcpyDeviceToHost));
+    if (err) {
+      set_error("loam_voxel_grid_pcl: capacity (unique voxels or sort lists)");
+      return LOAM_ERR_CAPACITY;
+    }
+    if (cnt) LOAM_HIP(hipMemcpy(out, dout.p, sizeof(float4) * cnt, hipMemcpyDeviceToHost));
+    *n_out = (int32_t)cnt;
+    return LOAM_OK;
+  }
   DevBuf din, dout, de, da, db, ds, dseg, dcnt, derr;
   const int cap = ss_cap(n);
   LOAM_HIP(dmalloc<int>(dseg, 6 * (size_t)cap));

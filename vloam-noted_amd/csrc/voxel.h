@@ -33,6 +33,17 @@ constexpr int VX_ERR_CAPACITY = 1;
 constexpr int VX_ERR_OUTPUT = 2;
 constexpr int VX_LDS_WORDS = 40960;  // 160 KiB
 
+// PCL's summation order (exact_voxel_order, voxel_hot.h): what the input-order filter records for
+// the voxels of 3 or more members ("hot"), whose centroids depend on std::sort's order.  Global
+// scratch of one filter; n points.
+struct VxHot {
+  uint32_t* rk;    // [n] per point: output slot << 1 | hot
+  uint32_t* hl;    // [n] the hot voxels' member lists (point indices), grouped by voxel, any order
+  uint32_t* hv;    // [3 * cap_h] per hot voxel: output slot, list start, member count
+  uint32_t* fpos;  // [n] per hot point: its position after the emulated sort (voxel_hot.h)
+  uint32_t cap_h;
+};
+
 struct VoxSeg {
   const float4* src0;
   int n0;
@@ -57,6 +68,8 @@ struct VoxSeg {
   unsigned long long* prof = nullptr;  // optional: merge phase cycles [bbox, sort, runs, pass A, pass B]
   unsigned long long* prof_seg = nullptr;  // optional: full filter phase cycles [gather + bbox,
                                            // hash, sort + scan, member lists + centroids]
+  VxHot hot{};  // exact order (hot.rk set): record the hot voxels instead of summing them (the
+                // stable token then covers the cold voxels only; voxel_hot.h)
 };
 
 // thread 0 adds the cycles since *t to prof[k] and restarts *t (phase counters; call after a barrier)
@@ -123,10 +136,29 @@ struct VxMisc {
   int sfail;
   int moved;
   uint32_t nbig;
+  uint32_t hot_n, hot_l;  // exact order (VxHot): hot voxels recorded, their member-list length
   VxGeom g;
   float bb[VX_WAVES][6];
 };
 static_assert(sizeof(VxMisc) <= 192 * 4, "misc area");
+
+
+// a hot voxel (output slot, cnt members member(0 ..)) -> hv / hl / rk.  One thread; counters in M
+template <typename MF>
+__device__ inline void vh_record(const VxHot& H, VxMisc& M, uint32_t slot, uint32_t cnt, const MF& member) {
+  const uint32_t h = atomicAdd(&M.hot_n, 1u);
+  const uint32_t st = atomicAdd(&M.hot_l, cnt);
+  if (h < H.cap_h) {
+    H.hv[3 * h] = slot;
+    H.hv[3 * h + 1] = st;
+    H.hv[3 * h + 2] = cnt;
+  }
+  for (uint32_t a = 0; a < cnt; ++a) {
+    const uint32_t i = member(a);
+    H.hl[st + a] = i;
+    H.rk[i] = (slot << 1) | 1u;
+  }
+}
 
 
 struct VxSrc {
@@ -177,7 +209,8 @@ __device__ inline bool vx_centroids(const VxGeom& g, const VxSrc& P, uint32_t N,
                                     uint32_t klo, uint32_t khi, uint32_t U, const uint32_t* ukey,
                                     const uint32_t* uoff, uint32_t* ufill, float4* out,
                                     uint32_t* big_list, uint32_t big_cap, VxMisc& M,
-                                    unsigned long long* dprof = nullptr) {
+                                    unsigned long long* dprof = nullptr, const VxHot* H = nullptr,
+                                    uint32_t rank0 = 0) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   unsigned long long tq = __builtin_readcyclecounter();
   bool moved = false;
@@ -197,6 +230,7 @@ __device__ inline bool vx_centroids(const VxGeom& g, const VxSrc& P, uint32_t N,
         }
         const uint32_t pos = uoff[lo] + atomicAdd(&ufill[lo], 1u);
         members[pos] = (MT)i;
+        if (H) H->rk[i] = (rank0 + lo) << 1;  // the hot ones are re-marked below
       }
     }
     __syncthreads();
@@ -207,6 +241,10 @@ __device__ inline bool vx_centroids(const VxGeom& g, const VxSrc& P, uint32_t N,
   for (uint32_t j = tid; j < U; j += VX_THREADS) {
     const uint32_t b = uoff[j];
     const uint32_t n = ufill[j];
+    if (H && n >= 3) {  // exact order: summed later in std::sort's order (voxel_hot.h)
+      vh_record(*H, M, rank0 + j, n, [&](uint32_t a) { return (uint32_t)members[b + a]; });
+      continue;
+    }
     for (uint32_t a = 1; a < n; ++a) {  // insertion sort (nearly ordered lists)
       const MT v = members[b + a];
       uint32_t q = a;
@@ -278,7 +316,7 @@ __device__ inline void vx_bitonic_regs(uint64_t* sk, uint64_t* xb0, uint64_t* xb
 __device__ inline uint32_t vx_group(const VoxSeg& S, const VxGeom& g, const VxSrc& P, uint32_t N,
                                     int* members, uint32_t klo, uint32_t khi, uint32_t out_base,
                                     uint32_t lds_limit, uint32_t* lds, uint32_t* ws, VxMisc& M,
-                                    int* moved_out) {
+                                    int* moved_out, uint32_t rank0 = 0) {
   const int tid = threadIdx.x;
   unsigned long long tp = __builtin_readcyclecounter();
   uint32_t* hkey = lds;
@@ -420,11 +458,13 @@ __device__ inline uint32_t vx_group(const VoxSeg& S, const VxGeom& g, const VxSr
   if (N <= 65536u && 3 * U + mem_words + 64 <= lds_limit) {
     uint32_t* big = lds + 3 * U + mem_words;
     moved = vx_centroids(g, P, N, reinterpret_cast<uint16_t*>(lds + 3 * U), klo, khi, U, ukey, uoff,
-                         ufill, S.out + ob, big, lds_limit - (3 * U + mem_words), M, S.prof_seg ? S.prof_seg + 4 : nullptr);
+                         ufill, S.out + ob, big, lds_limit - (3 * U + mem_words), M, S.prof_seg ? S.prof_seg + 4 : nullptr,
+                         S.hot.rk ? &S.hot : nullptr, rank0);
   } else {
     uint32_t* big = lds + 3 * U;
     const uint32_t cap = lds_limit > 3 * U ? lds_limit - 3 * U : 0u;
-    moved = vx_centroids(g, P, N, members, klo, khi, U, ukey, uoff, ufill, S.out + ob, big, cap, M);
+    moved = vx_centroids(g, P, N, members, klo, khi, U, ukey, uoff, ufill, S.out + ob, big, cap, M, nullptr,
+                         S.hot.rk ? &S.hot : nullptr, rank0);
   }
   if (moved) M.moved = 1;
   __syncthreads();
@@ -492,7 +532,7 @@ __device__ inline void vx_grouped(const VoxSeg& S, const VxGeom& g, const VxSrc&
   for (int gi = 0; gi < ng; ++gi) {
     const int ge = (int)gend[gi];
     const uint32_t U = vx_group(S, g, P, N, members, blo(gstart), ge >= VX_NB ? 0xFFFFFFFFu : blo(ge),
-                                ob + acc, VX_HIST_WORD, lds, ws, M, &moved);
+                                ob + acc, VX_HIST_WORD, lds, ws, M, &moved, acc);
     if (U == VX_OVERFLOW) {
       if (tid == 0) atomicOr(S.err, VX_ERR_CAPACITY);
       return;
@@ -577,6 +617,10 @@ __device__ inline void voxel_segment(const VoxSeg& S, uint32_t* lds) {
   const int wid = tid >> 6, lane = tid & 63;
   uint32_t* ws = lds + VX_LDS_WORDS - 256;  // scan scratch (64 words)
   VxMisc& M = *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192);
+  if (tid == 0) {
+    M.hot_n = 0;
+    M.hot_l = 0;
+  }
 
   // ---- 1. count secondary matches, allocate scratch, gather (stable)
   uint32_t m1 = 0;
@@ -801,17 +845,17 @@ __device__ inline void vx_copy_through(const VoxSeg& S, uint32_t* sbase) {
 // the voxels holding A points alone need sorting, and there are few: the map is dense where
 // new points land.  Returns false, with nothing written, when the grid overflows (the caller
 // then runs the full filter).
-// ORDER_FREE (PCL's summation order wanted, exact_voxel_order = 1): the merge is used only when
-// every voxel ends up with at most 2 members.  (0 + a) + b == (0 + b) + a in IEEE arithmetic
-// (commutative; the leading 0 + x turns a -0 into +0 either way), so such a voxel's centroid
-// does not depend on the order PCL's std::sort leaves its members in, and the merge gives
-// PCL's bits.  A voxel with 3 or more members returns false, nothing written, before anything
-// is allocated: the caller runs the PCL-order filter.
+// HOT (PCL's summation order wanted, exact_voxel_order = 1): a voxel of at most 2 members sums
+// alike in any order ((0 + a) + b == (0 + b) + a in IEEE arithmetic: commutative, and the leading
+// 0 + x turns a -0 into +0 either way), so the merge gives PCL's bits for it.  A voxel of 3 or
+// more members is not summed here but recorded in S.hot (its members, its output slot; every
+// point's slot), for voxel_hot.h to sum in std::sort's order; the stable token covers the
+// other voxels.
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t VX_MERGE_CAP = 4096;
 
 // NT threads, up to CAP new points, LW LDS words (scan scratch and misc in the last 256)
-template <int NT = VX_THREADS, int CAP = (int)VX_MERGE_CAP, int LW = VX_LDS_WORDS, bool ORDER_FREE = false>
+template <int NT = VX_THREADS, int CAP = (int)VX_MERGE_CAP, int LW = VX_LDS_WORDS, bool HOT = false>
 __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
   constexpr int TMAX = 2 * CAP;       // hash slots (load factor <= 1/2)
   constexpr int RX = 2 * TMAX + CAP;  // start of the shared region: C hits, then the sort
@@ -929,21 +973,6 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
     if (h != NONE) hit[h] = (int)k;
   }
   __syncthreads();
-  if constexpr (ORDER_FREE) {  // a voxel of 3+ members: its sum depends on PCL's order
-    int many = 0;
-#pragma unroll
-    for (int q = 0; q < SPT; ++q) {
-      const uint32_t h = tid + q * NT;
-      if (h < T && (hcnt[h] & 0x1FFFu) + (hit[h] >= 0 ? 1u : 0u) >= 3u) many = 1;
-    }
-    if (tid == 0) M.moved = 0;
-    __syncthreads();
-    if (many) M.moved = 1;
-    __syncthreads();
-    const bool any_many = M.moved != 0;
-    __syncthreads();
-    if (any_many) return false;
-  }
   vx_phase(S.prof, 1, &tp);
   // 4. the voxels holding A points only, listed then sorted by key
   uint32_t fmask = 0, cnt = 0;
@@ -977,6 +1006,8 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
   for (uint32_t r = tid; r <= Dn; r += NT) cbelow[r] = 0;
   if (tid == 0) {
     M.moved = 0;
+    M.hot_n = 0;
+    M.hot_l = 0;
     uint32_t b = S.tail ? atomicAdd(S.tail, n0 + Dn) : 0;
     if (b + n0 + Dn > S.cap) {
       atomicOr(S.err, VX_ERR_OUTPUT);
@@ -1033,9 +1064,18 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
     atomicAdd(&cbelow[b], 1u);
     float4 v = c;
     if (h != NONE) {
+      if constexpr (HOT) {
+        const uint32_t e = hcnt[h], m0 = e >> 13, mc = e & 0x1FFFu;
+        if (mc + 1 >= 3) {
+          vh_record(S.hot, M, k + b, mc + 1, [&](uint32_t a) { return a == 0 ? k : n0 + mem[m0 + a - 1]; });
+          return;
+        }
+        for (uint32_t a = 0; a < mc; ++a) S.hot.rk[n0 + mem[m0 + a]] = (k + b) << 1;
+      }
       v = centroid(h, 0.f + c.x, 0.f + c.y, 0.f + c.z, 0.f + c.w, 1u);
       moved |= vx_key(g, v) != key;
     }
+    if constexpr (HOT) S.hot.rk[k] = (k + b) << 1;
     out[k + b] = v;
   };
 #pragma unroll
@@ -1058,6 +1098,14 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
   }
   for (uint32_t r = tid; r < Dn; r += NT) {
     const uint32_t h = (uint32_t)srt[r];
+    if constexpr (HOT) {
+      const uint32_t e = hcnt[h], m0 = e >> 13, mc = e & 0x1FFFu, slot = r + cbelow[r];
+      if (mc >= 3) {
+        vh_record(S.hot, M, slot, mc, [&](uint32_t a) { return n0 + mem[m0 + a]; });
+        continue;
+      }
+      for (uint32_t a = 0; a < mc; ++a) S.hot.rk[n0 + mem[m0 + a]] = slot << 1;
+    }
     const float4 v = centroid(h, 0.f, 0.f, 0.f, 0.f, 0u);
     out[r + cbelow[r]] = v;
     moved |= vx_key(g, v) != (uint32_t)(srt[r] >> 32);

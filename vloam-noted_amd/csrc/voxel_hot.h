@@ -1,0 +1,616 @@
+// voxel_hot.h — PCL's VoxelGrid summation order (std::sort's permutation) for the voxels where it
+// shows, LDS-resident, pruned to the segments that can still reorder such a voxel.
+//
+// PCL 1.8-1.12 voxel_grid.hpp applyFilter sorts (idx, point) pairs with std::sort on idx alone
+// and sums each voxel's points in the sorted order (laser_mapping.cpp:492-500, :795-808,
+// scan_registration.cpp:497-501).  Float addition is not associative, but a voxel with at most
+// two members sums alike in either order ((0 + a) + b == (0 + b) + a), so only voxels with 3 or
+// more members ("hot") need that order.  And the order is cheap to read off: libstdc++'s
+// __final_insertion_sort is stable and never moves an element out of its final segment, so the
+// members of a voxel end in the order of their positions once the partitions (and the depth-limit
+// heap sorts) are done.  Hence, per filter:
+//   phase 1 (voxel.h, the input-order filter): every cold voxel's centroid (exact: order-free);
+//            per point its output slot and hot bit (VxHot::rk); the hot voxels' member lists;
+//   phase 2 (vh_sort): libstdc++'s __introsort_loop on E[i] = slot << 16 | hot << 15 | i in LDS,
+//            exactly (stdsort.h's parallel Hoare formulation), except that
+//              * a segment holding fewer than two hot elements is not partitioned: nothing below
+//                it can reorder two members of one hot voxel;
+//              * a depth-limit segment is heap-sorted (literally, one lane) only when two members
+//                of one hot voxel lie in it, else left as it is;
+//              * the final insertion sort is skipped (it keeps the position order);
+//            then each hot point's position -> VxHot::fpos;
+//   phase 3 (vh_centroids): each hot voxel summed in its members' position order.
+// The rule is pinned against libstdc++ itself on cube- and stack-shaped clouds
+// (tests/test_sort_rule.py::test_hot_pruned_rule_keeps_pcl_centroids) and on the GPU against the
+// oracle (tests/test_gpu_primitives.py, the mapping and long-stream tests in exact mode).
+//
+// Workgroup partitions (segments over VH_BIG elements, the first levels and the degenerate chains
+// of cube re-filters): each thread classifies a contiguous chunk held in registers, one block scan
+// places the stops; wave partitions (the subtrees below VH_BIG) run without barriers, one wave
+// each, smaller part first.  The Hoare scan's swap pairs (l_k, r_k) come from the test
+// l_k < r_k  <=>  k <= #(right stops right of l_k), so only r_1 .. r_{(m-1)/2} are listed (u16,
+// a segment [lo, hi) owns Bs[lo/2 ..)), and every read of the segment precedes every write.
+#pragma once
+#include "stdsort.h"
+#include "voxel.h"
+
+namespace loam {
+
+constexpr int VH_BIG = 1024;      // longer segments: partitioned by the workgroup
+constexpr int VH_MAX_N = 30720;   // LDS-resident emulation up to this many points (30 per thread)
+constexpr int VH_CHUNK = VH_MAX_N / VX_THREADS;  // positions per thread of a workgroup partition
+constexpr int VH_ROOTS = 512;     // pending wave subtrees
+constexpr int VH_BIGC = 64;       // workgroup segments of one level (segments > VH_BIG are disjoint: <= 30)
+constexpr int VH_LIFO = 8;        // wave-local pending parts (smaller part first: depth <= 6)
+constexpr int VH_WAVE_W = VH_LIFO + 64;  // per wave: LIFO + the dup check's keys
+constexpr int VH_SMALL = 32;      // hot voxels up to this many members: summed by one thread
+constexpr int VH_REG = 8;         // hot voxels up to 64 * VH_REG members: rank-sorted by a wave
+constexpr uint32_t VH_HOT = 0x8000u;
+constexpr int VH_ERR_ROOTS = 16, VH_ERR_LIST = 32;
+
+struct VhLess {
+  __device__ bool operator()(uint32_t a, uint32_t b) const { return (a >> 16) < (b >> 16); }
+};
+
+struct VhCtl {
+  int hot[2], S[2], cut[2];  // per segment, double-buffered by segment parity
+  int nbig[2];               // workgroup segments of this / the next level
+  int nroot, root_take;      // pending wave subtrees, the next one to claim
+  int dup;
+  int err;
+  uint32_t ws[VX_WAVES + 1];  // block-scan scratch of the workgroup partition
+};
+
+// a wave subtree / LIFO entry: lo (15 bits) | length (11 bits) | depth budget (5 bits)
+__device__ inline uint32_t vh_pack(int lo, int len, int d) {
+  return (uint32_t)lo | ((uint32_t)len << 15) | ((uint32_t)d << 26);
+}
+
+struct VhLds {
+  uint32_t* E;
+  uint16_t* Bs;
+  uint32_t* roots;
+  uint32_t* bigl;  // [2][VH_BIGC]: lo | hi << 15
+  uint32_t* wave;  // [waves][VH_WAVE_W]
+  VhCtl* C;
+};
+
+template <int NT>
+__device__ inline VhLds vh_layout(uint32_t* lds, int n) {
+  VhLds L;
+  L.E = lds;
+  L.Bs = reinterpret_cast<uint16_t*>(lds + n);
+  L.roots = lds + n + n / 4 + 2;
+  L.bigl = L.roots + VH_ROOTS;
+  L.wave = L.bigl + 2 * VH_BIGC;
+  L.C = reinterpret_cast<VhCtl*>(L.wave + (NT / 64) * VH_WAVE_W);
+  return L;
+}
+template <int NT>
+constexpr int vh_lds_words(int n) {
+  return n + n / 4 + 2 + VH_ROOTS + 2 * VH_BIGC + (NT / 64) * VH_WAVE_W + (int)(sizeof(VhCtl) / 4) + 1;
+}
+static_assert(vh_lds_words<VX_THREADS>(VH_MAX_N) <= VX_LDS_WORDS - 256, "hot sort LDS layout");
+
+// __move_median_to_first(lo, lo + 1, mid, hi - 1) on one lane
+__device__ inline void vh_median(uint32_t* E, int lo, int hi) {
+  const VhLess less;
+  const int a = lo + 1, b = lo + (hi - lo) / 2, c = hi - 1;
+  const uint32_t ea = E[a], eb = E[b], ec = E[c];
+  int m;
+  if (less(ea, eb)) {
+    if (less(eb, ec)) m = b;
+    else if (less(ea, ec)) m = c;
+    else m = a;
+  } else if (less(ea, ec)) {
+    m = a;
+  } else if (less(eb, ec)) {
+    m = c;
+  } else {
+    m = b;
+  }
+  const uint32_t t = E[lo];
+  E[lo] = E[m];
+  E[m] = t;
+}
+
+// One segment [lo, hi) (17 <= m <= VH_BIG) partitioned by one wave.  Returns the cut, or -1 when
+// fewer than two hot elements lie in it (nothing to do below it).  Every lane returns the same.
+__device__ inline int vh_partition_wave(uint32_t* E, uint16_t* Bs, int lo, int hi) {
+  constexpr int U = VH_BIG / 64;
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  if (lane == 0) vh_median(E, lo, hi);
+  ss_wave_fence();
+  const uint32_t pe = E[lo];
+  const uint32_t p = pe >> 16;
+  uint32_t e[U];
+  int nr = 1, nh = (pe & VH_HOT) ? 1 : 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = lo + 1 + u * 64 + lane;
+    const bool v = i < hi;
+    e[u] = v ? E[i] : 0u;
+    const uint32_t k = e[u] >> 16;
+    nr += __popcll(__ballot(v && !(p < k)));
+    nh += __popcll(__ballot(v && (e[u] & VH_HOT)));
+  }
+  if (nh < 2) return -1;
+  const int m = hi - lo, KB = (m - 1) / 2, bb = lo >> 1;
+  // S and the listed right stops r_k = Bs[bb + k - 1] (k <= KB)
+  int L = 0, R = 1, S = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = lo + 1 + u * 64 + lane;
+    const bool v = i < hi;
+    const uint32_t k = e[u] >> 16;
+    const bool isl = v && !(k < p), isr = v && !(p < k);
+    const uint64_t bl = __ballot(isl), br = __ballot(isr);
+    const int kl = L + __popcll(bl & lt) + 1;
+    const int t = R + __popcll(br & lt);     // ascending index among the right stops (pivot: 0)
+    const bool pred = isl && kl <= nr - (t + (isr ? 1 : 0));  // right stops strictly right of i
+    S += __popcll(__ballot(pred));
+    if (isr && nr - t <= KB) Bs[bb + nr - t - 1] = (uint16_t)i;
+    L += __popcll(bl);
+    R += __popcll(br);
+  }
+  if (lane == 0 && nr <= KB) Bs[bb + nr - 1] = (uint16_t)lo;
+  ss_wave_fence();
+  // the swaps: every pair (l_k, r_k), k <= S, is read and written by its own lane alone (l_k < cut
+  // <= r_k, and no position is two pairs'), so no ordering is needed between lanes
+  int lK = 0x7FFFFFFF;
+  L = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = lo + 1 + u * 64 + lane;
+    const bool isl = i < hi && !((e[u] >> 16) < p);
+    const uint64_t bl = __ballot(isl);
+    const int kl = L + __popcll(bl & lt) + 1;
+    if (isl && kl <= S) {
+      const int y = Bs[bb + kl - 1];
+      E[i] = E[y];
+      E[y] = e[u];
+    }
+    if (isl && kl == S + 1) lK = i;
+    L += __popcll(bl);
+  }
+  lK = wave_min_i(lK);
+  const int rS = S >= 1 ? (int)Bs[bb + S - 1] : hi;
+  ss_wave_fence();
+  return __builtin_amdgcn_readfirstlane(min(lK, rS));
+}
+
+// A depth-limit segment on one wave: heap-sorted literally when two members of one hot voxel lie
+// in it (their order is the heap's), else left as it is.  kb: the wave's 64-word key buffer.
+__device__ inline void vh_depth_limit_wave(uint32_t* E, int lo, int hi, uint32_t* kb) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  int nh = 0;
+  bool dup = false;
+  for (int c0 = lo; c0 < hi; c0 += 64) {
+    const int i = c0 + lane;
+    const uint32_t e = i < hi ? E[i] : 0u;
+    const bool h = i < hi && (e & VH_HOT);
+    const uint64_t b = __ballot(h);
+    const int slot = nh + __popcll(b & lt);
+    if (h && slot < 64) kb[slot] = e >> 16;
+    nh += __popcll(b);
+  }
+  if (nh < 2) return;
+  if (nh > 64) {
+    dup = true;  // more than the buffer: assume the order shows
+  } else {
+    ss_wave_fence();
+    const uint32_t mine = lane < nh ? kb[lane] : 0xFFFFFFFFu;
+    bool d = false;
+    for (int j = 0; j < nh; ++j) d |= lane < nh && j != lane && kb[j] == mine;
+    dup = __ballot(d) != 0ull;
+  }
+  if (!dup) return;
+  ss_wave_fence();
+  if (lane == 0) ss_heap_sort(E, lo, hi, VhLess{});
+  ss_wave_fence();
+}
+
+// The subtree below one pending segment, one wave, no barriers
+__device__ inline void vh_wave_subtree(uint32_t* E, uint16_t* Bs, uint32_t root, uint32_t* wa) {
+  const int lane = threadIdx.x & 63;
+  uint32_t* stk = wa;
+  uint32_t* kb = wa + VH_LIFO;
+  int top = 0;
+  uint32_t cur = root;
+  while (true) {
+    const int lo = (int)(cur & 0x7FFFu), len = (int)((cur >> 15) & 0x7FFu), d = (int)(cur >> 26);
+    const int hi = lo + len;
+    bool next = true;  // take the next pending entry
+    if (len > SS_THRESHOLD) {
+      if (d == 0) {
+        vh_depth_limit_wave(E, lo, hi, kb);
+      } else {
+        const int cut = vh_partition_wave(E, Bs, lo, hi);
+        if (cut >= 0) {
+          const int l0 = cut - lo, l1 = hi - cut;
+          const bool left_small = l0 <= l1;
+          const int sl = left_small ? lo : cut, sn = left_small ? l0 : l1;  // smaller part: now
+          const int bl_ = left_small ? cut : lo, bn = left_small ? l1 : l0;  // larger: pending
+          if (bn > SS_THRESHOLD) {
+            if (lane == 0 && top < VH_LIFO) stk[top] = vh_pack(bl_, bn, d - 1);
+            ++top;  // (overflow impossible: each pending part is larger than the current one)
+            ss_wave_fence();
+          }
+          if (sn > SS_THRESHOLD) {
+            cur = vh_pack(sl, sn, d - 1);
+            next = false;
+          }
+        }
+      }
+    }
+    if (next) {
+      if (top == 0) break;
+      --top;
+      cur = __builtin_amdgcn_readfirstlane(stk[min(top, VH_LIFO - 1)]);
+    }
+  }
+}
+
+// Drain the pending wave subtrees (all waves), then reset the list.  Uniform call.
+template <int NT>
+__device__ inline void vh_drain(const VhLds& L) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t* wa = L.wave + wid * VH_WAVE_W;
+  const int nroot = min(L.C->nroot, VH_ROOTS);
+  while (true) {
+    int k = 0;
+    if (lane == 0) k = atomicAdd(&L.C->root_take, 1);
+    k = __builtin_amdgcn_readfirstlane(k);
+    if (k >= nroot) break;
+    vh_wave_subtree(L.E, L.Bs, L.roots[k], wa);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    L.C->nroot = 0;
+    L.C->root_take = 0;
+  }
+  __syncthreads();
+}
+
+// One segment [lo, hi) (m > VH_BIG) partitioned by the workgroup.  par: the segment's parity
+// (its VhCtl slot; the other slot is reset here for the next segment).  Returns the cut, or -1
+// when fewer than two hot elements lie in it.  Uniform.
+template <int NT>
+__device__ inline int vh_partition_wg(const VhLds& L, int lo, int hi, int par) {
+  constexpr int NW = NT / 64;
+  constexpr int CH = VH_MAX_N / NT;
+  static_assert(CH <= 32, "chunk masks in one word");
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  uint32_t* E = L.E;
+  VhCtl* C = L.C;
+  uint32_t* ws = C->ws;
+  static_assert(NW <= VX_WAVES, "scan scratch");
+  if (tid == 0) vh_median(E, lo, hi);
+  __syncthreads();
+  if (tid == 0) {  // the next segment's slot: every read of it (two segments back) is done
+    C->hot[par ^ 1] = 0;
+    C->S[par ^ 1] = 0;
+    C->cut[par ^ 1] = 0x7FFFFFFF;
+  }
+  const uint32_t pe = E[lo];
+  const uint32_t p = pe >> 16;
+  const int len = hi - lo - 1;  // the scanned positions lo + 1 .. hi - 1
+  const int c = (len + NT - 1) / NT;
+  const int b0 = lo + 1 + tid * c;
+  uint32_t ml = 0, mr = 0;
+  int nh = 0;
+#pragma unroll
+  for (int u = 0; u < CH; ++u) {
+    const int i = b0 + u;
+    if (u < c && i < hi) {
+      const uint32_t e = E[i];
+      const uint32_t k = e >> 16;
+      if (!(k < p)) ml |= 1u << u;
+      if (!(p < k)) mr |= 1u << u;
+      nh += (e & VH_HOT) ? 1 : 0;
+    }
+  }
+  nh = wave_sum_i(nh);
+  if (lane == 0 && nh) atomicAdd(&C->hot[par], nh);
+  const uint32_t v = (uint32_t)__popc(ml) | ((uint32_t)__popc(mr) << 16);  // totals < 2^16
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) ws[wid] = x;
+  __syncthreads();
+  if (C->hot[par] + ((pe & VH_HOT) ? 1 : 0) < 2) return -1;
+  uint32_t off = x - v, tot = 0;
+  for (int w = 0; w < NW; ++w) {
+    const uint32_t t = ws[w];
+    off += w < wid ? t : 0u;
+    tot += t;
+  }
+  const int nr = 1 + (int)(tot >> 16);
+  const int m = hi - lo, KB = (m - 1) / 2, bb = lo >> 1;
+  uint16_t* Bs = L.Bs;
+  {
+    int kl = (int)(off & 0xFFFFu), t = 1 + (int)(off >> 16), S = 0;  // t: ascending right-stop index
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const bool isl = (ml >> u) & 1u, isr = (mr >> u) & 1u;
+      if (isl) {
+        ++kl;
+        S += kl <= nr - (t + (isr ? 1 : 0)) ? 1 : 0;
+      }
+      if (isr) {
+        if (nr - t <= KB) Bs[bb + nr - t - 1] = (uint16_t)(b0 + u);
+        ++t;
+      }
+    }
+    if (tid == 0 && nr <= KB) Bs[bb + nr - 1] = (uint16_t)lo;
+    S = wave_sum_i(S);
+    if (lane == 0 && S) atomicAdd(&C->S[par], S);
+  }
+  __syncthreads();
+  const int S = C->S[par];
+  {  // the swaps (each pair read and written by the thread of its left stop alone) and the cut
+    int kl = (int)(off & 0xFFFFu);
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      if ((ml >> u) & 1u) {
+        ++kl;
+        if (kl <= S) {
+          const int y = Bs[bb + kl - 1];
+          const uint32_t t = E[y];
+          E[y] = E[b0 + u];
+          E[b0 + u] = t;
+        }
+        if (kl == S + 1) atomicMin(&C->cut[par], b0 + u);
+      }
+    }
+    if (tid == 0) atomicMin(&C->cut[par], S >= 1 ? (int)Bs[bb + S - 1] : hi);
+  }
+  __syncthreads();
+  return C->cut[par];
+}
+
+// A depth-limit segment of the workgroup: the dup check on a bitmap of slots (in the Bs area,
+// free between partitions), then, if two members of one hot voxel lie in it, the literal heap sort
+template <int NT>
+__device__ inline void vh_depth_limit_wg(const VhLds& L, int n, int lo, int hi) {
+  const int tid = threadIdx.x;
+  uint32_t* bm = reinterpret_cast<uint32_t*>(L.Bs);
+  const int nw = (n >> 5) + 1;  // slot < n
+  for (int w = tid; w < nw; w += NT) bm[w] = 0u;
+  if (tid == 0) L.C->dup = 0;
+  __syncthreads();
+  bool d = false;
+  for (int i = lo + tid; i < hi; i += NT) {
+    const uint32_t e = L.E[i];
+    if (e & VH_HOT) {
+      const uint32_t s = e >> 16, bit = 1u << (s & 31u);
+      d |= (atomicOr(&bm[s >> 5], bit) & bit) != 0u;
+    }
+  }
+  if (__ballot(d) != 0ull && (tid & 63) == 0) L.C->dup = 1;
+  __syncthreads();
+  if (L.C->dup && tid == 0) ss_heap_sort(L.E, lo, hi, VhLess{});
+  __syncthreads();
+}
+
+// Phase 2: the pruned emulation over the n points (n <= VH_MAX_N; all NT threads), then
+// H.fpos[i] for every hot point i.  *err |= VH_ERR_ROOTS on a list overflow (cannot happen).
+template <int NT>
+__device__ inline void vh_sort(uint32_t* lds, int n, const VxHot& H, int* err) {
+  const int tid = threadIdx.x;
+  const VhLds L = vh_layout<NT>(lds, n);
+  VhCtl* C = L.C;
+  for (int i = tid; i < n; i += NT) {
+    const uint32_t r = H.rk[i];
+    L.E[i] = ((r >> 1) << 16) | ((r & 1u) << 15) | (uint32_t)i;
+  }
+  const int D0 = n > 1 ? 2 * (31 - __clz(n)) : 0;  // 2 * __lg(n)
+  if (tid == 0) {
+    C->nbig[0] = C->nbig[1] = 0;
+    C->nroot = C->root_take = 0;
+    C->err = 0;
+    C->hot[0] = C->S[0] = 0;
+    C->cut[0] = 0x7FFFFFFF;
+    if (n > SS_THRESHOLD) {
+      if (n > VH_BIG) {
+        L.bigl[0] = (uint32_t)n << 15;
+        C->nbig[0] = 1;
+      } else {
+        L.roots[0] = vh_pack(0, n, D0);
+        C->nroot = 1;
+      }
+    }
+  }
+  __syncthreads();
+  int seg = 0;
+  for (int lev = 0;; ++lev) {
+    const int cur = lev & 1, nxt = cur ^ 1;
+    const int nb = min(C->nbig[cur], VH_BIGC);
+    if (nb == 0) break;
+    const int d = D0 - lev;
+    for (int t = 0; t < nb; ++t) {
+      const uint32_t ent = L.bigl[cur * VH_BIGC + t];
+      const int lo = (int)(ent & 0x7FFFu), hi = (int)(ent >> 15);
+      if (d == 0) {
+        vh_depth_limit_wg<NT>(L, n, lo, hi);
+        seg = 0;  // (its barriers order every slot; restart the parity)
+        if (tid == 0) {
+          C->hot[0] = C->S[0] = 0;
+          C->cut[0] = 0x7FFFFFFF;
+        }
+        __syncthreads();
+        continue;
+      }
+      const int cut = vh_partition_wg<NT>(L, lo, hi, seg & 1);
+      ++seg;
+      if (cut < 0 || tid != 0) continue;
+      const int parts[2][2] = {{lo, cut}, {cut, hi}};
+      for (int q = 0; q < 2; ++q) {
+        const int a = parts[q][0], b = parts[q][1];
+        if (b - a > VH_BIG) {
+          const int s = C->nbig[nxt]++;
+          if (s < VH_BIGC) L.bigl[nxt * VH_BIGC + s] = (uint32_t)a | ((uint32_t)b << 15);
+          else C->err |= VH_ERR_ROOTS;
+        } else if (b - a > SS_THRESHOLD) {
+          const int s = C->nroot++;
+          if (s < VH_ROOTS) L.roots[s] = vh_pack(a, b - a, d - 1);
+          else C->err |= VH_ERR_ROOTS;
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == 0) C->nbig[cur] = 0;
+    const bool drain = C->nroot > VH_ROOTS - 2 * VH_BIGC;
+    __syncthreads();
+    if (drain) vh_drain<NT>(L);
+  }
+  vh_drain<NT>(L);
+  if (tid == 0 && C->err) atomicOr(err, C->err);
+  for (int q = tid; q < n; q += NT) {
+    const uint32_t e = L.E[q];
+    if (e & VH_HOT) H.fpos[e & 0x7FFFu] = (uint32_t)q;
+  }
+  __syncthreads();
+}
+
+// Phase 3: every hot voxel's centroid from its members in position order -> out[slot].  The
+// members' (position << 15 | point) go to LDS (lds[0 .. list length)), each voxel's run is
+// sorted (one thread up to VH_SMALL members, else one wave by rank), then summed in that order
+// from 0 in float (PCL's CentroidPoint), divided by (float)count.  Returns whether some centroid
+// left its voxel (then the filter's output is not a VoxelGrid fixed point).  All NT threads;
+// M.hot_n / hot_l from phase 1.
+template <int NT, typename PF>
+__device__ inline bool vh_centroids(const PF& P, float4* out, const VxHot& H, const VxGeom& g, uint32_t* lds,
+                                    uint32_t lds_words, VxMisc& M, int* err) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint32_t nh = min(M.hot_n, H.cap_h), nl = M.hot_l;
+  uint32_t* Lh = lds;
+  uint32_t* big = lds + nl;  // the voxels left to the waves
+  if (nl + 64 > lds_words) {  // cannot happen: nl <= n <= VH_MAX_N
+    if (tid == 0) atomicOr(err, VH_ERR_LIST);
+    return true;
+  }
+  const uint32_t big_cap = lds_words - nl;
+  for (uint32_t j = tid; j < nl; j += NT) {
+    const uint32_t i = H.hl[j];
+    Lh[j] = (H.fpos[i] << 15) | i;
+  }
+  if (tid == 0) {
+    M.nbig = 0;
+    M.moved = 0;
+  }
+  __syncthreads();
+  bool moved = false;
+  auto finish = [&](uint32_t slot, float sx, float sy, float sz, float si, uint32_t n, uint32_t i0) {
+    const float fn = (float)n;
+    const float4 cc = make_float4(sx / fn, sy / fn, sz / fn, si / fn);
+    out[slot] = cc;
+    moved |= vx_key(g, cc) != vx_key(g, P(i0));
+  };
+  for (uint32_t h = tid; h < nh; h += NT) {
+    const uint32_t slot = H.hv[3 * h], st = H.hv[3 * h + 1], cnt = H.hv[3 * h + 2];
+    if (cnt > (uint32_t)VH_SMALL) {
+      const uint32_t e = atomicAdd(&M.nbig, 1u);
+      if (e < big_cap) big[e] = h;
+      continue;
+    }
+    for (uint32_t a = 1; a < cnt; ++a) {
+      const uint32_t x = Lh[st + a];
+      uint32_t b = a;
+      while (b > 0 && Lh[st + b - 1] > x) {
+        Lh[st + b] = Lh[st + b - 1];
+        --b;
+      }
+      Lh[st + b] = x;
+    }
+    float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
+    for (uint32_t a = 0; a < cnt; a += 4) {
+      float4 pp[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (a + u < cnt) pp[u] = P(Lh[st + a + u] & 0x7FFFu);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (a + u < cnt) {
+          sx += pp[u].x; sy += pp[u].y; sz += pp[u].z; si += pp[u].w;
+        }
+    }
+    finish(slot, sx, sy, sz, si, cnt, Lh[st] & 0x7FFFu);
+  }
+  __syncthreads();
+  const uint32_t nbig = min(M.nbig, big_cap);
+  for (uint32_t q = wid; q < nbig; q += NT / 64) {
+    const uint32_t h = big[q];
+    const uint32_t slot = H.hv[3 * h], st = H.hv[3 * h + 1], cnt = H.hv[3 * h + 2];
+    if (cnt <= 64u * VH_REG) {  // rank sort: positions are distinct
+      uint32_t v[VH_REG], r[VH_REG];
+#pragma unroll
+      for (int u = 0; u < VH_REG; ++u) {
+        const uint32_t a = lane + 64u * u;
+        v[u] = a < cnt ? Lh[st + a] : 0u;
+        r[u] = 0;
+      }
+      for (uint32_t j = 0; j < cnt; ++j) {
+        const uint32_t y = Lh[st + j];
+#pragma unroll
+        for (int u = 0; u < VH_REG; ++u) r[u] += y < v[u] ? 1u : 0u;
+      }
+      ss_wave_fence();
+#pragma unroll
+      for (int u = 0; u < VH_REG; ++u)
+        if (lane + 64u * u < cnt) Lh[st + r[u]] = v[u];
+      ss_wave_fence();
+    } else if (lane == 0) {  // (larger voxels: one lane)
+      for (uint32_t a = 1; a < cnt; ++a) {
+        const uint32_t x = Lh[st + a];
+        uint32_t b = a;
+        while (b > 0 && Lh[st + b - 1] > x) {
+          Lh[st + b] = Lh[st + b - 1];
+          --b;
+        }
+        Lh[st + b] = x;
+      }
+    }
+    ss_wave_fence();
+    float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;  // every lane keeps the same running sum
+    for (uint32_t a = 0; a < cnt; a += 64) {
+      float4 pp = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (a + lane < cnt) pp = P(Lh[st + a + lane] & 0x7FFFu);
+      const uint32_t mm = min(64u, cnt - a);
+      for (uint32_t l = 0; l < mm; ++l) {
+        sx += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pp.x), (int)l));
+        sy += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pp.y), (int)l));
+        sz += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pp.z), (int)l));
+        si += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pp.w), (int)l));
+      }
+    }
+    if (lane == 0) finish(slot, sx, sy, sz, si, cnt, Lh[st] & 0x7FFFu);
+  }
+  if (moved) M.moved = 1;
+  __syncthreads();
+  return M.moved != 0;
+}
+
+// After phase 1 (voxel_segment or vx_merge_fixed_point<.., HOT> with S.hot = H, on the n points
+// P(0 .. n), n <= VH_MAX_N; output slots relative to out + M.sbase[1]): when a voxel has 3 or more
+// members, the pruned emulation and those voxels' centroids.  The stable token phase 1 wrote
+// (cold voxels) is cleared when a hot centroid left its voxel.  All NT threads; uniform.
+template <int NT, typename PF>
+__device__ inline void vh_fixup(const PF& P, int n, float4* out, const VxHot& H, uint32_t* lds, uint32_t lds_words,
+                                VxMisc& M, uint32_t* stable_out, int* err) {
+  __syncthreads();
+  if (M.hot_n == 0) return;
+  const VxGeom g = M.g;
+  float4* o = out + M.sbase[1];
+  vh_sort<NT>(lds, n, H, err);
+  const bool mv = vh_centroids<NT>(P, o, H, g, lds, lds_words, M, err);
+  if (mv && threadIdx.x == 0 && stable_out) *stable_out = 0u;
+  __syncthreads();
+}
+
+}  // namespace loam
