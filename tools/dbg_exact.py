@@ -35,4 +35,7 @@ for exact in (1, 0):
           f"cube phases {[round(v / 20e6, 3) for v in dc[11:15] + [dc[64]]]}; revox items merge/full/append {dc[4:7]} "
           f"filter Mcycles {[round(v / 20e6, 2) for v in dc[0:3]]} index {round(dc[8] / 20e6, 2)}; "
           f"cubes per size bucket (<1k,<2k,..) {cnt}; kcycles per cube {per}; depth-limit segments cubes {dc[66]} of {dc[67]} elements, stacks {dc[68]} of {dc[69]}; "
+          f"hot fix-ups cubes: sort/centroid Mcycles {[round(v / 20e6, 3) for v in dc[50:52]]} in {dc[52]} filters, heap-sorted {dc[72]}, "
+          f"sort phases setup/wg/waves/positions {[round(v / 20e6, 3) for v in dc[73:77]]}; "
+          f"stacks: {[round(v / 20e6, 3) for v in dc[54:56]]} in {dc[56]}, heap-sorted {dc[77]}, phases {[round(v / 20e6, 3) for v in dc[78:82]]}; "
           f"stacks {st.corner_stack},{st.surf_stack}", flush=True)

@@ -61,7 +61,7 @@ constexpr int SUBMAP_BLOCKS = 64;
 constexpr int INS_SLOTS = WIN_VALID_MAX + EXTRA_CAP;
 constexpr int MAP_ERR_SUBMAP = 4, MAP_ERR_EXTRA = 8, MAP_ERR_HASH = 16, MAP_ERR_LM_SYNC = 32,
               MAP_ERR_INDEX = 64, MAP_ERR_LIVE = 128, MAP_ERR_SORT = 256,
-              MAP_ERR_STACK = 512, MAP_ERR_TILE = 1024, MAP_ERR_STACK_WAIT = 2048;
+              MAP_ERR_STACK = 512, MAP_ERR_STACK_WAIT = 2048;
 
 struct StreamFrame {
   double pose[7];  // in: initial guess (transformAssociateToMap); out: optimised pose
@@ -88,7 +88,6 @@ struct StreamFrame {
   int err;
   const float4* in_ptr[2];        // input clouds (mapper staging buffer or caller's HBM)
   unsigned long long cand[2];     // map points in the queries' 27-cell neighbourhoods, per round
-  int ntile[2];                   // occupied 2 m query tiles of this round (k_tile_bin)
   unsigned long long vx_bytes;    // algorithmic bytes of this frame's re-VoxelGrid + cell index
   double wodom[7];  // the frame's odometry pose q_wodom (xyzw), t_wodom
   // q_wmap_wodom, t_wmap_wodom: the frame's initial guess (:206-207) is taken with it, and k_insert_bucket
@@ -195,13 +194,6 @@ struct MapperDev {
   int* stk_err;          // [B] error flags of the stack kernels (merged by k_stack_counts)
   float4* stk_pts;       // [B][2][max_in] scratch of the input-order stack filter
   int* stk_idx;          // [B][2][max_in]
-  // tile kNN (k_tile_bin / k_knn_tile): per (stream, map) the queries grouped by 2 m tile
-  uint2* tile_r;         // [B][2][max_in] a query's (tile table slot, rank in its tile), slot empty if none
-  uint2* tiles;          // [B][2][max_in] occupied 4 m tiles: (key | count << 18, first position in tile_q)
-  float4* tile_q;        // [B][2][max_in] queries in tile order: map-frame xyz + record index (int bits)
-  uint32_t* tile_tab;    // [B][2][tile_tab_n] the tile hash of stacks too large for the LDS table
-  uint32_t tile_tab_n = 0;
-  int tk_blk = 32;       // k_knn_tile workgroups per stream
   int knn_blk = CORR_BLK;  // k_knn workgroups per stream of the cell-split variant
   const FrameIn* fin = nullptr;  // [B] (page-locked host memory) the graph path's frame inputs
   unsigned long long* stk_ready = nullptr;  // the last stack launch done into this parity (k_stack_done)
@@ -387,7 +379,8 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
   voxel_segment(S, lds);
   if (PCL)  // PCL's summation order for the voxels of 3+ members (voxel_hot.h)
     vh_fixup<VX_THREADS>(VxSrc{I.p[m], I.n[m], nullptr}, I.n[m], S.out, S.hot, lds, VX_LDS_WORDS - 256,
-                         *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192), nullptr, err);
+                         *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192), nullptr, err, D.pdbg ? D.pdbg + 54 : nullptr,
+                         D.pdbg ? D.pdbg + 77 : nullptr);
 }
 
 // Few streams: the input-order stack VoxelGrid of a (stream, map) over stack_k workgroups.
@@ -1009,544 +1002,6 @@ __global__ void __launch_bounds__(CORR_THREADS) __attribute__((amdgpu_waves_per_
   if ((threadIdx.x & 63) == 0 && wc) atomicAdd(&F.cand[round], wc);
 }
 
-// ---------------------------------------------------------------------------------------
-// Tile kNN: the exact 5-NN of k_knn with the map reads cut by space instead of
-// by query.  k_tile_bin groups a (stream, map)'s queries by the 4 m tile of their 1 m cell (an
-// LDS hash) and writes them, transformed to the map frame, in tile order.  k_knn_tile runs one
-// wave per tile: the tile's 6 x 6 x 6 cells (every cell within one cell of any of its queries'
-// cells) are probed in one round, their points are staged in LDS in one round of independent
-// loads, grouped by cell, and then every query searches its own 27 cells in LDS, nearest cell
-// first with the gap bound, exactly as k_knn searched them in global memory.  The per-query
-// chain of dependent probe -> point loads becomes a chain of LDS reads, and one probe and one
-// point load serve all of a tile's queries (~40).
-// Same result: a query's 27 cells are staged whole.  Candidates at float distance >= 1 are not
-// offered: they cannot displace one below 1, and a query with fewer than 5 below 1 is rejected
-// (laser_mapping.cpp:557, :642) either way.  Ties: (d, submap index), as k_knn.
-// ---------------------------------------------------------------------------------------
-constexpr int TB_THREADS = 1024;
-constexpr uint32_t TB_LDS_T = 4096;   // LDS tile table: up to TB_LDS_T / 2 tiles per (stream, map)
-constexpr uint32_t TB_EMPTY = 0xFFFFFFFFu;
-constexpr uint32_t TB_KEY_BITS = 18, TB_KEY_MASK = (1u << TB_KEY_BITS) - 1;
-constexpr uint32_t TB_CNT_MAX = (1u << (32 - TB_KEY_BITS)) - 2;  // queries per tile (count field)
-constexpr int TK_E = 6, TK_CELLS = TK_E * TK_E * TK_E;  // cells per tile edge / per tile
-constexpr int TK_THREADS = 128, TK_WAVES = TK_THREADS / 64;
-constexpr int TK_STAGE = 512;  // map points staged per wave (larger tiles take the chunked scan)
-constexpr int TK_EXTRA = 128;  // cube-edge duplicate runs per tile (at most 127: one plane per axis)
-
-// LDS hand-off between the lanes of one wave (k_knn_tile: each wave owns its LDS): wave-scope
-// fences order the LDS accesses; a workgroup-scope fence would also wait for every outstanding
-// global load and store of the wave
-__device__ inline void tk_wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ inline uint32_t tb_hash(uint32_t k, uint32_t mask) {
-  uint32_t h = k * 0x9E3779B1u;
-  h ^= h >> 16;
-  return h & mask;
-}
-
-// the 4 m tile of a query's cell relative to the window origin (F.origin: 2 cells below the
-// 5 x 5 x 3 cube window); false if the cell is more than one cell outside the window (no map
-// point can lie within 1 m)
-__device__ inline bool tile_of(const StreamFrame& F, const float4& q, uint32_t* key) {
-  const float rx = floorf(q.x) - (float)F.origin[0], ry = floorf(q.y) - (float)F.origin[1],
-              rz = floorf(q.z) - (float)F.origin[2];
-  if (!(rx >= 0.f && rx < 254.f && ry >= 0.f && ry < 254.f && rz >= 0.f && rz < 154.f)) return false;
-  *key = ((uint32_t)rx >> 2) | (((uint32_t)ry >> 2) << 6) | (((uint32_t)rz >> 2) << 12);
-  return true;
-}
-
-// a query with no map point within reach: rejected (k_geom writes no factor)
-__device__ inline void knn_reject(MapperDev& D, int s, int ridx) {
-  if (D.sharded) {
-    NnRec& o = D.nn_send[D.q_off[s] + ridx];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      o.d[k] = INFINITY;
-      o.id[k] = 0x7FFFFFFF;
-      o.x[k] = o.y[k] = o.z[k] = 0.f;
-    }
-  } else {
-    D.knn_id[(size_t)s * 2 * D.max_in + ridx] = -1;
-  }
-}
-
-// insert every query's tile into tab (T entries); false when more than T / 2 tiles (the caller
-// retries with a larger table).  tile_r: per query (slot, rank in its tile), slot empty if none.
-__device__ __forceinline__ bool tile_bin_insert(const MapperDev& D, StreamFrame& F, int s, int m, const double* X,
-                                                uint32_t* tab, uint32_t T, uint32_t* ntiles) {
-  const int tid = threadIdx.x;
-  const int nq = m == 0 ? F.nc_stack : F.ns_stack;
-  const uint32_t mask = T - 1;
-  uint2* tr = D.tile_r + sm_index(s, m) * D.max_in;
-  for (uint32_t i = tid; i < T; i += TB_THREADS) tab[i] = TB_EMPTY;
-  if (tid == 0) *ntiles = 0;
-  __syncthreads();
-  const float4* stk = D.stack[m] + (size_t)s * D.max_in;
-  bool over = false, full = false;
-  for (int i = tid; i < nq; i += TB_THREADS) {
-    uint32_t key;
-    uint2 r = make_uint2(TB_EMPTY, 0u);
-    if (tile_of(F, to_map(X, stk[i]), &key)) {
-      uint32_t h = tb_hash(key, mask);
-      for (uint32_t probe = 0;; ++probe) {
-        if (probe == T) {  // cannot happen below T / 2 tiles; defensive
-          full = true;
-          break;
-        }
-        const uint32_t old = atomicCAS(&tab[h], TB_EMPTY, key | (1u << TB_KEY_BITS));
-        if (old == TB_EMPTY) {
-          r = make_uint2(h, 0u);
-          full |= atomicAdd(ntiles, 1u) >= T / 2;
-          break;
-        }
-        if ((old & TB_KEY_MASK) == key) {
-          const uint32_t rank = atomicAdd(&tab[h], 1u << TB_KEY_BITS) >> TB_KEY_BITS;
-          over |= rank >= TB_CNT_MAX;
-          r = make_uint2(h, rank);
-          break;
-        }
-        h = (h + 1) & mask;
-      }
-    }
-    tr[i] = r;
-  }
-  if (over) atomicOr(&F.err, MAP_ERR_TILE);
-  return !__syncthreads_or(full);
-}
-
-// the tile list and the queries in tile order (transformed, with their record index)
-__device__ __forceinline__ void tile_bin_emit(MapperDev& D, StreamFrame& F, int s, int m, const double* X,
-                                              uint32_t* tab, uint32_t T, uint32_t* ws) {
-  const int tid = threadIdx.x;
-  const int nq = m == 0 ? F.nc_stack : F.ns_stack, roff = m == 0 ? 0 : F.nc_stack;
-  const size_t sm = sm_index(s, m);
-  // occupied slots -> tile list; each slot's word becomes its tile's first position in tile_q
-  uint32_t ntl = 0, cnt = 0;
-  for (uint32_t h = tid; h < T; h += TB_THREADS) {
-    const uint32_t e = tab[h];
-    if (e != TB_EMPTY) {
-      ++ntl;
-      cnt += e >> TB_KEY_BITS;
-    }
-  }
-  uint32_t ntot, qtot;
-  uint32_t ti = ci_block_scan<TB_THREADS>(ntl, ws, &ntot);
-  uint32_t start = ci_block_scan<TB_THREADS>(cnt, ws, &qtot);
-  uint2* tl = D.tiles + sm * D.max_in;
-  for (uint32_t h = tid; h < T; h += TB_THREADS) {
-    const uint32_t e = tab[h];
-    if (e != TB_EMPTY) {
-      tl[ti++] = make_uint2(e, start);
-      tab[h] = start;
-      start += e >> TB_KEY_BITS;
-    }
-  }
-  __syncthreads();
-  const uint2* tr = D.tile_r + sm * D.max_in;
-  const float4* stk = D.stack[m] + (size_t)s * D.max_in;
-  float4* tq = D.tile_q + sm * D.max_in;
-  for (int i = tid; i < nq; i += TB_THREADS) {
-    const uint2 r = tr[i];
-    if (r.x != TB_EMPTY) {
-      const float4 q = to_map(X, stk[i]);
-      tq[tab[r.x] + r.y] = make_float4(q.x, q.y, q.z, __int_as_float(roff + i));
-    } else {
-      knn_reject(D, s, roff + i);
-    }
-  }
-  if (tid == 0) F.ntile[m] = (int)ntot;
-}
-
-// one workgroup per (stream, map); also starts the round's LM state (as k_knn did)
-__global__ void __launch_bounds__(TB_THREADS) k_tile_bin(MapperDev D, int round) {
-  __shared__ uint32_t tab[TB_LDS_T];
-  __shared__ uint32_t ws[TB_THREADS / 64 + 1];
-  __shared__ uint32_t ntiles;
-  const int s = D.s0 + (blockIdx.x >> 1), m = blockIdx.x & 1;
-  StreamFrame& F = D.fr[s];
-  if (!F.active) return;
-  double X[7];
-#pragma unroll
-  for (int i = 0; i < 7; ++i) X[i] = F.pose[i];
-  if (m == 0 && threadIdx.x < LM_SYNC_WORDS) D.lm_sync[((size_t)s * 2 + round) * LM_SYNC_WORDS + threadIdx.x] = 0;
-  if (m == 0 && threadIdx.x == 0) lm_init(F.lm[round], X, 4, F.optimize != 0);
-  if (!F.optimize) return;  // k_geom types every record 0
-  if (tile_bin_insert(D, F, s, m, X, tab, TB_LDS_T, &ntiles)) {
-    tile_bin_emit(D, F, s, m, X, tab, TB_LDS_T, ws);
-  } else {  // more tiles than the LDS table holds: a table in global memory sized by the queries
-    const int nq = m == 0 ? F.nc_stack : F.ns_stack;
-    uint32_t* gt = D.tile_tab + sm_index(s, m) * D.tile_tab_n;
-    const uint32_t T = ci_table_size((uint32_t)max(nq, 32));
-    tile_bin_insert(D, F, s, m, X, gt, T, &ntiles);
-    tile_bin_emit(D, F, s, m, X, gt, T, ws);
-  }
-}
-
-struct TkWave {  // one wave's LDS in k_knn_tile
-  float4 pts[TK_STAGE];  // staged map points, grouped by cell: xyz + tie-break key (int bits)
-  // per cell of the 6 x 6 x 6: its run in the cube the reference files it in, and where the
-  // cell's points (that run, then its cube-edge duplicates) start in pts
-  uint32_t cpos[TK_CELLS], ccnt[TK_CELLS], cstart[TK_CELLS + 1];
-  int ckey[TK_CELLS];  // submap index of the run's cube start (the key base)
-  uint32_t ctot[TK_CELLS];
-  // cube-edge duplicate runs: cell, arena position, count, key base, offset within the cell
-  uint32_t xcell[TK_EXTRA], xpos[TK_EXTRA], xcnt[TK_EXTRA], xoff[TK_EXTRA];
-  int xkey[TK_EXTRA];
-  uint32_t nx;
-};
-
-// the run of one 1 m cell in one window cube: count, arena position and submap key base
-__device__ inline uint32_t tk_cell(const WinMap& WM, const int* slot_of, const uint2* ct, const int* wc, int bi,
-                                   int bj, int bk, int ax, int ay, int az, uint32_t* pos, int* key0) {
-  const int wx = bi - wc[0], wy = bj - wc[1], wz = bk - wc[2];
-  if (wx < 0 || wx > 4 || wy < 0 || wy > 4 || wz < 0 || wz > 2) return 0;  // not in the submap
-  const int sl = slot_of[wx * 15 + wy * 3 + wz];
-  if (sl < 0 || WM.n[sl] == 0) return 0;
-  const uint32_t off = WM.off[sl];
-  const uint2 e = ci_find(ct + 4 * (size_t)off, WM.tsize[sl], (uint32_t)ax | ((uint32_t)ay << 6) | ((uint32_t)az << 12));
-  *pos = off + e.x;
-  *key0 = WM.sub[sl];
-  return e.y;
-}
-
-// staged point g (position in the tile's cell-grouped order) -> arena position and key base
-__device__ inline uint32_t tk_locate(const TkWave& V, uint32_t g, int* key0) {
-  int lo = 0, hi = TK_CELLS;  // the last cell starting at or before g (empty cells share starts)
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (V.cstart[mid] <= g) lo = mid;
-    else hi = mid;
-  }
-  const uint32_t r = g - V.cstart[lo];
-  if (r < V.ccnt[lo]) {
-    *key0 = V.ckey[lo];
-    return V.cpos[lo] + r;
-  }
-  for (uint32_t x = 0; x < V.nx; ++x)  // a cube-edge duplicate (rare)
-    if (V.xcell[x] == (uint32_t)lo && r >= V.xoff[x] && r < V.xoff[x] + V.xcnt[x]) {
-      *key0 = V.xkey[x];
-      return V.xpos[x] + (r - V.xoff[x]);
-    }
-  *key0 = 0;
-  return 0;  // unreachable
-}
-
-// stage points [pc, pc + np) into V.pts (one round of independent loads)
-__device__ inline void tk_stage(const MapperDev& D, TkWave& V, const float4* cp, uint32_t pc, uint32_t np, int lane) {
-  constexpr int U = TK_STAGE / 64;
-  uint32_t gpos[U];
-  int gkey[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) gpos[u] = lane + 64 * u < (int)np ? tk_locate(V, pc + lane + 64 * u, &gkey[u]) : 0u;
-  float4 gp[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-    if (lane + 64 * u < (int)np) gp[u] = cp[gpos[u]];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int k = lane + 64 * u;
-    if (k < (int)np) {
-      // sharded: submap position x ranks + rank keeps the key unique (k_knn)
-      const int kk = (gkey[u] + __float_as_int(gp[u].w)) * D.nrank + D.rank;
-      V.pts[k] = make_float4(gp[u].x, gp[u].y, gp[u].z, __int_as_float(kk));
-    }
-  }
-  tk_wave_sync();
-}
-
-// result of one query (T.pos: staged positions): the sharded candidate record, or the 5 arena
-// positions when accepted
-__device__ inline void tk_emit(MapperDev& D, const TkWave& V, int s, int ridx, const Near5& T, const float4* cp) {
-  int pos[5];
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    int k0;
-    pos[k] = T.pos[k] >= 0 ? (int)tk_locate(V, (uint32_t)T.pos[k], &k0) : -1;
-  }
-  if (D.sharded) {  // this rank's candidates; the 1 m test follows the merge (k_nn_merge)
-    NnRec& o = D.nn_send[D.q_off[s] + ridx];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      o.d[k] = T.d[k];
-      o.id[k] = T.id[k];
-      const float4 p = pos[k] >= 0 ? cp[pos[k]] : make_float4(0.f, 0.f, 0.f, 0.f);
-      o.x[k] = p.x;
-      o.y[k] = p.y;
-      o.z[k] = p.z;
-    }
-  } else {
-    const bool ok = T.d[4] < 1.0f;
-    const size_t rb = (size_t)s * 2 * D.max_in;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) D.knn_id[k * D.knn_stride + rb + ridx] = ok ? pos[k] : -1;
-  }
-}
-
-__device__ inline void near5_init(Near5& T) {
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    T.d[k] = INFINITY;
-    T.id[k] = 0x7FFFFFFF;
-    T.pos[k] = -1;
-  }
-}
-
-// phase timing of k_knn_tile (debug counters 50.., LOAM_PHASE_COUNTERS=1)
-#define TK_PHASE(k)                                              \
-  if (D.pdbg) {                                                  \
-    const unsigned long long tn_ = __builtin_readcyclecounter(); \
-    ph[k] += tn_ - tp;                                           \
-    tp = tn_;                                                    \
-  }
-
-__global__ void __launch_bounds__(TK_THREADS) k_knn_tile(MapperDev D, int round) {
-  __shared__ WinMap W[2];
-  __shared__ int slot_of[75];
-  __shared__ TkWave Vs[TK_WAVES];
-  int s, blk;
-  corr_block(D, &s, &blk);
-  StreamFrame& F = D.fr[s];
-  if (!F.active || !F.optimize) return;
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const int wc[3] = {F.center[0] - 2, F.center[1] - 2, F.center[2] - 1};
-  if (tid < 75) slot_of[tid] = -1;
-  __syncthreads();
-  if (tid < F.valid_num) {
-    const int cube = F.window[tid];
-    const int ci = cube % CW, cj = (cube / CW) % CH, ck = cube / (CW * CH);
-    slot_of[(ci - wc[0]) * 15 + (cj - wc[1]) * 3 + (ck - wc[2])] = tid;
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const uint2 cv = D.cube_tab[sm_index(s, m) * NCUBE + cube];
-      W[m].off[tid] = cv.x;
-      W[m].n[tid] = cv.y;
-      W[m].tsize[tid] = cv.y ? ci_table_size(cv.y) : 0u;
-      W[m].sub[tid] = F.sub_off[m][tid];
-    }
-  }
-  __syncthreads();
-  TkWave& V = Vs[wid];
-  const int nt0 = F.ntile[0], ntt = nt0 + F.ntile[1];
-  uint32_t ncand = 0;
-  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // phase cycles / counts (LOAM_PHASE_COUNTERS)
-  for (int t = blk * TK_WAVES + wid; t < ntt; t += D.tk_blk * TK_WAVES) {
-    unsigned long long tp = D.pdbg ? __builtin_readcyclecounter() : 0ull;
-    const int m = t < nt0 ? 0 : 1;
-    const size_t sm = sm_index(s, m);
-    const uint2 tile = D.tiles[sm * D.max_in + (m ? t - nt0 : t)];
-    const uint32_t key = tile.x & TB_KEY_MASK, Q = tile.x >> TB_KEY_BITS;
-    const float4* tq = D.tile_q + sm * D.max_in + tile.y;
-    // the first 64 queries, loaded ahead of the probes (one lane each)
-    float4 q = (uint32_t)lane < Q ? tq[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const int bx = F.origin[0] + 4 * (int)(key & 63u) - 1, by = F.origin[1] + 4 * (int)((key >> 6) & 63u) - 1,
-              bz = F.origin[2] + 4 * (int)(key >> 12) - 1;
-    const float4* cp = carena_base(D, s, m, F.arena_active[m]);
-    const uint2* ct = ctab_base(D, s, m, F.arena_active[m]);
-    const WinMap& WM = W[m];
-    TK_PHASE(0);
-    // 1. the 6 x 6 x 6 cells, four per lane: each cell's run in the cube the reference files
-    //    it in; a point at an exact negative multiple of 50 (v + 25) is filed in the cube below
-    //    (laser_mapping.cpp:747-756), at local coordinate 50 there: a second run (rare)
-    if (lane == 0) V.nx = 0;
-    bool any_edge = false;
-    {
-      constexpr int NC = (TK_CELLS + 63) / 64;  // cells per lane, probed together
-      const uint2* tb[NC];
-      uint32_t ky[NC], hh[NC], msk[NC], off[NC];
-      int sub[NC];
-      bool ok[NC];
-#pragma unroll
-      for (int i = 0; i < NC; ++i) {
-        const int c = lane + 64 * i;
-        const int ix = c % TK_E, iy = (c / TK_E) % TK_E, iz = c / (TK_E * TK_E);
-        const int cv[3] = {bx + ix, by + iy, bz + iz};
-        int cb[3], lc[3];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-          cb[a] = floor_div50(cv[a] + 25) + F.cen[a];
-          lc[a] = cv[a] - ci_corner(cb[a], F.cen[a]);
-          any_edge |= c < TK_CELLS && cv[a] + 25 < 0 && (cv[a] + 25) % 50 == 0;
-        }
-        const int wx = cb[0] - wc[0], wy = cb[1] - wc[1], wz = cb[2] - wc[2];
-        ok[i] = c < TK_CELLS && wx >= 0 && wx <= 4 && wy >= 0 && wy <= 4 && wz >= 0 && wz <= 2;
-        const int sl = ok[i] ? slot_of[wx * 15 + wy * 3 + wz] : -1;
-        ok[i] = sl >= 0 && WM.n[sl] > 0;
-        off[i] = ok[i] ? WM.off[sl] : 0u;
-        sub[i] = ok[i] ? WM.sub[sl] : 0;
-        msk[i] = ok[i] ? WM.tsize[sl] - 1 : 0u;
-        tb[i] = ct + 4 * (size_t)off[i];
-        ky[i] = (uint32_t)lc[0] | ((uint32_t)lc[1] << 6) | ((uint32_t)lc[2] << 12);
-        hh[i] = ci_hash(ky[i], msk[i]);
-      }
-      uint2 e[NC];
-#pragma unroll
-      for (int i = 0; i < NC; ++i) e[i] = ok[i] ? tb[i][hh[i]] : make_uint2(CI_EMPTY, 0u);
-#pragma unroll
-      for (int i = 0; i < NC; ++i) {
-        while (e[i].x != CI_EMPTY && (e[i].x & CI_KEY_MASK) != ky[i]) {  // collisions (a load factor <= 1/2)
-          hh[i] = (hh[i] + 1) & msk[i];
-          e[i] = tb[i][hh[i]];
-        }
-        const int c = lane + 64 * i;
-        if (c < TK_CELLS) {
-          const uint32_t n0 = e[i].x != CI_EMPTY ? e[i].x >> 18 : 0u;
-          V.cpos[c] = off[i] + e[i].y;
-          V.ccnt[c] = n0;
-          V.ckey[c] = sub[i];
-          V.ctot[c] = n0;
-        }
-      }
-    }
-    tk_wave_sync();
-    if (__ballot(any_edge)) {
-      for (int c = lane; c < TK_CELLS; c += 64) {
-        const int ix = c % TK_E, iy = (c / TK_E) % TK_E, iz = c / (TK_E * TK_E);
-        const int cv[3] = {bx + ix, by + iy, bz + iz};
-        int cb[3], lc[3], edge = 0;
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-          cb[a] = floor_div50(cv[a] + 25) + F.cen[a];
-          lc[a] = cv[a] - ci_corner(cb[a], F.cen[a]);
-          if (cv[a] + 25 < 0 && (cv[a] + 25) % 50 == 0) edge |= 1 << a;
-        }
-        for (int e = edge; e; e = (e - 1) & edge) {
-          int b2[3], l2[3];
-#pragma unroll
-          for (int a = 0; a < 3; ++a) {
-            b2[a] = (e >> a) & 1 ? cb[a] - 1 : cb[a];
-            l2[a] = (e >> a) & 1 ? 50 : lc[a];
-          }
-          uint32_t p2 = 0;
-          int k2 = 0;
-          const uint32_t c2 = tk_cell(WM, slot_of, ct, wc, b2[0], b2[1], b2[2], l2[0], l2[1], l2[2], &p2, &k2);
-          if (c2) {
-            const uint32_t x = atomicAdd(&V.nx, 1u);  // < TK_EXTRA
-            V.xcell[x] = (uint32_t)c;
-            V.xpos[x] = p2;
-            V.xcnt[x] = c2;
-            V.xkey[x] = k2;
-            V.xoff[x] = atomicAdd(&V.ctot[c], c2);
-          }
-        }
-      }
-      tk_wave_sync();
-    }
-    // 2. cell starts: four consecutive cells per lane (216 = 54 x 4)
-    uint32_t c4[4] = {0, 0, 0, 0}, sum = 0;
-    if (lane < TK_CELLS / 4) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        c4[i] = V.ctot[4 * lane + i];
-        sum += c4[i];
-      }
-    }
-    const uint32_t inc = wave_incl_scan_u(sum);
-    if (lane < TK_CELLS / 4) {
-      uint32_t a = inc - sum;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        V.cstart[4 * lane + i] = a;
-        a += c4[i];
-      }
-    }
-    const uint32_t P = __shfl(inc, 63, 64);
-    if (lane == 0) V.cstart[TK_CELLS] = P;
-    tk_wave_sync();
-    TK_PHASE(1);
-    if (D.pdbg) {
-      ph[5] += 1;
-      ph[6] += Q;
-      ph[7] += P;
-    }
-    const bool fits = P <= (uint32_t)TK_STAGE;
-    if (fits) tk_stage(D, V, cp, 0, P, lane);
-    TK_PHASE(2);
-    // 3. the queries, one lane each, 64 at a time
-    for (uint32_t qc = 0; qc < Q; qc += 64) {
-      if (qc > 0) q = qc + lane < Q ? tq[qc + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-      const bool act = qc + lane < Q;
-      Near5 T;
-      near5_init(T);
-      const int ox = (int)floorf(q.x) - bx, oy = (int)floorf(q.y) - by, oz = (int)floorf(q.z) - bz;
-      if (fits) {
-        // the query's 27 cells as 9 rows of 3 (dx = -1..1), contiguous in pts; rows nearest
-        // first, pruned by their gap (k_knn's search, in LDS); 4 candidates per step
-        const float fy = floorf(q.y), fz = floorf(q.z);
-        const float ly = q.y - fy, hy = (fy + 1.0f) - q.y;
-        const float lz = q.z - fz, hz = (fz + 1.0f) - q.z;
-        if (act) {
-          for (int r = 0; r < 9; ++r) {
-            // row order (dy, dz): centre, 4 faces, 4 edges
-            const int dy = r == 0 ? 0 : (r < 5 ? (r == 1 ? -1 : (r == 2 ? 1 : 0)) : (r & 1 ? -1 : 1));
-            const int dz = r == 0 ? 0 : (r < 5 ? (r == 3 ? -1 : (r == 4 ? 1 : 0)) : (r < 7 ? -1 : 1));
-            const int c = (ox - 1) + TK_E * (oy + dy) + TK_E * TK_E * (oz + dz);
-            const uint32_t s0 = V.cstart[c], s3 = V.cstart[c + 3];
-            ncand += s3 - s0;
-            const float gy = dy < 0 ? ly : (dy > 0 ? hy : 0.f);
-            const float gz = dz < 0 ? lz : (dz > 0 ? hz : 0.f);
-            const float bound = fminf(T.d[4], 1.0f) * 1.01f + 1e-6f;  // rounding margin
-            if (gy * gy + gz * gz > bound || s0 == s3) continue;
-            for (uint32_t k = s0; k < s3; k += 4) {
-              float4 p[4];
-              float d[4];
-#pragma unroll
-              for (int u = 0; u < 4; ++u) p[u] = V.pts[min(k + u, s3 - 1)];
-#pragma unroll
-              for (int u = 0; u < 4; ++u) d[u] = k + u < s3 ? fdist2(q.x, q.y, q.z, p[u].x, p[u].y, p[u].z) : INFINITY;
-              if (fminf(fminf(d[0], d[1]), fminf(d[2], d[3])) < 1.0f) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                  if (d[u] < 1.0f) near5_offer(T, d[u], __float_as_int(p[u].w), (int)(k + u));
-              }
-            }
-          }
-        }
-      } else {
-        // more points than the stage holds: every point of the tile, in passes
-        if (act)
-          for (int dz = -1; dz <= 1; ++dz)
-            for (int dy = -1; dy <= 1; ++dy) {
-              const int c = (ox - 1) + TK_E * (oy + dy) + TK_E * TK_E * (oz + dz);
-              ncand += V.cstart[c + 3] - V.cstart[c];
-            }
-        for (uint32_t pc = 0; pc < P; pc += TK_STAGE) {
-          const uint32_t np = min((uint32_t)TK_STAGE, P - pc);
-          tk_stage(D, V, cp, pc, np, lane);
-          if (act)
-            for (uint32_t k = 0; k < np; k += 4) {
-              float4 p[4];
-              float d[4];
-#pragma unroll
-              for (int u = 0; u < 4; ++u) p[u] = V.pts[min(k + u, np - 1)];
-#pragma unroll
-              for (int u = 0; u < 4; ++u) d[u] = k + u < np ? fdist2(q.x, q.y, q.z, p[u].x, p[u].y, p[u].z) : INFINITY;
-              if (fminf(fminf(d[0], d[1]), fminf(d[2], d[3])) < 1.0f) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                  if (d[u] < 1.0f) near5_offer(T, d[u], __float_as_int(p[u].w), (int)(pc + k + u));
-              }
-            }
-          tk_wave_sync();  // before the next pass overwrites them
-        }
-      }
-      TK_PHASE(3);
-      if (act) tk_emit(D, V, s, __float_as_int(q.w), T, cp);
-      TK_PHASE(4);
-    }
-    tk_wave_sync();  // the next tile rewrites this wave's LDS
-  }
-  unsigned long long wcn = ncand;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) wcn += __shfl_xor(wcn, o, 64);
-  if (lane == 0 && wcn) atomicAdd(&F.cand[round], wcn);
-  if (D.pdbg && lane == 0)
-    for (int k = 0; k < 8; ++k) atomicAdd(&D.pdbg[50 + k], ph[k]);
-}
-
 // sharded: merge every rank's 5 candidates into the exact 5-NN of the whole submap (each
 // rank's list is exact over its own points, so the union's 5 smallest (d, key) are the
 // unsharded result), then the 1 m acceptance (:557, :642).  Neighbours go to nn_xyz.
@@ -1988,7 +1443,8 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
         }
         if (!merged) voxel_segment(S, lds);
         vh_fixup<VX_THREADS>(VxSrc{ar + cv.x, (int)cv.y, D.ins_sorted + sm_index(s, m) * D.max_in + i0}, (int)n, ar,
-                             S.hot, lds, LW - 256, *reinterpret_cast<VxMisc*>(lds + LW - 192), tok, &F.err);
+                             S.hot, lds, LW - 256, *reinterpret_cast<VxMisc*>(lds + LW - 192), tok, &F.err,
+                             D.pdbg ? D.pdbg + 50 : nullptr, D.pdbg ? D.pdbg + 72 : nullptr);
       }
     } else {  // the whole std::sort emulated in global memory (voxel_pcl.h)
       VxPclOut O;
@@ -2279,7 +1735,6 @@ inline std::string map_err_text(int e) {
   add(MAP_ERR_LIVE, "live map larger than the arena's compaction bound");
   add(MAP_ERR_SORT, "PCL-order VoxelGrid input larger than its sort lists / scratch");
   add(MAP_ERR_STACK, "split stack VoxelGrid: a range has more voxels than its LDS groups");
-  add(MAP_ERR_TILE, "more than 2046 queries in one 2 m tile (unfiltered stack)");
   add(MAP_ERR_STACK_WAIT, "the frame's stack VoxelGrid did not finish in time (device wait)");
   return m + " (flags " + std::to_string(e) + ")";
 }
@@ -2335,9 +1790,8 @@ struct loam_mapper {
   // the window that receive points; a write past the capacity is reported (err flags)
   uint32_t compact_at = 0;
   int lm_G = 0;  // workgroups per stream of k_lm_round (0: two-kernel path k_lm_eval / k_lm_step)
-  int knn_lanes = 1;  // lanes per query of k_knn (1, or 2 for handles of <= 4 streams)
-  int knn_tile = 0;   // LOAM_KNN_TILE=1: the tile kNN (k_tile_bin + k_knn_tile) instead of k_knn
-  int knn_cs = 0;     // lanes per query of k_knn's cell split (8 for <= 4 streams; LOAM_KNN_CS)
+  int knn_cs = 0;     // k_knn: 8 lanes per query splitting the cells (handles of <= 4 streams), else 0
+                      // (one lane per query)
   loam_comm* comm = nullptr;  // sharded mode (loam_mapper_create_sharded)
   PinnedArray<int> q_off;     // [B + 1] query offsets of the sharded kNN exchange
   int* d_q_off = nullptr;
@@ -2355,24 +1809,12 @@ struct loam_mapper {
   PinnedArray<StreamFrame> hfo[2];   // [stack parity] the records after that parity's frame
   PinnedArray<FrameIn> fin[2];       // [stack parity] the graph path's frame inputs (k_frame_prep)
   const FrameIn* fin_dev[2] = {nullptr, nullptr};
-  FrameIn* d_fin[2] = {nullptr, nullptr};  // LOAM_FIN_DEVICE=1 (measurement): FrameIn uploaded to HBM
-  int fin_device = 0, rec_copy_out = 0;    // LOAM_REC_COPY_OUT=1 (measurement): records D2H after the graph
   hipEvent_t ev_fr[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [parity] frame start / records back (timed)
-  hipEvent_t ev_done[2] = {nullptr, nullptr};  // [parity] records back (untimed: what a queued frame records)
-  // the graph path's records and done word, written by k_revox's last workgroup (LOAM_FRAME_FLAG=0: a D2H
-  // copy and an event instead)
-  int frame_flag = 1;
-  int stack_event = 0;  // LOAM_STACK_EVENT=1: graph frames wait for their stacks with an event
-  // the graph path's kernel sequence launched directly instead of as a hipGraph: frames queued
-  // behind the one in flight (-1, the default; the graph launch costs 14 against 6 us between
-  // two frames at one stream, rocprofv3 trace), always (LOAM_GRAPH_DIRECT=1) or never (0)
-  int graph_direct = -1;
   unsigned long long stack_seq = 0;
   unsigned long long* d_stk_ready = nullptr;  // [2 parities]
   PinnedArray<unsigned long long> done;  // [2 parities]
   unsigned long long* done_dev = nullptr;
   StreamFrame* hfo_dev[2] = {nullptr, nullptr};
-  int chain = 1;             // LOAM_CHAIN=0: never queue a frame behind another
   uint32_t grow_max = 0;     // largest arena growth of one frame seen (compaction foresight)
   std::vector<std::array<uint32_t, 2>> last_tail;
   hipEvent_t ev_stack = nullptr;   // after the last stack launch (on st2)
@@ -2425,8 +1867,6 @@ void free_all(loam_mapper* h) {
   for (auto& ep : h->ev_fr)
     for (auto& e : ep)
       if (e) (void)hipEventDestroy(e);
-  for (auto& e : h->ev_done)
-    if (e) (void)hipEventDestroy(e);
   h->ev_pool.clear();
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
@@ -2533,12 +1973,9 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     }
   }
   D.pcl_order = h->P.exact_voxel_order ? 1 : 0;
-  {  // few streams: the stack VoxelGrid over 8 workgroups per (stream, map) (k_stack_part)
-    const char* kenv = std::getenv("LOAM_STACK_K");  // measurement override
-    int k = (n_streams <= 4 && !D.pcl_order) ? 8 : 0;
-    if (kenv) k = std::atoi(kenv);
-    D.stack_k = D.pcl_order ? 0 : std::max(0, std::min(STACK_K_MAX, k));
-  }
+  // few streams: the input-order stack VoxelGrid over 8 workgroups per (stream, map)
+  // (k_stack_part; 4 / 6 / 12 ranges measured slower)
+  D.stack_k = (n_streams <= 4 && !D.pcl_order) ? 8 : 0;
   D.leaf[0] = (float)h->P.mapping_line_resolution;
   D.leaf[1] = (float)h->P.mapping_plane_resolution;
   const size_t B = n_streams;
@@ -2564,37 +2001,18 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   for (auto& ep : h->ev_fr)
     for (auto& e : ep)
       if (hipEventCreate(&e) != hipSuccess) return fail(LOAM_ERR_HIP);
-  for (auto& e : h->ev_done)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(LOAM_ERR_HIP);
   {
-    const char* cenv = std::getenv("LOAM_CHAIN");
-    h->chain = (cenv && cenv[0] == '0') ? 0 : 1;
     const char* denv = std::getenv("LOAM_DEFER_EVERY");  // tests: force the deferral path
     D.defer_every = denv ? std::max(0, std::atoi(denv)) : 0;
   }
   // graphs pay off where launch gaps are the cost (B = 1: 0.750 -> 0.733 ms per frame); with
   // two handles of 64 streams, graph launches measured 20% slower (375k vs 470k iterations/s)
   h->use_graph = n_streams <= 4 ? 1 : 0;
-  // 2 lanes per query when few streams leave the chip idle (B = 1: 0.254 -> 0.190 ms of
-  // correspondence per frame); 1 lane once the streams fill it (B = 64: 2 lanes are 1.4x slower)
-  h->knn_lanes = n_streams <= 4 ? 2 : 1;
-  {
-    // the tile kNN is exact and tested, but measured slower than k_knn: opt-in
-    const char* tenv = std::getenv("LOAM_KNN_TILE");
-    h->knn_tile = (tenv && tenv[0] == '1') ? 1 : 0;
-    // tile waves per stream: few streams leave the chip to one stream's ~1.5k tiles
-    D.tk_blk = n_streams <= 4 ? 256 : 16;  // few streams: about one tile per wave
-    const char* benv = std::getenv("LOAM_TK_BLK");  // measurement override
-    if (benv && std::atoi(benv) > 0) D.tk_blk = std::atoi(benv);
-    // cell split at few streams: B = 1 correspondence search 67.8 -> 35.6 us per round (8 lanes;
-    // 4 lanes 43.4, 16 lanes 41.3); at B = 128 it costs 1.2x (more lanes idle on pruned cells)
-    const char* cenv = std::getenv("LOAM_KNN_CS");  // measurement override (0: point split)
-    const int cs = cenv ? std::atoi(cenv) : (n_streams <= 4 ? 8 : 0);
-    h->knn_cs = (cs == 4 || cs == 8 || cs == 16) ? cs : 0;
-    D.knn_blk = n_streams <= 4 ? 4 * CORR_BLK : CORR_BLK;
-    const char* kenv = std::getenv("LOAM_KNN_BLK");  // measurement override
-    if (kenv && std::atoi(kenv) > 0) D.knn_blk = std::atoi(kenv);
-  }
+  // cell split at few streams: B = 1 correspondence search 67.8 -> 35.6 us per round (8 lanes;
+  // 4 lanes 43.4, 16 lanes 41.3, 2 lanes per query splitting the points 0.19 ms per frame); at
+  // B = 128 it costs 1.2x (more lanes idle on pruned cells): one lane per query there
+  h->knn_cs = n_streams <= 4 ? 8 : 0;
+  D.knn_blk = n_streams <= 4 ? 4 * CORR_BLK : CORR_BLK;
   ALLOC(D.fr, B);
   for (int m = 0; m < 2; ++m) {
     ALLOC(D.in_pts[m], B * D.max_in);
@@ -2651,11 +2069,6 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   ALLOC(h->d_stk_ready, 2);
   ALLOC(D.stk_pts, B * 2 * (size_t)D.max_in);
   ALLOC(D.stk_idx, B * 2 * (size_t)D.max_in);
-  ALLOC(D.tile_r, B * 2 * (size_t)D.max_in);
-  ALLOC(D.tiles, B * 2 * (size_t)D.max_in);
-  ALLOC(D.tile_q, B * 2 * (size_t)D.max_in);
-  D.tile_tab_n = ci_table_size((uint32_t)std::max(D.max_in, 32));
-  ALLOC(D.tile_tab, B * 2 * (size_t)D.tile_tab_n);
   ALLOC(D.partials, B * (size_t)D.max_chunks * LM_NACC);
   ALLOC(D.lm_sync, B * 2 * LM_SYNC_WORDS);
   ALLOC(D.lm_xpub, B * 2 * 8);
@@ -2699,10 +2112,6 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     h->fin_dev[p] = reinterpret_cast<const FrameIn*>(dp);
     if (hipHostGetDevicePointer(&dp, h->hfo[p].data(), 0) != hipSuccess) return fail(LOAM_ERR_HIP);
     h->hfo_dev[p] = reinterpret_cast<StreamFrame*>(dp);
-    void* q = nullptr;
-    if (hipMalloc(&q, sizeof(FrameIn) * B) != hipSuccess) return fail(LOAM_ERR_HIP);
-    h->allocs.push_back(q);
-    h->d_fin[p] = reinterpret_cast<FrameIn*>(q);
   }
   {
     void* dp = nullptr;
@@ -2710,18 +2119,6 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
         hipHostGetDevicePointer(&dp, h->done.data(), 0) != hipSuccess)
       return fail(LOAM_ERR_HIP);
     h->done_dev = reinterpret_cast<unsigned long long*>(dp);
-    const char* fenv = std::getenv("LOAM_FRAME_FLAG");
-    h->frame_flag = (fenv && fenv[0] == '0') ? 0 : 1;
-    const char* senv = std::getenv("LOAM_STACK_EVENT");
-    h->stack_event = (senv && senv[0] == '1') ? 1 : 0;
-    const char* genv2 = std::getenv("LOAM_GRAPH_DIRECT");
-    if (genv2 && (genv2[0] == '0' || genv2[0] == '1')) h->graph_direct = genv2[0] - '0';
-  }
-  {
-    const char* e1 = std::getenv("LOAM_FIN_DEVICE");
-    const char* e2 = std::getenv("LOAM_REC_COPY_OUT");
-    h->fin_device = (e1 && e1[0] == '1') ? 1 : 0;
-    h->rec_copy_out = (e2 && e2[0] == '1') ? 1 : 0;
   }
   h->hs.assign(B, HostStream{});
   h->last_tail.assign(B, std::array<uint32_t, 2>{0u, 0u});
@@ -2988,28 +2385,15 @@ static void capture_frame(loam_mapper* h, const MapperDev& D, int fpar, hipStrea
   const int B = h->B;
   k_frame_prep<<<B, 128, 0, st>>>(D);
   for (int round = 0; round < 2; ++round) {
-    if (h->knn_tile) {
-      k_tile_bin<<<B * 2, TB_THREADS, 0, st>>>(D, round);
-      k_knn_tile<<<B * D.tk_blk, TK_THREADS, 0, st>>>(D, round);
-    } else if (h->knn_cs == 4) {
-      k_knn<4, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round);
-    } else if (h->knn_cs == 8) {
-      k_knn<8, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round);
-    } else if (h->knn_cs == 16) {
-      k_knn<16, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round);
-    } else if (h->knn_lanes == 2) {
-      k_knn<2><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
-    } else {
-      k_knn<1><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
-    }
+    if (h->knn_cs) k_knn<8, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round);
+    else k_knn<1><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
     k_geom<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
     k_lm_round<<<lm_padded(B) * h->lm_G, LM_THREADS, 0, st>>>(D, round, h->lm_G);
   }
   k_insert_bucket<<<B * 2, VX_THREADS, 0, st>>>(D);
   if (D.pcl_order) k_revox<true><<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D);
   else k_revox<false><<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D);
-  if (h->frame_flag) k_frame_out<<<1, 256, 0, st>>>(D, h->hfo_dev[fpar], h->done_dev + fpar);
-  else if (!h->rec_copy_out) (void)hipMemcpyAsync(h->hfo[fpar].data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st);
+  k_frame_out<<<1, 256, 0, st>>>(D, h->hfo_dev[fpar], h->done_dev + fpar);
 }
 
 // Enqueue one solveMapping of every stream with an input (the work of loam_mapper_solve up to
@@ -3025,7 +2409,7 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
   D.sin = h->sin_buf[fpar];
   D.stk_n = h->stk_n_buf[fpar];
   D.stk_err = h->stk_err_buf[fpar];
-  D.fin = h->fin_device ? h->d_fin[fpar] : h->fin_dev[fpar];
+  D.fin = h->fin_dev[fpar];
   D.stk_ready = h->d_stk_ready + fpar;
   for (int m = 0; m < 2; ++m) D.stack[m] = h->stack_buf[fpar][m];
   R = FrameRec{};
@@ -3112,7 +2496,7 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
   // frames rarely meet a due compaction (they would be deferred); the moves are verbatim, the
   // results do not depend on when they happen.
   uint32_t due_at = h->compact_at;
-  if (h->chain && chain_capable(h)) {
+  if (chain_capable(h)) {
     const uint64_t ahead = 3ull * h->grow_max + 4096ull;
     due_at = (uint32_t)std::max<uint64_t>(h->compact_at / 2, h->compact_at > ahead ? h->compact_at - ahead : 0);
   }
@@ -3126,7 +2510,9 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
   R.graph = graph;
   if (graph) {
     hipGraphExec_t& ge = h->gexec[h->parity][fpar];
-    const bool direct = h->graph_direct < 0 ? chained : h->graph_direct == 1;
+    // a frame queued behind the one in flight is launched kernel by kernel: a graph launch costs
+    // 14 against 6 us between two frames at one stream (rocprofv3 trace); the others as the graph
+    const bool direct = chained;
     if (!ge && !direct) {
       hipGraph_t gr = nullptr;
       LOAM_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
@@ -3146,22 +2532,16 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
       LOAM_HIP(hipGetLastError());
     }
     // the frame's stacks: waited for by k_frame_prep on the device (stack_seq)
-    if (h->stack_event && hipEventQuery(h->ev_stack) != hipSuccess) LOAM_HIP(hipStreamWaitEvent(st, h->ev_stack, 0));
     // a queued frame is not timed: its start is its predecessor's end, and the timing markers
     // between two graph launches would cost the device time
     if (!chained) LOAM_HIP(hipEventRecord(h->ev_fr[fpar][0], st));
-    if (h->fin_device)
-      LOAM_HIP(hipMemcpyAsync(h->d_fin[fpar], h->fin[fpar].data(), sizeof(FrameIn) * B, hipMemcpyHostToDevice, st));
     if (direct) {
       capture_frame(h, D, fpar, st);
       LOAM_HIP(hipGetLastError());
     } else {
       LOAM_HIP(hipGraphLaunch(ge, st));
     }
-    if (h->rec_copy_out)
-      LOAM_HIP(hipMemcpyAsync(h->hfo[fpar].data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
     if (!chained) LOAM_HIP(hipEventRecord(h->ev_fr[fpar][1], st));
-    else if (!h->frame_flag) LOAM_HIP(hipEventRecord(h->ev_done[fpar], st));
     R.epoch = h->frame_counter;
     h->spar ^= 1;  // the next frame's stacks go to the other buffers
     return LOAM_OK;
@@ -3213,20 +2593,8 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
     LOAM_HIP(hipMemcpyAsync(h->d_q_off, qo, sizeof(int) * (B + 1), hipMemcpyHostToDevice, st));
   }
   for (int round = 0; round < 2; ++round) {
-    if (h->knn_tile) {
-      LAUNCH(FAM_CORR, k_tile_bin<<<B * 2, TB_THREADS, 0, st>>>(D, round));
-      LAUNCH(FAM_CORR, k_knn_tile<<<B * D.tk_blk, TK_THREADS, 0, st>>>(D, round));
-    } else if (h->knn_cs == 4) {
-      LAUNCH(FAM_CORR, (k_knn<4, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round)));
-    } else if (h->knn_cs == 8) {
-      LAUNCH(FAM_CORR, (k_knn<8, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round)));
-    } else if (h->knn_cs == 16) {
-      LAUNCH(FAM_CORR, (k_knn<16, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round)));
-    } else if (h->knn_lanes == 2) {
-      LAUNCH(FAM_CORR, k_knn<2><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round));
-    } else {
-      LAUNCH(FAM_CORR, k_knn<1><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round));
-    }
+    if (h->knn_cs) LAUNCH(FAM_CORR, (k_knn<8, true><<<B * D.knn_blk, CORR_THREADS, 0, st>>>(D, round)));
+    else LAUNCH(FAM_CORR, k_knn<1><<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round));
     if (D.sharded) {  // every rank's candidates -> the exact 5-NN on every rank
       if (multi)
         TRY(comm_allgather(h->comm, D.nn_send, const_cast<NnRec*>(D.nn_recv), (int64_t)(q_tot * sizeof(NnRec)), st));
@@ -3289,10 +2657,8 @@ static int32_t wait_done(loam_mapper* h, const FrameRec& R) {
 static int32_t mapper_finish_rec(loam_mapper* h, const FrameRec& R, bool replay) {
   const int B = h->B;
   float ms_total = 0, ms_opt = 0;  // (0 for a queued frame: not timed)
-  if (R.chained && h->frame_flag) {
+  if (R.chained) {
     TRY(wait_done(h, R));
-  } else if (R.chained) {
-    LOAM_HIP(hipEventSynchronize(h->ev_done[R.fpar]));
   } else {
     LOAM_HIP(hipEventSynchronize(h->ev_fr[R.fpar][1]));
     LOAM_HIP(hipEventElapsedTime(&ms_total, h->ev_fr[R.fpar][0], h->ev_fr[R.fpar][1]));
@@ -3497,7 +2863,7 @@ static bool chain_capable(const loam_mapper* h) {
 }
 
 static bool chain_ok(const loam_mapper* h) {
-  if (!h->chain || !chain_capable(h)) return false;
+  if (!chain_capable(h)) return false;
   for (const FrameRec& Q : h->q)
     if (Q.has_deferred || Q.pending) return false;
   const int dims[3] = {CW, CH, CD};

@@ -593,8 +593,6 @@ int32_t loam_odometry_create(const loam_params* p, int32_t device, int32_t n_str
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_od_lm, OD_LM_THREADS, 0) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess)
       h->G = std::max(1, std::min(OD_PBLK, std::min(4, std::min(occ, 1) * cus / n_streams)));
-    const char* genv = std::getenv("LOAM_OD_LM_G");  // measurement override
-    if (genv && std::atoi(genv) > 0) h->G = std::min(OD_PBLK, std::atoi(genv));
   }
   h->hf.assign(B, OdomFrame{});
   h->hs.assign(B, OdomHost{});

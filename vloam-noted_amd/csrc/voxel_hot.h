@@ -58,6 +58,7 @@ struct VhCtl {
   int nroot, root_take;      // pending wave subtrees, the next one to claim
   int dup;
   int err;
+  int heap_el;  // elements heap-sorted literally (diagnostics)
   uint32_t ws[VX_WAVES + 1];  // block-scan scratch of the workgroup partition
 };
 
@@ -114,10 +115,11 @@ __device__ inline void vh_median(uint32_t* E, int lo, int hi) {
   E[m] = t;
 }
 
-// One segment [lo, hi) (17 <= m <= VH_BIG) partitioned by one wave.  Returns the cut, or -1 when
-// fewer than two hot elements lie in it (nothing to do below it).  Every lane returns the same.
-__device__ inline int vh_partition_wave(uint32_t* E, uint16_t* Bs, int lo, int hi) {
-  constexpr int U = VH_BIG / 64;
+// One segment [lo, hi) (17 <= m <= 64 U + 1) partitioned by one wave, its positions lo + 1 ..
+// held U per lane.  Returns the cut, or -1 when fewer than two hot elements lie in it (nothing to
+// do below it).  Every lane returns the same.
+template <int U>
+__device__ inline int vh_partition_wave_u(uint32_t* E, uint16_t* Bs, int lo, int hi) {
   const int lane = threadIdx.x & 63;
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   if (lane == 0) vh_median(E, lo, hi);
@@ -179,10 +181,96 @@ __device__ inline int vh_partition_wave(uint32_t* E, uint16_t* Bs, int lo, int h
   ss_wave_fence();
   return __builtin_amdgcn_readfirstlane(min(lK, rS));
 }
+__device__ inline int vh_partition_wave(uint32_t* E, uint16_t* Bs, int lo, int hi) {
+  static_assert(VH_BIG == 1024, "size classes");
+  const int m = hi - lo;  // positions lo + 1 .. hi - 1: m - 1 of them
+  if (m <= 65) return vh_partition_wave_u<1>(E, Bs, lo, hi);
+  if (m <= 129) return vh_partition_wave_u<2>(E, Bs, lo, hi);
+  if (m <= 257) return vh_partition_wave_u<4>(E, Bs, lo, hi);
+  if (m <= 513) return vh_partition_wave_u<8>(E, Bs, lo, hi);
+  return vh_partition_wave_u<16>(E, Bs, lo, hi);
+}
+
+// libstdc++'s __partial_sort(first, last, last) (= __make_heap + __sort_heap) on E[lo, hi), one
+// whole wave, the same permutation as the one-lane restatement ss_heap_sort:
+//   * __make_heap calls __adjust_heap(parent) for parent = (len - 2) / 2 down to 0; one call only
+//     touches the parent's subtree, so the parents of one depth (disjoint subtrees, all after
+//     the deeper ones) run on separate lanes;
+//   * each __pop_heap's hole descends to a leaf along the larger children (the right one unless
+//     right < left): the wave loads the 5 levels below the hole at once (62 lanes), decides every
+//     pair with one shuffle and one ballot, and follows the path in scalar registers; the path's
+//     values then shift up one place and __push_heap's value lands below the lowest ancestor not
+//     less than it (the path is non-increasing downwards, so that is one ballot): one write round.
+__device__ inline void vh_heap_sort_wave(uint32_t* E, int lo, int hi) {
+  const int lane = threadIdx.x & 63;
+  const VhLess less;
+  const int len = hi - lo;
+  if (len < 2) return;
+  {  // __make_heap
+    const int pmax = (len - 2) / 2;
+    for (int d = 31 - __clz(pmax + 1); d >= 0; --d) {
+      const int a = (1 << d) - 1, b = min(pmax, (1 << (d + 1)) - 2);
+      for (int p = b - lane; p >= a; p -= 64) ss_adjust_heap(E, lo, p, len, E[lo + p], less);
+      ss_wave_fence();
+    }
+  }
+  // lane l < 62 of a look-ahead: depth j = 1 .. 5 below the hole, index t in that depth
+  const int lj = 31 - __clz(lane + 2), lt = lane + 2 - (1 << lj);
+  for (int last = hi - 1; last > lo; --last) {  // __sort_heap
+    const int n = last - lo;
+    const uint32_t v = E[last], top = E[lo];
+    const int lim = (n - 1) / 2;
+    int h = 0, k = 0;   // hole; path length
+    uint32_t pv = 0;    // lane j < k: the value of path node j + 1 (the j-th child moved up)
+    int pp = 0;         //             its position
+    while (h < lim) {
+      const int node = ((h + 1) << lj) - 1 + lt;
+      const uint32_t x = (lane < 62 && node < n) ? E[lo + node] : 0u;
+      const uint32_t xr = __shfl_down(x, 1, 64);  // the right sibling (left children: t even)
+      const uint64_t rw = __ballot(!less(xr, x));
+      int tt = 0;
+#pragma unroll
+      for (int jj = 0; jj < 5; ++jj) {
+        if (h >= lim) break;
+        const int ll = (1 << (jj + 1)) - 2 + 2 * tt;  // lane of the left child
+        const int dir = (int)((rw >> ll) & 1ull);
+        const int child = 2 * h + 1 + dir;
+        const uint32_t cv = __builtin_amdgcn_readlane(x, ll + dir);
+        if (lane == k) {
+          pv = cv;
+          pp = child;
+        }
+        tt = 2 * tt + dir;
+        h = child;
+        ++k;
+      }
+    }
+    if ((n & 1) == 0 && h == (n - 2) / 2) {  // one child left
+      const int child = 2 * h + 1;
+      const uint32_t cv = E[lo + child];
+      if (lane == k) {
+        pv = cv;
+        pp = child;
+      }
+      h = child;
+      ++k;
+    }
+    // __push_heap: v rises while its parent is less; path node j holds pv of lane j - 1 after the
+    // shift, so the hole stops at q = k - #{j < k : pv_j < v}
+    const int q = k - __popcll(__ballot(lane < k && less(pv, v)));
+    const int hp = __shfl_up(pp, 1, 64);  // position of path node j (lane j): node 0 is the root
+    const int hj = lane == 0 ? 0 : hp;
+    ss_wave_fence();  // every read of this pop before its writes
+    if (lane < q) E[lo + hj] = pv;
+    if (lane == q) E[lo + hj] = v;
+    if (lane == 0) E[last] = top;
+    ss_wave_fence();
+  }
+}
 
 // A depth-limit segment on one wave: heap-sorted literally when two members of one hot voxel lie
 // in it (their order is the heap's), else left as it is.  kb: the wave's 64-word key buffer.
-__device__ inline void vh_depth_limit_wave(uint32_t* E, int lo, int hi, uint32_t* kb) {
+__device__ inline void vh_depth_limit_wave(uint32_t* E, int lo, int hi, uint32_t* kb, int* heap_el) {
   const int lane = threadIdx.x & 63;
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   int nh = 0;
@@ -208,12 +296,12 @@ __device__ inline void vh_depth_limit_wave(uint32_t* E, int lo, int hi, uint32_t
   }
   if (!dup) return;
   ss_wave_fence();
-  if (lane == 0) ss_heap_sort(E, lo, hi, VhLess{});
-  ss_wave_fence();
+  if (lane == 0) atomicAdd(heap_el, hi - lo);
+  vh_heap_sort_wave(E, lo, hi);
 }
 
 // The subtree below one pending segment, one wave, no barriers
-__device__ inline void vh_wave_subtree(uint32_t* E, uint16_t* Bs, uint32_t root, uint32_t* wa) {
+__device__ inline void vh_wave_subtree(uint32_t* E, uint16_t* Bs, uint32_t root, uint32_t* wa, int* heap_el) {
   const int lane = threadIdx.x & 63;
   uint32_t* stk = wa;
   uint32_t* kb = wa + VH_LIFO;
@@ -225,7 +313,7 @@ __device__ inline void vh_wave_subtree(uint32_t* E, uint16_t* Bs, uint32_t root,
     bool next = true;  // take the next pending entry
     if (len > SS_THRESHOLD) {
       if (d == 0) {
-        vh_depth_limit_wave(E, lo, hi, kb);
+        vh_depth_limit_wave(E, lo, hi, kb, heap_el);
       } else {
         const int cut = vh_partition_wave(E, Bs, lo, hi);
         if (cut >= 0) {
@@ -264,7 +352,7 @@ __device__ inline void vh_drain(const VhLds& L) {
     if (lane == 0) k = atomicAdd(&L.C->root_take, 1);
     k = __builtin_amdgcn_readfirstlane(k);
     if (k >= nroot) break;
-    vh_wave_subtree(L.E, L.Bs, L.roots[k], wa);
+    vh_wave_subtree(L.E, L.Bs, L.roots[k], wa, &L.C->heap_el);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -277,10 +365,9 @@ __device__ inline void vh_drain(const VhLds& L) {
 // One segment [lo, hi) (m > VH_BIG) partitioned by the workgroup.  par: the segment's parity
 // (its VhCtl slot; the other slot is reset here for the next segment).  Returns the cut, or -1
 // when fewer than two hot elements lie in it.  Uniform.
-template <int NT>
-__device__ inline int vh_partition_wg(const VhLds& L, int lo, int hi, int par) {
+template <int NT, int CH>
+__device__ inline int vh_partition_wg_c(const VhLds& L, int lo, int hi, int par) {
   constexpr int NW = NT / 64;
-  constexpr int CH = VH_MAX_N / NT;
   static_assert(CH <= 32, "chunk masks in one word");
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   uint32_t* E = L.E;
@@ -373,6 +460,16 @@ __device__ inline int vh_partition_wg(const VhLds& L, int lo, int hi, int par) {
   __syncthreads();
   return C->cut[par];
 }
+template <int NT>
+__device__ inline int vh_partition_wg(const VhLds& L, int lo, int hi, int par) {
+  static_assert(VH_MAX_N / NT <= 32, "chunk masks in one word");
+  const int c = (hi - lo - 1 + NT - 1) / NT;  // positions per thread
+  if (c <= 2) return vh_partition_wg_c<NT, 2>(L, lo, hi, par);
+  if (c <= 4) return vh_partition_wg_c<NT, 4>(L, lo, hi, par);
+  if (c <= 8) return vh_partition_wg_c<NT, 8>(L, lo, hi, par);
+  if (c <= 16) return vh_partition_wg_c<NT, 16>(L, lo, hi, par);
+  return vh_partition_wg_c<NT, VH_MAX_N / NT>(L, lo, hi, par);
+}
 
 // A depth-limit segment of the workgroup: the dup check on a bitmap of slots (in the Bs area,
 // free between partitions), then, if two members of one hot voxel lie in it, the literal heap sort
@@ -394,15 +491,21 @@ __device__ inline void vh_depth_limit_wg(const VhLds& L, int n, int lo, int hi) 
   }
   if (__ballot(d) != 0ull && (tid & 63) == 0) L.C->dup = 1;
   __syncthreads();
-  if (L.C->dup && tid == 0) ss_heap_sort(L.E, lo, hi, VhLess{});
+  if (L.C->dup && tid < 64) {
+    if (tid == 0) L.C->heap_el += hi - lo;
+    vh_heap_sort_wave(L.E, lo, hi);
+  }
   __syncthreads();
 }
 
 // Phase 2: the pruned emulation over the n points (n <= VH_MAX_N; all NT threads), then
 // H.fpos[i] for every hot point i.  *err |= VH_ERR_ROOTS on a list overflow (cannot happen).
+// prof (optional, diagnostics): [0] elements heap-sorted literally; [1..4] cycles of the setup, the
+// workgroup partitions (and depth-limit segments), the wave subtrees, the positions
 template <int NT>
-__device__ inline void vh_sort(uint32_t* lds, int n, const VxHot& H, int* err) {
+__device__ inline void vh_sort(uint32_t* lds, int n, const VxHot& H, int* err, unsigned long long* prof = nullptr) {
   const int tid = threadIdx.x;
+  unsigned long long tp = __builtin_readcyclecounter(), t_drain = 0;
   const VhLds L = vh_layout<NT>(lds, n);
   VhCtl* C = L.C;
   for (int i = tid; i < n; i += NT) {
@@ -414,6 +517,7 @@ __device__ inline void vh_sort(uint32_t* lds, int n, const VxHot& H, int* err) {
     C->nbig[0] = C->nbig[1] = 0;
     C->nroot = C->root_take = 0;
     C->err = 0;
+    C->heap_el = 0;
     C->hot[0] = C->S[0] = 0;
     C->cut[0] = 0x7FFFFFFF;
     if (n > SS_THRESHOLD) {
@@ -427,6 +531,7 @@ __device__ inline void vh_sort(uint32_t* lds, int n, const VxHot& H, int* err) {
     }
   }
   __syncthreads();
+  vx_phase(prof ? prof + 1 : nullptr, 0, &tp);
   int seg = 0;
   for (int lev = 0;; ++lev) {
     const int cur = lev & 1, nxt = cur ^ 1;
@@ -467,15 +572,28 @@ __device__ inline void vh_sort(uint32_t* lds, int n, const VxHot& H, int* err) {
     if (tid == 0) C->nbig[cur] = 0;
     const bool drain = C->nroot > VH_ROOTS - 2 * VH_BIGC;
     __syncthreads();
-    if (drain) vh_drain<NT>(L);
+    if (drain) {
+      const unsigned long long t0 = __builtin_readcyclecounter();
+      vh_drain<NT>(L);
+      t_drain += __builtin_readcyclecounter() - t0;
+    }
+  }
+  if (prof && tid == 0) {  // the workgroup levels without the drains inside them
+    const unsigned long long now = __builtin_readcyclecounter();
+    atomicAdd(prof + 2, now - tp - t_drain);
+    atomicAdd(prof + 3, t_drain);
+    tp = now;
   }
   vh_drain<NT>(L);
+  vx_phase(prof ? prof + 3 : nullptr, 0, &tp);
   if (tid == 0 && C->err) atomicOr(err, C->err);
+  if (tid == 0 && prof) atomicAdd(prof, (unsigned long long)C->heap_el);
   for (int q = tid; q < n; q += NT) {
     const uint32_t e = L.E[q];
     if (e & VH_HOT) H.fpos[e & 0x7FFFu] = (uint32_t)q;
   }
   __syncthreads();
+  vx_phase(prof ? prof + 4 : nullptr, 0, &tp);
 }
 
 // Phase 3: every hot voxel's centroid from its members in position order -> out[slot].  The
@@ -600,16 +718,27 @@ __device__ inline bool vh_centroids(const PF& P, float4* out, const VxHot& H, co
 // P(0 .. n), n <= VH_MAX_N; output slots relative to out + M.sbase[1]): when a voxel has 3 or more
 // members, the pruned emulation and those voxels' centroids.  The stable token phase 1 wrote
 // (cold voxels) is cleared when a hot centroid left its voxel.  All NT threads; uniform.
+// prof (optional, diagnostics): [0] cycles of the emulated sort, [1] of the hot centroids, [2]
+// filters with a hot voxel; sprof: vh_sort's (literal heap elements, setup, workgroup levels,
+// wave subtrees, positions)
 template <int NT, typename PF>
 __device__ inline void vh_fixup(const PF& P, int n, float4* out, const VxHot& H, uint32_t* lds, uint32_t lds_words,
-                                VxMisc& M, uint32_t* stable_out, int* err) {
+                                VxMisc& M, uint32_t* stable_out, int* err, unsigned long long* prof = nullptr,
+                                unsigned long long* sprof = nullptr) {
   __syncthreads();
   if (M.hot_n == 0) return;
   const VxGeom g = M.g;
   float4* o = out + M.sbase[1];
-  vh_sort<NT>(lds, n, H, err);
+  const unsigned long long t0 = __builtin_readcyclecounter();
+  vh_sort<NT>(lds, n, H, err, sprof);
+  const unsigned long long t1 = __builtin_readcyclecounter();
   const bool mv = vh_centroids<NT>(P, o, H, g, lds, lds_words, M, err);
   if (mv && threadIdx.x == 0 && stable_out) *stable_out = 0u;
+  if (prof && threadIdx.x == 0) {
+    atomicAdd(prof, t1 - t0);
+    atomicAdd(prof + 1, __builtin_readcyclecounter() - t1);
+    atomicAdd(prof + 2, 1ull);
+  }
   __syncthreads();
 }
 

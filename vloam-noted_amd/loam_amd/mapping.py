@@ -101,8 +101,8 @@ class BatchMapper:
         return list(out)
 
     def debug_counters(self, reset=False):
-        out = np.zeros(72, dtype=np.uint64)  # LOAM_DEBUG_COUNTERS
-        check(lib().loam_mapper_debug_counters(self.h, ptr(out), 72, int(reset)))
+        out = np.zeros(96, dtype=np.uint64)  # LOAM_DEBUG_COUNTERS
+        check(lib().loam_mapper_debug_counters(self.h, ptr(out), len(out), int(reset)))
         return out
 
     def solve(self):
