@@ -262,12 +262,14 @@ int32_t loam_mapper_stats(loam_mapper* h, int32_t stream, loam_map_stats* st);
  * std::sort emulation, of those voxels' centroids, filters (voxel_hot.h), [54..56] the same for
  * the stack VoxelGrids, [72..76] the cube emulation's elements heap-sorted literally, then cycles
  * of its setup, workgroup partitions, wave subtrees, positions, [77..81] the same for stacks,
+ * [82..90] the cube emulation's wave partitions by length (<= 65, 129, 257, 513, 1025), wave
+ * cycles in subtrees (sum, longest drain), heap-sort cycles, subtrees,
  * [58..61] k_frame_prep cycles: FrameIn load, device preparation, stack sizes, submap offsets,
  * [62] its launches, [63] of them frames prepared on the device, [64..65] PCL-order VoxelGrid
  * (exact_voxel_order = 1) sorts in global memory: cycles of their own levels, cubes / stacks
  * ([11..14] / [42..45] hold the rest), [66..67] cube sorts' depth-limit segments and their
  * elements, [68..69] the same for stack sorts.
- * The cycle counters (all but [40], [41], [48], [49]; [52], [56], [66..69], [72], [77] count) run only in a handle created with the
+ * The cycle counters (all but [40], [41], [48], [49]; [52], [56], [66..69], [72], [77], [82..86], [90] count) run only in a handle created with the
  * environment variable LOAM_PHASE_COUNTERS=1 (they cost atomics in the kernels); else they stay 0. */
 #define LOAM_DEBUG_COUNTERS 96
 int32_t loam_mapper_debug_counters(loam_mapper* h, uint64_t* out, int32_t n, int32_t reset);

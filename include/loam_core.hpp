@@ -154,6 +154,15 @@ class BatchMapper {
     check(loam_mapper_input_device(h_, stream, corner, nc, surf, ns, q_wodom, t_wodom, skip_frame ? 1 : 0));
   }
   void solve() { check(loam_mapper_solve(h_)); }
+  // solve() in two halves (loam_mapper_solve_async / _wait): enqueue the frame and return; wait
+  // for the oldest frame not yet waited for.  Two frames may be in the queue: give frame f + 1's
+  // input and solve_async() while frame f is in flight (on a graph-path handle, <= 4 streams, the
+  // device runs f + 1 right behind f).  A throw from solve_async() with LOAM_ERR_CAPACITY or
+  // LOAM_ERR_SYNC reports the older frame it finished; the new frame is enqueued all the same.
+  void solve_async() { check(loam_mapper_solve_async(h_)); }
+  void wait() { check(loam_mapper_wait(h_)); }
+  // queue the stack VoxelGrids of the inputs given so far (they run beside the frame in flight)
+  void prefetch() { check(loam_mapper_prefetch(h_)); }
   void pose(int32_t stream, double q_w[4], double t_w[3]) const { check(loam_mapper_pose(h_, stream, q_w, t_w)); }
   // /laser_cloud_map (laser_mapping.cpp:884-899)
   Cloud map(int32_t stream) const {
@@ -200,7 +209,14 @@ class LaserMapping {
     m_.input(0, corner_last, surf_last, q_wodom_curr, t_wodom_curr, skip_frame);
   }
   void solveMapping() { m_.solve(); }
-  // q_w_curr / t_w_curr: what publish() sends on /aft_mapped_to_init (laser_mapping.cpp:816-874)
+  // solveMapping split so that the node publishes frame f - 1 while frame f runs (INTEGRATION.md,
+  // "Pipelined mapping"): input(f); solveMappingAsync(); waitMapping() finishes f - 1, whose
+  // output() / stats() / laserCloudMap() are then read.  Host clouds are copied at input().
+  void solveMappingAsync() { m_.solve_async(); }
+  void waitMapping() { m_.wait(); }
+  void prefetch() { m_.prefetch(); }
+  // q_w_curr / t_w_curr: what publish() sends on /aft_mapped_to_init (laser_mapping.cpp:816-874);
+  // after waitMapping(): the frame it finished
   void output(double q_w_curr[4], double t_w_curr[3]) const { m_.pose(0, q_w_curr, t_w_curr); }
   loam_map_stats stats() const { return m_.stats(0); }
   // publish() payloads: laserCloudMap and laserCloudFullRes in the map frame

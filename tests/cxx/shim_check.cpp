@@ -1,9 +1,12 @@
 // Compiles the header-only shim (include/loam_core.hpp) with plain g++ against the built
 // library: version, defaults, argument errors, and (without a GPU) the loud no-device error.
-// With a GPU (argv[1] = "1"): four synthetic HDL-64E frames through the shim's
+// With a GPU (argv[1] = "1"): six synthetic HDL-64E frames through the shim's
 // ScanRegistration -> LaserOdometry -> LaserMapping with host clouds between the stages, the
 // way the reference nodes call them (lidar_odometry_mapping.cpp:40-176), against the CPU oracle
-// pipeline (test infrastructure, linked for the comparison only): poses within 1e-4.
+// pipeline (test infrastructure, linked for the comparison only): poses within 1e-4; once with
+// the blocking solveMapping and once with the frames queued (solveMappingAsync / waitMapping,
+// frame f - 1 published while frame f runs).
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <vector>
@@ -35,34 +38,16 @@ int32_t oracle_map_solve(oracle_map* h);
 int32_t oracle_map_pose(oracle_map* h, double* q_w, double* t_w);
 }
 
-static int frames_through_the_shim() {
-  loam_params p = loam_amd::default_params();
-  p.exact_voxel_order = 1;  // free-running frames: PCL's VoxelGrid order, like the oracle
-  loam_amd::ScanRegistration sr(p, 0);
-  loam_amd::LaserOdometry lo(p, 0);
-  loam_amd::LaserMapping lm(p, 0);
+// the oracle pipeline's mapping poses (q xyzw, t) for frames 0 .. nf - 1
+static std::vector<std::array<double, 7>> oracle_poses(int nf, int n_az) {
   oracle_scanreg* osr = oracle_scanreg_create(64, 5.0);
   oracle_odom* olo = oracle_odom_create(1);
   oracle_map* olm = oracle_map_create(0.4f, 0.8f);
-  const int n_az = 1000;
   std::vector<float> xyz(64 * n_az * 3);
   double gt[7];
-  double worst = 0.0;
-  for (int f = 0; f < 4; ++f) {
+  std::vector<std::array<double, 7>> out;
+  for (int f = 0; f < nf; ++f) {
     const int n = synth_frame(23, f, n_az, 1.0, xyz.data(), gt);
-    // device pipeline through the shim, host clouds between the stages
-    sr.input(xyz.data(), n, 3);
-    loam_amd::Cloud full, sharp, less_sharp, flat, less_flat;
-    sr.output(full, sharp, less_sharp, flat, less_flat);
-    lo.input(sharp, less_sharp, flat, less_flat);
-    lo.solveLO();
-    double q[4], t[3];
-    const bool skip = lo.output(q, t);
-    lm.input(lo.copy_last(0), lo.copy_last(1), q, t, skip);
-    lm.solveMapping();
-    double qm[4], tm[3];
-    lm.output(qm, tm);
-    // oracle
     oracle_scanreg_input(osr, xyz.data(), n, 3);
     std::vector<float> c[5];
     for (int k = 0; k < 5; ++k) {
@@ -82,14 +67,67 @@ static int frames_through_the_shim() {
     oracle_map_input(olm, cl.data(), oracle_odom_count(olo, 0), sl.data(), oracle_odom_count(olo, 1), nullptr, 0, oq,
                      ot, oskip);
     oracle_map_solve(olm);
-    double oqm[4], otm[3];
-    oracle_map_pose(olm, oqm, otm);
-    double d = 0.0;
-    for (int i = 0; i < 3; ++i) d = std::fmax(d, std::fabs(tm[i] - otm[i]));
-    for (int i = 0; i < 4; ++i) d = std::fmax(d, std::fabs(std::fabs(qm[i]) - std::fabs(oqm[i])));
+    std::array<double, 7> r;
+    oracle_map_pose(olm, r.data(), r.data() + 4);
+    out.push_back(r);
+  }
+  return out;
+}
+
+static double pose_diff(const double q[4], const double t[3], const std::array<double, 7>& r) {
+  double d = 0.0;
+  for (int i = 0; i < 3; ++i) d = std::fmax(d, std::fabs(t[i] - r[4 + i]));
+  for (int i = 0; i < 4; ++i) d = std::fmax(d, std::fabs(std::fabs(q[i]) - std::fabs(r[i])));
+  return d;
+}
+
+// queued = false: each frame's solveMapping blocks (the reference's facade,
+// lidar_odometry_mapping.cpp:144-176); queued = true: frame f is enqueued with solveMappingAsync
+// and frame f - 1 is waited for and "published" after it (pipelined mapping)
+static int frames_through_the_shim(bool queued, const std::vector<std::array<double, 7>>& ref, int n_az) {
+  loam_params p = loam_amd::default_params();
+  p.exact_voxel_order = 1;  // free-running frames: PCL's VoxelGrid order, like the oracle
+  loam_amd::ScanRegistration sr(p, 0);
+  loam_amd::LaserOdometry lo(p, 0);
+  loam_amd::LaserMapping lm(p, 0);
+  std::vector<float> xyz(64 * n_az * 3);
+  double gt[7];
+  double worst = 0.0;
+  const int nf = static_cast<int>(ref.size());
+  auto publish = [&](int f) {  // what publish() would send for frame f
+    double qm[4], tm[3];
+    lm.output(qm, tm);
+    const double d = pose_diff(qm, tm, ref[f]);
     worst = std::fmax(worst, d);
-    std::printf("frame %d: %d points, %zu / %zu features, mapping t (%.4f %.4f %.4f), |d| %.3e\n", f, n,
-                less_sharp.size() / 4, less_flat.size() / 4, tm[0], tm[1], tm[2], d);
+    const loam_map_stats st = lm.stats();
+    std::printf("%s frame %d: mapping t (%.4f %.4f %.4f), LM iterations %d + %d, |d| %.3e\n",
+                queued ? "queued" : "blocking", f, tm[0], tm[1], tm[2], st.lm[0].iterations, st.lm[1].iterations, d);
+  };
+  for (int f = 0; f < nf; ++f) {
+    const int n = synth_frame(23, f, n_az, 1.0, xyz.data(), gt);
+    // device pipeline through the shim, host clouds between the stages
+    sr.input(xyz.data(), n, 3);
+    loam_amd::Cloud full, sharp, less_sharp, flat, less_flat;
+    sr.output(full, sharp, less_sharp, flat, less_flat);
+    lo.input(sharp, less_sharp, flat, less_flat);
+    lo.solveLO();
+    double q[4], t[3];
+    const bool skip = lo.output(q, t);
+    lm.input(lo.copy_last(0), lo.copy_last(1), q, t, skip);
+    if (!queued) {
+      lm.solveMapping();
+      publish(f);
+    } else {
+      lm.solveMappingAsync();  // frame f, behind f - 1 on the device
+      if (f > 0) {
+        lm.waitMapping();  // frame f - 1
+        publish(f - 1);
+      }
+    }
+  }
+  if (queued) {
+    lm.waitMapping();
+    publish(nf - 1);
   }
   return worst < 1e-4 ? 0 : 9;
 }
@@ -123,5 +161,9 @@ int main(int argc, char** argv) {
     std::printf("no device: %d %s\n", e.code(), e.what());
     return (!expect_device && (e.code() == LOAM_ERR_NODEVICE || e.code() == LOAM_ERR_HIP)) ? 0 : 6;
   }
-  return frames_through_the_shim();
+  const int n_az = 1000;
+  const std::vector<std::array<double, 7>> ref = oracle_poses(6, n_az);
+  const int rc = frames_through_the_shim(false, ref, n_az);
+  if (rc) return rc;
+  return frames_through_the_shim(true, ref, n_az);
 }

@@ -67,9 +67,10 @@ def test_pipeline_zero_copy():
 
 
 def test_cxx_shim_frames(tmp_path):
-    """the header-only C++ shim (include/loam_core.hpp) driving four frames through
+    """the header-only C++ shim (include/loam_core.hpp) driving six frames through
     ScanRegistration -> LaserOdometry -> LaserMapping with host clouds between the stages, as the
-    reference nodes would (tests/cxx/shim_check.cpp), against the oracle pipeline: within 1e-4"""
+    reference nodes would (tests/cxx/shim_check.cpp), against the oracle pipeline: within 1e-4,
+    with the blocking solveMapping and with frames queued (solveMappingAsync / waitMapping)"""
     import os
     import subprocess
     from conftest import ROOT
@@ -84,7 +85,7 @@ def test_cxx_shim_frames(tmp_path):
     r = subprocess.run([exe, "1"], capture_output=True, text=True, timeout=120)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "frame 3" in r.stdout
+    assert "blocking frame 5" in r.stdout and "queued frame 5" in r.stdout
 
 
 def test_pipelined_chain_matches_sequential():

@@ -38,4 +38,6 @@ for exact in (1, 0):
           f"hot fix-ups cubes: sort/centroid Mcycles {[round(v / 20e6, 3) for v in dc[50:52]]} in {dc[52]} filters, heap-sorted {dc[72]}, "
           f"sort phases setup/wg/waves/positions {[round(v / 20e6, 3) for v in dc[73:77]]}; "
           f"stacks: {[round(v / 20e6, 3) for v in dc[54:56]]} in {dc[56]}, heap-sorted {dc[77]}, phases {[round(v / 20e6, 3) for v in dc[78:82]]}; "
+          f"cube wave partitions by class (<=65,129,257,513,1025) {dc[82:87]}, wave busy Mcycles {round(dc[87] / 20e6, 3)}, "
+          f"longest drain Mcycles {round(dc[88] / 1e6, 3)}, heap Mcycles {round(dc[89] / 20e6, 3)}, subtrees {dc[90]}; "
           f"stacks {st.corner_stack},{st.surf_stack}", flush=True)

@@ -69,6 +69,30 @@ __device__ inline int wave_min_i(int v) {
   for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
   return v;
 }
+// DPP (GFX9 data-parallel primitives, no LDS round trip): inclusive prefix sum of a u32 across the
+// wave (row_shr 1/2/4/8 within each row of 16, then row_bcast 15 / 31 across the rows; lanes whose
+// source is outside keep the 0 given as the old value), the wave total, and whole-wave shifts
+__device__ inline uint32_t dpp_incl_scan_u(uint32_t v) {
+  int x = (int)v;
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return (uint32_t)x;
+}
+__device__ inline uint32_t dpp_wave_sum_u(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)dpp_incl_scan_u(v), 63);
+}
+// lane i <- lane i + 1 (lane 63 <- 0) / lane i <- lane i - 1 (lane 0 <- 0)
+__device__ inline uint32_t dpp_from_next(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);  // wave_shl:1
+}
+__device__ inline uint32_t dpp_from_prev(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);  // wave_shr:1
+}
+
 // inclusive prefix sum across the wave
 __device__ inline uint32_t wave_incl_scan_u(uint32_t v) {
   int l = wave_lane();

@@ -1444,7 +1444,8 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
         if (!merged) voxel_segment(S, lds);
         vh_fixup<VX_THREADS>(VxSrc{ar + cv.x, (int)cv.y, D.ins_sorted + sm_index(s, m) * D.max_in + i0}, (int)n, ar,
                              S.hot, lds, LW - 256, *reinterpret_cast<VxMisc*>(lds + LW - 192), tok, &F.err,
-                             D.pdbg ? D.pdbg + 50 : nullptr, D.pdbg ? D.pdbg + 72 : nullptr);
+                             D.pdbg ? D.pdbg + 50 : nullptr, D.pdbg ? D.pdbg + 72 : nullptr,
+                             D.pdbg ? D.pdbg + 82 : nullptr);
       }
     } else {  // the whole std::sort emulated in global memory (voxel_pcl.h)
       VxPclOut O;

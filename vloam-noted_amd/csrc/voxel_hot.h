@@ -59,6 +59,9 @@ struct VhCtl {
   int dup;
   int err;
   int heap_el;  // elements heap-sorted literally (diagnostics)
+  unsigned long long* dprof;  // optional detail counters (diagnostics): wave partitions by size
+                              // class (5), wave busy cycles in drains, the longest wave's, heap-sort
+                              // cycles, subtrees
   uint32_t ws[VX_WAVES + 1];  // block-scan scratch of the workgroup partition
 };
 
@@ -93,98 +96,116 @@ constexpr int vh_lds_words(int n) {
 }
 static_assert(vh_lds_words<VX_THREADS>(VH_MAX_N) <= VX_LDS_WORDS - 256, "hot sort LDS layout");
 
-// __move_median_to_first(lo, lo + 1, mid, hi - 1) on one lane
-__device__ inline void vh_median(uint32_t* E, int lo, int hi) {
-  const VhLess less;
-  const int a = lo + 1, b = lo + (hi - lo) / 2, c = hi - 1;
-  const uint32_t ea = E[a], eb = E[b], ec = E[c];
-  int m;
-  if (less(ea, eb)) {
-    if (less(eb, ec)) m = b;
-    else if (less(ea, ec)) m = c;
-    else m = a;
-  } else if (less(ea, ec)) {
-    m = a;
-  } else if (less(eb, ec)) {
-    m = c;
-  } else {
-    m = b;
-  }
-  const uint32_t t = E[lo];
-  E[lo] = E[m];
-  E[m] = t;
-}
-
-// One segment [lo, hi) (17 <= m <= 64 U + 1) partitioned by one wave, its positions lo + 1 ..
-// held U per lane.  Returns the cut, or -1 when fewer than two hot elements lie in it (nothing to
-// do below it).  Every lane returns the same.
+// One segment [lo, hi) (65 < m <= 64 U + 1) partitioned by one wave: lane l classifies the c
+// consecutive positions lo + 1 + l c .. (c = ceil((m - 1) / 64) <= U) into two bit masks, one
+// DPP scan of the packed counts places every stop, and the lane walks its positions in order
+// (ranks by counting, no per-chunk ballots).  Returns the cut, or -1 when fewer than two hot
+// elements lie in it (nothing to do below it).  Every lane returns the same.
 template <int U>
 __device__ inline int vh_partition_wave_u(uint32_t* E, uint16_t* Bs, int lo, int hi) {
+  static_assert(U <= 32, "masks in one word");
   const int lane = threadIdx.x & 63;
-  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-  if (lane == 0) vh_median(E, lo, hi);
-  ss_wave_fence();
-  const uint32_t pe = E[lo];
-  const uint32_t p = pe >> 16;
-  uint32_t e[U];
-  int nr = 1, nh = (pe & VH_HOT) ? 1 : 0;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int i = lo + 1 + u * 64 + lane;
-    const bool v = i < hi;
-    e[u] = v ? E[i] : 0u;
-    const uint32_t k = e[u] >> 16;
-    nr += __popcll(__ballot(v && !(p < k)));
-    nh += __popcll(__ballot(v && (e[u] & VH_HOT)));
-  }
-  if (nh < 2) return -1;
-  const int m = hi - lo, KB = (m - 1) / 2, bb = lo >> 1;
-  // S and the listed right stops r_k = Bs[bb + k - 1] (k <= KB)
-  int L = 0, R = 1, S = 0;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int i = lo + 1 + u * 64 + lane;
-    const bool v = i < hi;
-    const uint32_t k = e[u] >> 16;
-    const bool isl = v && !(k < p), isr = v && !(p < k);
-    const uint64_t bl = __ballot(isl), br = __ballot(isr);
-    const int kl = L + __popcll(bl & lt) + 1;
-    const int t = R + __popcll(br & lt);     // ascending index among the right stops (pivot: 0)
-    const bool pred = isl && kl <= nr - (t + (isr ? 1 : 0));  // right stops strictly right of i
-    S += __popcll(__ballot(pred));
-    if (isr && nr - t <= KB) Bs[bb + nr - t - 1] = (uint16_t)i;
-    L += __popcll(bl);
-    R += __popcll(br);
-  }
-  if (lane == 0 && nr <= KB) Bs[bb + nr - 1] = (uint16_t)lo;
-  ss_wave_fence();
-  // the swaps: every pair (l_k, r_k), k <= S, is read and written by its own lane alone (l_k < cut
-  // <= r_k, and no position is two pairs'), so no ordering is needed between lanes
-  int lK = 0x7FFFFFFF;
-  L = 0;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int i = lo + 1 + u * 64 + lane;
-    const bool isl = i < hi && !((e[u] >> 16) < p);
-    const uint64_t bl = __ballot(isl);
-    const int kl = L + __popcll(bl & lt) + 1;
-    if (isl && kl <= S) {
-      const int y = Bs[bb + kl - 1];
-      E[i] = E[y];
-      E[y] = e[u];
+  // __move_median_to_first on every lane: the classification sees the swap, lane 0 makes it later
+  const VhLess less;
+  const uint32_t elo = E[lo];
+  int mm;
+  uint32_t pe;
+  {
+    const int a = lo + 1, b = lo + (hi - lo) / 2, c = hi - 1;
+    const uint32_t ea = E[a], eb = E[b], ec = E[c];
+    if (less(ea, eb)) {
+      if (less(eb, ec)) mm = b;
+      else if (less(ea, ec)) mm = c;
+      else mm = a;
+    } else if (less(ea, ec)) {
+      mm = a;
+    } else if (less(eb, ec)) {
+      mm = c;
+    } else {
+      mm = b;
     }
-    if (isl && kl == S + 1) lK = i;
-    L += __popcll(bl);
+    pe = mm == a ? ea : (mm == b ? eb : ec);
   }
-  lK = wave_min_i(lK);
+  const uint32_t p = pe >> 16;
+  const int c = (hi - lo - 1 + 63) >> 6;
+  const int b0 = lo + 1 + lane * c;
+  uint32_t ml = 0, mr = 0, nh = 0;
+  {
+    uint32_t e[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) e[u] = E[min(b0 + u, hi - 1)];  // (clamped: every load issued at once)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = b0 + u;
+      if (u < c && i < hi) {
+        const uint32_t x = i == mm ? elo : e[u];
+        const uint32_t k = x >> 16;
+        ml |= (k < p ? 0u : 1u) << u;
+        mr |= (p < k ? 0u : 1u) << u;
+        nh += (x & VH_HOT) ? 1u : 0u;
+      }
+    }
+  }
+  if (dpp_wave_sum_u(nh) + ((pe & VH_HOT) ? 1u : 0u) < 2u) return -1;
+  ss_wave_fence();  // every lane's reads of E before the median swap
+  if (lane == 0) {
+    E[lo] = pe;
+    E[mm] = elo;
+  }
+  const uint32_t v = (uint32_t)__popc(ml) | ((uint32_t)__popc(mr) << 16);  // totals < 2^16
+  const uint32_t x = dpp_incl_scan_u(v);
+  const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+  const uint32_t off = x - v;
+  const int nr = 1 + (int)(tot >> 16), nl = (int)(tot & 0xFFFFu);
+  const int m = hi - lo, KB = (m - 1) / 2, bb = lo >> 1;
+  uint32_t S = 0;
+  {
+    int kl = (int)(off & 0xFFFFu), t = 1 + (int)(off >> 16);  // t: ascending right-stop index
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool isl = (ml >> u) & 1u, isr = (mr >> u) & 1u;
+      if (isl) {
+        ++kl;
+        S += kl <= nr - (t + (isr ? 1 : 0)) ? 1u : 0u;
+      }
+      if (isr) {
+        if (nr - t <= KB) Bs[bb + nr - t - 1] = (uint16_t)(b0 + u);
+        ++t;
+      }
+    }
+    if (lane == 0 && nr <= KB) Bs[bb + nr - 1] = (uint16_t)lo;
+  }
+  S = dpp_wave_sum_u(S);
+  ss_wave_fence();
+  // the swaps (each pair (l_k, r_k), k <= S, read and written by the lane of l_k alone: l_k < cut
+  // <= r_k, no position is in two pairs) and l_{S+1}
+  int lK = 0x7FFFFFFF;
+  {
+    int kl = (int)(off & 0xFFFFu);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if ((ml >> u) & 1u) {
+        ++kl;
+        if (kl <= (int)S) {
+          const int y = Bs[bb + kl - 1];
+          const uint32_t tv = E[y];
+          E[y] = E[b0 + u];
+          E[b0 + u] = tv;
+        }
+        if (kl == (int)S + 1) lK = b0 + u;
+      }
+    }
+  }
+  const uint64_t hk = __ballot(lK != 0x7FFFFFFF);  // at most one lane holds l_{S+1}
+  const int lKs = (int)S + 1 <= nl ? __builtin_amdgcn_readlane(lK, __ffsll((unsigned long long)hk) - 1) : 0x7FFFFFFF;
   const int rS = S >= 1 ? (int)Bs[bb + S - 1] : hi;
   ss_wave_fence();
-  return __builtin_amdgcn_readfirstlane(min(lK, rS));
+  return __builtin_amdgcn_readfirstlane(min(lKs, rS));
 }
-__device__ inline int vh_partition_wave(uint32_t* E, uint16_t* Bs, int lo, int hi) {
+__device__ inline int vh_partition_wave(uint32_t* E, uint16_t* Bs, int lo, int hi, unsigned long long* dp = nullptr) {
   static_assert(VH_BIG == 1024, "size classes");
   const int m = hi - lo;  // positions lo + 1 .. hi - 1: m - 1 of them
-  if (m <= 65) return vh_partition_wave_u<1>(E, Bs, lo, hi);
+  if (dp && (threadIdx.x & 63) == 0) atomicAdd(dp + (m <= 65 ? 0 : m <= 129 ? 1 : m <= 257 ? 2 : m <= 513 ? 3 : 4), 1ull);
   if (m <= 129) return vh_partition_wave_u<2>(E, Bs, lo, hi);
   if (m <= 257) return vh_partition_wave_u<4>(E, Bs, lo, hi);
   if (m <= 513) return vh_partition_wave_u<8>(E, Bs, lo, hi);
@@ -226,7 +247,7 @@ __device__ inline void vh_heap_sort_wave(uint32_t* E, int lo, int hi) {
     while (h < lim) {
       const int node = ((h + 1) << lj) - 1 + lt;
       const uint32_t x = (lane < 62 && node < n) ? E[lo + node] : 0u;
-      const uint32_t xr = __shfl_down(x, 1, 64);  // the right sibling (left children: t even)
+      const uint32_t xr = dpp_from_next(x);  // the right sibling (left children: t even)
       const uint64_t rw = __ballot(!less(xr, x));
       int tt = 0;
 #pragma unroll
@@ -258,7 +279,7 @@ __device__ inline void vh_heap_sort_wave(uint32_t* E, int lo, int hi) {
     // __push_heap: v rises while its parent is less; path node j holds pv of lane j - 1 after the
     // shift, so the hole stops at q = k - #{j < k : pv_j < v}
     const int q = k - __popcll(__ballot(lane < k && less(pv, v)));
-    const int hp = __shfl_up(pp, 1, 64);  // position of path node j (lane j): node 0 is the root
+    const int hp = (int)dpp_from_prev((uint32_t)pp);  // position of path node j (lane j): node 0 is the root
     const int hj = lane == 0 ? 0 : hp;
     ss_wave_fence();  // every read of this pop before its writes
     if (lane < q) E[lo + hj] = pv;
@@ -300,8 +321,121 @@ __device__ inline void vh_depth_limit_wave(uint32_t* E, int lo, int hi, uint32_t
   vh_heap_sort_wave(E, lo, hi);
 }
 
+// position of the k-th highest / lowest set bit of m (k >= 1, at least k bits set), per lane
+__device__ inline int vh_kth_high(uint64_t m, int k) {
+  int t = 0;
+#pragma unroll
+  for (int s = 32; s; s >>= 1)
+    if (__popcll(m >> (t + s)) >= k) t += s;
+  return t;
+}
+__device__ inline int vh_kth_low(uint64_t m, int k) {
+  int t = 0;
+#pragma unroll
+  for (int s = 32; s; s >>= 1)
+    if (__popcll(m & ((1ull << (t + s)) - 1ull)) < k) t += s;
+  return t;
+}
+
+// The whole subtree of a segment of at most 64 elements in one wave's registers (lane i: the
+// element at lo + i): every partition is ballots over the segment's lanes, the Hoare pairs
+// (l_k, r_k) are found per lane from the stop masks and exchanged with one lane permutation, the
+// smaller part goes first; a depth-limit segment goes through the LDS (vh_depth_limit_wave).  The
+// same pruning as the LDS partitions: parts with fewer than two hot elements are left.
+__device__ inline void vh_subtree64(uint32_t* E, int lo, int len, int d, uint32_t* kb, int* heap_el) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  const uint64_t gt = lane == 63 ? 0ull : (~0ull << (lane + 1));
+  const VhLess less;
+  uint32_t e = lane < len ? E[lo + lane] : 0u;
+  if (__popcll(__ballot(lane < len && (e & VH_HOT))) < 2) return;
+  bool dirty = false;
+  // pending parts (a | b << 8 | d << 16) as a 3-deep register stack p0 (top), p1, p2: the smaller
+  // part goes first, so each pending part is larger than the one worked on and at most 2 wait
+  uint32_t p0 = 0, p1 = 0, p2 = 0;
+  int top = 0;
+  int a = 0, b = len, dd = d;
+  while (true) {
+    bool next = true;
+    const uint64_t rng = (b >= 64 ? ~0ull : ((1ull << b) - 1ull)) & ~((1ull << a) - 1ull);
+    if (b - a > SS_THRESHOLD && __popcll(__ballot(e & VH_HOT) & rng) >= 2) {
+      if (dd == 0) {
+        if (dirty && lane < len) E[lo + lane] = e;
+        ss_wave_fence();
+        vh_depth_limit_wave(E, lo + a, lo + b, kb, heap_el);
+        e = lane < len ? E[lo + lane] : 0u;
+        dirty = false;
+      } else {
+        const int ia = a + 1, ib = a + (b - a) / 2, ic = b - 1;
+        const uint32_t ea = __builtin_amdgcn_readlane(e, ia), eb = __builtin_amdgcn_readlane(e, ib),
+                       ec = __builtin_amdgcn_readlane(e, ic), ev = __builtin_amdgcn_readlane(e, a);
+        int mm;
+        if (less(ea, eb)) {
+          if (less(eb, ec)) mm = ib;
+          else if (less(ea, ec)) mm = ic;
+          else mm = ia;
+        } else if (less(ea, ec)) {
+          mm = ia;
+        } else if (less(eb, ec)) {
+          mm = ic;
+        } else {
+          mm = ib;
+        }
+        const uint32_t em = mm == ia ? ea : (mm == ib ? eb : ec);
+        if (lane == a) e = em;
+        if (lane == mm) e = ev;
+        const uint32_t p = em >> 16, k = e >> 16;
+        const bool in = lane > a && lane < b;
+        const uint64_t bl = __ballot(in && !(k < p));
+        const uint64_t br = __ballot(in && !(p < k)) | (1ull << a);
+        const bool isl = (bl >> lane) & 1ull, isr = (br >> lane) & 1ull;
+        const int kl = __popcll(bl & lt) + 1;  // ascending rank among the left stops
+        const int kr = __popcll(br & gt) + 1;  // descending rank among the right stops
+        const int S = __popcll(__ballot(isl && kl <= kr - 1));  // #right stops above l_k >= k
+        int partner = lane;
+        if (isl && kl <= S) partner = vh_kth_high(br, kl);
+        if (isr && kr <= S) partner = vh_kth_low(bl, kr);
+        e = __shfl(e, partner, 64);
+        const uint64_t bk = __ballot(isl && kl == S + 1), bs = __ballot(isr && kr == S);
+        const int lK = bk ? __ffsll((unsigned long long)bk) - 1 : 64;
+        const int rS = S >= 1 ? __ffsll((unsigned long long)bs) - 1 : b;
+        const int cut = min(lK, rS);
+        dirty = true;
+        --dd;
+        const int l0 = cut - a, l1 = b - cut;
+        const bool left_small = l0 <= l1;
+        const int sa = left_small ? a : cut, sb = left_small ? cut : b;
+        const int ba = left_small ? cut : a, bb = left_small ? b : cut;
+        if (bb - ba > SS_THRESHOLD) {
+          p2 = p1;
+          p1 = p0;
+          p0 = (uint32_t)ba | ((uint32_t)bb << 8) | ((uint32_t)dd << 16);
+          ++top;
+        }
+        if (sb - sa > SS_THRESHOLD) {
+          a = sa;
+          b = sb;
+          next = false;
+        }
+      }
+    }
+    if (next) {
+      if (top == 0) break;
+      const uint32_t q = p0;
+      p0 = p1;
+      p1 = p2;
+      --top;
+      a = (int)(q & 0xFFu);
+      b = (int)((q >> 8) & 0xFFu);
+      dd = (int)(q >> 16);
+    }
+  }
+  if (dirty && lane < len) E[lo + lane] = e;
+}
+
 // The subtree below one pending segment, one wave, no barriers
-__device__ inline void vh_wave_subtree(uint32_t* E, uint16_t* Bs, uint32_t root, uint32_t* wa, int* heap_el) {
+__device__ inline void vh_wave_subtree(uint32_t* E, uint16_t* Bs, uint32_t root, uint32_t* wa, int* heap_el,
+                                       unsigned long long* dp = nullptr) {
   const int lane = threadIdx.x & 63;
   uint32_t* stk = wa;
   uint32_t* kb = wa + VH_LIFO;
@@ -311,11 +445,16 @@ __device__ inline void vh_wave_subtree(uint32_t* E, uint16_t* Bs, uint32_t root,
     const int lo = (int)(cur & 0x7FFFu), len = (int)((cur >> 15) & 0x7FFu), d = (int)(cur >> 26);
     const int hi = lo + len;
     bool next = true;  // take the next pending entry
-    if (len > SS_THRESHOLD) {
+    if (len > SS_THRESHOLD && len <= 64) {
+      vh_subtree64(E, lo, len, d, kb, heap_el);
+      ss_wave_fence();
+    } else if (len > SS_THRESHOLD) {
       if (d == 0) {
+        const unsigned long long th = __builtin_readcyclecounter();
         vh_depth_limit_wave(E, lo, hi, kb, heap_el);
+        if (dp && lane == 0) atomicAdd(dp + 7, __builtin_readcyclecounter() - th);
       } else {
-        const int cut = vh_partition_wave(E, Bs, lo, hi);
+        const int cut = vh_partition_wave(E, Bs, lo, hi, dp);
         if (cut >= 0) {
           const int l0 = cut - lo, l1 = hi - cut;
           const bool left_small = l0 <= l1;
@@ -347,12 +486,20 @@ __device__ inline void vh_drain(const VhLds& L) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t* wa = L.wave + wid * VH_WAVE_W;
   const int nroot = min(L.C->nroot, VH_ROOTS);
+  unsigned long long* dp = L.C->dprof;
+  const unsigned long long t0 = __builtin_readcyclecounter();
   while (true) {
     int k = 0;
     if (lane == 0) k = atomicAdd(&L.C->root_take, 1);
     k = __builtin_amdgcn_readfirstlane(k);
     if (k >= nroot) break;
-    vh_wave_subtree(L.E, L.Bs, L.roots[k], wa, &L.C->heap_el);
+    vh_wave_subtree(L.E, L.Bs, L.roots[k], wa, &L.C->heap_el, dp);
+    if (dp && lane == 0) atomicAdd(dp + 8, 1ull);
+  }
+  if (dp && lane == 0) {
+    const unsigned long long b = __builtin_readcyclecounter() - t0;
+    atomicAdd(dp + 5, b);
+    atomicMax(dp + 6, b);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -374,43 +521,64 @@ __device__ inline int vh_partition_wg_c(const VhLds& L, int lo, int hi, int par)
   VhCtl* C = L.C;
   uint32_t* ws = C->ws;
   static_assert(NW <= VX_WAVES, "scan scratch");
-  if (tid == 0) vh_median(E, lo, hi);
-  __syncthreads();
-  if (tid == 0) {  // the next segment's slot: every read of it (two segments back) is done
-    C->hot[par ^ 1] = 0;
-    C->S[par ^ 1] = 0;
-    C->cut[par ^ 1] = 0x7FFFFFFF;
+  // __move_median_to_first(lo, lo + 1, mid, hi - 1), computed by every thread: the classification
+  // sees the swap (position mm holds E[lo]), tid 0 makes it after the scan's barrier
+  const VhLess less;
+  const uint32_t elo = E[lo];
+  int mm;
+  uint32_t pe;
+  {
+    const int a = lo + 1, b = lo + (hi - lo) / 2, c = hi - 1;
+    const uint32_t ea = E[a], eb = E[b], ec = E[c];
+    if (less(ea, eb)) {
+      if (less(eb, ec)) mm = b;
+      else if (less(ea, ec)) mm = c;
+      else mm = a;
+    } else if (less(ea, ec)) {
+      mm = a;
+    } else if (less(eb, ec)) {
+      mm = c;
+    } else {
+      mm = b;
+    }
+    pe = mm == a ? ea : (mm == b ? eb : ec);
   }
-  const uint32_t pe = E[lo];
   const uint32_t p = pe >> 16;
   const int len = hi - lo - 1;  // the scanned positions lo + 1 .. hi - 1
   const int c = (len + NT - 1) / NT;
   const int b0 = lo + 1 + tid * c;
   uint32_t ml = 0, mr = 0;
   int nh = 0;
+  uint32_t ev[CH];
+#pragma unroll
+  for (int u = 0; u < CH; ++u) ev[u] = E[min(b0 + u, hi - 1)];  // (clamped: every load issued at once)
 #pragma unroll
   for (int u = 0; u < CH; ++u) {
     const int i = b0 + u;
     if (u < c && i < hi) {
-      const uint32_t e = E[i];
+      const uint32_t e = i == mm ? elo : ev[u];
       const uint32_t k = e >> 16;
       if (!(k < p)) ml |= 1u << u;
       if (!(p < k)) mr |= 1u << u;
       nh += (e & VH_HOT) ? 1 : 0;
     }
   }
-  nh = wave_sum_i(nh);
+  nh = (int)dpp_wave_sum_u((uint32_t)nh);
   if (lane == 0 && nh) atomicAdd(&C->hot[par], nh);
   const uint32_t v = (uint32_t)__popc(ml) | ((uint32_t)__popc(mr) << 16);  // totals < 2^16
-  uint32_t x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
+  const uint32_t x = dpp_incl_scan_u(v);
   if (lane == 63) ws[wid] = x;
   __syncthreads();
+  if (tid == 0) {
+    C->hot[par ^ 1] = 0;  // the next segment's slot: every use of it (two segments back) is done
+    C->S[par ^ 1] = 0;
+    C->cut[par ^ 1] = 0x7FFFFFFF;
+  }
   if (C->hot[par] + ((pe & VH_HOT) ? 1 : 0) < 2) return -1;
+  if (tid == 0) {  // the median swap (read by nobody before the next barrier)
+    E[lo] = pe;
+    E[mm] = elo;
+  }
   uint32_t off = x - v, tot = 0;
   for (int w = 0; w < NW; ++w) {
     const uint32_t t = ws[w];
@@ -435,7 +603,7 @@ __device__ inline int vh_partition_wg_c(const VhLds& L, int lo, int hi, int par)
       }
     }
     if (tid == 0 && nr <= KB) Bs[bb + nr - 1] = (uint16_t)lo;
-    S = wave_sum_i(S);
+    S = (int)dpp_wave_sum_u((uint32_t)S);
     if (lane == 0 && S) atomicAdd(&C->S[par], S);
   }
   __syncthreads();
@@ -503,7 +671,8 @@ __device__ inline void vh_depth_limit_wg(const VhLds& L, int n, int lo, int hi) 
 // prof (optional, diagnostics): [0] elements heap-sorted literally; [1..4] cycles of the setup, the
 // workgroup partitions (and depth-limit segments), the wave subtrees, the positions
 template <int NT>
-__device__ inline void vh_sort(uint32_t* lds, int n, const VxHot& H, int* err, unsigned long long* prof = nullptr) {
+__device__ inline void vh_sort(uint32_t* lds, int n, const VxHot& H, int* err, unsigned long long* prof = nullptr,
+                               unsigned long long* dprof = nullptr) {
   const int tid = threadIdx.x;
   unsigned long long tp = __builtin_readcyclecounter(), t_drain = 0;
   const VhLds L = vh_layout<NT>(lds, n);
@@ -518,6 +687,7 @@ __device__ inline void vh_sort(uint32_t* lds, int n, const VxHot& H, int* err, u
     C->nroot = C->root_take = 0;
     C->err = 0;
     C->heap_el = 0;
+    C->dprof = dprof;
     C->hot[0] = C->S[0] = 0;
     C->cut[0] = 0x7FFFFFFF;
     if (n > SS_THRESHOLD) {
@@ -724,13 +894,13 @@ __device__ inline bool vh_centroids(const PF& P, float4* out, const VxHot& H, co
 template <int NT, typename PF>
 __device__ inline void vh_fixup(const PF& P, int n, float4* out, const VxHot& H, uint32_t* lds, uint32_t lds_words,
                                 VxMisc& M, uint32_t* stable_out, int* err, unsigned long long* prof = nullptr,
-                                unsigned long long* sprof = nullptr) {
+                                unsigned long long* sprof = nullptr, unsigned long long* dprof = nullptr) {
   __syncthreads();
   if (M.hot_n == 0) return;
   const VxGeom g = M.g;
   float4* o = out + M.sbase[1];
   const unsigned long long t0 = __builtin_readcyclecounter();
-  vh_sort<NT>(lds, n, H, err, sprof);
+  vh_sort<NT>(lds, n, H, err, sprof, dprof);
   const unsigned long long t1 = __builtin_readcyclecounter();
   const bool mv = vh_centroids<NT>(P, o, H, g, lds, lds_words, M, err);
   if (mv && threadIdx.x == 0 && stable_out) *stable_out = 0u;
