@@ -129,9 +129,9 @@ int32_t loam_scanreg_curvature(loam_scanreg* h, float* curv, int32_t* label, int
 /* device time of the last input (ms) */
 double loam_scanreg_ms(loam_scanreg* h);
 /* cumulative device cycle counters of the per-ring PCL-order VoxelGrid (k_sr_ringvox), summed
- * over rings and frames: [0] bounding box + keys, [1] sort levels, [2] final sort pass,
- * [3] centroids; reset = 1 zeroes them after the copy.  Counted only in a handle created with
- * LOAM_PHASE_COUNTERS=1 in the environment. */
+ * over rings and frames: [0] cycles of the std::sort emulation for the voxels of 3+ members,
+ * [1] of their centroids, [2] rings that had such a voxel; reset = 1 zeroes them after the copy.
+ * Counted only in a handle created with LOAM_PHASE_COUNTERS=1 in the environment. */
 #define LOAM_SR_DEBUG_COUNTERS 8
 int32_t loam_scanreg_debug_counters(loam_scanreg* h, uint64_t* out, int32_t n, int32_t reset);
 

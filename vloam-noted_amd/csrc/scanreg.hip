@@ -16,7 +16,8 @@
 //                   picks with +-5 neighbour suppression (:352-493): one wave runs the
 //                   (inherently sequential) greedy scan with 64-wide ballots, all in LDS
 //   k_sr_ringvox    VoxelGrid 0.2 m of each ring's lessFlat candidates (:497-503), in PCL's
-//                   summation order (voxel_pcl.h)
+//                   summation order (voxel.h + voxel_hot.h: std::sort's order only where a
+//                   voxel has 3+ members)
 //   k_sr_gather     concatenation of the per-ring outputs in ring order
 // The reference sorts each sector with std::sort (unstable).  The bitonic sort by (curvature,
 // index) is std::sort's order whenever a sector's curvatures are distinct; a sector with a tie
@@ -32,7 +33,7 @@
 #include "libm_f32.h"
 #include "stdsort.h"
 #include "voxel.h"
-#include "voxel_pcl.h"
+#include "voxel_hot.h"
 
 namespace loam {
 
@@ -661,39 +662,44 @@ __global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(SrDev D) {
   }
 }
 
-// PCL VoxelGrid of one ring's lessFlat candidates in PCL's summation order (voxel_pcl.h): the
-// std::sort emulation in LDS up to SRV_LDS points, else in the global scratch
-constexpr int SRV_THREADS = 1024;
-constexpr int SRV_LDS = 4096;
-constexpr int SRV_SEG = SR_RING_CAP / 17 + 2;  // level list (<= n / 17 + 1 segments per level)
+// PCL VoxelGrid of one ring's lessFlat candidates (scan_registration.cpp:497-501) in PCL's
+// summation order, one workgroup per ring: the input-order filter (voxel.h) sums every voxel of at
+// most 2 members (order-free) and records the others, then voxel_hot.h runs the pruned std::sort
+// emulation in LDS and sums those voxels in its order.  Scratch: the ring's region of the
+// sector sort's arrays (k_sr_select is done with them).
+constexpr int SRV_THREADS = VX_THREADS;
+static_assert(SR_RING_CAP <= VH_MAX_N, "a ring's lessFlat cloud fits the LDS emulation");
+
+// (a separate function holding the LDS: the ROCm 7.2 compiler crashes in InstCombine when the
+// filter is inlined into the kernel; declared here, the array keeps its LDS address space)
+__device__ __noinline__ void sr_ringvox(const VoxSeg& S, int n, int* err, unsigned long long* prof) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
+  voxel_segment(S, lds);
+  vh_fixup<SRV_THREADS>(VxSrc{S.src0, n, nullptr}, n, S.out, S.hot, lds, VX_LDS_WORDS - 256,
+                        *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192), nullptr, err, prof);
+}
 
 __global__ void __launch_bounds__(SRV_THREADS) k_sr_ringvox(SrDev D) {
-  __shared__ uint64_t sE[SRV_LDS], sS[SRV_LDS];
-  __shared__ uint32_t sA[SRV_LDS], sB[SRV_LDS];
-  __shared__ int seg[2][3 * SRV_SEG];
-  __shared__ SsLevels lev;
-  __shared__ VxMisc M;
-  __shared__ uint32_t ws[SRV_THREADS / 64 + 1];
   const int r = blockIdx.x;
   SrFrame& F = *D.fr;
   const int base = F.ring_off[r];
   const int n = F.n_less_flat_scan[r];
-  const bool lds = n <= SRV_LDS;
-  VxPclOut O;
-  O.out = D.less_flat_ds + base;
-  O.res_cnt = &F.n_less_flat[r];
-  // two inlined copies: with the sort arrays named directly as __shared__ the compiler emits
-  // LDS instructions (ds_*) for the sort, where a pointer selected between LDS and global
-  // memory would be generic (flat_*, slower)
-  if (lds) {
-    VxPclScratch X{sE, sA, sB, sS, &lev, {seg[0], seg[1]}, SRV_SEG};
-    X.prof = D.pdbg;  // ring VoxelGrid phase cycles, summed over the rings (or null)
-    voxel_grid_pcl<SRV_THREADS>(VxPtrSrc{D.less_flat_scan + base}, n, 0.2f, O, X, M, ws, &F.err);
-  } else {
-    VxPclScratch X{D.ss_e + base, D.ss_a + base, D.ss_b + base, D.ss_s + base, &lev, {seg[0], seg[1]}, SRV_SEG};
-    X.prof = D.pdbg;
-    voxel_grid_pcl<SRV_THREADS>(VxPtrSrc{D.less_flat_scan + base}, n, 0.2f, O, X, M, ws, &F.err);
-  }
+  VoxSeg S{};
+  S.src0 = D.less_flat_scan + base;
+  S.n0 = n;
+  S.leaf = 0.2f;
+  S.out = D.less_flat_ds + base;
+  S.cap = (uint32_t)n;
+  S.res_cnt = &F.n_less_flat[r];
+  S.scratch_idx = reinterpret_cast<int*>(D.ss_b + base);
+  S.scratch_cap = (uint32_t)n;
+  S.err = &F.err;
+  S.hot.rk = D.ss_a + base;
+  S.hot.hl = reinterpret_cast<uint32_t*>(D.ss_e + base);
+  S.hot.hv = S.hot.hl + n;  // 3 words per hot voxel, at most n / 3 of them: within the ring's 2 n
+  S.hot.fpos = reinterpret_cast<uint32_t*>(D.ss_s + base);
+  S.hot.cap_h = (uint32_t)n / 3;
+  sr_ringvox(S, n, &F.err, D.pdbg);
 }
 
 // concatenation of the per-ring outputs in ring order
