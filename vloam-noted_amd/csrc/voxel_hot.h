@@ -222,6 +222,62 @@ __device__ inline int vh_partition_wave(uint32_t* E, uint16_t* Bs, int lo, int h
 //     pair with one shuffle and one ballot, and follows the path in scalar registers; the path's
 //     values then shift up one place and __push_heap's value lands below the lowest ancestor not
 //     less than it (the path is non-increasing downwards, so that is one ballot): one write round.
+typedef uint32_t vh_u32x16 __attribute__((ext_vector_type(16)));
+// node j of a heap held in a wave's registers (j = 64 r + lane: register r of lane j % 64); the
+// register index is uniform, so the compiler indexes the VGPRs (s_set_gpr_idx), no memory
+__device__ inline uint32_t vh_rget(const vh_u32x16& v, int j) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v[j >> 6], j & 63);
+}
+__device__ inline void vh_rset(vh_u32x16& v, int j, uint32_t x, int lane) {
+  const uint32_t w = v[j >> 6];
+  v[j >> 6] = lane == (j & 63) ? x : w;
+}
+
+// __sort_heap on a heap of at most 1024 elements held in registers: libstdc++'s __pop_heap /
+// __adjust_heap / __push_heap literally, every access a register read or write (no LDS latency
+// on the dependent chain)
+__device__ inline void vh_sort_heap_regs(uint32_t* E, int lo, int len) {
+  const int lane = threadIdx.x & 63;
+  const VhLess less;
+  vh_u32x16 v;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = r * 64 + lane < len ? E[lo + r * 64 + lane] : 0u;
+  for (int last = len - 1; last > 0; --last) {
+    const uint32_t value = vh_rget(v, last);
+    vh_rset(v, last, vh_rget(v, 0), lane);
+    const int n = last;  // __adjust_heap(first, 0, n, value)
+    int hole = 0, second = 0;
+    while (second < (n - 1) / 2) {
+      second = 2 * (second + 1);
+      const uint32_t a = vh_rget(v, second), b = vh_rget(v, second - 1);
+      uint32_t c = a;
+      if (less(a, b)) {
+        second--;
+        c = b;
+      }
+      vh_rset(v, hole, c, lane);
+      hole = second;
+    }
+    if ((n & 1) == 0 && second == (n - 2) / 2) {
+      second = 2 * (second + 1);
+      vh_rset(v, hole, vh_rget(v, second - 1), lane);
+      hole = second - 1;
+    }
+    int parent = (hole - 1) / 2;  // __push_heap(first, hole, 0, value)
+    while (hole > 0) {
+      const uint32_t pv = vh_rget(v, parent);
+      if (!less(pv, value)) break;
+      vh_rset(v, hole, pv, lane);
+      hole = parent;
+      parent = (hole - 1) / 2;
+    }
+    vh_rset(v, hole, value, lane);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    if (r * 64 + lane < len) E[lo + r * 64 + lane] = v[r];
+}
+
 __device__ inline void vh_heap_sort_wave(uint32_t* E, int lo, int hi) {
   const int lane = threadIdx.x & 63;
   const VhLess less;
@@ -234,6 +290,11 @@ __device__ inline void vh_heap_sort_wave(uint32_t* E, int lo, int hi) {
       for (int p = b - lane; p >= a; p -= 64) ss_adjust_heap(E, lo, p, len, E[lo + p], less);
       ss_wave_fence();
     }
+  }
+  if (len <= 1024) {
+    vh_sort_heap_regs(E, lo, len);
+    ss_wave_fence();
+    return;
   }
   // lane l < 62 of a look-ahead: depth j = 1 .. 5 below the hole, index t in that depth
   const int lj = 31 - __clz(lane + 2), lt = lane + 2 - (1 << lj);
@@ -677,9 +738,15 @@ __device__ inline void vh_sort(uint32_t* lds, int n, const VxHot& H, int* err, u
   unsigned long long tp = __builtin_readcyclecounter(), t_drain = 0;
   const VhLds L = vh_layout<NT>(lds, n);
   VhCtl* C = L.C;
-  for (int i = tid; i < n; i += NT) {
-    const uint32_t r = H.rk[i];
-    L.E[i] = ((r >> 1) << 16) | ((r & 1u) << 15) | (uint32_t)i;
+  for (int i0 = tid; i0 < n; i0 += 8 * NT) {  // 8 loads in flight per thread
+    uint32_t r[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) r[u] = i0 + u * NT < n ? H.rk[i0 + u * NT] : 0u;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * NT;
+      if (i < n) L.E[i] = ((r[u] >> 1) << 16) | ((r[u] & 1u) << 15) | (uint32_t)i;
+    }
   }
   const int D0 = n > 1 ? 2 * (31 - __clz(n)) : 0;  // 2 * __lg(n)
   if (tid == 0) {
@@ -784,9 +851,15 @@ __device__ inline bool vh_centroids(const PF& P, float4* out, const VxHot& H, co
     return true;
   }
   const uint32_t big_cap = lds_words - nl;
-  for (uint32_t j = tid; j < nl; j += NT) {
-    const uint32_t i = H.hl[j];
-    Lh[j] = (H.fpos[i] << 15) | i;
+  for (uint32_t j0 = tid; j0 < nl; j0 += 8 * NT) {  // 8 gathers in flight per thread
+    uint32_t ii[8], fp[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) ii[u] = j0 + u * NT < nl ? H.hl[j0 + u * NT] : 0u;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) fp[u] = j0 + u * NT < nl ? H.fpos[ii[u]] : 0u;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (j0 + u * NT < nl) Lh[j0 + u * NT] = (fp[u] << 15) | ii[u];
   }
   if (tid == 0) {
     M.nbig = 0;
