@@ -796,12 +796,13 @@ def main():
 
     def thread_rank_overhead(splan, pre, n_streams=8, steps=10):
         """the multi-rank schedule on this one GPU: R = 2, 3 ranks as host threads,
-        each a sharded handle of the first n_streams streams, exchanging through host-buffer
-        callbacks (loam_amd.comm.ThreadGroup); every rank's kernels share the GPU, so the time
+        each a sharded handle of the first n_streams streams, exchanging through the library's
+        device-ordered transport (loam_comm_create_local: collectives staged and summed on the
+        ranks' HIP streams, ordered by events); every rank's kernels share the GPU, so the time
         includes R times the redundant per-rank work plus the exchanges, against the unsharded
         handle on the same streams and frames"""
         import threading
-        from loam_amd.comm import ThreadGroup
+        from loam_amd.comm import Comm
         plan = [tuple(a[:n_streams] for a in step) for step in splan[:pre + steps]]
         um = BatchMapper(n_streams, device=local, max_map_points=args.map_points)
         run_steps(um, plan, 0, pre)
@@ -812,15 +813,17 @@ def main():
         u_rate = uit / (time.perf_counter() - t0)
         um.close()
         res = {"streams": n_streams, "steps": steps, "unsharded": round(u_rate, 1),
-               "transport": "host-buffer callbacks between threads (ThreadGroup), one GPU"}
+               "transport": "loam_comm_create_local: ranks as threads on one GPU, each collective staged and "
+                            "summed on the ranks' own HIP streams, ordered by events (threads meet only when they "
+                            "enqueue it)"}
         for R in (2, 3):
-            group = ThreadGroup(R)
+            comms = Comm.local_group(R, local)
             times, iters, errs = [0.0] * R, [0] * R, []
             start = threading.Barrier(R)
 
             def work(r):
                 try:
-                    m = BatchMapper(n_streams, device=local, max_map_points=args.map_points, comm=group.comm(r))
+                    m = BatchMapper(n_streams, device=local, max_map_points=args.map_points, comm=comms[r])
                     run_steps(m, plan, 0, pre)
                     torch.cuda.synchronize(local)
                     start.wait()
@@ -831,8 +834,7 @@ def main():
                     m.close()
                 except BaseException as e:  # noqa: BLE001 - recorded below
                     errs.append(repr(e))
-                    group.barrier.abort()
-                    start.abort()
+                    start.abort()  # (the other ranks' collectives fail at the group's timeout)
 
             th = [threading.Thread(target=work, args=(r,)) for r in range(R)]
             for t in th:
@@ -842,6 +844,8 @@ def main():
             if errs or any(t.is_alive() for t in th):
                 res[f"ranks_{R}"] = {"error": errs[0] if errs else "timeout"}
                 continue
+            for c in comms:
+                c.close()
             rate = iters[0] / max(times)
             res[f"ranks_{R}"] = {"value": round(rate, 1), "over_unsharded": round(rate / u_rate, 4),
                                  "ms_per_step": round(1e3 * max(times) / steps, 3)}

@@ -129,7 +129,7 @@ int32_t loam_scanreg_curvature(loam_scanreg* h, float* curv, int32_t* label, int
 /* device time of the last input (ms) */
 double loam_scanreg_ms(loam_scanreg* h);
 /* cumulative device cycle counters of the per-ring PCL-order VoxelGrid (k_sr_ringvox), summed
- * over rings and frames: [0] cycles of the std::sort emulation for the voxels of 3+ members,
+ * over rings and frames: [0] cycles of the sort emulation (libstdc++ introsort) for the voxels of 3+ members,
  * [1] of their centroids, [2] rings that had such a voxel; reset = 1 zeroes them after the copy.
  * Counted only in a handle created with LOAM_PHASE_COUNTERS=1 in the environment. */
 #define LOAM_SR_DEBUG_COUNTERS 8
@@ -259,7 +259,7 @@ int32_t loam_mapper_stats(loam_mapper* h, int32_t stream, loam_map_stats* st);
  * member lists + centroids, [46..47] of the latter: member lists, per-voxel sort + sums,
  * [48..49] arena compactions of the corner / surf maps (summed over streams), [50..52] exact
  * order (exact_voxel_order = 1) cube re-filters with a voxel of 3+ members: cycles of the pruned
- * std::sort emulation, of those voxels' centroids, filters (voxel_hot.h), [54..56] the same for
+ * sort emulation (libstdc++ introsort), of those voxels' centroids, filters (voxel_hot.h), [54..56] the same for
  * the stack VoxelGrids, [72..76] the cube emulation's elements heap-sorted literally, then cycles
  * of its setup, workgroup partitions, wave subtrees, positions, [77..81] the same for stacks,
  * [82..90] the cube emulation's wave partitions by length (<= 65, 129, 257, 513, 1025), wave
@@ -358,6 +358,13 @@ int32_t loam_comm_create(int32_t rank, int32_t size, const loam_comm_ops* ops, l
 int32_t loam_comm_rccl_unique_id(uint8_t* id);
 int32_t loam_comm_create_rccl(int32_t rank, int32_t size, const uint8_t* id, int32_t device,
                               loam_comm** out);
+/* `size` ranks of ONE process sharing one device (threads, one sharded handle each): out[r] is
+ * rank r's comm.  The collectives are ordered on the ranks' HIP streams by events (device-side
+ * staging, an on-stream sum in rank order); the host threads meet once per collective when they
+ * enqueue it and never wait for the device.  For running and measuring the multi-rank schedule
+ * on one GPU; each comm is destroyed on its own (the shared state goes with the last). */
+#define LOAM_LOCAL_MAX_RANKS 8
+int32_t loam_comm_create_local(int32_t size, int32_t device, loam_comm** out);
 int32_t loam_comm_destroy(loam_comm* c);
 /* collectives through a comm on a device buffer (for tests and callers' own exchanges) */
 int32_t loam_comm_allreduce_sum(loam_comm* c, void* d_buf, int64_t count, int32_t dtype,

@@ -1,7 +1,8 @@
 """GPU: the sharded LaserMapping (include/loam_core.h "Sharded LaserMapping").
 
 One mapping stream split over R ranks (threads of this process on the one GPU of the box,
-meeting in loam_amd.comm.ThreadGroup collectives; RCCL with one rank for the transport):
+meeting in loam_amd.comm.ThreadGroup collectives or in the library's device-ordered transport
+Comm.local_group; RCCL with one rank for the transport):
   - every rank ends every frame with the bit-identical pose (same all-reduced sums, same step);
   - poses, submap sizes, correspondence and LM iteration counts equal the unsharded mapper's;
   - the union of the ranks' cubes is the unsharded map, point for point (bit-exact), and every
@@ -46,10 +47,12 @@ def _stat_tuple(st):
             tuple(st.surf_num), st.lm[0].iterations, st.lm[1].iterations, tuple(st.center), st.valid_num)
 
 
-def _run_ranks(size, body):
-    """body(rank, comm) on `size` threads; returns the per-rank results, re-raises failures"""
-    group = ThreadGroup(size)
-    comms = [group.comm(r) for r in range(size)]
+def _run_ranks(size, body, transport="threads"):
+    """body(rank, comm) on `size` threads; returns the per-rank results, re-raises failures.
+    transport "threads": host-buffer callbacks meeting in Python (ThreadGroup); "device": the
+    library's device-ordered transport (Comm.local_group: on-stream staging and sums, events)"""
+    group = ThreadGroup(size) if transport == "threads" else None
+    comms = [group.comm(r) for r in range(size)] if group else Comm.local_group(size)
     res, errs = [None] * size, []
 
     def run(r):
@@ -57,7 +60,8 @@ def _run_ranks(size, body):
             res[r] = body(r, comms[r])
         except BaseException as e:  # noqa: BLE001
             errs.append(e)
-            group.barrier.abort()  # release the other ranks' collectives
+            if group:
+                group.barrier.abort()  # release the other ranks' collectives (device: they time out)
 
     th = [threading.Thread(target=run, args=(r,)) for r in range(size)]
     for t in th:
@@ -67,6 +71,9 @@ def _run_ranks(size, body):
     if errs:
         raise errs[0]
     assert all(not t.is_alive() for t in th)
+    if not group:
+        for c in comms:
+            c.close()
     return res
 
 
@@ -105,10 +112,10 @@ def test_single_rank_comm_matches_unsharded(seq, unsharded):
             assert np.array_equal(_rows(maps[which][cube]), _rows(pts))
 
 
-@pytest.mark.parametrize("size", [2, 3])
-def test_ranks_match_unsharded(seq, unsharded, size):
+@pytest.mark.parametrize("size,transport", [(2, "threads"), (3, "threads"), (2, "device"), (3, "device")])
+def test_ranks_match_unsharded(seq, unsharded, size, transport):
     ref, ref_maps = unsharded
-    res = _run_ranks(size, _sequence_body(seq))
+    res = _run_ranks(size, _sequence_body(seq), transport)
     for f in range(N_FRAMES):
         q0, t0 = res[0][0][f]
         for r in range(1, size):  # identical step on every rank

@@ -6,9 +6,15 @@
 #pragma once
 #include "common.h"
 
+namespace loam {
+struct LocalGroup;
+}
+
 struct loam_comm {
   int rank = 0, size = 1;
-  int kind = 0;  // 0 callbacks, 1 RCCL
+  int kind = 0;  // 0 callbacks, 1 RCCL, 2 ranks of one process on one device (loam_comm_create_local)
+  loam::LocalGroup* local = nullptr;
+  uint64_t seq = 0;  // kind 2: collectives this rank has enqueued
   loam_comm_ops ops{};
   void* nccl = nullptr;  // ncclComm_t
   int device = 0;

@@ -6,7 +6,10 @@
 // touches it.
 #include <dlfcn.h>
 
+#include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
 #include <mutex>
 
@@ -77,12 +80,126 @@ int32_t ensure_staging(loam_comm* c, size_t send_bytes, size_t recv_bytes) {
 
 namespace loam {
 
+// Ranks of one process sharing one device (loam_comm_create_local): the collectives are ordered
+// on the ranks' own HIP streams by events, and the host threads meet only when they enqueue (one
+// barrier per collective), never waiting for the device.  Collective k of rank r, buffers of
+// parity k & 1:
+//   1. wait until every rank has finished reading this parity's staging (collective k - 2),
+//      copy the input into its staging buffer, record evA[r];
+//   2. host barrier: every rank has enqueued step 1 of collective k;
+//   3. wait for every rank's evA, combine all ranks' staging buffers in rank order (a sum kernel
+//      for the all-reduce: every rank adds the same values in the same order, so the results are
+//      bit-identical; copies for the all-gather), record evB[r].
+struct LocalGroup {
+  int size = 1, device = 0;
+  int alive = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t generation = 0;
+  void* stage[2][LOAM_LOCAL_MAX_RANKS] = {};
+  size_t cap[2][LOAM_LOCAL_MAX_RANKS] = {};
+  hipEvent_t evA[2][LOAM_LOCAL_MAX_RANKS] = {};
+  hipEvent_t evB[2][LOAM_LOCAL_MAX_RANKS] = {};
+  bool usedB[2][LOAM_LOCAL_MAX_RANKS] = {};
+
+  bool broken = false;
+  // false: a rank did not arrive within the timeout (it failed or stopped); the group is broken
+  // and every later collective fails at once instead of hanging
+  bool barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    if (broken) return false;
+    const uint64_t g = generation;
+    if (++arrived == size) {
+      arrived = 0;
+      ++generation;
+      cv.notify_all();
+      return true;
+    }
+    if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return generation != g || broken; }) || broken) {
+      broken = true;
+      cv.notify_all();
+      return false;
+    }
+    return true;
+  }
+};
+
+struct LocalSum {
+  const void* src[LOAM_LOCAL_MAX_RANKS];
+};
+
+template <typename T>
+__global__ void k_local_sum(LocalSum in, int nsrc, T* out, int64_t count) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
+    T v = static_cast<const T*>(in.src[0])[i];
+    for (int q = 1; q < nsrc; ++q) v += static_cast<const T*>(in.src[q])[i];
+    out[i] = v;
+  }
+}
+
+// steps 1 and 2; returns the parity
+static int32_t local_stage(loam_comm* c, const void* d_in, size_t bytes, hipStream_t st, int* par) {
+  LocalGroup& G = *c->local;
+  const int r = c->rank, p = (int)(c->seq++ & 1);
+  *par = p;
+  for (int q = 0; q < G.size; ++q)
+    if (G.usedB[p][q]) LOAM_HIP(hipStreamWaitEvent(st, G.evB[p][q], 0));
+  if (G.cap[p][r] < bytes) {  // (grows rarely; hipFree waits for the device)
+    if (G.stage[p][r]) LOAM_HIP(hipFree(G.stage[p][r]));
+    G.stage[p][r] = nullptr;
+    G.cap[p][r] = 0;
+    LOAM_HIP(hipMalloc(&G.stage[p][r], bytes));
+    G.cap[p][r] = bytes;
+  }
+  LOAM_HIP(hipMemcpyAsync(G.stage[p][r], d_in, bytes, hipMemcpyDeviceToDevice, st));
+  LOAM_HIP(hipEventRecord(G.evA[p][r], st));
+  if (!G.barrier()) {
+    set_error("local comm: a rank did not reach the collective (group broken)");
+    return LOAM_ERR_SYNC;
+  }
+  for (int q = 0; q < G.size; ++q)
+    if (q != r) LOAM_HIP(hipStreamWaitEvent(st, G.evA[p][q], 0));
+  return LOAM_OK;
+}
+
+static int32_t local_allreduce(loam_comm* c, void* d_buf, int64_t count, int32_t dtype, hipStream_t st) {
+  LocalGroup& G = *c->local;
+  const size_t bytes = (size_t)count * dtype_size(dtype);
+  int p = 0;
+  TRY(local_stage(c, d_buf, bytes, st, &p));
+  LocalSum in{};
+  for (int q = 0; q < G.size; ++q) in.src[q] = G.stage[p][q];
+  const int blocks = (int)std::min<int64_t>(1024, (count + 255) / 256);
+  if (dtype == LOAM_DT_F64)
+    k_local_sum<double><<<blocks, 256, 0, st>>>(in, G.size, static_cast<double*>(d_buf), count);
+  else
+    k_local_sum<int32_t><<<blocks, 256, 0, st>>>(in, G.size, static_cast<int32_t*>(d_buf), count);
+  LOAM_HIP(hipGetLastError());
+  LOAM_HIP(hipEventRecord(G.evB[p][c->rank], st));
+  G.usedB[p][c->rank] = true;
+  return LOAM_OK;
+}
+
+static int32_t local_allgather(loam_comm* c, const void* d_send, void* d_recv, int64_t bytes, hipStream_t st) {
+  LocalGroup& G = *c->local;
+  int p = 0;
+  TRY(local_stage(c, d_send, (size_t)bytes, st, &p));
+  for (int q = 0; q < G.size; ++q)
+    LOAM_HIP(hipMemcpyAsync(static_cast<char*>(d_recv) + (size_t)q * bytes, G.stage[p][q], (size_t)bytes,
+                            hipMemcpyDeviceToDevice, st));
+  LOAM_HIP(hipEventRecord(G.evB[p][c->rank], st));
+  G.usedB[p][c->rank] = true;
+  return LOAM_OK;
+}
+
 int32_t comm_allreduce(loam_comm* c, void* d_buf, int64_t count, int32_t dtype, hipStream_t st) {
   if (!c || count < 0 || (dtype != LOAM_DT_F64 && dtype != LOAM_DT_I32)) {
     set_error("comm allreduce: bad arguments");
     return LOAM_ERR_ARG;
   }
   if (count == 0) return LOAM_OK;
+  if (c->kind == 2) return c->size == 1 ? LOAM_OK : local_allreduce(c, d_buf, count, dtype, st);
   if (c->kind == 1)  // RCCL runs even at one rank (the transport is then exercised by tests)
     return rccl_check(rccl().all_reduce(d_buf, d_buf, (size_t)count, dtype == LOAM_DT_F64 ? ncclFloat64 : ncclInt32,
                                         ncclSum, static_cast<ncclComm_t>(c->nccl), st),
@@ -113,6 +230,7 @@ int32_t comm_allgather(loam_comm* c, const void* d_send, void* d_recv, int64_t b
     return LOAM_ERR_ARG;
   }
   if (bytes == 0) return LOAM_OK;
+  if (c->kind == 2 && c->size > 1) return local_allgather(c, d_send, d_recv, bytes, st);
   if (c->kind == 1)
     return rccl_check(rccl().all_gather(d_send, d_recv, (size_t)bytes, ncclUint8, static_cast<ncclComm_t>(c->nccl), st),
                       "ncclAllGather");
@@ -196,8 +314,59 @@ int32_t loam_comm_create_rccl(int32_t rank, int32_t size, const uint8_t* id, int
   return LOAM_OK;
 }
 
+int32_t loam_comm_create_local(int32_t size, int32_t device, loam_comm** out) {
+  if (!out || size < 1 || size > LOAM_LOCAL_MAX_RANKS) {
+    loam::set_error("loam_comm_create_local: bad arguments");
+    return LOAM_ERR_ARG;
+  }
+  TRY(loam::ensure_device(device));
+  LOAM_HIP(hipSetDevice(device));
+  auto* G = new loam::LocalGroup;
+  G->size = size;
+  G->device = device;
+  G->alive = size;
+  for (int p = 0; p < 2; ++p)
+    for (int r = 0; r < size; ++r)
+      if (hipEventCreateWithFlags(&G->evA[p][r], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&G->evB[p][r], hipEventDisableTiming) != hipSuccess) {
+        loam::set_error("loam_comm_create_local: hipEventCreate failed");
+        return LOAM_ERR_HIP;
+      }
+  for (int r = 0; r < size; ++r) {
+    auto* c = new loam_comm;
+    c->rank = r;
+    c->size = size;
+    c->kind = 2;
+    c->local = G;
+    c->device = device;
+    out[r] = c;
+  }
+  return LOAM_OK;
+}
+
 int32_t loam_comm_destroy(loam_comm* c) {
   if (!c) return LOAM_ERR_ARG;
+  if (c->kind == 2 && c->local) {
+    loam::LocalGroup* G = c->local;
+    bool last;
+    {
+      std::lock_guard<std::mutex> lk(G->mu);
+      last = --G->alive == 0;
+    }
+    if (last) {
+      (void)hipSetDevice(G->device);
+      (void)hipDeviceSynchronize();
+      for (int p = 0; p < 2; ++p)
+        for (int r = 0; r < G->size; ++r) {
+          if (G->stage[p][r]) (void)hipFree(G->stage[p][r]);
+          if (G->evA[p][r]) (void)hipEventDestroy(G->evA[p][r]);
+          if (G->evB[p][r]) (void)hipEventDestroy(G->evB[p][r]);
+        }
+      delete G;
+    }
+    delete c;
+    return LOAM_OK;
+  }
   if (c->kind == 1 && c->nccl) {
     (void)hipSetDevice(c->device);
     (void)rccl().comm_destroy(static_cast<ncclComm_t>(c->nccl));

@@ -162,6 +162,7 @@ struct MapperDev {
   uint32_t* lm_sync;   // [B][2 rounds][LM_SYNC_WORDS] (lm.h)
   double* lm_xpub;     // [B][2 rounds][8]: eval point published to the workers
   uint32_t* tickets;  // [B]
+  uint32_t* lm_tick;  // [B] k_lm_eval's workgroups done (sharded: the last one reduces)
   // sharded mode (loam_mapper_create_sharded): this rank of nrank; map points are stored by
   // the rank owning their 4 m block (comm.h, shard_owner); blk_v: voxels per block edge
   uint32_t compact_at = 0;  // an arena whose tail passed this is compacted
@@ -1129,7 +1130,10 @@ __global__ void __launch_bounds__(CORR_THREADS) k_geom(MapperDev D, int round) {
 }
 
 // LM evaluation pass at the state's evaluation point (lm.h)
-__global__ void __launch_bounds__(LM_THREADS) k_lm_eval(MapperDev D, int round) {
+// reduce: sharded over several ranks, the stream's last workgroup to finish also sums the
+// stream's partials in a fixed order into lm_red[s] (then all-reduced over the ranks): plain
+// partial stores + agent-scope release + a ticket; the last acquires before it reads
+__global__ void __launch_bounds__(LM_THREADS) k_lm_eval(MapperDev D, int round, int reduce) {
   const int s = D.s0 + blockIdx.x / LM_EBLK, blk = blockIdx.x % LM_EBLK;
   const StreamFrame& F = D.fr[s];
   if (!F.active) return;
@@ -1139,19 +1143,26 @@ __global__ void __launch_bounds__(LM_THREADS) k_lm_eval(MapperDev D, int round) 
   // sharded: this rank's workgroups are blocks rank * LM_EBLK + blk of nrank * LM_EBLK
   lm_eval_block<LM_THREADS>(R, F.nc_stack + F.ns_stack, F.lm[round], D.rank * LM_EBLK + blk, D.nrank * LM_EBLK,
                             D.partials + ((size_t)s * LM_EBLK + blk) * LM_NACC);
-}
-
-// sharded: this rank's partials -> lm_red[s] (fixed order), then all-reduced over the ranks
-__global__ void __launch_bounds__(64) k_lm_reduce(MapperDev D, int round) {
-  const int s = D.s0 + blockIdx.x;
-  const StreamFrame& F = D.fr[s];
-  if (!F.active || F.lm[round].status == LM_DONE) return;
-  const int lane = threadIdx.x;
-  if (lane < LM_NACC) {
+  if (!reduce || F.lm[round].status == LM_DONE) return;  // (uniform over the stream's workgroups)
+  __shared__ int last;
+  __syncthreads();  // this workgroup's partial stored
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const uint32_t t = __hip_atomic_fetch_add(&D.lm_tick[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == (uint32_t)LM_EBLK - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(&D.lm_tick[s], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (every reading wave)
+  if (threadIdx.x < LM_NACC) {
     const double* p = D.partials + (size_t)s * LM_EBLK * LM_NACC;
     double v = 0.0;
-    for (int c = 0; c < LM_EBLK; ++c) v += p[(size_t)c * LM_NACC + lane];
-    D.lm_red[(size_t)s * LM_NACC + lane] = v;
+    for (int c = 0; c < LM_EBLK; ++c) v += p[(size_t)c * LM_NACC + threadIdx.x];
+    D.lm_red[(size_t)s * LM_NACC + threadIdx.x] = v;
   }
 }
 
@@ -2074,6 +2085,7 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   ALLOC(D.lm_sync, B * 2 * LM_SYNC_WORDS);
   ALLOC(D.lm_xpub, B * 2 * 8);
   ALLOC(D.tickets, B);
+  ALLOC(D.lm_tick, B);
   ALLOC(h->d_map_off, 2 * NCUBE + 1);
   ALLOC(h->d_new_off, B * 2 * (NCUBE + 1));
   if (D.sharded) {
@@ -2606,11 +2618,10 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
       LAUNCH(FAM_LM, k_lm_round<<<lm_padded(B) * h->lm_G, LM_THREADS, 0, st>>>(D, round, h->lm_G));
     } else {
       for (int it = 0; it < 5; ++it) {  // iteration 0 + max_num_iterations = 4 candidates
-        LAUNCH(FAM_LM, k_lm_eval<<<B * LM_EBLK, LM_THREADS, 0, st>>>(D, round));
-        if (D.sharded) {  // per Ceres iteration: all-reduce of the 6x6 normal equations
-          LAUNCH(FAM_LM, k_lm_reduce<<<B, 64, 0, st>>>(D, round));
-          TRY(comm_allreduce(h->comm, D.lm_red, (int64_t)B * LM_NACC, LOAM_DT_F64, st));
-        }
+        // sharded: evaluation + this rank's sums (last workgroup), then per Ceres iteration the
+        // all-reduce of the 6x6 normal equations
+        LAUNCH(FAM_LM, k_lm_eval<<<B * LM_EBLK, LM_THREADS, 0, st>>>(D, round, D.sharded ? 1 : 0));
+        if (D.sharded) TRY(comm_allreduce(h->comm, D.lm_red, (int64_t)B * LM_NACC, LOAM_DT_F64, st));
         LAUNCH(FAM_LM, k_lm_step<<<B, 64, 0, st>>>(D, round));
       }
     }

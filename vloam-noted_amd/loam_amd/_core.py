@@ -126,6 +126,7 @@ SIGNATURES = {
     "loam_comm_create": (c_i32, [c_i32, c_i32, vp, ctypes.POINTER(vp)]),
     "loam_comm_rccl_unique_id": (c_i32, [vp]),
     "loam_comm_create_rccl": (c_i32, [c_i32, c_i32, vp, c_i32, ctypes.POINTER(vp)]),
+    "loam_comm_create_local": (c_i32, [c_i32, c_i32, ctypes.POINTER(vp)]),
     "loam_comm_destroy": (c_i32, [vp]),
     "loam_comm_allreduce_sum": (c_i32, [vp, vp, ctypes.c_int64, c_i32, vp]),
     "loam_comm_allgather": (c_i32, [vp, vp, vp, ctypes.c_int64, vp]),

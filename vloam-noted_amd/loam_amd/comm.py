@@ -8,6 +8,9 @@ sums.  Transports:
 - ``Comm.rccl(rank, size, uid, device)`` — RCCL over xGMI, collectives enqueued on the
   mapper's HIP stream (no host synchronisation).  ``Comm.rccl_unique_id()`` on rank 0, shared
   by the caller (``bench.py`` uses torch.distributed's object broadcast).
+- ``Comm.local_group(size, device)`` — ranks as threads of one process on one device: the
+  library stages each collective on the device and orders it with events on the ranks' own HIP
+  streams (the threads meet only when they enqueue; no device synchronisation).
 - ``ThreadGroup(size).comm(rank)`` — ranks as threads of one process (one GPU or several):
   host-buffer callbacks meeting at a barrier, summed in rank order.
 - ``TorchDistComm.create()`` — host-buffer callbacks over an initialised torch.distributed group
@@ -130,6 +133,15 @@ class Comm:
         h = ctypes.c_void_p()
         check(lib().loam_comm_create(rank, size, ctypes.byref(ops), ctypes.byref(h)))
         return cls(h, rank, size, keep=(ops, ops.allreduce_sum, ops.allgather, ar, ag))
+
+    @classmethod
+    def local_group(cls, size, device=0):
+        """``size`` ranks of this process on one device (one thread and one sharded handle per
+        rank): the collectives are ordered on the ranks' HIP streams by events, the threads meet
+        only when they enqueue one (loam_comm_create_local)"""
+        hs = (ctypes.c_void_p * size)()
+        check(lib().loam_comm_create_local(size, device, hs))
+        return [cls(ctypes.c_void_p(hs[r]), r, size) for r in range(size)]
 
     @classmethod
     def single(cls):
