@@ -905,6 +905,7 @@ __global__ void __launch_bounds__(CORR_THREADS) __attribute__((amdgpu_waves_per_
     }
     const float fx = floorf(q.x), fy = floorf(q.y), fz = floorf(q.z);
     const int qx = (int)fx, qy = (int)fy, qz = (int)fz;
+    const float lx = q.x - fx, hx = (fx + 1.0f) - q.x;
     const float ly = q.y - fy, hy = (fy + 1.0f) - q.y;
     const float lz = q.z - fz, hz = (fz + 1.0f) - q.z;
     // the x runs, shared by every row: cells qx - 1 .. qx + 1 split by cube and brick, and a cell
@@ -935,18 +936,28 @@ __global__ void __launch_bounds__(CORR_THREADS) __attribute__((amdgpu_waves_per_
       }
       push(pbi, la, lb);
     }
-    // rows (dy, dz), coded (dy + 1) | (dz + 1) << 2: centre first, then the four faces, then the
-    // four corners (the 5th distance shrinks early and prunes the rows that follow)
-    for (int ob = 0; ob < 9; ob += CS ? L : 1) {
+    // rows (dy, dz), coded (dy + 1) | (dz + 1) << 2: the centre cell, the centre row's two x
+    // neighbours, the four face rows, the four corner rows (the 5th distance shrinks early and
+    // prunes what follows); in each row only the x cells within the bound
+    for (int ob = 0; ob < 10; ob += CS ? L : 1) {
       const int o = CS ? ob + gsub : ob;
-      const uint32_t code = (uint32_t)((0xA82064915ull >> (4 * (o < 9 ? o : 0))) & 15u);  // 5 1 9 4 6 0 2 8 10
+      const uint32_t code = (uint32_t)((0xA820649155ull >> (4 * (o < 10 ? o : 0))) & 15u);  // 5 5 1 9 4 6 0 2 8 10
       const int dy = (int)(code & 3u) - 1, dz = (int)(code >> 2) - 1;
       const float gy = dy < 0 ? ly : (dy > 0 ? hy : 0.f);
       const float gz = dz < 0 ? lz : (dz > 0 ? hz : 0.f);
       float bound = fminf(T.d[4], 1.0f) * 1.01f + 1e-6f;  // rounding margin
 #pragma unroll
       for (int o2 = 1; o2 < L; o2 <<= 1) bound = fminf(bound, __shfl_xor(bound, o2, 64));
-      if (o >= 9 || gy * gy + gz * gz > bound) continue;
+      const float gyz = gy * gy + gz * gz;
+      if (o >= 10 || gyz > bound) continue;
+      // x cells of this row within the bound: [xa0, xb0]; the centre row is visited twice, its
+      // centre cell first, then its x neighbours as two intervals
+      const int xa0 = o == 0 ? qx : (lx * lx + gyz <= bound ? qx - 1 : qx);
+      const int xb0 = o == 0 ? qx : (hx * hx + gyz <= bound ? qx + 1 : qx);
+      for (int it = 0; it < (o == 1 ? 2 : 1); ++it) {
+      const int xa = o == 1 ? (it == 0 ? xa0 : qx + 1) : xa0;
+      const int xb = o == 1 ? (it == 0 ? qx - 1 : xb0) : xb0;
+      if (xa > xb) continue;
       const int y = qy + dy, z = qz + dz;
       const int bj0 = floor_div50(y + 25) + F.cen[1], bk0 = floor_div50(z + 25) + F.cen[2];
       const int ay0 = y - ci_corner(bj0, F.cen[1]), az0 = z - ci_corner(bk0, F.cen[2]);
@@ -961,9 +972,11 @@ __global__ void __launch_bounds__(CORR_THREADS) __attribute__((amdgpu_waves_per_
         if (wy < 0 || wy > 4 || wz < 0 || wz > 2) continue;  // not in the submap
         for (int r = 0; r < nxr; ++r) {
           const uint32_t e14 = (uint32_t)(xr >> (14 * r)) & 0x3FFFu;
-          const int bi = bi0 - 1 + (int)(e14 & 3u), la = (int)((e14 >> 2) & 63u), lb = (int)(e14 >> 8);
+          const int bi = bi0 - 1 + (int)(e14 & 3u);
+          const int cx = ci_corner(bi, F.cen[0]);
+          const int la = max((int)((e14 >> 2) & 63u), xa - cx), lb = min((int)(e14 >> 8), xb - cx);
           const int wx = bi - c0;
-          if (wx < 0 || wx > 4) continue;
+          if (la > lb || wx < 0 || wx > 4) continue;
           const int sl = slot_of[wx * 15 + wy * 3 + wz];
           if (sl < 0) continue;
           const uint32_t n = WM.n[sl];
@@ -1006,6 +1019,7 @@ __global__ void __launch_bounds__(CORR_THREADS) __attribute__((amdgpu_waves_per_
             near5_offer(T, fdist2(q.x, q.y, q.z, p.x, p.y, p.z), kb + __float_as_int(p.w) * D.nrank, (int)(off + k));
           }
         }
+      }
       }
     }
 #pragma unroll
