@@ -1,0 +1,74 @@
+"""The LM hand-off without fences (the default build) against the memory model's fence recipe.
+
+The persistent LM (lm.h, `k_lm_round`) hands partial sums and the evaluation point between
+workgroups with agent-scope atomic stores, a `vmcnt(0)` drain and relaxed polls: correct on
+gfx950 by how its L2 / write-through path behaves, not by the HIP memory model.
+`libloam_core_fences.so` is the same source built with LM_HANDOFF_FENCES=1 (release / acquire
+fences, cdna_hip_programming.md §6 Guideline 16).  Both run the same free-running frames on
+several streams (persistent LM, hand-offs every pass) and must agree bit for bit: a stale read
+in the fence-free build would change a pose.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from helpers import run_sequence
+from loam_amd.mapping import BatchMapper
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FENCES = os.path.join(ROOT, "vloam-noted_amd", "loam_amd", "_lib", "libloam_core_fences.so")
+N_STREAMS = 4
+
+CHILD = r"""
+import json, sys
+import numpy as np
+sys.path.insert(0, sys.argv[2])
+from loam_amd.mapping import BatchMapper
+d = np.load(sys.argv[1])
+n_frames, n_streams = int(d["n_frames"]), int(d["n_streams"])
+m = BatchMapper(n_streams)
+out = []
+for f in range(n_frames):
+    for s in range(n_streams):
+        k = (f + 3 * s) % n_frames
+        m.input(s, d[f"c{k}"], d[f"s{k}"], d[f"q{k}"], d[f"t{k}"])
+    m.solve()
+    out.append([np.concatenate(m.pose(s)).tolist() for s in range(n_streams)])
+print(json.dumps(out))
+"""
+
+
+def _run(m, d, n_frames, n_streams):
+    out = []
+    for f in range(n_frames):
+        for s in range(n_streams):
+            k = (f + 3 * s) % n_frames
+            m.input(s, d[f"c{k}"], d[f"s{k}"], d[f"q{k}"], d[f"t{k}"])
+        m.solve()
+        out.append([np.concatenate(m.pose(s)).tolist() for s in range(n_streams)])
+    return out
+
+
+def test_fence_free_handoff_matches_fenced_build(tmp_path):
+    if not os.path.exists(FENCES):
+        pytest.fail(f"{FENCES} missing: run make -C vloam-noted_amd")
+    seq = run_sequence(seed=5, n_frames=10)
+    d = {"n_frames": np.int64(len(seq)), "n_streams": np.int64(N_STREAMS)}
+    for k, rec in enumerate(seq):
+        d[f"c{k}"], d[f"s{k}"] = rec["corner"], rec["surf"]
+        d[f"q{k}"], d[f"t{k}"] = rec["q_wodom"], rec["t_wodom"]
+    path = tmp_path / "frames.npz"
+    np.savez(path, **d)
+    env = dict(os.environ, LOAM_CORE_LIB=FENCES)
+    r = subprocess.run([sys.executable, "-c", CHILD, str(path), os.path.join(ROOT, "vloam-noted_amd")],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    fenced = json.loads(r.stdout.strip().splitlines()[-1])
+    plain = _run(BatchMapper(N_STREAMS), dict(np.load(path)), len(seq), N_STREAMS)
+    assert np.array_equal(np.array(plain), np.array(fenced))

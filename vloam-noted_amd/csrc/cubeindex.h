@@ -1,66 +1,53 @@
 // cubeindex.h — persistent 1 m cell index of every map cube (replaces the per-frame KD-tree
-// build of laser_mapping.cpp:519-520), probe-free.
+// build of laser_mapping.cpp:519-520).
 //
 // A cube's content lives at arena[off .. off + n) in the reference order (VoxelGrid output
 // order: the submap index of laser_mapping.cpp:448-489 is sub_off[window slot] + position).
-// Its index is kept at the same offsets in two parallel arenas, so moving content (compaction)
-// moves its index verbatim:
-//   cpts[off + k]        the points grouped by 1 m cell, w = position in the cube (int bits)
-//   dir[8 off + ..]      (the ctab arena as u32 words, 8 per point slot) a brick directory:
-//     word 0             words used (the compaction copies that many)
-//     word 1             word offset of cstart (0: a tiny cube, no directory: scan all points)
-//     words 2 ..         per 64 bricks: occupancy bits (2 words) + occupied bricks before (1)
-//     CI_BE ..           per occupied brick (in brick order): its 64-bit cell mask + the index of
-//                        its first occupied cell
-//     cstart[0 .. cells] cpts position of each occupied cell (brick order, then bit order), and
-//                        the total
-// Cells are grouped into bricks of 16 x 2 x 2 (x fastest within a brick: the bit of cell
-// (x, y, z) is (2 (z & 1) + (y & 1)) 16 + (x & 15)), so the cells x - 1 .. x + 1 of a row (y, z)
-// that fall in one brick are a contiguous bit range and their points one contiguous run of cpts:
-// a query's 3 x 3 x 3 neighbourhood is 9 row segments (two where a row crosses a brick or cube
-// boundary), each found by three dependent loads (occupancy word, brick entry, cstart pair) and
-// no probing.  Directory size: 131 + 3 (bricks) + (cells) + 1 words <= 8 n for n >= CI_TINY.
+// Its index is kept at the same offsets in two parallel arenas:
+//   cpts[off + k]      the points sorted by 1 m cell, w = position in the cube (int bits)
+//   ctab[4*off + h]    open-addressing table of the cube's cells, T = next_pow2(2n) <= 4n
+//                      entries: x = local cell key | count << 18, y = start (in cpts)
+// so moving content (compaction) moves its index verbatim and the table size needs no
+// descriptor.  The index is rebuilt whenever a cube's content is rewritten (k_revox) or
+// set through the API; unchanged cubes keep theirs across frames.
 //
 // Local cell coordinates are relative to the cube's lower corner, (cube - cen) * 50 - 25 m
 // per axis.  The reference's cube rule (laser_mapping.cpp:747-756: int((v + 25) / 50), minus
 // one when v + 25 < 0) files a point with v + 25 an exact negative multiple of 50 in the cube
-// below, where its local coordinate is 50: 51 cells per axis.
+// below, where its local coordinate is 50: 6 bits per axis hold 0..50.
 #pragma once
 #include "common.h"
 #include "device_math.h"
 
 namespace loam {
 
-constexpr int CI_BX = 4, CI_BY = 26, CI_BZ = 26;            // bricks per axis (16 x 2 x 2 cells each)
-constexpr int CI_NB = CI_BX * CI_BY * CI_BZ;                 // 2704
-constexpr int CI_NW = (CI_NB + 63) / 64;                     // 43 occupancy words
-constexpr int CI_OCC = 2;                                    // occupancy (lo, hi, before) triples
-constexpr int CI_BE = CI_OCC + 3 * CI_NW;                    // 131: brick entries (lo, hi, first cell)
-constexpr uint32_t CI_TINY = 40;                             // fewer points: no directory
-constexpr int CI_LDS_WORDS = 2 * CI_NB + CI_NB + 64;         // build scratch before the cell counts
+constexpr uint32_t CI_EMPTY = 0xFFFFFFFFu;
+constexpr uint32_t CI_KEY_MASK = (1u << 18) - 1;
+constexpr int CI_LDS_MAX_T = 32768;  // table entries built in LDS (one packed word each)
 
-__host__ __device__ inline uint32_t ci_max_words(uint32_t n) { return 8u * n; }
+__host__ __device__ inline uint32_t ci_table_size(uint32_t n) {
+  uint32_t t = 1;
+  while (t < 2 * n) t <<= 1;
+  return t;
+}
+__device__ inline uint32_t ci_hash(uint32_t k, uint32_t mask) {
+  uint32_t h = k * 0x9E3779B1u;
+  h ^= h >> 15;
+  return h & mask;
+}
 // lower corner (integer metres) of the cube whose grid index is c along an axis with centre cen
 __device__ inline int ci_corner(int c, int cen) { return (c - cen) * 50 - 25; }
-__device__ inline void ci_local(const float4& p, const int corner[3], int l[3]) {
-  l[0] = ((int)floorf(p.x) - corner[0]) & 63;
-  l[1] = ((int)floorf(p.y) - corner[1]) & 63;
-  l[2] = ((int)floorf(p.z) - corner[2]) & 63;
+__device__ inline uint32_t ci_local_key(const float4& p, const int corner[3]) {
+  const int lx = (int)floorf(p.x) - corner[0], ly = (int)floorf(p.y) - corner[1], lz = (int)floorf(p.z) - corner[2];
+  return (uint32_t)(lx & 63) | ((uint32_t)(ly & 63) << 6) | ((uint32_t)(lz & 63) << 12);
 }
-__host__ __device__ inline uint32_t ci_brick(int lx, int ly, int lz) {
-  return (uint32_t)(((lz >> 1) * CI_BY + (ly >> 1)) * CI_BX + (lx >> 4));
-}
-__host__ __device__ inline uint32_t ci_bit(int lx, int ly, int lz) {
-  return (uint32_t)((((lz & 1) << 1) | (ly & 1)) << 4) | (uint32_t)(lx & 15);
-}
-__device__ inline uint64_t ci_below(uint32_t b) { return b ? (~0ull >> (64 - b)) : 0ull; }
 
 // block-wide exclusive scan (nthreads threads); ws: nthreads / 64 + 1 LDS words
 template <int nthreads>
 __device__ inline uint32_t ci_block_scan(uint32_t v, uint32_t* ws, uint32_t* total) {
   constexpr int W = nthreads / 64;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t inc = dpp_incl_scan_u(v);
+  const uint32_t inc = wave_incl_scan_u(v);
   if (lane == 63) ws[wid] = inc;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -79,175 +66,140 @@ __device__ inline uint32_t ci_block_scan(uint32_t v, uint32_t* ws, uint32_t* tot
   return r;
 }
 
-// Build the index of one cube (whole workgroup of nthreads; n points at pts).  lds: lds_words
-// words; the cell counters live there when the cells fit (lds_words - CI_LDS_WORDS of them),
-// else in the directory's own cstart array (global atomics).  Returns false when the directory
-// would not fit its 8 n words (n >= 2^16 points; fewer cannot overflow: 131 + 3 bricks + cells
-// + 1 <= 131 + 4 n + 1 <= 8 n for n >= CI_TINY); *words_out: the directory's words.
-template <int nthreads>
+// Build the index of one cube (whole workgroup of nthreads, n points at pts).  lds: at least
+// CI_LDS_MAX_T + nthreads / 64 + 1 words.  Cubes with 2n > CI_LDS_MAX_T build their
+// table in global memory.  Returns false if a cell holds more points than the entry can
+// count (2^14 - 1).
+template <int nthreads, int MAXT = CI_LDS_MAX_T>
 __device__ inline bool cube_index_build(const float4* pts, uint32_t n, const int corner[3], float4* cpts,
-                                        uint32_t* dir, uint32_t* lds, uint32_t lds_words,
-                                        unsigned long long* prof = nullptr, uint32_t* words_out = nullptr) {
+                                        uint2* ctab, uint32_t* lds, unsigned long long* prof = nullptr) {
   const int tid = threadIdx.x;
-  if (words_out) *words_out = n == 0 ? 0u : (n < CI_TINY ? 2u : 0u);
   if (n == 0) return true;
-  if (n < CI_TINY) {  // tiny: the points as they are, scanned whole
-    for (uint32_t i = tid; i < n; i += nthreads) {
-      const float4 p = pts[i];
-      cpts[i] = make_float4(p.x, p.y, p.z, __int_as_float((int)i));
+  const uint32_t T = ci_table_size(n), mask = T - 1;
+  uint32_t* ws = lds + MAXT;
+  bool ok = true;
+  if (prof && tid == 0 && T <= (uint32_t)MAXT && n < (1u << 14)) atomicAdd(prof, 0ull - __builtin_readcyclecounter());
+  if (T <= (uint32_t)MAXT && n < (1u << 14)) {  // counts fit the packed word
+    uint32_t* lent = lds;  // key | count << 18 (count < n <= 2^14)
+    for (uint32_t i = tid; i < T; i += nthreads) lent[i] = CI_EMPTY;
+    __syncthreads();
+    // 1. cells + per-point rank, kept in registers (n <= MAXT / 2 here); the keys first, so
+    //    every load is in flight before the first LDS atomic
+    constexpr int PER = (MAXT / 2 + nthreads - 1) / nthreads;
+    uint32_t sr[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const uint32_t i = tid + k * nthreads;
+      sr[k] = i < n ? ci_local_key(pts[i], corner) : CI_EMPTY;
     }
-    if (tid == 0) {
-      dir[0] = 2;
-      dir[1] = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (sr[k] == CI_EMPTY) continue;
+      const uint32_t key = sr[k];
+      uint32_t h = ci_hash(key, mask);
+      uint32_t rank;
+      while (true) {
+        const uint32_t old = atomicCAS(&lent[h], CI_EMPTY, key | (1u << 18));
+        if (old == CI_EMPTY) {
+          rank = 0;
+          break;
+        }
+        if ((old & CI_KEY_MASK) == key) {
+          rank = atomicAdd(&lent[h], 1u << 18) >> 18;
+          break;
+        }
+        h = (h + 1) & mask;
+      }
+      sr[k] = (h << 15) | rank;  // slot < 2^15, rank < n <= 2^14
     }
     __syncthreads();
-    return true;
-  }
-  const unsigned long long t0 = prof ? __builtin_readcyclecounter() : 0ull;
-  uint64_t* bmask = reinterpret_cast<uint64_t*>(lds);  // [CI_NB] cell masks
-  uint32_t* bfirst = lds + 2 * CI_NB;                   // [CI_NB] first cell index
-  uint32_t* ws = lds + 3 * CI_NB;                       // scan scratch (64 words)
-  uint32_t* lcnt = lds + CI_LDS_WORDS;                  // cell counters, when they fit
-  const uint32_t lcap = lds_words > (uint32_t)CI_LDS_WORDS ? lds_words - CI_LDS_WORDS : 0u;
-  for (int b = tid; b < CI_NB; b += nthreads) bmask[b] = 0ull;
-  __syncthreads();
-  // 1. occupied cells
-  for (uint32_t i0 = tid; i0 < n; i0 += 4 * nthreads) {
-    float4 p[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (i0 + u * nthreads < n) p[u] = pts[i0 + u * nthreads];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (i0 + u * nthreads >= n) continue;
-      int l[3];
-      ci_local(p[u], corner, l);
-      atomicOr(reinterpret_cast<unsigned long long*>(&bmask[ci_brick(l[0], l[1], l[2])]),
-               1ull << ci_bit(l[0], l[1], l[2]));
+    if (prof && tid == 0) atomicAdd(prof, __builtin_readcyclecounter());  // minus the start below
+    // 2. starts: exclusive scan of the counts over the slots a thread owns (tid, tid + nthreads,
+    //    ...: the cells' order in cpts is free, and the table writes coalesce); the LDS word
+    //    becomes the start
+    uint32_t sum = 0;
+    for (uint32_t h = tid; h < T; h += nthreads) {
+      const uint32_t e = lent[h];
+      if (e != CI_EMPTY) sum += e >> 18;
     }
+    uint32_t tot;
+    uint32_t pre = ci_block_scan<nthreads>(sum, ws, &tot);
+    for (uint32_t h = tid; h < T; h += nthreads) {
+      const uint32_t e = lent[h];
+      ctab[h] = make_uint2(e, pre);
+      lent[h] = pre;
+      if (e != CI_EMPTY) pre += e >> 18;
+    }
+    __syncthreads();
+    // 3. points by cell
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const uint32_t i = tid + k * nthreads;
+      if (i < n) {
+        const float4 p = pts[i];
+        cpts[lent[sr[k] >> 15] + (sr[k] & 0x7FFFu)] = make_float4(p.x, p.y, p.z, __int_as_float((int)i));
+      }
+    }
+    __syncthreads();
+    return ok;
+  }
+  // large cube: the same with the table in global memory (y = count, then start + fill)
+  for (uint32_t i = tid; i < T; i += nthreads) ctab[i] = make_uint2(CI_EMPTY, 0);
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += nthreads) {
+    const uint32_t key = ci_local_key(pts[i], corner);
+    uint32_t h = ci_hash(key, mask);
+    while (true) {
+      const uint32_t old = atomicCAS(&ctab[h].x, CI_EMPTY, key);
+      if (old == CI_EMPTY || old == key) break;
+      h = (h + 1) & mask;
+    }
+    atomicAdd(&ctab[h].y, 1u);
   }
   __syncthreads();
-  // 2. first cell of every brick, occupied bricks before it: one scan of (cells | bricks << 16)
-  constexpr int BPT = (CI_NB + nthreads - 1) / nthreads;  // bricks per thread (consecutive)
-  uint32_t v = 0;
-#pragma unroll
-  for (int k = 0; k < BPT; ++k) {
-    const int b = tid * BPT + k;
-    if (b < CI_NB) {
-      const uint64_t m = bmask[b];
-      v += (uint32_t)__popcll(m) | (m ? (1u << 16) : 0u);
-    }
+  uint32_t sum = 0;
+  for (uint32_t h = tid; h < T; h += nthreads) {
+    const uint2 e = ctab[h];
+    if (e.x != CI_EMPTY) sum += e.y;
   }
   uint32_t tot;
-  uint32_t pre = ci_block_scan<nthreads>(v, ws, &tot);  // (cells < 2^16 for n < 2^16; checked below)
-  const uint32_t ncell = tot & 0xFFFFu, nb = tot >> 16;
-  const uint32_t cs = (uint32_t)CI_BE + 3u * nb;  // cstart word offset
-  const uint32_t words = cs + ncell + 1;
-  if (n >= 65536u || words > ci_max_words(n)) return false;  // (uniform)
-  if (words_out) *words_out = words;
-  for (int k = 0; k < BPT; ++k) {
-    const int b = tid * BPT + k;
-    if (b >= CI_NB) break;
-    const uint64_t m = bmask[b];
-    bfirst[b] = pre & 0xFFFFu;
-    if (m) {
-      const uint32_t e = CI_BE + 3u * (pre >> 16);
-      dir[e] = (uint32_t)m;
-      dir[e + 1] = (uint32_t)(m >> 32);
-      dir[e + 2] = pre & 0xFFFFu;
-    }
-    pre += (uint32_t)__popcll(m) | (m ? (1u << 16) : 0u);
+  uint32_t pre = ci_block_scan<nthreads>(sum, ws, &tot);
+  for (uint32_t h = tid; h < T; h += nthreads) {
+    const uint2 e = ctab[h];
+    if (e.x == CI_EMPTY) continue;
+    ok &= e.y < (1u << 14);
+    ctab[h] = make_uint2(e.x | (e.y << 18), pre);
+    pre += e.y;
   }
-  // occupancy words: the thread of word w (w < 43) gathers its 64 bricks; the bricks before it
-  // are the first brick's scan value (bricks are consecutive per thread, 3 per thread at 1024)
   __syncthreads();
-  for (int w = tid; w < CI_NW; w += nthreads) {
-    uint64_t occ = 0;
-    for (int k = 0; k < 64; ++k) {
-      const int b = 64 * w + k;
-      if (b < CI_NB && bmask[b]) occ |= 1ull << k;
-    }
-    dir[CI_OCC + 3 * w] = (uint32_t)occ;
-    dir[CI_OCC + 3 * w + 1] = (uint32_t)(occ >> 32);
-  }
-  {
-    // occupied bricks before word w: a second small scan over the 43 words (one wave)
-    if (tid < 64) {
-      uint32_t c = 0;
-      if (tid < CI_NW)
-        for (int k = 0; k < 64; ++k) {
-          const int b = 64 * tid + k;
-          c += (b < CI_NB && bmask[b]) ? 1u : 0u;
-        }
-      const uint32_t inc = dpp_incl_scan_u(c);
-      if (tid < CI_NW) dir[CI_OCC + 3 * tid + 2] = inc - c;
-    }
-  }
-  // 3. cells: counts (LDS when they fit, else the cstart array itself), then exclusive starts
-  //    in place (cnt[ncell] = n)
-  const bool in_lds = ncell + 1 <= lcap;
-  uint32_t* cnt = in_lds ? lcnt : dir + cs;
-  for (uint32_t c = tid; c <= ncell; c += nthreads) cnt[c] = 0u;
-  __syncthreads();
-  auto cell_of = [&](const float4& p) -> uint32_t {
-    int l[3];
-    ci_local(p, corner, l);
-    const uint32_t b = ci_brick(l[0], l[1], l[2]);
-    return bfirst[b] + (uint32_t)__popcll(bmask[b] & ci_below(ci_bit(l[0], l[1], l[2])));
-  };
-  for (uint32_t i = tid; i < n; i += nthreads) atomicAdd(&cnt[cell_of(pts[i])], 1u);
-  __syncthreads();
-  {
-    constexpr int CPT = 16;  // consecutive cells per thread per pass
-    uint32_t base = 0;
-    for (uint32_t c0 = 0; c0 <= ncell; c0 += CPT * nthreads) {
-      const uint32_t a0 = c0 + tid * CPT;
-      uint32_t cc[CPT], sum = 0;
-#pragma unroll
-      for (int k = 0; k < CPT; ++k) {
-        cc[k] = a0 + k < ncell ? cnt[a0 + k] : 0u;
-        sum += cc[k];
-      }
-      uint32_t t2;
-      uint32_t x = ci_block_scan<nthreads>(sum, ws, &t2) + base;  // (its barriers order the reads)
-#pragma unroll
-      for (int k = 0; k < CPT; ++k) {
-        if (a0 + k <= ncell) {
-          cnt[a0 + k] = x;
-          if (in_lds) dir[cs + a0 + k] = x;
-        }
-        x += cc[k];
-      }
-      base += t2;
-      __syncthreads();
-    }
-  }
-  // 4. points by cell (the order inside a cell is free: a query keeps the (d, key) smallest)
-  for (uint32_t i = tid; i < n; i += nthreads) {
+  for (uint32_t i = tid; i < n; i += nthreads) {  // y: start -> start + count while filling
     const float4 p = pts[i];
-    const uint32_t pos = atomicAdd(&cnt[cell_of(p)], 1u);
+    const uint32_t key = ci_local_key(p, corner);
+    uint32_t h = ci_hash(key, mask);
+    while ((ctab[h].x & CI_KEY_MASK) != key) h = (h + 1) & mask;
+    const uint32_t pos = atomicAdd(&ctab[h].y, 1u);
     cpts[pos] = make_float4(p.x, p.y, p.z, __int_as_float((int)i));
   }
   __syncthreads();
-  if (!in_lds) {
-    // the fill moved every start to its cell's end (= the next cell's start): shift back by one,
-    // a chunk at a time (every read of a chunk before its writes)
-    for (int32_t c0 = (int32_t)ncell; c0 > 0; c0 -= nthreads) {
-      const int32_t c = c0 - tid;
-      const uint32_t prev = c >= 1 ? dir[cs + c - 1] : 0u;
-      __syncthreads();
-      if (c >= 1) dir[cs + c] = prev;
-      __syncthreads();
-    }
-    if (tid == 0) dir[cs] = 0u;
-  }
-  if (tid == 0) {
-    dir[0] = words;
-    dir[1] = cs;
+  for (uint32_t h = tid; h < T; h += nthreads) {
+    const uint2 e = ctab[h];
+    if (e.x != CI_EMPTY) ctab[h].y = e.y - (e.x >> 18);
   }
   __syncthreads();
-  if (prof && tid == 0) atomicAdd(prof, __builtin_readcyclecounter() - t0);
-  return true;
+  return ok;
+}
+
+// Look up cell (local key) in a cube's table: returns (start, count) or count 0
+__device__ inline uint2 ci_find(const uint2* ctab, uint32_t T, uint32_t key) {
+  const uint32_t mask = T - 1;
+  uint32_t h = ci_hash(key, mask);
+  for (uint32_t p = 0; p < T; ++p) {
+    const uint2 e = ctab[h];
+    if (e.x == CI_EMPTY) break;
+    if ((e.x & CI_KEY_MASK) == key) return make_uint2(e.y, e.x >> 18);
+    h = (h + 1) & mask;
+  }
+  return make_uint2(0, 0);
 }
 
 }  // namespace loam

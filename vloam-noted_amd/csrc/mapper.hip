@@ -136,7 +136,7 @@ struct MapperDev {
   float4* stack[2];
   float4* arena;  // [B][2 maps][2 arenas][map_cap]
   float4* carena; // same shape: each cube's points sorted by 1 m cell (cubeindex.h)
-  uint2* ctab;    // [B][2 maps][2 arenas][4 * map_cap]: each cube's brick directory (cubeindex.h)
+  uint2* ctab;    // [B][2 maps][2 arenas][4 * map_cap]: each cube's cell table
   uint2* cube_tab;  // [B][2 maps][NCUBE] (off, cnt) — current parity
   uint32_t* extra_flag;  // [B][2][NCUBE]
   int* knn_id;      // [5][B][2*max_in] neighbour ids (submap index) per query, -1: none
@@ -827,10 +827,15 @@ __device__ inline void near5_offer(Near5& T, float d, int id, int pos) {
 __device__ inline int floor_div50(int v) { return v >= 0 ? v / 50 : -((-v + 49) / 50); }
 
 struct WinMap {  // per (stream, map) window cubes, in LDS
-  uint32_t off[WIN_MAX], n[WIN_MAX], cs[WIN_MAX];  // cs: the directory's cstart offset (0: tiny cube)
+  uint32_t off[WIN_MAX], n[WIN_MAX], tsize[WIN_MAX];
   int sub[WIN_MAX];
 };
 
+// L lanes per query (L | 64): the lanes of a group visit the same cells and split each cell's
+// points; the pruning bound is the group minimum of the lanes' 5th distances (each bounds the
+// union's 5th from above, so it is safe), and a butterfly merge leaves the union's 5 nearest in
+// every lane.  The result is the L = 1 result (the minimum over (d, key) of the same
+// candidates); L > 1 shortens each query's chain of dependent loads.
 // block -> (stream, member): stream b % B, member b / B (a stream's blocks on one XCD, b % 8,
 // when B is a multiple of 8: they share that XCD's L2 copy of the stream's cell indexes)
 __device__ inline void corr_block(const MapperDev& D, int* s, int* blk) {
@@ -841,16 +846,11 @@ __device__ inline void corr_block(const MapperDev& D, int* s, int* blk) {
 #ifndef KNN_WAVES
 #define KNN_WAVES 7  // 72 VGPRs, 20 B spill outside the cell loop: 6 -> 7 waves, correspondence -8%
 #endif
-// Exact 5-NN of every query over the submap (laser_mapping.cpp:554, :633) in the cubes' brick
-// directories (cubeindex.h).  A query's 3 x 3 x 3 cells are 9 rows (dy, dz) of three x cells;
-// the x cells of a row that share a cube and a brick are one run of points, found by three
-// dependent loads (occupancy word, brick entry, cstart pair).  Rows are taken centre first, then
-// the face rows, then the corner rows, each skipped when its gap (y, z only) exceeds the bound
-// min(5th distance, 1 m) (+ rounding margin): the points of skipped rows cannot enter an
-// accepted 5-NN, and a superset of the pruned cells changes nothing (the 5 smallest (d, key) of
-// the candidates, then the 1 m test, :557, :642).
-// L = 1: one lane per query.  CS (L = 8, few streams): the 8 lanes of a query take different
-// rows, with the group minimum of their 5th distances as the shared bound, and merge at the end.
+// CS (cell split): the L lanes of a query take different cells, lane g the cells g, g + L, ...
+// of the nearest-first order, each scanning all of its cell's points, with the group minimum of
+// their 5th distances as the shared pruning bound: a query's chain of dependent probes is 27 / L
+// steps long instead of 27 (few streams leave the chip mostly idle: latency, not issue, bounds
+// the search).  Without CS the lanes share each cell and split its points.
 template <int L, bool CS = false>
 __global__ void __launch_bounds__(CORR_THREADS) __attribute__((amdgpu_waves_per_eu(CS ? 4 : KNN_WAVES, 8))) k_knn(MapperDev D, int round) {
   __shared__ WinMap W[2];
@@ -878,8 +878,7 @@ __global__ void __launch_bounds__(CORR_THREADS) __attribute__((amdgpu_waves_per_
       const uint2 cv = D.cube_tab[sm_index(s, m) * NCUBE + cube];
       W[m].off[tid] = cv.x;
       W[m].n[tid] = cv.y;
-      W[m].cs[tid] = cv.y ? reinterpret_cast<const uint32_t*>(ctab_base(D, s, m, F.arena_active[m]) + 4 * (size_t)cv.x)[1]
-                          : 0u;
+      W[m].tsize[tid] = cv.y ? ci_table_size(cv.y) : 0u;
       W[m].sub[tid] = F.sub_off[m][tid];
     }
   }
@@ -894,7 +893,7 @@ __global__ void __launch_bounds__(CORR_THREADS) __attribute__((amdgpu_waves_per_
     const int qi = m == 0 ? ridx : ridx - nc;
     const float4 q = to_map(X, D.stack[m][(size_t)s * D.max_in + qi]);
     const float4* cp = carena_base(D, s, m, F.arena_active[m]);
-    const uint32_t* dirs = reinterpret_cast<const uint32_t*>(ctab_base(D, s, m, F.arena_active[m]));
+    const uint2* ct = ctab_base(D, s, m, F.arena_active[m]);
     const WinMap& WM = W[m];
     Near5 T;
 #pragma unroll
@@ -908,118 +907,62 @@ __global__ void __launch_bounds__(CORR_THREADS) __attribute__((amdgpu_waves_per_
     const float lx = q.x - fx, hx = (fx + 1.0f) - q.x;
     const float ly = q.y - fy, hy = (fy + 1.0f) - q.y;
     const float lz = q.z - fz, hz = (fz + 1.0f) - q.z;
-    // the x runs, shared by every row: cells qx - 1 .. qx + 1 split by cube and brick, and a cell
-    // on a negative cube edge also in the cube below at local 50 (laser_mapping.cpp:747-756);
-    // 14 bits each: cube - bi0 + 1 (2), first local x (6), last local x (6)
-    const int bi0 = floor_div50(qx - 1 + 25) + F.cen[0];
-    uint64_t xr = 0;
-    int nxr = 0;
-    {
-      int pbi = 0, la = 0, lb = 0;
-      auto push = [&](int bi, int a0, int a1) {
-        xr |= (uint64_t)((uint32_t)(bi - bi0 + 1) | ((uint32_t)a0 << 2) | ((uint32_t)a1 << 8)) << (14 * nxr);
-        ++nxr;
-      };
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const int x = qx - 1 + k;
-        const int bi = floor_div50(x + 25) + F.cen[0];
-        const int lx = x - ci_corner(bi, F.cen[0]);
-        if (k > 0 && bi == pbi && (lx >> 4) == (la >> 4)) {
-          lb = lx;
-        } else {
-          if (k > 0) push(pbi, la, lb);
-          pbi = bi;
-          la = lb = lx;
-        }
-        if (x + 25 < 0 && (x + 25) % 50 == 0) push(bi - 1, 50, 50);
+    // points of cell (x, y, z) filed in cube (bi, bj, bk) at local (ax, ay, az)
+    auto scan = [&](int bi, int bj, int bk, int ax, int ay, int az) {
+      const int wx = bi - c0, wy = bj - c1, wz = bk - c2;
+      if (wx < 0 || wx > 4 || wy < 0 || wy > 4 || wz < 0 || wz > 2) return;  // not in the submap
+      const int sl = slot_of[wx * 15 + wy * 3 + wz];
+      if (sl < 0) return;
+      const uint32_t n = WM.n[sl];
+      if (n == 0) return;
+      const uint32_t off = WM.off[sl];
+      const uint2 e = ci_find(ct + 4 * (size_t)off, WM.tsize[sl],
+                              (uint32_t)ax | ((uint32_t)ay << 6) | ((uint32_t)az << 12));
+      ncand += e.y;
+      const int sub = WM.sub[sl];
+      for (uint32_t k = CS ? 0 : gsub; k < e.y; k += CS ? 1 : L) {
+        const uint32_t pos = off + e.x + k;
+        const float4 p = cp[pos];
+        // sharded: submap position x ranks + rank keeps the key unique (and equal to the
+        // unsharded key at one rank)
+        const int key = (sub + __float_as_int(p.w)) * D.nrank + D.rank;
+        near5_offer(T, fdist2(q.x, q.y, q.z, p.x, p.y, p.z), key, (int)pos);
       }
-      push(pbi, la, lb);
-    }
-    // rows (dy, dz), coded (dy + 1) | (dz + 1) << 2: the centre cell, the centre row's two x
-    // neighbours, the four face rows, the four corner rows (the 5th distance shrinks early and
-    // prunes what follows); in each row only the x cells within the bound
-    for (int ob = 0; ob < 10; ob += CS ? L : 1) {
+    };
+    for (int ob = 0; ob < 27; ob += CS ? L : 1) {
       const int o = CS ? ob + gsub : ob;
-      const uint32_t code = (uint32_t)((0xA820649155ull >> (4 * (o < 10 ? o : 0))) & 15u);  // 5 5 1 9 4 6 0 2 8 10
-      const int dy = (int)(code & 3u) - 1, dz = (int)(code >> 2) - 1;
+      const uint32_t code = cell_order_code(o < 27 ? o : 0);
+      const int dx = (int)(code & 3u) - 1, dy = (int)((code >> 2) & 3u) - 1, dz = (int)(code >> 4) - 1;
+      const float gx = dx < 0 ? lx : (dx > 0 ? hx : 0.f);
       const float gy = dy < 0 ? ly : (dy > 0 ? hy : 0.f);
       const float gz = dz < 0 ? lz : (dz > 0 ? hz : 0.f);
       float bound = fminf(T.d[4], 1.0f) * 1.01f + 1e-6f;  // rounding margin
 #pragma unroll
       for (int o2 = 1; o2 < L; o2 <<= 1) bound = fminf(bound, __shfl_xor(bound, o2, 64));
-      const float gyz = gy * gy + gz * gz;
-      if (o >= 10 || gyz > bound) continue;
-      // x cells of this row within the bound: [xa0, xb0]; the centre row is visited twice, its
-      // centre cell first, then its x neighbours as two intervals
-      const int xa0 = o == 0 ? qx : (lx * lx + gyz <= bound ? qx - 1 : qx);
-      const int xb0 = o == 0 ? qx : (hx * hx + gyz <= bound ? qx + 1 : qx);
-      for (int it = 0; it < (o == 1 ? 2 : 1); ++it) {
-      const int xa = o == 1 ? (it == 0 ? xa0 : qx + 1) : xa0;
-      const int xb = o == 1 ? (it == 0 ? qx - 1 : xb0) : xb0;
-      if (xa > xb) continue;
-      const int y = qy + dy, z = qz + dz;
-      const int bj0 = floor_div50(y + 25) + F.cen[1], bk0 = floor_div50(z + 25) + F.cen[2];
-      const int ay0 = y - ci_corner(bj0, F.cen[1]), az0 = z - ci_corner(bk0, F.cen[2]);
-      // variants: the row's own cube row, and on a negative edge also the cube below (local 50)
-      const uint32_t vmask = 1u | ((y + 25 < 0 && (y + 25) % 50 == 0) ? 2u : 0u) |
-                             ((z + 25 < 0 && (z + 25) % 50 == 0) ? 4u : 0u);
-      for (int v = 0; v < 4; ++v) {
-        if (((v & 1) && !(vmask & 2u)) || ((v & 2) && !(vmask & 4u))) continue;
-        const int bj = bj0 - (v & 1), bk = bk0 - ((v >> 1) & 1);
-        const int ay = (v & 1) ? 50 : ay0, az = (v & 2) ? 50 : az0;
-        const int wy = bj - c1, wz = bk - c2;
-        if (wy < 0 || wy > 4 || wz < 0 || wz > 2) continue;  // not in the submap
-        for (int r = 0; r < nxr; ++r) {
-          const uint32_t e14 = (uint32_t)(xr >> (14 * r)) & 0x3FFFu;
-          const int bi = bi0 - 1 + (int)(e14 & 3u);
-          const int cx = ci_corner(bi, F.cen[0]);
-          const int la = max((int)((e14 >> 2) & 63u), xa - cx), lb = min((int)(e14 >> 8), xb - cx);
-          const int wx = bi - c0;
-          if (la > lb || wx < 0 || wx > 4) continue;
-          const int sl = slot_of[wx * 15 + wy * 3 + wz];
-          if (sl < 0) continue;
-          const uint32_t n = WM.n[sl];
-          if (n == 0) continue;
-          const uint32_t off = WM.off[sl], cs = WM.cs[sl];
-          // sharded: submap position x ranks + rank keeps the key unique (and equal to the
-          // unsharded key at one rank)
-          const int kb = WM.sub[sl] * D.nrank + D.rank;
-          uint32_t s0, s1;
-          if (cs == 0) {  // tiny cube: every point, filtered by cell
-            s0 = 0;
-            s1 = n;
-          } else {
-            const uint32_t* dir = dirs + 8 * (size_t)off;
-            const uint32_t brick = ci_brick(la, ay, az), w = brick >> 6;
-            const uint64_t occ = ((uint64_t)dir[CI_OCC + 3 * w + 1] << 32) | dir[CI_OCC + 3 * w];
-            if (!((occ >> (brick & 63)) & 1ull)) continue;
-            const uint32_t rk = dir[CI_OCC + 3 * w + 2] + (uint32_t)__popcll(occ & ci_below(brick & 63));
-            const uint32_t* e = dir + CI_BE + 3 * rk;
-            const uint64_t mask = ((uint64_t)e[1] << 32) | e[0];
-            const uint32_t b1 = ci_bit(lb, ay, az) + 1;
-            const uint32_t ca = e[2] + (uint32_t)__popcll(mask & ci_below(ci_bit(la, ay, az)));
-            const uint32_t cb = e[2] + (uint32_t)__popcll(mask & (b1 >= 64 ? ~0ull : ci_below(b1)));
-            if (ca == cb) continue;
-            s0 = dir[cs + ca];
-            s1 = dir[cs + cb];
-          }
-          int corner[3];
-          corner[0] = ci_corner(bi, F.cen[0]);
-          corner[1] = ci_corner(bj, F.cen[1]);
-          corner[2] = ci_corner(bk, F.cen[2]);
-          for (uint32_t k = s0; k < s1; ++k) {
-            const float4 p = cp[off + k];
-            if (cs == 0) {
-              int l[3];
-              ci_local(p, corner, l);
-              if (l[0] < la || l[0] > lb || l[1] != ay || l[2] != az) continue;
-            }
-            ++ncand;
-            near5_offer(T, fdist2(q.x, q.y, q.z, p.x, p.y, p.z), kb + __float_as_int(p.w) * D.nrank, (int)(off + k));
-          }
+      if (o >= 27 || gx * gx + gy * gy + gz * gz > bound) continue;
+      const int x = qx + dx, y = qy + dy, z = qz + dz;
+      const int bi = floor_div50(x + 25) + F.cen[0], bj = floor_div50(y + 25) + F.cen[1],
+                bk = floor_div50(z + 25) + F.cen[2];
+      int cx[3] = {bi, bj, bk};
+      int lc[3];
+      const int cv[3] = {x, y, z};
+#pragma unroll
+      for (int a = 0; a < 3; ++a) lc[a] = cv[a] - ci_corner(cx[a], F.cen[a]);
+      scan(bi, bj, bk, lc[0], lc[1], lc[2]);
+      // the reference files points at an exact negative multiple of 50 (v + 25) in the cube
+      // below (laser_mapping.cpp:747-756): local coordinate 50 there
+      int edge = 0;
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+        if (cv[a] + 25 < 0 && (cv[a] + 25) % 50 == 0) edge |= 1 << a;
+      for (int e = edge; e; e = (e - 1) & edge) {
+        int b2[3], l2[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          b2[a] = (e >> a) & 1 ? cx[a] - 1 : cx[a];
+          l2[a] = (e >> a) & 1 ? 50 : lc[a];
         }
-      }
+        scan(b2[0], b2[1], b2[2], l2[0], l2[1], l2[2]);
       }
     }
 #pragma unroll
@@ -1548,16 +1491,14 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
   __syncthreads();  // res may lie in the index build's LDS
   int corner[3];
   cube_corner(cube, F.cen, corner);
-  uint32_t words = 0;
-  if (!cube_index_build<VX_THREADS>(ar + off, n, corner, carena_base(D, s, m, F.arena_active[m]) + off,
-                                    reinterpret_cast<uint32_t*>(ctab_base(D, s, m, F.arena_active[m]) + 4 * (size_t)off),
-                                    lds, LW, D.pdbg ? D.pdbg + 16 : nullptr, &words) &&
+  if (!cube_index_build<VX_THREADS, CI_LDS_MAX_T>(ar + off, n, corner, carena_base(D, s, m, F.arena_active[m]) + off,
+                                  ctab_base(D, s, m, F.arena_active[m]) + 4 * (size_t)off, lds, D.pdbg ? D.pdbg + 16 : nullptr) &&
       threadIdx.x == 0)
     atomicOr(&F.err, MAP_ERR_INDEX);
-  // read old content + new points, write the filtered cube, then its index (read it twice, write
-  // the cell-sorted copy and the directory)
+  // read old content + new points, write the filtered cube, then its index (read it, write
+  // the cell-sorted copy and the table)
   if (threadIdx.x == 0)
-    atomicAdd(&F.vx_bytes, 16ull * (cv.y + n_new) + 16ull * 3 * n + 4ull * words);
+    atomicAdd(&F.vx_bytes, 16ull * (cv.y + n_new) + 16ull * 3 * n + (n ? 8ull * ci_table_size(n) : 0ull));
   if (threadIdx.x == 0 && D.pdbg) {
     const unsigned long long t2 = __builtin_readcyclecounter();
     const int k = merged ? 0 : (append ? 2 : 1);
@@ -1592,7 +1533,7 @@ __global__ void __launch_bounds__(VX_THREADS) k_revox(MapperDev D) {
 // cell index of one cube whose content was set through the API (cen: the host's grid centre)
 __global__ void __launch_bounds__(VX_THREADS) k_cube_index(MapperDev D, int s, int m, int c0, int c1,
                                                            int3 cen) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
+  __shared__ __attribute__((aligned(16))) uint32_t lds[CI_LDS_MAX_T + VX_WAVES + 1];
   const int cube = c0 + blockIdx.x;
   if (cube >= c1) return;
   StreamFrame& F = D.fr[s];
@@ -1604,8 +1545,7 @@ __global__ void __launch_bounds__(VX_THREADS) k_cube_index(MapperDev D, int s, i
   const int active = F.arena_active[m];
   if (!cube_index_build<VX_THREADS>(arena_base(D, s, m, active) + cv.x, cv.y, corner,
                                     carena_base(D, s, m, active) + cv.x,
-                                    reinterpret_cast<uint32_t*>(ctab_base(D, s, m, active) + 4 * (size_t)cv.x), lds,
-                                    VX_LDS_WORDS) &&
+                                    ctab_base(D, s, m, active) + 4 * (size_t)cv.x, lds) &&
       threadIdx.x == 0)
     atomicOr(&F.err, MAP_ERR_INDEX);
 }
@@ -1657,17 +1597,17 @@ __global__ void k_compact_copy(MapperDev D, const uint32_t* new_off) {
   float4* dst = arena_base(D, s, m, 1 - F.arena_active[m]);
   const float4* csrc = carena_base(D, s, m, F.arena_active[m]);
   float4* cdst = carena_base(D, s, m, 1 - F.arena_active[m]);
-  const uint32_t* tsrc = reinterpret_cast<const uint32_t*>(ctab_base(D, s, m, F.arena_active[m]));
-  uint32_t* tdst = reinterpret_cast<uint32_t*>(ctab_base(D, s, m, 1 - F.arena_active[m]));
+  const uint2* tsrc = ctab_base(D, s, m, F.arena_active[m]);
+  uint2* tdst = ctab_base(D, s, m, 1 - F.arena_active[m]);
   for (int c = blockIdx.x; c < NCUBE; c += gridDim.x) {
     const uint2 cv = tab[c];
     for (uint32_t i = threadIdx.x; i < cv.y; i += blockDim.x) {
       dst[no[c] + i] = src[cv.x + i];
       cdst[no[c] + i] = csrc[cv.x + i];  // the cell index moves verbatim (offsets are local)
     }
-    if (cv.y) {  // the directory: its word 0 counts its words
-      const uint32_t T = tsrc[8 * (size_t)cv.x];
-      for (uint32_t h = threadIdx.x; h < T; h += blockDim.x) tdst[8 * (size_t)no[c] + h] = tsrc[8 * (size_t)cv.x + h];
+    if (cv.y) {
+      const uint32_t T = ci_table_size(cv.y);
+      for (uint32_t h = threadIdx.x; h < T; h += blockDim.x) tdst[4 * (size_t)no[c] + h] = tsrc[4 * (size_t)cv.x + h];
     }
   }
 }

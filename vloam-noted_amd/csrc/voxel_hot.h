@@ -39,7 +39,8 @@ namespace loam {
 constexpr int VH_BIG = 1024;      // longer segments: partitioned by the workgroup
 constexpr int VH_MAX_N = 30720;   // LDS-resident emulation up to this many points (30 per thread)
 constexpr int VH_CHUNK = VH_MAX_N / VX_THREADS;  // positions per thread of a workgroup partition
-constexpr int VH_ROOTS = 512;     // pending wave subtrees
+constexpr int VH_ROOTS = 512;     // wave subtrees listed per drain
+constexpr int VH_SHARE = 96;      // a wave lists the larger part of a partition when longer (others may take it)
 constexpr int VH_BIGC = 64;       // workgroup segments of one level (segments > VH_BIG are disjoint: <= 30)
 constexpr int VH_LIFO = 8;        // wave-local pending parts (smaller part first: depth <= 6)
 constexpr int VH_WAVE_W = VH_LIFO + 64;  // per wave: LIFO + the dup check's keys
@@ -55,7 +56,8 @@ struct VhLess {
 struct VhCtl {
   int hot[2], S[2], cut[2];  // per segment, double-buffered by segment parity
   int nbig[2];               // workgroup segments of this / the next level
-  int nroot, root_take;      // pending wave subtrees, the next one to claim
+  int nroot, root_take;      // wave subtrees listed, the next one to claim
+  int pending;               // listed subtrees not finished (a drain ends at 0)
   int dup;
   int err;
   int heap_el;  // elements heap-sorted literally (diagnostics)
@@ -218,136 +220,77 @@ __device__ inline int vh_partition_wave(uint32_t* E, uint16_t* Bs, int lo, int h
 //     touches the parent's subtree, so the parents of one depth (disjoint subtrees, all after
 //     the deeper ones) run on separate lanes;
 //   * each __pop_heap's hole descends to a leaf along the larger children (the right one unless
-//     right < left): the wave loads the 5 levels below the hole at once (62 lanes), decides every
-//     pair with one shuffle and one ballot, and follows the path in scalar registers; the path's
-//     values then shift up one place and __push_heap's value lands below the lowest ancestor not
-//     less than it (the path is non-increasing downwards, so that is one ballot): one write round.
-typedef uint32_t vh_u32x16 __attribute__((ext_vector_type(16)));
-// node j of a heap held in a wave's registers (j = 64 r + lane: register r of lane j % 64); the
-// register index is uniform, so the compiler indexes the VGPRs (s_set_gpr_idx), no memory
-__device__ inline uint32_t vh_rget(const vh_u32x16& v, int j) {
-  return (uint32_t)__builtin_amdgcn_readlane((int)v[j >> 6], j & 63);
-}
-__device__ inline void vh_rset(vh_u32x16& v, int j, uint32_t x, int lane) {
-  const uint32_t w = v[j >> 6];
-  v[j >> 6] = lane == (j & 63) ? x : w;
-}
-
-// __sort_heap on a heap of at most 1024 elements held in registers: libstdc++'s __pop_heap /
-// __adjust_heap / __push_heap literally, every access a register read or write (no LDS latency
-// on the dependent chain)
-__device__ inline void vh_sort_heap_regs(uint32_t* E, int lo, int len) {
-  const int lane = threadIdx.x & 63;
-  const VhLess less;
-  vh_u32x16 v;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = r * 64 + lane < len ? E[lo + r * 64 + lane] : 0u;
-  for (int last = len - 1; last > 0; --last) {
-    const uint32_t value = vh_rget(v, last);
-    vh_rset(v, last, vh_rget(v, 0), lane);
-    const int n = last;  // __adjust_heap(first, 0, n, value)
-    int hole = 0, second = 0;
-    while (second < (n - 1) / 2) {
-      second = 2 * (second + 1);
-      const uint32_t a = vh_rget(v, second), b = vh_rget(v, second - 1);
-      uint32_t c = a;
-      if (less(a, b)) {
-        second--;
-        c = b;
-      }
-      vh_rset(v, hole, c, lane);
-      hole = second;
-    }
-    if ((n & 1) == 0 && second == (n - 2) / 2) {
-      second = 2 * (second + 1);
-      vh_rset(v, hole, vh_rget(v, second - 1), lane);
-      hole = second - 1;
-    }
-    int parent = (hole - 1) / 2;  // __push_heap(first, hole, 0, value)
-    while (hole > 0) {
-      const uint32_t pv = vh_rget(v, parent);
-      if (!less(pv, value)) break;
-      vh_rset(v, hole, pv, lane);
-      hole = parent;
-      parent = (hole - 1) / 2;
-    }
-    vh_rset(v, hole, value, lane);
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r)
-    if (r * 64 + lane < len) E[lo + r * 64 + lane] = v[r];
-}
-
-__device__ inline void vh_heap_sort_wave(uint32_t* E, int lo, int hi) {
+//     right < left).  The wave loads the 5 levels below the hole at once (62 lanes) and decides
+//     every sibling pair with one DPP shift and one ballot; the scalar unit follows the path
+//     through the ballot bits (no lane reads on the chain) and keeps it as a bit code: path node
+//     j is (1 << j) - 1 + (the code's first j bits).  Then every lane loads its path node's child
+//     at once, the path's values shift up one place, and __push_heap's value lands below the
+//     lowest ancestor not less than it (the path is non-increasing downwards: one ballot).
+// __make_heap on E[lo, hi), one wave: the parents of one depth on separate lanes
+__device__ inline void vh_make_heap_wave(uint32_t* E, int lo, int hi) {
   const int lane = threadIdx.x & 63;
   const VhLess less;
   const int len = hi - lo;
-  if (len < 2) return;
-  {  // __make_heap
-    const int pmax = (len - 2) / 2;
-    for (int d = 31 - __clz(pmax + 1); d >= 0; --d) {
-      const int a = (1 << d) - 1, b = min(pmax, (1 << (d + 1)) - 2);
-      for (int p = b - lane; p >= a; p -= 64) ss_adjust_heap(E, lo, p, len, E[lo + p], less);
-      ss_wave_fence();
-    }
-  }
-  if (len <= 1024) {
-    vh_sort_heap_regs(E, lo, len);
+  const int pmax = (len - 2) / 2;
+  for (int d = 31 - __clz(pmax + 1); d >= 0; --d) {
+    const int a = (1 << d) - 1, b = min(pmax, (1 << (d + 1)) - 2);
+    for (int p = b - lane; p >= a; p -= 64) ss_adjust_heap(E, lo, p, len, E[lo + p], less);
     ss_wave_fence();
-    return;
   }
-  // lane l < 62 of a look-ahead: depth j = 1 .. 5 below the hole, index t in that depth
+}
+
+// __sort_heap on the heap E[lo, hi) in LDS, one wave
+__device__ inline void vh_sort_heap_wave(uint32_t* E, int lo, int hi) {
+  const int lane = threadIdx.x & 63;
+  const VhLess less;
+  // lane l < 62 of a look-ahead: depth lj = 1 .. 5 below the hole, index lt in that depth
   const int lj = 31 - __clz(lane + 2), lt = lane + 2 - (1 << lj);
-  for (int last = hi - 1; last > lo; --last) {  // __sort_heap
+  for (int last = hi - 1; last > lo; --last) {
     const int n = last - lo;
     const uint32_t v = E[last], top = E[lo];
     const int lim = (n - 1) / 2;
-    int h = 0, k = 0;   // hole; path length
-    uint32_t pv = 0;    // lane j < k: the value of path node j + 1 (the j-th child moved up)
-    int pp = 0;         //             its position
+    int h = 0, k = 0;  // hole; path length
+    uint32_t code = 0;  // the path's directions, first step highest (k <= 15)
     while (h < lim) {
       const int node = ((h + 1) << lj) - 1 + lt;
       const uint32_t x = (lane < 62 && node < n) ? E[lo + node] : 0u;
-      const uint32_t xr = dpp_from_next(x);  // the right sibling (left children: t even)
+      const uint32_t xr = dpp_from_next(x);  // the right sibling (left children: lt even)
       const uint64_t rw = __ballot(!less(xr, x));
       int tt = 0;
 #pragma unroll
       for (int jj = 0; jj < 5; ++jj) {
         if (h >= lim) break;
-        const int ll = (1 << (jj + 1)) - 2 + 2 * tt;  // lane of the left child
-        const int dir = (int)((rw >> ll) & 1ull);
-        const int child = 2 * h + 1 + dir;
-        const uint32_t cv = __builtin_amdgcn_readlane(x, ll + dir);
-        if (lane == k) {
-          pv = cv;
-          pp = child;
-        }
+        const int dir = (int)((rw >> ((1 << (jj + 1)) - 2 + 2 * tt)) & 1ull);
+        h = 2 * h + 1 + dir;
         tt = 2 * tt + dir;
-        h = child;
+        code = 2 * code + (uint32_t)dir;
         ++k;
       }
     }
     if ((n & 1) == 0 && h == (n - 2) / 2) {  // one child left
-      const int child = 2 * h + 1;
-      const uint32_t cv = E[lo + child];
-      if (lane == k) {
-        pv = cv;
-        pp = child;
-      }
-      h = child;
+      h = 2 * h + 1;
+      code = 2 * code;
       ++k;
     }
-    // __push_heap: v rises while its parent is less; path node j holds pv of lane j - 1 after the
-    // shift, so the hole stops at q = k - #{j < k : pv_j < v}
+    // lane j < k: path node j (its position hj) takes the value of path node j + 1 (pv)
+    const int j1 = lane + 1;
+    const int hj = lane == 0 || lane > k ? 0 : (1 << lane) - 1 + (int)(code >> (k - lane));
+    const int cj = j1 <= k ? (1 << j1) - 1 + (int)(code >> (k - j1)) : 0;
+    const uint32_t pv = lane < k ? E[lo + cj] : 0u;
+    // __push_heap: v rises while its parent is less; it stops at q = k - #{j < k : pv_j < v}
     const int q = k - __popcll(__ballot(lane < k && less(pv, v)));
-    const int hp = (int)dpp_from_prev((uint32_t)pp);  // position of path node j (lane j): node 0 is the root
-    const int hj = lane == 0 ? 0 : hp;
     ss_wave_fence();  // every read of this pop before its writes
     if (lane < q) E[lo + hj] = pv;
     if (lane == q) E[lo + hj] = v;
     if (lane == 0) E[last] = top;
     ss_wave_fence();
   }
+}
+
+__device__ inline void vh_heap_sort_wave(uint32_t* E, int lo, int hi) {
+  if (hi - lo < 2) return;
+  vh_make_heap_wave(E, lo, hi);
+  vh_sort_heap_wave(E, lo, hi);
 }
 
 // A depth-limit segment on one wave: heap-sorted literally when two members of one hot voxel lie
@@ -496,7 +439,7 @@ __device__ inline void vh_subtree64(uint32_t* E, int lo, int len, int d, uint32_
 
 // The subtree below one pending segment, one wave, no barriers
 __device__ inline void vh_wave_subtree(uint32_t* E, uint16_t* Bs, uint32_t root, uint32_t* wa, int* heap_el,
-                                       unsigned long long* dp = nullptr) {
+                                       VhCtl* C, uint32_t* roots, unsigned long long* dp = nullptr) {
   const int lane = threadIdx.x & 63;
   uint32_t* stk = wa;
   uint32_t* kb = wa + VH_LIFO;
@@ -522,8 +465,21 @@ __device__ inline void vh_wave_subtree(uint32_t* E, uint16_t* Bs, uint32_t root,
           const int sl = left_small ? lo : cut, sn = left_small ? l0 : l1;  // smaller part: now
           const int bl_ = left_small ? cut : lo, bn = left_small ? l1 : l0;  // larger: pending
           if (bn > SS_THRESHOLD) {
-            if (lane == 0 && top < VH_LIFO) stk[top] = vh_pack(bl_, bn, d - 1);
-            ++top;  // (overflow impossible: each pending part is larger than the current one)
+            int s = VH_ROOTS;
+            if (bn > VH_SHARE && lane == 0 && __hip_atomic_load(&C->nroot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < VH_ROOTS - 64) {
+              // listed for any wave: counted pending before it is visible
+              s = atomicAdd(&C->nroot, 1);
+              if (s < VH_ROOTS) {
+                atomicAdd(&C->pending, 1);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __hip_atomic_store(&roots[s], vh_pack(bl_, bn, d - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              }
+            }
+            s = __builtin_amdgcn_readfirstlane(s);
+            if (s >= VH_ROOTS) {  // kept by this wave
+              if (lane == 0 && top < VH_LIFO) stk[top] = vh_pack(bl_, bn, d - 1);
+              ++top;  // (overflow impossible: each kept part is larger than the current one)
+            }
             ss_wave_fence();
           }
           if (sn > SS_THRESHOLD) {
@@ -541,20 +497,49 @@ __device__ inline void vh_wave_subtree(uint32_t* E, uint16_t* Bs, uint32_t root,
   }
 }
 
-// Drain the pending wave subtrees (all waves), then reset the list.  Uniform call.
+// Drain the listed wave subtrees (all waves), then reset the list.  Uniform call.  A wave claims
+// list entries in order (a ticket); an entry not yet listed is waited for while some listed
+// subtree is unfinished (its partitions may list more: the larger part of a partition over
+// VH_SHARE elements), so one wave's deep subtree is shared out.  Entries are zero until listed
+// and zeroed when taken (the list starts zeroed, vh_sort).
 template <int NT>
 __device__ inline void vh_drain(const VhLds& L) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t* wa = L.wave + wid * VH_WAVE_W;
-  const int nroot = min(L.C->nroot, VH_ROOTS);
-  unsigned long long* dp = L.C->dprof;
+  VhCtl* C = L.C;
+  unsigned long long* dp = C->dprof;
+  if (threadIdx.x == 0) C->pending = min(C->nroot, VH_ROOTS);
+  __syncthreads();
   const unsigned long long t0 = __builtin_readcyclecounter();
   while (true) {
     int k = 0;
-    if (lane == 0) k = atomicAdd(&L.C->root_take, 1);
+    if (lane == 0) k = atomicAdd(&C->root_take, 1);
     k = __builtin_amdgcn_readfirstlane(k);
-    if (k >= nroot) break;
-    vh_wave_subtree(L.E, L.Bs, L.roots[k], wa, &L.C->heap_el, dp);
+    uint32_t item = 0;
+    for (uint32_t spins = 0;; ++spins) {
+      uint32_t it = 0;
+      int pend = 0;
+      if (lane == 0) {
+        pend = __hip_atomic_load(&C->pending, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        it = k < VH_ROOTS ? __hip_atomic_load(&L.roots[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0u;
+      }
+      it = __builtin_amdgcn_readfirstlane(it);
+      pend = __builtin_amdgcn_readfirstlane(pend);
+      if (it) {
+        item = it;
+        break;
+      }
+      if (pend == 0 || spins > (1u << 24)) break;  // (bounded: cannot run out)
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (!item) break;
+    if (lane == 0) L.roots[k] = 0u;
+    vh_wave_subtree(L.E, L.Bs, item, wa, &C->heap_el, C, L.roots, dp);
+    if (lane == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // its listings before its end
+      atomicSub(&C->pending, 1);
+    }
     if (dp && lane == 0) atomicAdd(dp + 8, 1ull);
   }
   if (dp && lane == 0) {
@@ -748,6 +733,8 @@ __device__ inline void vh_sort(uint32_t* lds, int n, const VxHot& H, int* err, u
       if (i < n) L.E[i] = ((r[u] >> 1) << 16) | ((r[u] & 1u) << 15) | (uint32_t)i;
     }
   }
+  for (int i = tid; i < VH_ROOTS; i += NT) L.roots[i] = 0u;
+  __syncthreads();  // (the entries are zero until listed: tid 0 lists below)
   const int D0 = n > 1 ? 2 * (31 - __clz(n)) : 0;  // 2 * __lg(n)
   if (tid == 0) {
     C->nbig[0] = C->nbig[1] = 0;
