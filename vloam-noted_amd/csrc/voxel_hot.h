@@ -41,7 +41,7 @@ constexpr int VH_MAX_N = 30720;   // LDS-resident emulation up to this many poin
 constexpr int VH_CHUNK = VH_MAX_N / VX_THREADS;  // positions per thread of a workgroup partition
 constexpr int VH_ROOTS = 512;     // wave subtrees listed per drain
 constexpr int VH_SHARE = 96;      // a wave lists the larger part of a partition when longer (others may take it)
-constexpr int VH_BIGC = 64;       // workgroup segments of one level (segments > VH_BIG are disjoint: <= 30)
+constexpr int VH_BIGC = 32;       // workgroup segments of one level (segments > VH_BIG are disjoint: <= 30)
 constexpr int VH_LIFO = 8;        // wave-local pending parts (smaller part first: depth <= 6)
 constexpr int VH_WAVE_W = VH_LIFO + 64;  // per wave: LIFO + the dup check's keys
 constexpr int VH_SMALL = 32;      // hot voxels up to this many members: summed by one thread
@@ -53,8 +53,15 @@ struct VhLess {
   __device__ bool operator()(uint32_t a, uint32_t b) const { return (a >> 16) < (b >> 16); }
 };
 
+struct VhLvl {  // the workgroup partitions of one level, all its segments at once
+  int tstart[VH_BIGC + 1];   // each segment's first thread (and the end)
+  int hot[VH_BIGC], S[VH_BIGC], cut[VH_BIGC];
+  uint32_t base[VH_BIGC], endv[VH_BIGC];  // the packed scan before the segment's first thread / after its last
+  int c;                     // positions per thread
+};
+
 struct VhCtl {
-  int hot[2], S[2], cut[2];  // per segment, double-buffered by segment parity
+  VhLvl lv;
   int nbig[2];               // workgroup segments of this / the next level
   int nroot, root_take;      // wave subtrees listed, the next one to claim
   int pending;               // listed subtrees not finished (a drain ends at 0)
@@ -555,53 +562,76 @@ __device__ inline void vh_drain(const VhLds& L) {
   __syncthreads();
 }
 
-// One segment [lo, hi) (m > VH_BIG) partitioned by the workgroup.  par: the segment's parity
-// (its VhCtl slot; the other slot is reset here for the next segment).  Returns the cut, or -1
-// when fewer than two hot elements lie in it.  Uniform.
+// Every segment of one workgroup level [lo, hi) (m > VH_BIG; L.bigl[cur], nb of them) partitioned
+// at once: segment s owns threads tstart[s] .. tstart[s + 1] - 1, each classifying c consecutive
+// positions (a chunk never crosses a segment) into two bit masks; one block scan of the packed
+// counts places every stop of every segment (offsets relative to the scan before the segment's
+// first thread), so a level costs four barriers whatever its segment count.  Per segment:
+// lv.cut[s], or -1 when fewer than two hot elements lie in it.  Uniform; lv.tstart / c, hot = S = 0
+// and cut = INT_MAX set by the caller.
 template <int NT, int CH>
-__device__ inline int vh_partition_wg_c(const VhLds& L, int lo, int hi, int par) {
+__device__ inline void vh_partition_level_c(const VhLds& L, int cur, int nb) {
   constexpr int NW = NT / 64;
   static_assert(CH <= 32, "chunk masks in one word");
+  static_assert(NW <= VX_WAVES, "scan scratch");
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   uint32_t* E = L.E;
   VhCtl* C = L.C;
+  VhLvl& V = C->lv;
   uint32_t* ws = C->ws;
-  static_assert(NW <= VX_WAVES, "scan scratch");
-  // __move_median_to_first(lo, lo + 1, mid, hi - 1), computed by every thread: the classification
-  // sees the swap (position mm holds E[lo]), tid 0 makes it after the scan's barrier
   const VhLess less;
-  const uint32_t elo = E[lo];
-  int mm;
-  uint32_t pe;
-  {
-    const int a = lo + 1, b = lo + (hi - lo) / 2, c = hi - 1;
-    const uint32_t ea = E[a], eb = E[b], ec = E[c];
+  const int c = V.c;
+  // this thread's segment (nb <= 32: binary search over the thread starts)
+  int sg = -1;
+  if (tid < V.tstart[nb]) {
+    int a = 0, b = nb - 1;
+    while (a < b) {
+      const int mid = (a + b + 1) >> 1;
+      if (V.tstart[mid] <= tid) a = mid;
+      else b = mid - 1;
+    }
+    sg = a;
+  }
+  int lo = 0, hi = 0, r = 0;
+  if (sg >= 0) {
+    const uint32_t ent = L.bigl[cur * VH_BIGC + sg];
+    lo = (int)(ent & 0x7FFFu);
+    hi = (int)(ent >> 15);
+    r = tid - V.tstart[sg];
+  }
+  // __move_median_to_first(lo, lo + 1, mid, hi - 1), computed by every thread of the segment: the
+  // classification sees the swap (position mm holds E[lo]), the segment's first thread makes it
+  // after the scan's barriers
+  uint32_t elo = 0, pe = 0;
+  int mm = -1;
+  if (sg >= 0) {
+    elo = E[lo];
+    const int a = lo + 1, b = lo + (hi - lo) / 2, cc = hi - 1;
+    const uint32_t ea = E[a], eb = E[b], ec = E[cc];
     if (less(ea, eb)) {
       if (less(eb, ec)) mm = b;
-      else if (less(ea, ec)) mm = c;
+      else if (less(ea, ec)) mm = cc;
       else mm = a;
     } else if (less(ea, ec)) {
       mm = a;
     } else if (less(eb, ec)) {
-      mm = c;
+      mm = cc;
     } else {
       mm = b;
     }
     pe = mm == a ? ea : (mm == b ? eb : ec);
   }
   const uint32_t p = pe >> 16;
-  const int len = hi - lo - 1;  // the scanned positions lo + 1 .. hi - 1
-  const int c = (len + NT - 1) / NT;
-  const int b0 = lo + 1 + tid * c;
+  const int b0 = lo + 1 + r * c, e0 = min(b0 + c, hi);  // this thread's positions [b0, e0)
   uint32_t ml = 0, mr = 0;
   int nh = 0;
   uint32_t ev[CH];
 #pragma unroll
-  for (int u = 0; u < CH; ++u) ev[u] = E[min(b0 + u, hi - 1)];  // (clamped: every load issued at once)
+  for (int u = 0; u < CH; ++u) ev[u] = sg >= 0 ? E[min(b0 + u, hi - 1)] : 0u;  // (clamped: every load issued at once)
 #pragma unroll
   for (int u = 0; u < CH; ++u) {
     const int i = b0 + u;
-    if (u < c && i < hi) {
+    if (i < e0) {
       const uint32_t e = i == mm ? elo : ev[u];
       const uint32_t k = e >> 16;
       if (!(k < p)) ml |= 1u << u;
@@ -609,33 +639,37 @@ __device__ inline int vh_partition_wg_c(const VhLds& L, int lo, int hi, int par)
       nh += (e & VH_HOT) ? 1 : 0;
     }
   }
-  nh = (int)dpp_wave_sum_u((uint32_t)nh);
-  if (lane == 0 && nh) atomicAdd(&C->hot[par], nh);
+  // per-segment sums: one atomic per wave when the wave lies in one segment
+  auto seg_add = [&](int* arr, int val) {
+    const int s0 = __builtin_amdgcn_readfirstlane(sg);
+    if (__ballot(sg != s0) == 0ull) {
+      const int t = (int)dpp_wave_sum_u((uint32_t)val);
+      if (lane == 0 && t && s0 >= 0) atomicAdd(&arr[s0], t);
+    } else if (sg >= 0 && val) {
+      atomicAdd(&arr[sg], val);
+    }
+  };
+  seg_add(V.hot, nh);
   const uint32_t v = (uint32_t)__popc(ml) | ((uint32_t)__popc(mr) << 16);  // totals < 2^16
-  const uint32_t x = dpp_incl_scan_u(v);
+  uint32_t x = dpp_incl_scan_u(v);
   if (lane == 63) ws[wid] = x;
   __syncthreads();
-  if (tid == 0) {
-    C->hot[par ^ 1] = 0;  // the next segment's slot: every use of it (two segments back) is done
-    C->S[par ^ 1] = 0;
-    C->cut[par ^ 1] = 0x7FFFFFFF;
-  }
-  if (C->hot[par] + ((pe & VH_HOT) ? 1 : 0) < 2) return -1;
-  if (tid == 0) {  // the median swap (read by nobody before the next barrier)
+  for (int w = 0; w < NW; ++w) x += w < wid ? ws[w] : 0u;  // inclusive over the block
+  if (sg >= 0 && r == 0) V.base[sg] = x - v;
+  if (sg >= 0 && tid == V.tstart[sg + 1] - 1) V.endv[sg] = x;
+  __syncthreads();
+  const bool act = sg >= 0 && V.hot[sg] + ((pe & VH_HOT) ? 1 : 0) >= 2;
+  if (act && r == 0) {  // the median swap (read by nobody before the next barrier)
     E[lo] = pe;
     E[mm] = elo;
   }
-  uint32_t off = x - v, tot = 0;
-  for (int w = 0; w < NW; ++w) {
-    const uint32_t t = ws[w];
-    off += w < wid ? t : 0u;
-    tot += t;
-  }
-  const int nr = 1 + (int)(tot >> 16);
-  const int m = hi - lo, KB = (m - 1) / 2, bb = lo >> 1;
   uint16_t* Bs = L.Bs;
-  {
-    int kl = (int)(off & 0xFFFFu), t = 1 + (int)(off >> 16), S = 0;  // t: ascending right-stop index
+  const int m = hi - lo, KB = (m - 1) / 2, bb = lo >> 1;
+  const uint32_t off = act ? x - v - V.base[sg] : 0u, tot = act ? V.endv[sg] - V.base[sg] : 0u;
+  const int nr = 1 + (int)(tot >> 16);
+  int S = 0;
+  if (act) {
+    int kl = (int)(off & 0xFFFFu), t = 1 + (int)(off >> 16);  // t: ascending right-stop index
 #pragma unroll
     for (int u = 0; u < CH; ++u) {
       const bool isl = (ml >> u) & 1u, isr = (mr >> u) & 1u;
@@ -648,41 +682,69 @@ __device__ inline int vh_partition_wg_c(const VhLds& L, int lo, int hi, int par)
         ++t;
       }
     }
-    if (tid == 0 && nr <= KB) Bs[bb + nr - 1] = (uint16_t)lo;
-    S = (int)dpp_wave_sum_u((uint32_t)S);
-    if (lane == 0 && S) atomicAdd(&C->S[par], S);
+    if (r == 0 && nr <= KB) Bs[bb + nr - 1] = (uint16_t)lo;
   }
+  seg_add(V.S, S);
   __syncthreads();
-  const int S = C->S[par];
-  {  // the swaps (each pair read and written by the thread of its left stop alone) and the cut
+  if (act) {  // the swaps (each pair read and written by the thread of its left stop alone) and the cut
+    const int Sg = V.S[sg];
     int kl = (int)(off & 0xFFFFu);
 #pragma unroll
     for (int u = 0; u < CH; ++u) {
       if ((ml >> u) & 1u) {
         ++kl;
-        if (kl <= S) {
+        if (kl <= Sg) {
           const int y = Bs[bb + kl - 1];
           const uint32_t t = E[y];
           E[y] = E[b0 + u];
           E[b0 + u] = t;
         }
-        if (kl == S + 1) atomicMin(&C->cut[par], b0 + u);
+        if (kl == Sg + 1) atomicMin(&V.cut[sg], b0 + u);
       }
     }
-    if (tid == 0) atomicMin(&C->cut[par], S >= 1 ? (int)Bs[bb + S - 1] : hi);
+    if (r == 0) atomicMin(&V.cut[sg], Sg >= 1 ? (int)Bs[bb + Sg - 1] : hi);
   }
+  if (sg >= 0 && r == 0 && !act) V.cut[sg] = -1;
   __syncthreads();
-  return C->cut[par];
 }
 template <int NT>
-__device__ inline int vh_partition_wg(const VhLds& L, int lo, int hi, int par) {
-  static_assert(VH_MAX_N / NT <= 32, "chunk masks in one word");
-  const int c = (hi - lo - 1 + NT - 1) / NT;  // positions per thread
-  if (c <= 2) return vh_partition_wg_c<NT, 2>(L, lo, hi, par);
-  if (c <= 4) return vh_partition_wg_c<NT, 4>(L, lo, hi, par);
-  if (c <= 8) return vh_partition_wg_c<NT, 8>(L, lo, hi, par);
-  if (c <= 16) return vh_partition_wg_c<NT, 16>(L, lo, hi, par);
-  return vh_partition_wg_c<NT, VH_MAX_N / NT>(L, lo, hi, par);
+__device__ inline void vh_partition_level(const VhLds& L, int cur, int nb) {
+  const int c = L.C->lv.c;  // positions per thread (<= 31: see vh_level_setup)
+  if (c <= 2) vh_partition_level_c<NT, 2>(L, cur, nb);
+  else if (c <= 4) vh_partition_level_c<NT, 4>(L, cur, nb);
+  else if (c <= 8) vh_partition_level_c<NT, 8>(L, cur, nb);
+  else if (c <= 16) vh_partition_level_c<NT, 16>(L, cur, nb);
+  else vh_partition_level_c<NT, 32>(L, cur, nb);
+}
+
+// Thread shares of one level (wave 0; the caller's barrier follows): the least c with
+// sum over segments of ceil((m - 1) / c) <= NT (c <= 31 for n <= VH_MAX_N: with at most 30
+// segments over 1024, c = 31 gives at most 30720 / 31 + 30 < 1024 threads)
+template <int NT>
+__device__ inline void vh_level_setup(const VhLds& L, int cur, int nb) {
+  const int lane = threadIdx.x & 63;
+  VhLvl& V = L.C->lv;
+  int len = 0;
+  if (lane < nb) {
+    const uint32_t ent = L.bigl[cur * VH_BIGC + lane];
+    len = (int)(ent >> 15) - (int)(ent & 0x7FFFu) - 1;
+  }
+  const int tot = (int)dpp_wave_sum_u((uint32_t)len);
+  int c = max(1, (tot + NT - 1) / NT);
+  int th = 0;
+  for (;; ++c) {
+    th = lane < nb ? (len + c - 1) / c : 0;
+    if ((int)dpp_wave_sum_u((uint32_t)th) <= NT) break;
+  }
+  const uint32_t incl = dpp_incl_scan_u((uint32_t)th);
+  if (lane < nb) {
+    V.tstart[lane] = (int)(incl - th);
+    V.hot[lane] = 0;
+    V.S[lane] = 0;
+    V.cut[lane] = 0x7FFFFFFF;
+  }
+  if (lane == nb - 1) V.tstart[nb] = (int)incl;
+  if (lane == 0) V.c = c;
 }
 
 // A depth-limit segment of the workgroup: the dup check on a bitmap of slots (in the Bs area,
@@ -742,8 +804,6 @@ __device__ inline void vh_sort(uint32_t* lds, int n, const VxHot& H, int* err, u
     C->err = 0;
     C->heap_el = 0;
     C->dprof = dprof;
-    C->hot[0] = C->S[0] = 0;
-    C->cut[0] = 0x7FFFFFFF;
     if (n > SS_THRESHOLD) {
       if (n > VH_BIG) {
         L.bigl[0] = (uint32_t)n << 15;
@@ -756,39 +816,37 @@ __device__ inline void vh_sort(uint32_t* lds, int n, const VxHot& H, int* err, u
   }
   __syncthreads();
   vx_phase(prof ? prof + 1 : nullptr, 0, &tp);
-  int seg = 0;
   for (int lev = 0;; ++lev) {
     const int cur = lev & 1, nxt = cur ^ 1;
     const int nb = min(C->nbig[cur], VH_BIGC);
     if (nb == 0) break;
     const int d = D0 - lev;
-    for (int t = 0; t < nb; ++t) {
-      const uint32_t ent = L.bigl[cur * VH_BIGC + t];
-      const int lo = (int)(ent & 0x7FFFu), hi = (int)(ent >> 15);
-      if (d == 0) {
-        vh_depth_limit_wg<NT>(L, n, lo, hi);
-        seg = 0;  // (its barriers order every slot; restart the parity)
-        if (tid == 0) {
-          C->hot[0] = C->S[0] = 0;
-          C->cut[0] = 0x7FFFFFFF;
-        }
-        __syncthreads();
-        continue;
+    if (d == 0) {
+      for (int t = 0; t < nb; ++t) {
+        const uint32_t ent = L.bigl[cur * VH_BIGC + t];
+        vh_depth_limit_wg<NT>(L, n, (int)(ent & 0x7FFFu), (int)(ent >> 15));
       }
-      const int cut = vh_partition_wg<NT>(L, lo, hi, seg & 1);
-      ++seg;
-      if (cut < 0 || tid != 0) continue;
-      const int parts[2][2] = {{lo, cut}, {cut, hi}};
-      for (int q = 0; q < 2; ++q) {
-        const int a = parts[q][0], b = parts[q][1];
-        if (b - a > VH_BIG) {
-          const int s = C->nbig[nxt]++;
-          if (s < VH_BIGC) L.bigl[nxt * VH_BIGC + s] = (uint32_t)a | ((uint32_t)b << 15);
-          else C->err |= VH_ERR_ROOTS;
-        } else if (b - a > SS_THRESHOLD) {
-          const int s = C->nroot++;
-          if (s < VH_ROOTS) L.roots[s] = vh_pack(a, b - a, d - 1);
-          else C->err |= VH_ERR_ROOTS;
+    } else {
+      if (tid < 64) vh_level_setup<NT>(L, cur, nb);
+      __syncthreads();
+      vh_partition_level<NT>(L, cur, nb);
+      if (tid < nb) {  // one thread per segment lists its parts
+        const uint32_t ent = L.bigl[cur * VH_BIGC + tid];
+        const int lo = (int)(ent & 0x7FFFu), hi = (int)(ent >> 15), cut = C->lv.cut[tid];
+        if (cut >= 0) {
+          const int parts[2][2] = {{lo, cut}, {cut, hi}};
+          for (int q = 0; q < 2; ++q) {
+            const int a = parts[q][0], b = parts[q][1];
+            if (b - a > VH_BIG) {
+              const int s = atomicAdd(&C->nbig[nxt], 1);
+              if (s < VH_BIGC) L.bigl[nxt * VH_BIGC + s] = (uint32_t)a | ((uint32_t)b << 15);
+              else atomicOr(&C->err, VH_ERR_ROOTS);
+            } else if (b - a > SS_THRESHOLD) {
+              const int s = atomicAdd(&C->nroot, 1);
+              if (s < VH_ROOTS) L.roots[s] = vh_pack(a, b - a, d - 1);
+              else atomicOr(&C->err, VH_ERR_ROOTS);
+            }
+          }
         }
       }
     }
