@@ -738,6 +738,16 @@ def main():
         ei_all, edt_max = aggregate(ei, edt, world, f"cuda:{local}")
         exact_leg = {"value": ei_all / edt_max, "ms_per_step": 1e3 * edt_max / K, "poses": eposes,
                      "kernel_ms_per_step": {k: round(v["ms"] / K, 4) for k, v in ekt.items()}}
+        if ekt:  # its own roofline: the family with the largest device time in this mode
+            edom = max(ekt, key=lambda k: ekt[k]["ms"])
+            ed = ekt[edom]
+            each = ed["bytes"] / (ed["ms"] * 1e-3) / 1e9 if ed["ms"] > 0 else 0.0
+            exact_leg["roofline"] = {"bound": "hbm", "kernel": edom, "achieved": round(each, 2),
+                                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(each / HBM_PEAK_GBS, 5),
+                                     "traffic": None, "launches": ed["launches"],
+                                     "avg_launch_us": round(1e3 * ed["ms"] / max(1, ed["launches"]), 3),
+                                     "algorithmic_bytes_per_launch": round(ed["bytes"] / max(1, ed["launches"]), 1),
+                                     "families": family_rooflines(ekt, False)}
 
     # the north-star multi-GPU design beside the replica headline: Bs streams, each
     # split over all ranks (block-owned map shards, RCCL all-gather of the 5-NN candidates per
