@@ -59,6 +59,7 @@ constexpr int LM_THREADS = 256;
 constexpr int LM_EBLK = 32;     // LM evaluation workgroups per stream (grid-stride)
 constexpr int SUBMAP_BLOCKS = 64;
 constexpr int INS_SLOTS = WIN_VALID_MAX + EXTRA_CAP;
+constexpr int RQ_CLASSES = 8;  // re-VoxelGrid items by size: < 1k points, < 2k, .. < 64k, more
 constexpr int MAP_ERR_SUBMAP = 4, MAP_ERR_EXTRA = 8, MAP_ERR_HASH = 16, MAP_ERR_LM_SYNC = 32,
               MAP_ERR_INDEX = 64, MAP_ERR_LIVE = 128, MAP_ERR_SORT = 256,
               MAP_ERR_STACK = 512, MAP_ERR_STACK_WAIT = 2048;
@@ -163,6 +164,9 @@ struct MapperDev {
   double* lm_xpub;     // [B][2 rounds][8]: eval point published to the workers
   uint32_t* tickets;  // [B]
   uint32_t* lm_tick;  // [B] k_lm_eval's workgroups done (sharded: the last one reduces)
+  uint32_t* rq;       // [RQ_CLASSES][rq_cap] re-VoxelGrid items ((2 s + m) INS_SLOTS + slot) by size class
+  uint32_t* rq_ctl;   // [0, 8) items per class, [8, 16) items taken, [16] k_revox workgroups done
+  int rq_cap = 0;
   // sharded mode (loam_mapper_create_sharded): this rank of nrank; map points are stored by
   // the rank owning their 4 m block (comm.h, shard_owner); blk_v: voxels per block edge
   uint32_t compact_at = 0;  // an arena whose tail passed this is compacted
@@ -1389,6 +1393,15 @@ __global__ void __launch_bounds__(VX_THREADS) k_insert_bucket(MapperDev D) {
     if (sl >= 0) out[wcnt[wid][sl] + rank] = pts[i];
     __syncthreads();
   }
+  // this (stream, map)'s re-VoxelGrid items, listed by size class (k_revox takes the largest first)
+  for (int slot = tid; slot < INS_SLOTS; slot += VX_THREADS) {
+    int cube = 0, append = 0;
+    if (!revox_target(D, s, m, slot, &cube, &append)) continue;
+    const uint32_t nt = D.cube_tab[sm_index(s, m) * NCUBE + cube].y + (off[slot + 1] - off[slot]);
+    const int c = nt < 1024u ? 0 : min(RQ_CLASSES - 1, 32 - __clz(nt >> 10));
+    const uint32_t k = atomicAdd(&D.rq_ctl[c], 1u);
+    D.rq[(size_t)c * D.rq_cap + k] = (uint32_t)(sm * INS_SLOTS + slot);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1518,16 +1531,37 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
   }
 }
 
-// one workgroup per (stream, map, slot): block = slot item.  PCL: exact_voxel_order (its own
-// instantiation, so that the sort's registers do not weigh on the input-order kernel)
+// A worklist: each workgroup takes items (listed by k_insert_bucket) until none is left, the
+// largest size class first, so the longest items start first and no workgroup is spent on a
+// slot with nothing to do.  The last workgroup to finish resets the list for the next frame.
+// PCL: exact_voxel_order (its own instantiation, so that the sort's registers do not weigh on
+// the input-order kernel)
 template <bool PCL>
 __global__ void __launch_bounds__(VX_THREADS) k_revox(MapperDev D) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
-  const uint32_t item = 2 * (uint32_t)D.s0 * INS_SLOTS + blockIdx.x;
-  const int slot = (int)(item % INS_SLOTS), sm = (int)(item / INS_SLOTS);
-  int cube = 0, append = 0;
-  if (!revox_target(D, sm >> 1, sm & 1, slot, &cube, &append)) return;
-  revox_item<PCL>(D, sm >> 1, sm & 1, slot, cube, append, lds);
+  int& item_sh = reinterpret_cast<int&>(lds[VX_LDS_WORDS - 1]);  // free between items
+  uint32_t* ctl = D.rq_ctl;
+  while (true) {
+    if (threadIdx.x == 0) {
+      int it = -1;
+      for (int c = RQ_CLASSES - 1; c >= 0 && it < 0; --c) {
+        const uint32_t nc = ctl[c];
+        if (__hip_atomic_load(&ctl[RQ_CLASSES + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nc) continue;
+        const uint32_t k = atomicAdd(&ctl[RQ_CLASSES + c], 1u);
+        if (k < nc) it = (int)D.rq[(size_t)c * D.rq_cap + k];
+      }
+      item_sh = it;
+    }
+    __syncthreads();
+    const int item = item_sh;
+    if (item < 0) break;
+    const int slot = item % INS_SLOTS, sm = item / INS_SLOTS;
+    int cube = 0, append = 0;
+    if (revox_target(D, sm >> 1, sm & 1, slot, &cube, &append)) revox_item<PCL>(D, sm >> 1, sm & 1, slot, cube, append, lds);
+    __syncthreads();  // (item_sh and the LDS are reused)
+  }
+  if (threadIdx.x == 0 && atomicAdd(&ctl[2 * RQ_CLASSES], 1u) == gridDim.x - 1)
+    for (int k = 0; k <= 2 * RQ_CLASSES; ++k) ctl[k] = 0u;  // every workgroup is past its last take
 }
 
 // cell index of one cube whose content was set through the API (cen: the host's grid centre)
@@ -2086,6 +2120,9 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   ALLOC(D.lm_xpub, B * 2 * 8);
   ALLOC(D.tickets, B);
   ALLOC(D.lm_tick, B);
+  D.rq_cap = B * 2 * INS_SLOTS;
+  ALLOC(D.rq, (size_t)RQ_CLASSES * D.rq_cap);
+  ALLOC(D.rq_ctl, 2 * RQ_CLASSES + 1);
   ALLOC(h->d_map_off, 2 * NCUBE + 1);
   ALLOC(h->d_new_off, B * 2 * (NCUBE + 1));
   if (D.sharded) {
@@ -2390,6 +2427,11 @@ int32_t loam_mapper_prefetch(loam_mapper* h) {
   return launch_stacks(h);
 }
 
+// k_revox workgroups (one per CU at most: 160 KiB of LDS each): a handle of B streams takes
+// about 2 B of them, so two 64-stream handles share the GPU and a one-stream frame's items
+// (~20) each start at once
+static int revox_grid(const loam_mapper* h) { return std::max(32, std::min(h->n_cu, 2 * h->B)); }
+
 // the frame's kernel sequence for the hipGraph path: k_frame_prep (records of a queued frame,
 // stack sizes, submap offsets), 2 x (kNN, geometry, LM round), insertion, re-VoxelGrid, and the
 // records back to the D2H buffer of the frame's stack parity.  Every kernel argument is fixed per
@@ -2404,8 +2446,8 @@ static void capture_frame(loam_mapper* h, const MapperDev& D, int fpar, hipStrea
     k_lm_round<<<lm_padded(B) * h->lm_G, LM_THREADS, 0, st>>>(D, round, h->lm_G);
   }
   k_insert_bucket<<<B * 2, VX_THREADS, 0, st>>>(D);
-  if (D.pcl_order) k_revox<true><<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D);
-  else k_revox<false><<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D);
+  if (D.pcl_order) k_revox<true><<<revox_grid(h), VX_THREADS, 0, st>>>(D);
+  else k_revox<false><<<revox_grid(h), VX_THREADS, 0, st>>>(D);
   k_frame_out<<<1, 256, 0, st>>>(D, h->hfo_dev[fpar], h->done_dev + fpar);
 }
 
@@ -2634,8 +2676,8 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
   }
   LOAM_HIP(hipEventRecord(h->ev[2], st));
   LAUNCH(FAM_INSERT, k_insert_bucket<<<B * 2, VX_THREADS, 0, st>>>(D));
-  if (D.pcl_order) LAUNCH(FAM_REVOX, k_revox<true><<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D));
-  else LAUNCH(FAM_REVOX, k_revox<false><<<B * 2 * INS_SLOTS, VX_THREADS, 0, st>>>(D));
+  if (D.pcl_order) LAUNCH(FAM_REVOX, k_revox<true><<<revox_grid(h), VX_THREADS, 0, st>>>(D));
+  else LAUNCH(FAM_REVOX, k_revox<false><<<revox_grid(h), VX_THREADS, 0, st>>>(D));
   LOAM_HIP(hipGetLastError());
   LOAM_HIP(hipMemcpyAsync(h->hfo[fpar].data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
   LOAM_HIP(hipEventRecord(h->ev_fr[fpar][1], st));
