@@ -1417,8 +1417,10 @@ __global__ void __launch_bounds__(VX_THREADS) k_insert_bucket(MapperDev D) {
 // the merge path (a fixed-point cube plus a few new points, voxel.h vx_merge_fixed_point) or
 // the full filter in a VX_THREADS workgroup with the whole LDS, then the cube's cell index.
 // ---------------------------------------------------------------------------------------
+// (noinline: inlined into k_revox's worklist loop, its loop-invariant loads are hoisted out of
+// the loop and spill hundreds of registers)
 template <bool PCL>
-__device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube, int append, uint32_t* lds) {
+__device__ __noinline__ void revox_item(MapperDev& D, int s, int m, int slot, int cube, int append, uint32_t* lds) {
   constexpr int LW = VX_LDS_WORDS;
   StreamFrame& F = D.fr[s];
   const uint32_t* ioff = D.ins_off + sm_index(s, m) * (INS_SLOTS + 1);
