@@ -10,7 +10,7 @@ path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof/run_kernel_trace.c
 back = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 rows = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0].replace("loam::", ""))
               for r in csv.DictReader(open(path)))
-rv = [i for i, r in enumerate(rows) if r[2] == "k_revox"]
+rv = [i for i, r in enumerate(rows) if r[2].split("<")[0].replace("void ", "") == "k_revox"]
 a, b = rv[-back - 1], rv[-back]
 t0 = prev = rows[a][1]
 busy = 0

@@ -578,13 +578,17 @@ __host__ __device__ inline void frame_reset(StreamFrame& F) {
 
 // the frame's stack sizes and stack-filter errors into its stream records (after the stack
 // kernels, which may have run while the previous frame was in flight)
+// (agent-scope atomic loads: k_frame_prep reads them while other stacks of the same frame may
+// still be running, and the words of all streams share lines that another stream's block of this
+// XCD may have pulled into the L2 before this stack was written; an acquire fence instead would
+// invalidate the XCD's whole L2 and cost the frame's later kernels their cached cubes)
 __device__ inline void stack_counts(const MapperDev& D, int s, StreamFrame& F) {
-  F.nc_stack = D.stk_n[2 * s];
-  F.ns_stack = D.stk_n[2 * s + 1];
-  const int e = D.stk_err[s];
+  F.nc_stack = __hip_atomic_load(&D.stk_n[2 * s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  F.ns_stack = __hip_atomic_load(&D.stk_n[2 * s + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int e = __hip_atomic_load(&D.stk_err[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (e) {
     F.err |= e;
-    D.stk_err[s] = 0;
+    __hip_atomic_store(&D.stk_err[s], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -764,11 +768,8 @@ __global__ void __launch_bounds__(128) k_frame_prep(MapperDev D) {
       }
       __builtin_amdgcn_s_sleep(4);
     }
-    // acquire: the stack sizes this thread reads next (stack_counts) may share a line that
-    // another stream's block of this XCD pulled into the L2 before the stack kernel wrote it
-    // (streams of one frame can take stacks from different launches: loam_mapper_prefetch for
-    // some, the solve for the others); once per block per frame
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // the stack sizes are read with agent-scope loads (stack_counts); the stack points only by
+    // later kernels, which start after every stack of the frame has ended
   }
   __syncthreads();
   const unsigned long long t1 = __builtin_readcyclecounter();
