@@ -60,8 +60,6 @@ constexpr int LM_EBLK = 32;     // LM evaluation workgroups per stream (grid-str
 constexpr int SUBMAP_BLOCKS = 64;
 constexpr int INS_SLOTS = WIN_VALID_MAX + EXTRA_CAP;
 constexpr int RQ_CLASSES = 8;  // re-VoxelGrid items by size: < 1k points, < 2k, .. < 64k, more
-constexpr int RQ_XCD = 8;      // and by the XCD whose L2 holds the cube (its workgroups take it first)
-constexpr int RQ_LISTS = RQ_XCD * RQ_CLASSES;
 constexpr int MAP_ERR_SUBMAP = 4, MAP_ERR_EXTRA = 8, MAP_ERR_HASH = 16, MAP_ERR_LM_SYNC = 32,
               MAP_ERR_INDEX = 64, MAP_ERR_LIVE = 128, MAP_ERR_SORT = 256,
               MAP_ERR_STACK = 512, MAP_ERR_STACK_WAIT = 2048;
@@ -166,8 +164,8 @@ struct MapperDev {
   double* lm_xpub;     // [B][2 rounds][8]: eval point published to the workers
   uint32_t* tickets;  // [B]
   uint32_t* lm_tick;  // [B] k_lm_eval's workgroups done (sharded: the last one reduces)
-  uint32_t* rq;       // [RQ_XCD][RQ_CLASSES][rq_cap] re-VoxelGrid items ((2 s + m) INS_SLOTS + slot)
-  uint32_t* rq_ctl;   // [RQ_LISTS] items per list, [RQ_LISTS] items taken, [1] k_revox workgroups done
+  uint32_t* rq;       // [RQ_CLASSES][rq_cap] re-VoxelGrid items ((2 s + m) INS_SLOTS + slot) by size class
+  uint32_t* rq_ctl;   // [RQ_CLASSES] items per class (zeroed by the frame's first kernel)
   int rq_cap = 0;
   // sharded mode (loam_mapper_create_sharded): this rank of nrank; map points are stored by
   // the rank owning their 4 m block (comm.h, shard_owner); blk_v: voxels per block edge
@@ -745,6 +743,7 @@ __device__ inline void submap_prep(const MapperDev& D, int s, StreamFrame& F) {
 __global__ void __launch_bounds__(128) k_submap_prep(MapperDev D) {
   const int s = D.s0 + blockIdx.x;
   StreamFrame& F = D.fr[s];
+  if (blockIdx.x == 0 && threadIdx.x < RQ_CLASSES) D.rq_ctl[threadIdx.x] = 0u;  // this frame's k_revox list
   if (!F.active) return;
   submap_prep(D, s, F);
 }
@@ -754,6 +753,7 @@ __global__ void __launch_bounds__(128) k_submap_prep(MapperDev D) {
 __global__ void __launch_bounds__(128) k_frame_prep(MapperDev D) {
   const int s = D.s0 + blockIdx.x;
   StreamFrame& F = D.fr[s];
+  if (blockIdx.x == 0 && threadIdx.x < RQ_CLASSES) D.rq_ctl[threadIdx.x] = 0u;  // this frame's k_revox list
   __shared__ int go;
   __shared__ FrameIn I;
   const unsigned long long t0 = __builtin_readcyclecounter();
@@ -1402,13 +1402,8 @@ __global__ void __launch_bounds__(VX_THREADS) k_insert_bucket(MapperDev D) {
     if (!revox_target(D, s, m, slot, &cube, &append)) continue;
     const uint32_t nt = D.cube_tab[sm_index(s, m) * NCUBE + cube].y + (off[slot + 1] - off[slot]);
     const int c = nt < 1024u ? 0 : min(RQ_CLASSES - 1, 32 - __clz(nt >> 10));
-    // the XCD of the workgroup the item had when k_revox ran one workgroup per slot (block
-    // sm * INS_SLOTS + slot, dealt round-robin): a window cube keeps its slot from frame to frame
-    // while the window stays, so its content is re-read where the last frame wrote it
-    const int x = (sm * INS_SLOTS + slot) % RQ_XCD;
-    const int l = x * RQ_CLASSES + c;
-    const uint32_t k = atomicAdd(&D.rq_ctl[l], 1u);
-    D.rq[(size_t)l * D.rq_cap + k] = (uint32_t)(sm * INS_SLOTS + slot);
+    const uint32_t k = atomicAdd(&D.rq_ctl[c], 1u);
+    D.rq[(size_t)c * D.rq_cap + k] = (uint32_t)(sm * INS_SLOTS + slot);
   }
 }
 
@@ -1418,10 +1413,8 @@ __global__ void __launch_bounds__(VX_THREADS) k_insert_bucket(MapperDev D) {
 // the merge path (a fixed-point cube plus a few new points, voxel.h vx_merge_fixed_point) or
 // the full filter in a VX_THREADS workgroup with the whole LDS, then the cube's cell index.
 // ---------------------------------------------------------------------------------------
-// (noinline: inlined into k_revox's worklist loop, its loop-invariant loads are hoisted out of
-// the loop and spill hundreds of registers)
 template <bool PCL>
-__device__ __noinline__ void revox_item(MapperDev& D, int s, int m, int slot, int cube, int append, uint32_t* lds) {
+__device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube, int append, uint32_t* lds) {
   constexpr int LW = VX_LDS_WORDS;
   StreamFrame& F = D.fr[s];
   const uint32_t* ioff = D.ins_off + sm_index(s, m) * (INS_SLOTS + 1);
@@ -1541,44 +1534,29 @@ __device__ __noinline__ void revox_item(MapperDev& D, int s, int m, int slot, in
   }
 }
 
-// A worklist: each workgroup takes items (listed by k_insert_bucket) until none is left: those of
-// its own XCD first (blockIdx % 8: workgroups are dealt to the XCDs round-robin; the grid is a
-// multiple of 8), largest size class first, then any other XCD's.  The longest items start first
-// and no workgroup is spent on a slot with nothing to do.  The last workgroup to finish resets
-// the lists for the next frame.
-// PCL: exact_voxel_order (its own instantiation, so that the sort's registers do not weigh on
-// the input-order kernel)
+// One workgroup per item (no loop over items: a loop around revox_item spills hundreds of
+// registers): workgroup b takes the b-th item of the frame's list (k_insert_bucket), largest size
+// class first, so the longest items are dispatched first; workgroups past the list's end leave
+// after one load.  PCL: exact_voxel_order (its own instantiation, so that the sort's registers do
+// not weigh on the input-order kernel)
 template <bool PCL>
 __global__ void __launch_bounds__(VX_THREADS) k_revox(MapperDev D) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
-  int& item_sh = reinterpret_cast<int&>(lds[VX_LDS_WORDS - 1]);  // free between items
-  uint32_t* ctl = D.rq_ctl;
-  while (true) {
-    if (threadIdx.x == 0) {
-      int it = -1;
-      const int x0 = (int)(blockIdx.x % RQ_XCD);
-      for (int xi = 0; xi < RQ_XCD && it < 0; ++xi) {
-        const int x = (x0 + xi) % RQ_XCD;
-        for (int c = RQ_CLASSES - 1; c >= 0 && it < 0; --c) {
-          const int l = x * RQ_CLASSES + c;
-          const uint32_t nc = ctl[l];
-          if (__hip_atomic_load(&ctl[RQ_LISTS + l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nc) continue;
-          const uint32_t k = atomicAdd(&ctl[RQ_LISTS + l], 1u);
-          if (k < nc) it = (int)D.rq[(size_t)l * D.rq_cap + k];
-        }
-      }
-      item_sh = it;
+  uint32_t b = blockIdx.x;
+  int item = -1;
+  for (int c = RQ_CLASSES - 1; c >= 0; --c) {
+    const uint32_t nc = D.rq_ctl[c];
+    if (b < nc) {
+      item = (int)D.rq[(size_t)c * D.rq_cap + b];
+      break;
     }
-    __syncthreads();
-    const int item = item_sh;
-    if (item < 0) break;
-    const int slot = item % INS_SLOTS, sm = item / INS_SLOTS;
-    int cube = 0, append = 0;
-    if (revox_target(D, sm >> 1, sm & 1, slot, &cube, &append)) revox_item<PCL>(D, sm >> 1, sm & 1, slot, cube, append, lds);
-    __syncthreads();  // (item_sh and the LDS are reused)
+    b -= nc;
   }
-  if (threadIdx.x == 0 && atomicAdd(&ctl[2 * RQ_LISTS], 1u) == gridDim.x - 1)
-    for (int k = 0; k <= 2 * RQ_LISTS; ++k) ctl[k] = 0u;  // every workgroup is past its last take
+  if (item < 0) return;
+  const int slot = item % INS_SLOTS, sm = item / INS_SLOTS;
+  int cube = 0, append = 0;
+  if (!revox_target(D, sm >> 1, sm & 1, slot, &cube, &append)) return;
+  revox_item<PCL>(D, sm >> 1, sm & 1, slot, cube, append, lds);
 }
 
 // cell index of one cube whose content was set through the API (cen: the host's grid centre)
@@ -2138,8 +2116,8 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   ALLOC(D.tickets, B);
   ALLOC(D.lm_tick, B);
   D.rq_cap = B * 2 * INS_SLOTS;
-  ALLOC(D.rq, (size_t)RQ_LISTS * D.rq_cap);
-  ALLOC(D.rq_ctl, 2 * RQ_LISTS + 1);
+  ALLOC(D.rq, (size_t)RQ_CLASSES * D.rq_cap);
+  ALLOC(D.rq_ctl, RQ_CLASSES);
   ALLOC(h->d_map_off, 2 * NCUBE + 1);
   ALLOC(h->d_new_off, B * 2 * (NCUBE + 1));
   if (D.sharded) {
@@ -2444,10 +2422,8 @@ int32_t loam_mapper_prefetch(loam_mapper* h) {
   return launch_stacks(h);
 }
 
-// k_revox workgroups (one per CU at most: 160 KiB of LDS each): a handle of B streams takes
-// about 2 B of them, so two 64-stream handles share the GPU and a one-stream frame's items
-// (~20) each start at once
-static int revox_grid(const loam_mapper* h) { return std::max(32, std::min(h->n_cu, 2 * h->B)) & ~(RQ_XCD - 1); }
+// k_revox workgroups: one per possible item
+static int revox_grid(const loam_mapper* h) { return h->B * 2 * INS_SLOTS; }
 
 // the frame's kernel sequence for the hipGraph path: k_frame_prep (records of a queued frame,
 // stack sizes, submap offsets), 2 x (kNN, geometry, LM round), insertion, re-VoxelGrid, and the
