@@ -1,0 +1,7 @@
+#!/bin/bash
+# GPU tests, exact-mode phase counters, then the bench legs without CPU baselines
+cd "$(dirname "$0")/../.."
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1 && \
+timeout -k 10 300 python -u tools/dbg_exact.py > gpurun_out/dbg_exact.txt 2>&1 && \
+timeout -k 10 500 python bench.py --no-cpu --no-depth --shard-streams 0 > gpurun_out/bench_exact.json 2> gpurun_out/bench_exact.err
