@@ -1,11 +1,15 @@
 #!/bin/bash
-# round-end evidence, part 2: kernel-trace stats of the mapping bench, then one PMC pass per
-# counter group (kernel trace only, no other tracing)
+# round-end evidence, part 2: the heap-sort microbenchmark, exact-mode phase counters, kernel-trace
+# stats of the mapping bench (B = 128 and one stream), then one PMC pass per counter group (kernel
+# trace only, no other tracing)
 cd "$(dirname "$0")/../.."
 R="$(pwd)"
 mkdir -p gpurun_out
 A="--no-cpu --no-single-stream --no-depth --shard-streams 0"
+timeout -k 10 120 tools/bin/mb_heap > gpurun_out/mb_heap.txt 2>&1 && \
+timeout -k 10 300 python -u tools/dbg_exact.py > gpurun_out/dbg_exact.txt 2>&1 && \
 cd /tmp && export TMPDIR=/tmp && \
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" $A > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof_bench.err" && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof1" -o run --output-format csv -- python3 "$R/bench.py" $A --no-exact-leg --steps 30 --streams 1 --handles 1 --pipelined --no-prof > "$R/gpurun_out/prof1_bench.json" 2> "$R/gpurun_out/prof1_bench.err" && \
 timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$R/gpurun_out/pmc_fetch" -o run --output-format csv -- python3 "$R/bench.py" $A --no-exact-leg --no-prof --steps 5 > "$R/gpurun_out/pmc_fetch.json" 2> "$R/gpurun_out/pmc_fetch.err" && \
 timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$R/gpurun_out/pmc_write" -o run --output-format csv -- python3 "$R/bench.py" $A --no-exact-leg --no-prof --steps 5 > "$R/gpurun_out/pmc_write.json" 2> "$R/gpurun_out/pmc_write.err"
