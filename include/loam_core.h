@@ -130,9 +130,11 @@ int32_t loam_scanreg_curvature(loam_scanreg* h, float* curv, int32_t* label, int
 double loam_scanreg_ms(loam_scanreg* h);
 /* cumulative device cycle counters of the per-ring PCL-order VoxelGrid (k_sr_ringvox), summed
  * over rings and frames: [0] cycles of the sort emulation (libstdc++ introsort) for the voxels of 3+ members,
- * [1] of their centroids, [2] rings that had such a voxel; reset = 1 zeroes them after the copy.
- * Counted only in a handle created with LOAM_PHASE_COUNTERS=1 in the environment. */
-#define LOAM_SR_DEBUG_COUNTERS 8
+ * [1] of their centroids, [2] rings that had such a voxel, [8] elements heap-sorted at the depth
+ * limit, [9..12] cycles of the sort's setup, workgroup levels, wave subtrees and positions;
+ * reset = 1 zeroes them after the copy.  Counted only in a handle created with
+ * LOAM_PHASE_COUNTERS=1 in the environment. */
+#define LOAM_SR_DEBUG_COUNTERS 16
 int32_t loam_scanreg_debug_counters(loam_scanreg* h, uint64_t* out, int32_t n, int32_t reset);
 
 /* --------------------------------------------------------------------------------------

@@ -32,4 +32,6 @@ for k in range(len(frames)):
 c = sr.debug_counters()
 rings = 64 * len(frames)
 print("scanreg ms/frame", np.mean(ms))
-print("per ring cycles: keys %.0f  sort levels %.0f  final %.0f  centroids %.0f" % tuple(c[:4] / rings))
+print("per ring: hot sort cycles %.0f, hot centroids %.0f, filters with a hot voxel %.2f" % tuple(c[:3] / rings))
+print("per ring: elements heap-sorted %.1f; sort phases setup / workgroup levels / wave subtrees / positions %s"
+      % (c[8] / rings, [round(float(v) / rings) for v in c[9:13]]))

@@ -676,7 +676,8 @@ __device__ __noinline__ void sr_ringvox(const VoxSeg& S, int n, int* err, unsign
   __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
   voxel_segment(S, lds);
   vh_fixup<SRV_THREADS>(VxSrc{S.src0, n, nullptr}, n, S.out, S.hot, lds, VX_LDS_WORDS - 256,
-                        *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192), nullptr, err, prof);
+                        *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192), nullptr, err, prof,
+                        prof ? prof + 8 : nullptr);  // (diagnostics: [8] heap-sorted, [9..12] sort phases)
 }
 
 __global__ void __launch_bounds__(SRV_THREADS) k_sr_ringvox(SrDev D) {

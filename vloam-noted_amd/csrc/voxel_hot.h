@@ -801,7 +801,8 @@ __device__ inline void vh_sort(uint32_t* lds, int n, int nhot, const VxHot& H, i
   // segments longer than lvl partitioned level by level by the workgroup, shorter ones by waves.
   // Dense (a quarter of the points hot: stacks, scan rings): the whole workgroup down to 64
   // elements, as far as the level lists allow (lvl >= n / VH_BIGC); sparse (cube re-filters,
-  // narrow subtrees): above 1024 only
+  // narrow subtrees): above 1024 only (level passes of few segments cost small cubes more than
+  // the waves' chains)
   const int lvl = 4 * nhot >= n ? max(64, (n + VH_BIGC - 1) / VH_BIGC) : max(VH_BIG, (n + VH_BIGC - 1) / VH_BIGC);
   if (tid == 0) {
     C->nbig[0] = C->nbig[1] = 0;
