@@ -41,7 +41,7 @@ constexpr int VH_MAX_N = 30720;   // LDS-resident emulation up to this many poin
 constexpr int VH_CHUNK = VH_MAX_N / VX_THREADS;  // positions per thread of a workgroup partition
 constexpr int VH_ROOTS = 512;     // wave subtrees listed per drain
 constexpr int VH_SHARE = 96;      // a wave lists the larger part of a partition when longer (others may take it)
-constexpr int VH_BIGC = 64;       // workgroup segments of one level (disjoint, longer than the level threshold)
+constexpr int VH_BIGC = 32;       // workgroup segments of one level (segments > VH_BIG are disjoint: <= 30)
 constexpr int VH_LIFO = 8;        // wave-local pending parts (smaller part first: depth <= 6)
 constexpr int VH_WAVE_W = VH_LIFO + 64;  // per wave: LIFO + the dup check's keys
 constexpr int VH_SMALL = 32;      // hot voxels up to this many members: summed by one thread
@@ -714,12 +714,12 @@ __device__ inline void vh_partition_level(const VhLds& L, int cur, int nb) {
   else if (c <= 4) vh_partition_level_c<NT, 4>(L, cur, nb);
   else if (c <= 8) vh_partition_level_c<NT, 8>(L, cur, nb);
   else if (c <= 16) vh_partition_level_c<NT, 16>(L, cur, nb);
-  else vh_partition_level_c<NT, 32>(L, cur, nb);  // (c <= 32: 30720 / (1024 - 64) positions)
+  else vh_partition_level_c<NT, 32>(L, cur, nb);
 }
 
 // Thread shares of one level (wave 0; the caller's barrier follows): the least c with
-// sum over segments of ceil((m - 1) / c) <= NT (c <= 32 for n <= VH_MAX_N: with at most 64
-// segments, c = 32 gives at most 30720 / 32 + 64 = 1024 threads)
+// sum over segments of ceil((m - 1) / c) <= NT (c <= 31 for n <= VH_MAX_N: with at most 30
+// segments over 1024, c = 31 gives at most 30720 / 31 + 30 < 1024 threads)
 template <int NT>
 __device__ inline void vh_level_setup(const VhLds& L, int cur, int nb) {
   const int lane = threadIdx.x & 63;
@@ -779,7 +779,7 @@ __device__ inline void vh_depth_limit_wg(const VhLds& L, int n, int lo, int hi) 
 // prof (optional, diagnostics): [0] elements heap-sorted literally; [1..4] cycles of the setup, the
 // workgroup partitions (and depth-limit segments), the wave subtrees, the positions
 template <int NT>
-__device__ inline void vh_sort(uint32_t* lds, int n, int nhot, const VxHot& H, int* err, unsigned long long* prof = nullptr,
+__device__ inline void vh_sort(uint32_t* lds, int n, const VxHot& H, int* err, unsigned long long* prof = nullptr,
                                unsigned long long* dprof = nullptr) {
   const int tid = threadIdx.x;
   unsigned long long tp = __builtin_readcyclecounter(), t_drain = 0;
@@ -798,12 +798,6 @@ __device__ inline void vh_sort(uint32_t* lds, int n, int nhot, const VxHot& H, i
   for (int i = tid; i < VH_ROOTS; i += NT) L.roots[i] = 0u;
   __syncthreads();  // (the entries are zero until listed: tid 0 lists below)
   const int D0 = n > 1 ? 2 * (31 - __clz(n)) : 0;  // 2 * __lg(n)
-  // segments longer than lvl partitioned level by level by the workgroup, shorter ones by waves.
-  // Dense (a quarter of the points hot: stacks, scan rings): the whole workgroup down to 64
-  // elements, as far as the level lists allow (lvl >= n / VH_BIGC); sparse (cube re-filters,
-  // narrow subtrees): above 1024 only (level passes of few segments cost small cubes more than
-  // the waves' chains)
-  const int lvl = 4 * nhot >= n ? max(64, (n + VH_BIGC - 1) / VH_BIGC) : max(VH_BIG, (n + VH_BIGC - 1) / VH_BIGC);
   if (tid == 0) {
     C->nbig[0] = C->nbig[1] = 0;
     C->nroot = C->root_take = 0;
@@ -811,7 +805,7 @@ __device__ inline void vh_sort(uint32_t* lds, int n, int nhot, const VxHot& H, i
     C->heap_el = 0;
     C->dprof = dprof;
     if (n > SS_THRESHOLD) {
-      if (n > lvl) {
+      if (n > VH_BIG) {
         L.bigl[0] = (uint32_t)n << 15;
         C->nbig[0] = 1;
       } else {
@@ -827,17 +821,10 @@ __device__ inline void vh_sort(uint32_t* lds, int n, int nhot, const VxHot& H, i
     const int nb = min(C->nbig[cur], VH_BIGC);
     if (nb == 0) break;
     const int d = D0 - lev;
-    if (d == 0) {  // depth-limit segments: up to 1024 elements on a wave, longer ones here
+    if (d == 0) {
       for (int t = 0; t < nb; ++t) {
         const uint32_t ent = L.bigl[cur * VH_BIGC + t];
-        const int lo = (int)(ent & 0x7FFFu), hi = (int)(ent >> 15);
-        if (hi - lo > 1024) {
-          vh_depth_limit_wg<NT>(L, n, lo, hi);
-        } else if (tid == 0) {
-          const int s = C->nroot++;
-          if (s < VH_ROOTS) L.roots[s] = vh_pack(lo, hi - lo, 0);
-          else C->err |= VH_ERR_ROOTS;
-        }
+        vh_depth_limit_wg<NT>(L, n, (int)(ent & 0x7FFFu), (int)(ent >> 15));
       }
     } else {
       if (tid < 64) vh_level_setup<NT>(L, cur, nb);
@@ -850,7 +837,7 @@ __device__ inline void vh_sort(uint32_t* lds, int n, int nhot, const VxHot& H, i
           const int parts[2][2] = {{lo, cut}, {cut, hi}};
           for (int q = 0; q < 2; ++q) {
             const int a = parts[q][0], b = parts[q][1];
-            if (b - a > lvl) {
+            if (b - a > VH_BIG) {
               const int s = atomicAdd(&C->nbig[nxt], 1);
               if (s < VH_BIGC) L.bigl[nxt * VH_BIGC + s] = (uint32_t)a | ((uint32_t)b << 15);
               else atomicOr(&C->err, VH_ERR_ROOTS);
@@ -1031,7 +1018,7 @@ __device__ inline void vh_fixup(const PF& P, int n, float4* out, const VxHot& H,
   const VxGeom g = M.g;
   float4* o = out + M.sbase[1];
   const unsigned long long t0 = __builtin_readcyclecounter();
-  vh_sort<NT>(lds, n, (int)min(M.hot_l, (uint32_t)n), H, err, sprof, dprof);
+  vh_sort<NT>(lds, n, H, err, sprof, dprof);
   const unsigned long long t1 = __builtin_readcyclecounter();
   const bool mv = vh_centroids<NT>(P, o, H, g, lds, lds_words, M, err);
   if (mv && threadIdx.x == 0 && stable_out) *stable_out = 0u;
