@@ -120,6 +120,23 @@ def test_lm_paths_many_streams(seq, monkeypatch, persistent):
     m.close()
 
 
+def test_many_streams_exact_order(seq):
+    """24 streams in PCL's summation order: the re-VoxelGrid items of all streams go through
+    k_insert_bucket's size-class lists (k_revox dispatches them largest first); every stream's
+    pose, counts and updated map against the oracle"""
+    m = BatchMapper(24, exact_voxel_order=1)
+    for s in range(24):
+        fi = SNAP[s % len(SNAP)]
+        load_state(m, s, seq[fi]["before"])
+        m.input(s, seq[fi]["corner"], seq[fi]["surf"], seq[fi]["q_wodom"], seq[fi]["t_wodom"])
+    m.solve()
+    for s in range(24):
+        rec = seq[SNAP[s % len(SNAP)]]
+        _check_frame(m, s, rec)
+        _check_map(m, s, rec["after"])
+    m.close()
+
+
 @pytest.mark.parametrize("exact", [1, 0])
 @pytest.mark.parametrize("n_corner,n_surf", [(3000, 9000), (20000, 70000)])
 def test_stack_voxelgrid_bit_exact(n_corner, n_surf, exact):
