@@ -654,10 +654,21 @@ __device__ inline void vh_partition_level_c(const VhLds& L, int cur, int nb) {
   uint32_t x = dpp_incl_scan_u(v);
   if (lane == 63) ws[wid] = x;
   __syncthreads();
-  for (int w = 0; w < NW; ++w) x += w < wid ? ws[w] : 0u;  // inclusive over the block
-  if (sg >= 0 && r == 0) V.base[sg] = x - v;
-  if (sg >= 0 && tid == V.tstart[sg + 1] - 1) V.endv[sg] = x;
-  __syncthreads();
+  uint32_t all = 0;
+  for (int w = 0; w < NW; ++w) {
+    x += w < wid ? ws[w] : 0u;  // inclusive over the block
+    all += ws[w];
+  }
+  uint32_t sbase = 0, send = all;  // the scan before the segment's first thread / after its last
+  if (nb > 1) {  // (uniform; one segment: the block's own bounds, no barrier)
+    if (sg >= 0 && r == 0) V.base[sg] = x - v;
+    if (sg >= 0 && tid == V.tstart[sg + 1] - 1) V.endv[sg] = x;
+    __syncthreads();
+    if (sg >= 0) {
+      sbase = V.base[sg];
+      send = V.endv[sg];
+    }
+  }
   const bool act = sg >= 0 && V.hot[sg] + ((pe & VH_HOT) ? 1 : 0) >= 2;
   if (act && r == 0) {  // the median swap (read by nobody before the next barrier)
     E[lo] = pe;
@@ -665,7 +676,7 @@ __device__ inline void vh_partition_level_c(const VhLds& L, int cur, int nb) {
   }
   uint16_t* Bs = L.Bs;
   const int m = hi - lo, KB = (m - 1) / 2, bb = lo >> 1;
-  const uint32_t off = act ? x - v - V.base[sg] : 0u, tot = act ? V.endv[sg] - V.base[sg] : 0u;
+  const uint32_t off = act ? x - v - sbase : 0u, tot = act ? send - sbase : 0u;
   const int nr = 1 + (int)(tot >> 16);
   int S = 0;
   if (act) {
@@ -851,9 +862,9 @@ __device__ inline void vh_sort(uint32_t* lds, int n, const VxHot& H, int* err, u
       }
     }
     __syncthreads();
-    if (tid == 0) C->nbig[cur] = 0;
+    // (nbig[cur] is next read two levels on; nroot is not written before the drain)
     const bool drain = C->nroot > VH_ROOTS - 2 * VH_BIGC;
-    __syncthreads();
+    if (tid == 0) C->nbig[cur] = 0;
     if (drain) {
       const unsigned long long t0 = __builtin_readcyclecounter();
       vh_drain<NT>(L);
