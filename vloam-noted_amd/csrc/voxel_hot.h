@@ -229,9 +229,8 @@ __device__ inline int vh_partition_wave(uint32_t* E, uint16_t* Bs, int lo, int h
 //   * each __pop_heap's hole descends to a leaf along the larger children (the right one unless
 //     right < left).  The wave loads the 5 levels below the hole at once (62 lanes) and decides
 //     every sibling pair with one DPP shift and one ballot; the scalar unit follows the path
-//     through the ballot bits (four scalar instructions a level, no branches: the path length is
-//     known up front but for its last level) and keeps it as a bit code: path node j is
-//     (1 << j) - 1 + (the code's first j bits).  Then every lane loads its path node's child
+//     through the ballot bits (no lane reads on the chain) and keeps it as a bit code: path node
+//     j is (1 << j) - 1 + (the code's first j bits).  Then every lane loads its path node's child
 //     at once, the path's values shift up one place, and __push_heap's value lands below the
 //     lowest ancestor not less than it (the path is non-increasing downwards: one ballot).
 // __make_heap on E[lo, hi), one wave: the parents of one depth on separate lanes
@@ -256,29 +255,24 @@ __device__ inline void vh_sort_heap_wave(uint32_t* E, int lo, int hi) {
   for (int last = hi - 1; last > lo; --last) {
     const int n = last - lo;
     const uint32_t v = E[last], top = E[lo];
-    const int lim = (n - 1) / 2;  // the hole moves down while h < lim
-    // every node above depth F is below lim, and no node below depth F is: the path takes F
-    // levels, then one more when its depth-F node is below lim
-    const int F = 31 - __clz(lim + 1);
+    const int lim = (n - 1) / 2;
     int h = 0, k = 0;  // hole; path length
     uint32_t code = 0;  // the path's directions, first step highest (k <= 15)
-    while (true) {
-      const int need = F - k;
-      if (need < 0 || (need == 0 && h >= lim)) break;
+    while (h < lim) {
       const int node = ((h + 1) << lj) - 1 + lt;
       const uint32_t x = (lane < 62 && node < n) ? E[lo + node] : 0u;
       const uint32_t xr = dpp_from_next(x);  // the right sibling (left children: lt even)
       const uint64_t rw = __ballot(!less(xr, x));
-      // the 5-level path below h, taken speculatively (bits past the heap go unused)
-      uint32_t tt = 0;
+      int tt = 0;
 #pragma unroll
-      for (int jj = 0; jj < 5; ++jj) tt = 2u * tt + (uint32_t)((rw >> ((2u << jj) - 2u + 2u * tt)) & 1ull);
-      int lv = min(5, need);
-      if (lv < 5 && ((h + 1) << lv) - 1 + (int)(tt >> (5 - lv)) < lim) ++lv;  // the conditional level
-      const uint32_t tl = tt >> (5 - lv);
-      h = ((h + 1) << lv) - 1 + (int)tl;
-      code = (code << lv) | tl;
-      k += lv;
+      for (int jj = 0; jj < 5; ++jj) {
+        if (h >= lim) break;
+        const int dir = (int)((rw >> ((1 << (jj + 1)) - 2 + 2 * tt)) & 1ull);
+        h = 2 * h + 1 + dir;
+        tt = 2 * tt + dir;
+        code = 2 * code + (uint32_t)dir;
+        ++k;
+      }
     }
     if ((n & 1) == 0 && h == (n - 2) / 2) {  // one child left
       h = 2 * h + 1;
