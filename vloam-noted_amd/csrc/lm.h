@@ -771,17 +771,16 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
     if (wid == 0) {
       // lane i sums accumulator i over the shares in order (G <= 32: one lane per
       // accumulator beats a shuffle tree per accumulator)
-      if (lane < LM_NACC) {  // loads 8 at a time in flight, added in share order
+      if (lane < LM_NACC) {  // loads 8 at a time in flight (the last batch too), added in share order
         double v = bsum0[lane];
-        int c = 1;
-        for (; c + 8 <= G; c += 8) {
+        for (int c = 1; c < G; c += 8) {
           double q[8];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) q[u] = lm_part_load(&part[(size_t)(c + u) * LM_NACC + lane]);
+          for (int u = 0; u < 8; ++u) q[u] = c + u < G ? lm_part_load(&part[(size_t)(c + u) * LM_NACC + lane]) : 0.0;
 #pragma unroll
-          for (int u = 0; u < 8; ++u) v += q[u];
+          for (int u = 0; u < 8; ++u)
+            if (c + u < G) v += q[u];
         }
-        for (; c < G; ++c) v += lm_part_load(&part[(size_t)c * LM_NACC + lane]);
         sred[lane] = v;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
