@@ -2008,7 +2008,9 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
       // block per CU at some SGPR counts (MI355X_MICROARCH.md, correctness boundaries)
       occ = std::min(occ, 1);
       const int cap = occ * cus;
-      h->lm_G = std::min(LM_EBLK, std::min(8, cap / n_streams));  // 8: one stream 0.601 -> 0.583 ms per frame (16)
+      // 16 at one stream: LM pass 26.5k -> 24.9k cycles once the leader loads the share partials
+      // 8 at a time (4 / 8 / 12 / 16: 30.8k / 26.5k / 25.6k / 24.9k, tools/dbg_lm.py)
+      h->lm_G = std::min(LM_EBLK, std::min(16, cap / n_streams));
       const char* genv = std::getenv("LOAM_LM_G");  // measurement override
       if (genv && std::atoi(genv) > 0) h->lm_G = std::min(LM_EBLK, std::atoi(genv));
     }
