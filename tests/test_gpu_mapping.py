@@ -120,6 +120,21 @@ def test_lm_paths_many_streams(seq, monkeypatch, persistent):
     m.close()
 
 
+@pytest.mark.parametrize("g", ["1", "4", "32"])
+def test_lm_workgroups_override(seq, monkeypatch, g):
+    """LOAM_LM_G (workgroups per stream of the persistent LM round, read at create): the
+    leader's share plus g - 1 claimed shares, reduced in share order, at 1, 4 and 32"""
+    monkeypatch.setenv("LOAM_LM_G", g)
+    for fi in SNAP[:2]:
+        rec = seq[fi]
+        m = BatchMapper(1)
+        load_state(m, 0, rec["before"])
+        m.input(0, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+        m.solve()
+        _check_frame(m, 0, rec)
+        m.close()
+
+
 def test_many_streams_exact_order(seq):
     """24 streams in PCL's summation order: the re-VoxelGrid items of all streams go through
     k_insert_bucket's size-class lists (k_revox dispatches them largest first); every stream's
