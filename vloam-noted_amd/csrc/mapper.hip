@@ -1325,6 +1325,17 @@ __global__ void __launch_bounds__(VX_THREADS) k_insert_bucket(MapperDev D) {
   const int vn = F.valid_num, ne = min(F.extra_n[m], EXTRA_CAP);
   if (tid < vn) cslot[F.window[tid]] = tid;
   if (tid < ne) cslot[F.extra_list[m][tid]] = WIN_VALID_MAX + tid;
+  // this thread's slot (tid < INS_SLOTS) for the re-VoxelGrid list below: its cube's table entry and
+  // token are loaded now, their latency hidden behind the grouping (the revox_target test)
+  int my_cube = -1;
+  if (tid < vn) my_cube = F.window[tid];
+  else if (tid >= WIN_VALID_MAX && tid < WIN_VALID_MAX + ne) my_cube = F.extra_list[m][tid - WIN_VALID_MAX];
+  uint2 my_cv = make_uint2(0u, 0u);
+  uint32_t my_tok = 0u;
+  if (my_cube >= 0) {
+    my_cv = D.cube_tab[sm_index(s, m) * NCUBE + my_cube];
+    my_tok = D.stable_tok[sm_index(s, m) * NCUBE + my_cube];
+  }
   __syncthreads();
   for (int i = tid; i < n; i += VX_THREADS) {
     const int t = tag[i];
@@ -1332,6 +1343,8 @@ __global__ void __launch_bounds__(VX_THREADS) k_insert_bucket(MapperDev D) {
     if (sl >= 0) atomicAdd(&base[sl], 1u);
   }
   __syncthreads();
+  const uint32_t my_new = tid < INS_SLOTS ? base[tid] : 0u;  // points inserted into this slot's cube
+  __syncthreads();  // (every count read before the scan below rewrites base)
   if (wid == 0) {  // exclusive scan of the slot counts by one wave: lane l owns slots l*PL ..
     constexpr int PL = (INS_SLOTS + 63) / 64;
     uint32_t c[PL], sum = 0;
@@ -1396,14 +1409,18 @@ __global__ void __launch_bounds__(VX_THREADS) k_insert_bucket(MapperDev D) {
     if (sl >= 0) out[wcnt[wid][sl] + rank] = pts[i];
     __syncthreads();
   }
-  // this (stream, map)'s re-VoxelGrid items, listed by size class (k_revox takes the largest first)
-  for (int slot = tid; slot < INS_SLOTS; slot += VX_THREADS) {
-    int cube = 0, append = 0;
-    if (!revox_target(D, s, m, slot, &cube, &append)) continue;
-    const uint32_t nt = D.cube_tab[sm_index(s, m) * NCUBE + cube].y + (off[slot + 1] - off[slot]);
-    const int c = nt < 1024u ? 0 : min(RQ_CLASSES - 1, 32 - __clz(nt >> 10));
-    const uint32_t k = atomicAdd(&D.rq_ctl[c], 1u);
-    D.rq[(size_t)c * D.rq_cap + k] = (uint32_t)(sm * INS_SLOTS + slot);
+  // this (stream, map)'s re-VoxelGrid items, listed by size class (k_revox takes the largest
+  // first); the test is revox_target's: a window cube that received nothing and holds fixed-point
+  // (or no) content is skipped
+  static_assert(INS_SLOTS <= VX_THREADS, "one thread per slot");
+  if (my_cube >= 0) {
+    const bool append = tid >= WIN_VALID_MAX;
+    if (append || my_new != 0 || (my_cv.y != 0 && my_tok != my_cv.x + 1)) {
+      const uint32_t nt = my_cv.y + my_new;
+      const int c = nt < 1024u ? 0 : min(RQ_CLASSES - 1, 32 - __clz(nt >> 10));
+      const uint32_t k = atomicAdd(&D.rq_ctl[c], 1u);
+      D.rq[(size_t)c * D.rq_cap + k] = (uint32_t)(sm * INS_SLOTS + tid);
+    }
   }
 }
 
