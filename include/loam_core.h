@@ -128,13 +128,17 @@ int32_t loam_scanreg_device_ptr(loam_scanreg* h, int32_t which, const float** pt
 int32_t loam_scanreg_curvature(loam_scanreg* h, float* curv, int32_t* label, int32_t cap);
 /* device time of the last input (ms) */
 double loam_scanreg_ms(loam_scanreg* h);
-/* cumulative device cycle counters of the per-ring PCL-order VoxelGrid (k_sr_ringvox), summed
- * over rings and frames: [0] cycles of the sort emulation (libstdc++ introsort) for the voxels of 3+ members,
- * [1] of their centroids, [2] rings that had such a voxel, [8] elements heap-sorted at the depth
- * limit, [9..12] cycles of the sort's setup, workgroup levels, wave subtrees and positions;
- * reset = 1 zeroes them after the copy.  Counted only in a handle created with
- * LOAM_PHASE_COUNTERS=1 in the environment. */
-#define LOAM_SR_DEBUG_COUNTERS 16
+/* cumulative device cycle counters of scan registration, summed over rings and frames unless
+ * "max": the per-ring PCL-order VoxelGrid (k_sr_ringvox): [0] cycles of the sort emulation
+ * (libstdc++ introsort) for the voxels of 3+ members, [1] of their centroids, [2] rings that had
+ * such a voxel, [3] max cycles of one ring, [4] cycles of the input-order filter, [5] points,
+ * [6] max points of one ring, [7] max elements heap-sorted in one ring, [8] elements heap-sorted
+ * at the depth limit, [9..12] cycles of the sort's setup, workgroup levels, wave subtrees and
+ * positions; the feature selection (k_sr_select): [13] cycles of the sector sorts, [14] of the
+ * greedy picks, [15] max cycles of one ring; [16] the slowest ring's points, [17] its elements
+ * heap-sorted, [18] its sort cycles.  reset = 1 zeroes them after the copy.  Counted only in a
+ * handle created with LOAM_PHASE_COUNTERS=1 in the environment. */
+#define LOAM_SR_DEBUG_COUNTERS 24
 int32_t loam_scanreg_debug_counters(loam_scanreg* h, uint64_t* out, int32_t n, int32_t reset);
 
 /* --------------------------------------------------------------------------------------

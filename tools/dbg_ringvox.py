@@ -35,3 +35,9 @@ print("scanreg ms/frame", np.mean(ms))
 print("per ring: hot sort cycles %.0f, hot centroids %.0f, filters with a hot voxel %.2f" % tuple(c[:3] / rings))
 print("per ring: elements heap-sorted %.1f; sort phases setup / workgroup levels / wave subtrees / positions %s"
       % (c[8] / rings, [round(float(v) / rings) for v in c[9:13]]))
+print("per ring: input-order filter %.0f cycles, points %.0f (max %d, max heap-sorted %d); slowest ring %d cycles"
+      % (c[4] / rings, c[5] / rings, c[6], c[7], c[3]))
+s16, s18 = int(c[16]), int(c[18])
+print("slowest ring: %d cycles, %d points, %d heap-sorted, %d cycles after the input-order filter"
+      % (s16 >> 32, s16 & 0xFFFF, (s16 >> 16) & 0xFFFF, s18 & 0xFFFFFFFF))
+print("k_sr_select per ring: sector sorts %.0f, greedy %.0f cycles; slowest ring %d" % (c[13] / rings, c[14] / rings, c[15]))

@@ -358,15 +358,18 @@ __global__ void k_sr_curv(SrDev D) {
 // +-5 neighbour suppression of a pick (scan_registration.cpp:402-429): the reference walks
 // outwards while consecutive points are within sqrt(0.05); gapok[k] holds that test for the
 // pair (k, k + 1) of the ring (ring-local indices), precomputed in parallel.
-__device__ inline void sr_suppress(const uint8_t* gapok, uint8_t* picked, int ind) {
-  for (int l = 1; l <= 5; l++) {
-    if (!gapok[ind + l - 1]) break;
-    picked[ind + l] = 1;
+// The reference's neighbour suppression after a pick at ring position i (:389-404): up to 5
+// points on each side are marked picked, each side stopping at the first squared gap > 0.05
+// (gapok[k]: the gap k -> k+1 is not).  nf / nb: the chain lengths ahead and behind (0..5).
+__device__ inline void sr_chain(const uint8_t* gapok, int i, int& nf, int& nb) {
+  uint32_t f = 0, b = 0;
+#pragma unroll
+  for (int l = 0; l < 5; ++l) {
+    f |= (uint32_t)(gapok[i + l] != 0) << l;
+    b |= (uint32_t)(gapok[i - 1 - l] != 0) << l;
   }
-  for (int l = -1; l >= -5; l--) {
-    if (!gapok[ind + l]) break;
-    picked[ind + l] = 1;
-  }
+  nf = __builtin_ctz((~f & 31u) | 32u);
+  nb = __builtin_ctz((~b & 31u) | 32u);
 }
 
 // One wave sorts one sector in registers: E * 64 keys (curvature bits << 32 | index), bitonic,
@@ -453,94 +456,80 @@ __device__ inline void sr_exact_sector(const SrDev& D, int sp, int len, uint64_t
 }
 
 // sharp / lessSharp (descending curvature, :371-431) and flat (ascending, :439-483) picks of
-// one sector from its sorted keys K[0, len): one wave, 64 candidates tested per ballot
+// one sector from its sorted keys K[0, len): one wave.  A window of 64 sorted candidates is
+// loaded with its picked flags and each candidate's suppression chains (sr_chain); a pick then
+// costs no LDS read: the candidates its suppression covers (cloud index within the chains) drop
+// out of the window's mask by one ballot, and picked[] is written for the later windows and
+// sectors.  The reference's next candidate is the first unpicked one behind the pick.
+template <bool SHARP>
+__device__ inline void sr_greedy_pass(SrDev& D, int r, int base, const uint64_t* K, int len, uint8_t* picked,
+                                      int8_t* lab, const uint8_t* gapok, int& nsh, int& nls, int& nfl) {
+  const int lane = threadIdx.x & 63;
+  int count = 0;
+  for (int w = 0; w < len; w += 64) {
+    const int k = SHARP ? len - 1 - w - lane : w + lane;
+    bool cand = false;
+    int ind = base, nf = 0, nb = 0;
+    if (k >= 0 && k < len) {
+      const uint64_t key = K[k];
+      ind = (int)(key & 0xFFFFFFFFu);
+      const double c = (double)__uint_as_float((uint32_t)(key >> 32));
+      // the reference compares the float curvature with the double literal 0.1 (:381, :443): a
+      // curvature of exactly 0.1f (> 0.1) is an edge candidate
+      cand = SHARP ? c > 0.1 : c < 0.1;
+    }
+    // every curvature after the first non-candidate fails the test too (sorted order)
+    const uint64_t bx = __ballot(k >= 0 && k < len && !cand);
+    const int fx = bx ? __ffsll((long long)bx) - 1 : 64;
+    bool avl = cand && lane < fx && picked[ind - base] == 0;
+    if (avl) sr_chain(gapok, ind - base, nf, nb);
+    uint64_t avail = __ballot(avl);
+    while (avail) {
+      const int fc = __ffsll((long long)avail) - 1;
+      const int pind = __builtin_amdgcn_readlane(ind, fc) - base;
+      const int pf = __builtin_amdgcn_readlane(nf, fc), pb = __builtin_amdgcn_readlane(nb, fc);
+      count++;
+      if (SHARP) {
+        if (count > SR_LESS_SHARP) return;
+        if (lane == 0) {
+          if (count <= SR_SHARP) {
+            lab[pind] = 2;
+            D.ring_sharp[r * 6 * SR_SHARP + nsh++] = pind + base;
+          } else {
+            lab[pind] = 1;
+          }
+          D.ring_less_sharp[r * 6 * SR_LESS_SHARP + nls++] = pind + base;
+        }
+      } else {
+        if (lane == 0) {
+          lab[pind] = -1;
+          D.ring_flat[r * 6 * SR_FLAT + nfl++] = pind + base;
+        }
+        if (count >= SR_FLAT) return;
+      }
+      if (lane == 0) picked[pind] = 1;
+      if (lane < pf) picked[pind + 1 + lane] = 1;
+      else if (lane >= 5 && lane - 5 < pb) picked[pind - (lane - 4)] = 1;
+      const int rel = ind - base;
+      avail &= ~__ballot(rel >= pind - pb && rel <= pind + pf);  // the pick and its suppressed neighbours
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the window's writes before the next reads
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (fx < 64) return;
+  }
+}
+
 __device__ inline void sr_greedy(SrDev& D, int r, int base, const uint64_t* K, int len, uint8_t* picked,
                                  int8_t* lab, const uint8_t* gapok, int& nsh, int& nls, int& nfl) {
-  const int lane = threadIdx.x & 63;
-  int largest = 0;
-  int pos = len - 1;
-  while (pos >= 0) {
-    const int k = pos - lane;
-    bool cond = false, low = false;
-    int ind = 0;
-    if (k >= 0) {
-      const uint64_t key = K[k];
-      ind = (int)(key & 0xFFFFFFFFu);
-      const float c = __uint_as_float((uint32_t)(key >> 32));
-      // the reference compares the float curvature with the double literal 0.1 (:381): a
-      // curvature of exactly 0.1f (> 0.1) is an edge candidate
-      cond = picked[ind - base] == 0 && (double)c > 0.1;
-      low = !((double)c > 0.1);
-    }
-    const uint64_t bc = __ballot(cond);
-    const uint64_t bl = __ballot(low);
-    const int fc = bc ? __ffsll((long long)bc) - 1 : 64;
-    const int fl = bl ? __ffsll((long long)bl) - 1 : 64;
-    if (fc < fl) {
-      const int pind = __shfl(ind, fc, 64);
-      largest++;
-      if (largest > SR_LESS_SHARP) break;
-      if (lane == 0) {
-        if (largest <= SR_SHARP) {
-          lab[pind - base] = 2;
-          D.ring_sharp[r * 6 * SR_SHARP + nsh++] = pind;
-          D.ring_less_sharp[r * 6 * SR_LESS_SHARP + nls++] = pind;
-        } else {
-          lab[pind - base] = 1;
-          D.ring_less_sharp[r * 6 * SR_LESS_SHARP + nls++] = pind;
-        }
-        picked[pind - base] = 1;
-        sr_suppress(gapok, picked, pind - base);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      pos = pos - fc - 1;
-    } else if (fl < 64) {
-      break;  // every remaining curvature <= 0.1
-    } else {
-      pos -= 64;
-    }
-  }
-  int smallest = 0;
-  pos = 0;
-  while (pos < len) {
-    const int k = pos + lane;
-    bool cond = false, high = false;
-    int ind = 0;
-    if (k < len) {
-      const uint64_t key = K[k];
-      ind = (int)(key & 0xFFFFFFFFu);
-      const float c = __uint_as_float((uint32_t)(key >> 32));
-      cond = picked[ind - base] == 0 && (double)c < 0.1;  // :443, double literal
-      high = !((double)c < 0.1);
-    }
-    const uint64_t bc = __ballot(cond);
-    const uint64_t bh = __ballot(high);
-    const int fc = bc ? __ffsll((long long)bc) - 1 : 64;
-    const int fh = bh ? __ffsll((long long)bh) - 1 : 64;
-    if (fc < fh) {
-      const int pind = __shfl(ind, fc, 64);
-      if (lane == 0) {
-        lab[pind - base] = -1;
-        D.ring_flat[r * 6 * SR_FLAT + nfl++] = pind;
-      }
-      smallest++;
-      if (smallest >= SR_FLAT) break;
-      if (lane == 0) {
-        picked[pind - base] = 1;
-        sr_suppress(gapok, picked, pind - base);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      pos = pos + fc + 1;
-    } else if (fh < 64) {
-      break;
-    } else {
-      pos += 64;
-    }
-  }
+  sr_greedy_pass<true>(D, r, base, K, len, picked, lab, gapok, nsh, nls, nfl);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  sr_greedy_pass<false>(D, r, base, K, len, picked, lab, gapok, nsh, nls, nfl);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 __global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(SrDev D) {
@@ -587,6 +576,8 @@ __global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(SrDev D) {
     maxlen = max(maxlen, len[j]);
   }
   const bool fast = maxlen <= SR_WSORT_MAX;
+  unsigned long long* prof = D.pdbg;  // (diagnostics: [13] sector sorts, [14] greedy, [15] slowest ring)
+  const unsigned long long t0 = prof ? __builtin_readcyclecounter() : 0ull;
   if (!fast && maxlen > 6 * SR_WSORT_MAX) {
     if (tid == 0) atomicOr(&F.err, SR_ERR_RING);
     return;
@@ -598,6 +589,7 @@ __global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(SrDev D) {
                     ssSeg[wid][0], ssSeg[wid][1], SR_SS_SEG);
   }
   __syncthreads();
+  const unsigned long long t1 = prof ? __builtin_readcyclecounter() : 0ull;
   int nsh = 0, nls = 0, nfl = 0;  // valid in wave 0
   for (int j = 0; j < 6; j++) {
     const uint64_t* K = keys + j * SR_WSORT_MAX;
@@ -634,6 +626,12 @@ __global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(SrDev D) {
     if (!fast) __syncthreads();
   }
   __syncthreads();
+  if (prof && tid == 0) {
+    const unsigned long long t2 = __builtin_readcyclecounter();
+    atomicAdd(prof + 13, t1 - t0);
+    atomicAdd(prof + 14, t2 - t1);
+    atomicMax(prof + 15, t2 - t0);
+  }
   // lessFlat candidates: label <= 0 in index order (:486-493) over [s, e), the 6 sectors
   // back to back; stable block compaction
   int nlf = 0;
@@ -674,10 +672,23 @@ static_assert(SR_RING_CAP <= VH_MAX_N, "a ring's lessFlat cloud fits the LDS emu
 // filter is inlined into the kernel; declared here, the array keeps its LDS address space)
 __device__ __noinline__ void sr_ringvox(const VoxSeg& S, int n, int* err, unsigned long long* prof) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
+  const unsigned long long t0 = __builtin_readcyclecounter();
   voxel_segment(S, lds);
-  vh_fixup<SRV_THREADS>(VxSrc{S.src0, n, nullptr}, n, S.out, S.hot, lds, VX_LDS_WORDS - 256,
-                        *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192), nullptr, err, prof,
-                        prof ? prof + 8 : nullptr);  // (diagnostics: [8] heap-sorted, [9..12] sort phases)
+  const unsigned long long t1 = __builtin_readcyclecounter();
+  const int heap_el = vh_fixup<SRV_THREADS>(VxSrc{S.src0, n, nullptr}, n, S.out, S.hot, lds, VX_LDS_WORDS - 256,
+                                            *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192), nullptr, err,
+                                            prof, prof ? prof + 8 : nullptr);
+  if (prof && threadIdx.x == 0) {  // (diagnostics: include/loam_core.h LOAM_SR_DEBUG_COUNTERS)
+    const unsigned long long t2 = __builtin_readcyclecounter();
+    atomicAdd(prof + 4, t1 - t0);
+    atomicAdd(prof + 5, (unsigned long long)n);
+    atomicMax(prof + 6, (unsigned long long)n);
+    atomicMax(prof + 7, (unsigned long long)heap_el);
+    // the slowest ring: its cycles in the high bits, then its heap-sorted elements and points
+    atomicMax(prof + 3, t2 - t0);
+    atomicMax(prof + 16, ((t2 - t0) << 32) | ((unsigned long long)heap_el << 16) | (unsigned long long)n);
+    atomicMax(prof + 18, ((t2 - t0) << 32) | (t2 - t1));
+  }
 }
 
 __global__ void __launch_bounds__(SRV_THREADS) k_sr_ringvox(SrDev D) {

@@ -790,7 +790,7 @@ __device__ inline void vh_depth_limit_wg(const VhLds& L, int n, int lo, int hi) 
 // prof (optional, diagnostics): [0] elements heap-sorted literally; [1..4] cycles of the setup, the
 // workgroup partitions (and depth-limit segments), the wave subtrees, the positions
 template <int NT>
-__device__ inline void vh_sort(uint32_t* lds, int n, const VxHot& H, int* err, unsigned long long* prof = nullptr,
+__device__ inline int vh_sort(uint32_t* lds, int n, const VxHot& H, int* err, unsigned long long* prof = nullptr,
                                unsigned long long* dprof = nullptr) {
   const int tid = threadIdx.x;
   unsigned long long tp = __builtin_readcyclecounter(), t_drain = 0;
@@ -880,13 +880,15 @@ __device__ inline void vh_sort(uint32_t* lds, int n, const VxHot& H, int* err, u
   vh_drain<NT>(L);
   vx_phase(prof ? prof + 3 : nullptr, 0, &tp);
   if (tid == 0 && C->err) atomicOr(err, C->err);
-  if (tid == 0 && prof) atomicAdd(prof, (unsigned long long)C->heap_el);
+  const int heap_el = C->heap_el;
+  if (tid == 0 && prof) atomicAdd(prof, (unsigned long long)heap_el);
   for (int q = tid; q < n; q += NT) {
     const uint32_t e = L.E[q];
     if (e & VH_HOT) H.fpos[e & 0x7FFFu] = (uint32_t)q;
   }
   __syncthreads();
   vx_phase(prof ? prof + 4 : nullptr, 0, &tp);
+  return heap_el;
 }
 
 // Phase 3: every hot voxel's centroid from its members in position order -> out[slot].  The
@@ -1019,17 +1021,18 @@ __device__ inline bool vh_centroids(const PF& P, float4* out, const VxHot& H, co
 // (cold voxels) is cleared when a hot centroid left its voxel.  All NT threads; uniform.
 // prof (optional, diagnostics): [0] cycles of the emulated sort, [1] of the hot centroids, [2]
 // filters with a hot voxel; sprof: vh_sort's (literal heap elements, setup, workgroup levels,
-// wave subtrees, positions)
+// wave subtrees, positions).  Returns the elements heap-sorted at the depth limit (0 without a
+// hot voxel; diagnostics).
 template <int NT, typename PF>
-__device__ inline void vh_fixup(const PF& P, int n, float4* out, const VxHot& H, uint32_t* lds, uint32_t lds_words,
+__device__ inline int vh_fixup(const PF& P, int n, float4* out, const VxHot& H, uint32_t* lds, uint32_t lds_words,
                                 VxMisc& M, uint32_t* stable_out, int* err, unsigned long long* prof = nullptr,
                                 unsigned long long* sprof = nullptr, unsigned long long* dprof = nullptr) {
   __syncthreads();
-  if (M.hot_n == 0) return;
+  if (M.hot_n == 0) return 0;
   const VxGeom g = M.g;
   float4* o = out + M.sbase[1];
   const unsigned long long t0 = __builtin_readcyclecounter();
-  vh_sort<NT>(lds, n, H, err, sprof, dprof);
+  const int heap_el = vh_sort<NT>(lds, n, H, err, sprof, dprof);
   const unsigned long long t1 = __builtin_readcyclecounter();
   const bool mv = vh_centroids<NT>(P, o, H, g, lds, lds_words, M, err);
   if (mv && threadIdx.x == 0 && stable_out) *stable_out = 0u;
@@ -1039,6 +1042,7 @@ __device__ inline void vh_fixup(const PF& P, int n, float4* out, const VxHot& H,
     atomicAdd(prof + 2, 1ull);
   }
   __syncthreads();
+  return heap_el;
 }
 
 }  // namespace loam

@@ -105,6 +105,6 @@ class ScanRegistration:
 
     def debug_counters(self, reset=False):
         """ring VoxelGrid phase cycles (include/loam_core.h LOAM_SR_DEBUG_COUNTERS)"""
-        out = np.zeros(16, np.uint64)
-        check(lib().loam_scanreg_debug_counters(self.h, ptr(out), 16, int(reset)))
+        out = np.zeros(24, np.uint64)
+        check(lib().loam_scanreg_debug_counters(self.h, ptr(out), 24, int(reset)))
         return out
