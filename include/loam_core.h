@@ -135,9 +135,11 @@ double loam_scanreg_ms(loam_scanreg* h);
  * [6] max points of one ring, [7] max elements heap-sorted in one ring, [8] elements heap-sorted
  * at the depth limit, [9..12] cycles of the sort's setup, workgroup levels, wave subtrees and
  * positions; the feature selection (k_sr_select): [13] cycles of the sector sorts, [14] of the
- * greedy picks, [15] max cycles of one ring; [16] the slowest ring's points, [17] its elements
- * heap-sorted, [18] its sort cycles.  reset = 1 zeroes them after the copy.  Counted only in a
- * handle created with LOAM_PHASE_COUNTERS=1 in the environment. */
+ * greedy picks, [15] max cycles of one ring, [19] / [20] max of one ring's sector sorts / greedy
+ * picks; [16] the slowest VoxelGrid ring: its cycles << 32 | heap-sorted elements << 16 | points,
+ * [18] its cycles << 32 | its cycles after the input-order filter.  reset = 1 zeroes them
+ * after the copy.  Counted only in a handle created with LOAM_PHASE_COUNTERS=1 in the
+ * environment. */
 #define LOAM_SR_DEBUG_COUNTERS 24
 int32_t loam_scanreg_debug_counters(loam_scanreg* h, uint64_t* out, int32_t n, int32_t reset);
 

@@ -40,4 +40,5 @@ print("per ring: input-order filter %.0f cycles, points %.0f (max %d, max heap-s
 s16, s18 = int(c[16]), int(c[18])
 print("slowest ring: %d cycles, %d points, %d heap-sorted, %d cycles after the input-order filter"
       % (s16 >> 32, s16 & 0xFFFF, (s16 >> 16) & 0xFFFF, s18 & 0xFFFFFFFF))
-print("k_sr_select per ring: sector sorts %.0f, greedy %.0f cycles; slowest ring %d" % (c[13] / rings, c[14] / rings, c[15]))
+print("k_sr_select per ring: sector sorts %.0f (max %d), greedy %.0f (max %d) cycles; slowest ring %d"
+      % (c[13] / rings, c[19], c[14] / rings, c[20], c[15]))

@@ -225,64 +225,84 @@ __global__ void __launch_bounds__(1024) k_sr_oris(SrDev D, int nblocks) {
 __global__ void __launch_bounds__(1024) k_sr_ring_scan(SrDev D, int nblocks) {
   __shared__ uint32_t ws[VX_WAVES + 1];
   __shared__ int ring_tot[SR_MAX_RINGS];
+  __shared__ int wl[16];
   SrFrame& F = *D.fr;
   const int total = SR_MAX_RINGS * nblocks;
-  const int per = (total + 1023) / 1024;
-  const int b0 = threadIdx.x * per;
   {  // the halfPassed latch: the lowest of the blocks' first indices past startOri + pi
     int lt = 0x7FFFFFFF;
     for (int k = threadIdx.x; k < nblocks; k += 1024) lt = min(lt, D.blk_aux[2 * nblocks + k]);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) lt = min(lt, __shfl_xor(lt, o, 64));
-    if ((threadIdx.x & 63) == 0 && lt != 0x7FFFFFFF) atomicMin(&F.latch, lt);
+    if ((threadIdx.x & 63) == 0) wl[threadIdx.x >> 6] = lt;
+    __syncthreads();
+    if (threadIdx.x == 0) {  // one plain store (this workgroup is the only writer): 16 contended
+      for (int k = 0; k < 16; ++k) lt = min(lt, wl[k]);  // device atomics cost ~7 us
+      F.latch = lt;
+    }
   }
-  // exclusive scan of the flattened [ring][block] histogram: wave w owns a contiguous chunk and
-  // reads it 64 consecutive entries at a time (coalesced), wave totals -> chunk offsets -> the
-  // scan; a ring starts at the prefix of its block 0
+  // exclusive scan of the flattened [ring][block] histogram: thread t holds RS_PER consecutive
+  // entries in registers (all its loads in flight at once: the pass is one memory latency, not
+  // one per 64-entry step), one block scan of the thread sums, then the thread writes its
+  // prefixes; a ring starts at the prefix of its block 0
+  constexpr int RS_PER = 32;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int chunk = ((total + 16 * 256 - 1) / (16 * 256)) * 256;
-  const int c0 = wid * chunk, c1 = min(total, c0 + chunk);
-  uint32_t wsum = 0;
-  for (int e0 = c0; e0 < c1; e0 += 256) {  // four loads in flight
-    uint32_t v[4];
+  uint32_t carry = 0;
+  for (int r0 = 0; r0 < total; r0 += 1024 * RS_PER) {
+    const int e0 = r0 + threadIdx.x * RS_PER;
+    uint32_t v[RS_PER];
+    if (e0 + RS_PER <= total) {
+      const int4* src = reinterpret_cast<const int4*>(D.blk_hist + e0);  // e0 % 4 == 0: 16-byte aligned
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int e = e0 + 64 * j + lane;
-      v[j] = e < c1 ? (uint32_t)D.blk_hist[e] : 0u;
-    }
-    wsum += v[0] + v[1] + v[2] + v[3];
-  }
-  wsum = wave_sum_u(wsum);
-  if (lane == 0) ws[wid] = wsum;
-  __syncthreads();
-  uint32_t base = 0, tot = 0;
-  for (int k = 0; k < 16; ++k) {
-    const uint32_t v = ws[k];
-    base += k < wid ? v : 0u;
-    tot += v;
-  }
-  for (int e0 = c0; e0 < c1; e0 += 256) {
-    uint32_t vv[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int e = e0 + 64 * j + lane;
-      vv[j] = e < c1 ? (uint32_t)D.blk_hist[e] : 0u;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int e = e0 + 64 * j + lane;
-      const uint32_t v = vv[j];
-      const uint32_t inc = wave_incl_scan_u(v);
-      const uint32_t pre = base + inc - v;
-      if (e < c1) {
-        D.blk_off[e] = (int)pre;
-        if (e % nblocks == 0) ring_tot[e / nblocks] = (int)pre;
+      for (int j = 0; j < RS_PER / 4; ++j) {
+        const int4 q = src[j];
+        v[4 * j] = (uint32_t)q.x;
+        v[4 * j + 1] = (uint32_t)q.y;
+        v[4 * j + 2] = (uint32_t)q.z;
+        v[4 * j + 3] = (uint32_t)q.w;
       }
-      base += __shfl(inc, 63, 64);
+    } else {
+#pragma unroll
+      for (int j = 0; j < RS_PER; ++j) v[j] = e0 + j < total ? (uint32_t)D.blk_hist[e0 + j] : 0u;
     }
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < RS_PER; ++j) sum += v[j];
+    const uint32_t inc = wave_incl_scan_u(sum);
+    if (lane == 63) ws[wid] = inc;
+    __syncthreads();
+    uint32_t pre = carry + inc - sum, tot_r = 0;
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t w = ws[k];
+      pre += k < wid ? w : 0u;
+      tot_r += w;
+    }
+    if (e0 < total) {
+      int nxt = ((e0 + nblocks - 1) / nblocks) * nblocks;  // the first ring start at or after e0
+      uint32_t o[RS_PER];
+#pragma unroll
+      for (int j = 0; j < RS_PER; ++j) {
+        o[j] = pre;
+        if (e0 + j == nxt) {
+          ring_tot[nxt / nblocks] = (int)pre;
+          nxt += nblocks;
+        }
+        pre += v[j];
+      }
+      if (e0 + RS_PER <= total) {
+        int4* dst = reinterpret_cast<int4*>(D.blk_off + e0);
+#pragma unroll
+        for (int j = 0; j < RS_PER / 4; ++j)
+          dst[j] = make_int4((int)o[4 * j], (int)o[4 * j + 1], (int)o[4 * j + 2], (int)o[4 * j + 3]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < RS_PER; ++j)
+          if (e0 + j < total) D.blk_off[e0 + j] = (int)o[j];
+      }
+    }
+    carry += tot_r;
+    __syncthreads();  // ws is rewritten by the next round
   }
-  (void)per;
-  (void)b0;
+  const uint32_t tot = carry;
   __syncthreads();
   if (threadIdx.x <= SR_MAX_RINGS) {
     const int r = threadIdx.x;
@@ -631,6 +651,8 @@ __global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(SrDev D) {
     atomicAdd(prof + 13, t1 - t0);
     atomicAdd(prof + 14, t2 - t1);
     atomicMax(prof + 15, t2 - t0);
+    atomicMax(prof + 19, t1 - t0);
+    atomicMax(prof + 20, t2 - t1);
   }
   // lessFlat candidates: label <= 0 in index order (:486-493) over [s, e), the 6 sectors
   // back to back; stable block compaction
