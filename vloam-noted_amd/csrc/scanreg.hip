@@ -112,6 +112,20 @@ __device__ inline int sr_scan_id(float x, float y, float z, int n_scans) {
   return scanID;
 }
 
+// the frame record's initial state, written on the device (a pageable host-to-device copy of it
+// cost the stream a staging round trip per frame)
+__global__ void __launch_bounds__(256) k_sr_init(SrFrame* F, int n_in) {
+  uint32_t* w = reinterpret_cast<uint32_t*>(F);
+  for (int k = threadIdx.x; k < (int)(sizeof(SrFrame) / 4); k += 256) w[k] = 0u;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    F->n_in = n_in;
+    F->first = 0x7FFFFFFF;
+    F->last = -1;
+    F->latch = 0x7FFFFFFF;
+  }
+}
+
 // one point per thread; every block leaves its first / last valid index in blk_aux (one
 // contended device-scope atomic per block or wave cost ~100 us per frame)
 __global__ void __launch_bounds__(SR_BLOCK) k_sr_valid(SrDev D, int nblocks) {
@@ -913,13 +927,9 @@ static int32_t sr_launch(loam_scanreg* h, const float* xyz, int32_t n, int32_t s
     if (n) LOAM_HIP(hipMemcpyAsync(h->d_in, xyz, sizeof(float) * (size_t)n * stride, hipMemcpyHostToDevice, st));
     D.xyz = h->d_in;
   }
-  SrFrame f{};
-  f.n_in = n;
-  f.first = 0x7FFFFFFF;
-  f.last = -1;
-  f.latch = 0x7FFFFFFF;
+  static_assert(sizeof(SrFrame) % 4 == 0, "k_sr_init writes the record by words");
   LOAM_HIP(hipEventRecord(h->ev[0], st));
-  LOAM_HIP(hipMemcpyAsync(D.fr, &f, sizeof(SrFrame), hipMemcpyHostToDevice, st));
+  k_sr_init<<<1, 256, 0, st>>>(D.fr, n);
   const int nblocks = std::max(1, (n + SR_BLOCK - 1) / SR_BLOCK);
   if (n > 0) {
     k_sr_valid<<<nblocks, SR_BLOCK, 0, st>>>(D, nblocks);
