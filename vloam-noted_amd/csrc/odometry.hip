@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "common.h"
@@ -497,6 +498,7 @@ struct loam_odometry {
   loam_params P{};
   OdomDev D{};
   std::vector<OdomFrame> hf;
+  OdomFrame* hf_pin = nullptr;  // page-locked staging of hf: the per-solve copies stay DMA copies
   std::vector<OdomHost> hs;
   std::vector<void*> allocs;
   hipStream_t st = nullptr;
@@ -517,6 +519,9 @@ int32_t od_alloc(loam_odometry* h, T** p, size_t n) {
 }
 
 void od_free(loam_odometry* h) {
+  if (h->st) (void)hipStreamSynchronize(h->st);
+  if (h->hf_pin) (void)hipHostFree(h->hf_pin);
+  h->hf_pin = nullptr;
   for (void* p : h->allocs) (void)hipFree(p);
   h->allocs.clear();
   for (auto& e : h->ev)
@@ -597,6 +602,8 @@ int32_t loam_odometry_create(const loam_params* p, int32_t device, int32_t n_str
   h->hf.assign(B, OdomFrame{});
   h->hs.assign(B, OdomHost{});
   for (auto& F : h->hf) F.x[3] = 1.0;
+  if (hipHostMalloc(reinterpret_cast<void**>(&h->hf_pin), sizeof(OdomFrame) * B, hipHostMallocDefault) != hipSuccess)
+    return fail(LOAM_ERR_HIP);
   if (hipStreamSynchronize(h->st) != hipSuccess) return fail(LOAM_ERR_HIP);
   *out = h;
   return LOAM_OK;
@@ -698,8 +705,9 @@ int32_t loam_odometry_solve(loam_odometry* h) {
   if (!any) return LOAM_OK;
   hipStream_t st = h->st;
   OdomDev& D = h->D;
+  std::memcpy(h->hf_pin, h->hf.data(), sizeof(OdomFrame) * B);  // the stream is idle (synchronized below)
   LOAM_HIP(hipEventRecord(h->ev[0], st));
-  LOAM_HIP(hipMemcpyAsync(D.fr, h->hf.data(), sizeof(OdomFrame) * B, hipMemcpyHostToDevice, st));
+  LOAM_HIP(hipMemcpyAsync(D.fr, h->hf_pin, sizeof(OdomFrame) * B, hipMemcpyHostToDevice, st));
   if (any_inited) {
     // one wave per query: enough workgroups per stream for the largest query count
     int maxq = 1;
@@ -714,8 +722,9 @@ int32_t loam_odometry_solve(loam_odometry* h) {
   k_od_build<<<B * 2, OD_BUILD_THREADS, 0, st>>>(D);
   LOAM_HIP(hipGetLastError());
   LOAM_HIP(hipEventRecord(h->ev[1], st));
-  LOAM_HIP(hipMemcpyAsync(h->hf.data(), D.fr, sizeof(OdomFrame) * B, hipMemcpyDeviceToHost, st));
+  LOAM_HIP(hipMemcpyAsync(h->hf_pin, D.fr, sizeof(OdomFrame) * B, hipMemcpyDeviceToHost, st));
   LOAM_HIP(hipStreamSynchronize(st));
+  std::memcpy(h->hf.data(), h->hf_pin, sizeof(OdomFrame) * B);
   float ms = 0.f;
   LOAM_HIP(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
   int err = 0;
