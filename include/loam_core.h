@@ -31,8 +31,14 @@ extern "C" {
 #define LOAM_ERR_CAPACITY (-3)  /* a device buffer would overflow (see loam_params caps) */
 #define LOAM_ERR_STATE (-4)     /* call out of order (e.g. solve without input) */
 #define LOAM_ERR_NODEVICE (-5)  /* no HIP device / wrong architecture */
-#define LOAM_ERR_SYNC (-6)      /* a persistent LM round's workgroup hand-off timed out (lm.h spin
-                                   bound); the frame's state is not trustworthy: reset the stream */
+#define LOAM_ERR_SYNC (-6)      /* a bounded device wait ran out: a persistent LM round's workgroup
+                                   hand-off (lm.h), the frame's stack VoxelGrid, or a wave's wait in
+                                   the PCL-order sort's subtree drain (voxel_hot.h); the frame's state
+                                   is not trustworthy: reset the stream */
+#define LOAM_ERR_EARLIER (-7)   /* loam_mapper_wait / _solve: the frame this call finished is fine,
+                                   but an earlier one, finished by loam_mapper_solve_async to make
+                                   room, failed with LOAM_ERR_CAPACITY or _SYNC (loam_last_error
+                                   names it); that frame was committed as computed */
 
 /* ROS parameters of loam_velodyne_HDL_64_kitti.launch:3-16 + vloam_main.launch:4, plus
  * device capacities.  loam_params_default() gives the KITTI launch values. */
@@ -242,10 +248,14 @@ int32_t loam_mapper_solve(loam_mapper* h);
  * newest frame waited for (a frame enqueued with nothing before it in the queue is waited for by
  * them first); every other call waits for every frame in the queue.  Device inputs must stay
  * valid until the frame that takes them is waited for.
- * Status: _wait returns the status of the frame it finishes.  _async called with two frames in
- * the queue first finishes the oldest; a LOAM_ERR_CAPACITY / LOAM_ERR_SYNC it returns is that
- * older frame's (its pose and stats are readable as after _wait), and the new frame IS enqueued;
- * LOAM_ERR_HIP / _ARG / _STATE mean the new frame was not enqueued. */
+ * Status: _async returns LOAM_OK exactly when it enqueued the new frame; any other status means
+ * nothing was enqueued (give the same input again or drop it).  _async called with two frames in
+ * the queue first finishes the oldest (its pose and stats are readable as after _wait); if that
+ * frame failed (LOAM_ERR_CAPACITY / LOAM_ERR_SYNC) its status is held and the next _wait or
+ * loam_mapper_solve returns LOAM_ERR_EARLIER (unless the frame that call finishes fails itself,
+ * which is returned first; the held status then waits for the call after).  _wait returns the
+ * status of the frame it finishes.  A queued frame that could not be enqueued when its turn came
+ * is dropped, and the call that tried returns that error with "dropped" in loam_last_error. */
 int32_t loam_mapper_solve_async(loam_mapper* h);
 int32_t loam_mapper_wait(loam_mapper* h);
 /* queue the stack VoxelGrids of every stream's pending input now (no-op with profiling on) */

@@ -157,8 +157,9 @@ class BatchMapper {
   // solve() in two halves (loam_mapper_solve_async / _wait): enqueue the frame and return; wait
   // for the oldest frame not yet waited for.  Two frames may be in the queue: give frame f + 1's
   // input and solve_async() while frame f is in flight (on a graph-path handle, <= 4 streams, the
-  // device runs f + 1 right behind f).  A throw from solve_async() with LOAM_ERR_CAPACITY or
-  // LOAM_ERR_SYNC reports the older frame it finished; the new frame is enqueued all the same.
+  // device runs f + 1 right behind f).  solve_async() throws only when it did not enqueue the
+  // frame; an older frame it finished to make room that failed is reported by the next wait() /
+  // solve() (LOAM_ERR_EARLIER), so a caller that re-submits on a throw never queues a frame twice.
   void solve_async() { check(loam_mapper_solve_async(h_)); }
   void wait() { check(loam_mapper_wait(h_)); }
   // queue the stack VoxelGrids of the inputs given so far (they run beside the frame in flight)

@@ -525,13 +525,20 @@ def test_chained_solve_matches_blocking(seq, n_streams, exact, defer_every, monk
 
 
 @pytest.mark.parametrize("exact", [0, 1])
-def test_split_prefetch_matches_blocking(seq, exact):
+@pytest.mark.parametrize("n_streams", [2, 16])
+def test_split_prefetch_matches_blocking(seq, exact, n_streams):
     """streams of one frame taking their stacks from two different stack launches of the same
-    parity: stream 0's input is given and its stack VoxelGrid launched (loam_mapper_prefetch),
-    then stream 1's input, whose stack the solve launches; the frames queue behind each other
-    (graph path, k_frame_prep waits for each stream's own launch and then acquires before it reads
-    the stack sizes, which share one cache line).  Every pose and count equals the blocking solve"""
-    n_streams = 2
+    parity: the first half of the streams get their inputs and their stack VoxelGrids launched
+    (loam_mapper_prefetch), then the other half, whose stacks the solve launches; the frames queue
+    behind each other.  The stack points are written by k_stack_ds on the second HIP stream and
+    read by the kNN / insertion kernels on the first, on whichever XCD they land: k_frame_prep
+    waits for each stream's own stack launch (relaxed agent-scope loads of the launch counter and
+    of the stack sizes, which share cache lines), and the points themselves are ordered by kernel
+    boundaries (k_stack_ds's end-of-kernel release before k_stack_done's counter store on its
+    stream; the consumers' start-of-kernel acquire after k_frame_prep saw the counter; DESIGN.md
+    §6).  At 16 streams the stacks of one frame come from both launches, blocks of many XCDs.
+    Every pose and count equals the blocking solve"""
+    half = n_streams // 2
 
     def row(m, s):
         st = m.stats(s)
@@ -540,10 +547,10 @@ def test_split_prefetch_matches_blocking(seq, exact):
                 st.lm[0].iterations, st.lm[1].iterations)
 
     def give(m, f, s):
-        rec = seq[f + s]
+        rec = seq[f + s % 4]
         m.input(s, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
 
-    n = len(seq) - n_streams + 1
+    n = len(seq) - 3
     ref = BatchMapper(n_streams, exact_voxel_order=exact)
     want = []
     for f in range(n):
@@ -555,10 +562,12 @@ def test_split_prefetch_matches_blocking(seq, exact):
     m = BatchMapper(n_streams, exact_voxel_order=exact)
     got = []
     for f in range(n):
-        give(m, f, 0)
-        m.prefetch()  # stream 0's stack: its own launch
-        give(m, f, 1)
-        m.solve_async()  # stream 1's stack launched here; queued behind frame f - 1
+        for s in range(half):
+            give(m, f, s)
+        m.prefetch()  # the first half's stacks: their own launch
+        for s in range(half, n_streams):
+            give(m, f, s)
+        m.solve_async()  # the second half's stacks launched here; queued behind frame f - 1
         if f:
             m.wait()
             got.append([row(m, s) for s in range(n_streams)])
@@ -566,3 +575,61 @@ def test_split_prefetch_matches_blocking(seq, exact):
     got.append([row(m, s) for s in range(n_streams)])
     m.close()
     assert got == want
+
+
+def test_async_capacity_error_is_held_for_wait(seq):
+    """loam_mapper_solve_async returns OK exactly when it enqueued its frame.  With two frames in
+    the queue it first finishes the oldest; when that one fails (here: its submap exceeds
+    max_submap_points, a LOAM_ERR_CAPACITY committed as computed), the status is held and the next
+    wait returns LOAM_ERR_EARLIER, so a caller that re-submits on a failed solve_async cannot
+    queue a frame twice.  Every frame runs exactly once: the poses equal the blocking solve's,
+    which reports the same frames as failed."""
+    from loam_amd._core import LoamError
+
+    probe = BatchMapper(1)
+    sizes = []
+    for rec in seq:
+        probe.input(0, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+        probe.solve()
+        st = probe.stats(0)
+        sizes.append(max(st.corner_map, st.surf_map))
+    probe.close()
+    cap = sizes[5] + 1  # frames whose submap is larger fail from here on
+    assert any(v >= cap for v in sizes[6:]), sizes
+
+    def pose(m):
+        q, t = m.pose(0)
+        return np.concatenate([q, t]).tobytes()
+
+    ref = BatchMapper(1, max_submap_points=cap)
+    want, want_fail = [], []
+    for rec in seq:
+        ref.input(0, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+        try:
+            ref.solve()
+            want_fail.append(False)
+        except LoamError as e:
+            assert e.rc == -3, e
+            want_fail.append(True)
+        want.append(pose(ref))
+    ref.close()
+    assert any(want_fail) and not all(want_fail), want_fail
+
+    m = BatchMapper(1, max_submap_points=cap)
+    earlier = 0
+    for f, rec in enumerate(seq):
+        m.input(0, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+        m.solve_async()  # never raises here: every frame is enqueued (two in the queue from f = 1)
+    fails = 0
+    for _ in range(3):  # the last two frames, then the held status of the earlier ones
+        try:
+            m.wait()
+        except LoamError as e:
+            assert e.rc in (-3, -7), e
+            fails += 1
+            earlier += e.rc == -7
+    # the frames solve_async finished were failures held for a wait: at least one was reported
+    assert earlier >= 1
+    # every frame ran exactly once: the final pose is the blocking solve's
+    assert pose(m) == want[-1]
+    m.close()

@@ -28,6 +28,10 @@ namespace loam {
 
 int32_t comm_allreduce(loam_comm* c, void* d_buf, int64_t count, int32_t dtype, hipStream_t st);
 int32_t comm_allgather(loam_comm* c, const void* d_send, void* d_recv, int64_t bytes, hipStream_t st);
+// a rank's solve failed outside a collective: an in-process group (kind 2) is broken so the other
+// ranks fail their next collective at once instead of waiting out the timeout (no-op otherwise:
+// RCCL and callback transports own their failure handling)
+void comm_abort(loam_comm* c);
 
 // 4 m voxel-aligned ownership blocks: voxel v = floor(p / leaf) as PCL computes it
 // (floorf(p * (1/leaf)), voxel.h); block = floor(v / bv) with bv voxels per block edge, so a

@@ -123,6 +123,13 @@ struct LocalGroup {
     }
     return true;
   }
+  // a rank that fails between or inside collectives (or leaves the group) breaks it at once:
+  // the other ranks' barriers return false now instead of after their 120 s timeout
+  void break_group() {
+    std::lock_guard<std::mutex> lk(mu);
+    broken = true;
+    cv.notify_all();
+  }
 };
 
 struct LocalSum {
@@ -138,11 +145,9 @@ __global__ void k_local_sum(LocalSum in, int nsrc, T* out, int64_t count) {
   }
 }
 
-// steps 1 and 2; returns the parity
-static int32_t local_stage(loam_comm* c, const void* d_in, size_t bytes, hipStream_t st, int* par) {
-  LocalGroup& G = *c->local;
-  const int r = c->rank, p = (int)(c->seq++ & 1);
-  *par = p;
+// steps 1 and 2; returns the parity.  A HIP failure before the barrier breaks the group (the
+// other ranks would otherwise wait for this one until their timeout)
+static int32_t local_stage_hip(LocalGroup& G, int r, int p, const void* d_in, size_t bytes, hipStream_t st) {
   for (int q = 0; q < G.size; ++q)
     if (G.usedB[p][q]) LOAM_HIP(hipStreamWaitEvent(st, G.evB[p][q], 0));
   if (G.cap[p][r] < bytes) {  // (grows rarely; hipFree waits for the device)
@@ -154,6 +159,17 @@ static int32_t local_stage(loam_comm* c, const void* d_in, size_t bytes, hipStre
   }
   LOAM_HIP(hipMemcpyAsync(G.stage[p][r], d_in, bytes, hipMemcpyDeviceToDevice, st));
   LOAM_HIP(hipEventRecord(G.evA[p][r], st));
+  return LOAM_OK;
+}
+static int32_t local_stage(loam_comm* c, const void* d_in, size_t bytes, hipStream_t st, int* par) {
+  LocalGroup& G = *c->local;
+  const int r = c->rank, p = (int)(c->seq++ & 1);
+  *par = p;
+  const int32_t rc = local_stage_hip(G, r, p, d_in, bytes, st);
+  if (rc != LOAM_OK) {
+    G.break_group();
+    return rc;
+  }
   if (!G.barrier()) {
     set_error("local comm: a rank did not reach the collective (group broken)");
     return LOAM_ERR_SYNC;
@@ -191,6 +207,10 @@ static int32_t local_allgather(loam_comm* c, const void* d_send, void* d_recv, i
   LOAM_HIP(hipEventRecord(G.evB[p][c->rank], st));
   G.usedB[p][c->rank] = true;
   return LOAM_OK;
+}
+
+void comm_abort(loam_comm* c) {
+  if (c && c->kind == 2 && c->local) c->local->break_group();
 }
 
 int32_t comm_allreduce(loam_comm* c, void* d_buf, int64_t count, int32_t dtype, hipStream_t st) {
@@ -329,6 +349,12 @@ int32_t loam_comm_create_local(int32_t size, int32_t device, loam_comm** out) {
     for (int r = 0; r < size; ++r)
       if (hipEventCreateWithFlags(&G->evA[p][r], hipEventDisableTiming) != hipSuccess ||
           hipEventCreateWithFlags(&G->evB[p][r], hipEventDisableTiming) != hipSuccess) {
+        for (int pp = 0; pp < 2; ++pp)  // the events created so far, then the group
+          for (int rr = 0; rr < size; ++rr) {
+            if (G->evA[pp][rr]) (void)hipEventDestroy(G->evA[pp][rr]);
+            if (G->evB[pp][rr]) (void)hipEventDestroy(G->evB[pp][rr]);
+          }
+        delete G;
         loam::set_error("loam_comm_create_local: hipEventCreate failed");
         return LOAM_ERR_HIP;
       }
@@ -352,6 +378,9 @@ int32_t loam_comm_destroy(loam_comm* c) {
     {
       std::lock_guard<std::mutex> lk(G->mu);
       last = --G->alive == 0;
+      // a rank leaving while others live ends the group: their next collective fails at once
+      G->broken = true;
+      G->cv.notify_all();
     }
     if (last) {
       (void)hipSetDevice(G->device);

@@ -382,10 +382,11 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
   S.scratch_cap = D.max_in;
   if (PCL) S.hot = map_hot(D, sm, mp_stack_offset(D), (uint32_t)I.n[m]);
   voxel_segment(S, lds);
-  if (PCL)  // PCL's summation order for the voxels of 3+ members (voxel_hot.h)
+  if (PCL) {  // PCL's summation order for the voxels of 3+ members (voxel_hot.h)
     vh_fixup<VX_THREADS>(VxSrc{I.p[m], I.n[m], nullptr}, I.n[m], S.out, S.hot, lds, VX_LDS_WORDS - 256,
                          *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192), nullptr, err, D.pdbg ? D.pdbg + 54 : nullptr,
                          D.pdbg ? D.pdbg + 77 : nullptr);
+  }
 }
 
 // Few streams: the input-order stack VoxelGrid of a (stream, map) over stack_k workgroups.
@@ -1486,9 +1487,9 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
           __syncthreads();  // false: grid overflow, full filter below
         }
         if (!merged) voxel_segment(S, lds);
-        vh_fixup<VX_THREADS>(VxSrc{ar + cv.x, (int)cv.y, D.ins_sorted + sm_index(s, m) * D.max_in + i0}, (int)n, ar,
-                             S.hot, lds, LW - 256, *reinterpret_cast<VxMisc*>(lds + LW - 192), tok, &F.err,
-                             D.pdbg ? D.pdbg + 50 : nullptr, D.pdbg ? D.pdbg + 72 : nullptr,
+        const VxSrc P{ar + cv.x, (int)cv.y, D.ins_sorted + sm_index(s, m) * D.max_in + i0};
+        vh_fixup<VX_THREADS>(P, (int)n, ar, S.hot, lds, LW - 256, *reinterpret_cast<VxMisc*>(lds + LW - 192), tok,
+                             &F.err, D.pdbg ? D.pdbg + 50 : nullptr, D.pdbg ? D.pdbg + 72 : nullptr,
                              D.pdbg ? D.pdbg + 82 : nullptr);
       }
     } else {  // the whole std::sort emulated in global memory (voxel_pcl.h)
@@ -1794,6 +1795,8 @@ inline std::string map_err_text(int e) {
   add(MAP_ERR_SORT, "PCL-order VoxelGrid input larger than its sort lists / scratch");
   add(MAP_ERR_STACK, "split stack VoxelGrid: a range has more voxels than its LDS groups");
   add(MAP_ERR_STACK_WAIT, "the frame's stack VoxelGrid did not finish in time (device wait)");
+  add(VH_ERR_ROOTS | VH_ERR_LIST, "PCL-order VoxelGrid sort lists full");
+  add(VH_ERR_SPIN, "PCL-order VoxelGrid sort: a wave's wait for a listed subtree ran out");
   return m + " (flags " + std::to_string(e) + ")";
 }
 
@@ -1822,6 +1825,11 @@ struct FrameRec {
 };
 
 struct loam_mapper {
+  // the status of a frame loam_mapper_solve_async finished to make room (LOAM_ERR_CAPACITY /
+  // _SYNC), held for the next loam_mapper_wait / loam_mapper_solve (as LOAM_ERR_EARLIER): the
+  // solve_async that finished it returns OK, since it did enqueue its own frame
+  int32_t held_rc = 0;
+  std::string held_msg;
   loam_params P;
   bool prof = false;
   std::vector<hipEvent_t> ev_pool;
@@ -2197,11 +2205,13 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
 }
 
 int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_streams, loam_mapper** out) {
+  vh_spin_limit_from_env();
   return mapper_create(p, device, n_streams, nullptr, out);
 }
 
 int32_t loam_mapper_create_sharded(const loam_params* p, int32_t device, int32_t n_streams, loam_comm* comm,
                                    loam_mapper** out) {
+  vh_spin_limit_from_env();
   if (!comm) {
     set_error("loam_mapper_create_sharded: null comm");
     return LOAM_ERR_ARG;
@@ -2443,6 +2453,11 @@ int32_t loam_mapper_prefetch(loam_mapper* h) {
 
 // k_revox workgroups: one per possible item
 static int revox_grid(const loam_mapper* h) { return h->B * 2 * INS_SLOTS; }
+// the frame's re-VoxelGrid
+static void launch_revox(const loam_mapper* h, const MapperDev& D, hipStream_t st) {
+  if (D.pcl_order) k_revox<true><<<revox_grid(h), VX_THREADS, 0, st>>>(D);
+  else k_revox<false><<<revox_grid(h), VX_THREADS, 0, st>>>(D);
+}
 
 // the frame's kernel sequence for the hipGraph path: k_frame_prep (records of a queued frame,
 // stack sizes, submap offsets), 2 x (kNN, geometry, LM round), insertion, re-VoxelGrid, and the
@@ -2458,8 +2473,7 @@ static void capture_frame(loam_mapper* h, const MapperDev& D, int fpar, hipStrea
     k_lm_round<<<lm_padded(B) * h->lm_G, LM_THREADS, 0, st>>>(D, round, h->lm_G);
   }
   k_insert_bucket<<<B * 2, VX_THREADS, 0, st>>>(D);
-  if (D.pcl_order) k_revox<true><<<revox_grid(h), VX_THREADS, 0, st>>>(D);
-  else k_revox<false><<<revox_grid(h), VX_THREADS, 0, st>>>(D);
+  launch_revox(h, D, st);
   k_frame_out<<<1, 256, 0, st>>>(D, h->hfo_dev[fpar], h->done_dev + fpar);
 }
 
@@ -2688,8 +2702,7 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
   }
   LOAM_HIP(hipEventRecord(h->ev[2], st));
   LAUNCH(FAM_INSERT, k_insert_bucket<<<B * 2, VX_THREADS, 0, st>>>(D));
-  if (D.pcl_order) LAUNCH(FAM_REVOX, k_revox<true><<<revox_grid(h), VX_THREADS, 0, st>>>(D));
-  else LAUNCH(FAM_REVOX, k_revox<false><<<revox_grid(h), VX_THREADS, 0, st>>>(D));
+  LAUNCH(FAM_REVOX, launch_revox(h, D, st));
   LOAM_HIP(hipGetLastError());
   LOAM_HIP(hipMemcpyAsync(h->hfo[fpar].data(), D.fr, sizeof(StreamFrame) * B, hipMemcpyDeviceToHost, st));
   LOAM_HIP(hipEventRecord(h->ev_fr[fpar][1], st));
@@ -2814,7 +2827,7 @@ static int32_t mapper_finish_rec(loam_mapper* h, const FrameRec& R, bool replay)
       // the frame is committed as computed (pose, insertion, re-VoxelGrid ran on the device);
       // the status says it is not trustworthy: the caller resets the stream (include/loam_core.h)
       set_error("loam_mapper_solve: stream " + std::to_string(s) + ": " + map_err_text(F.err));
-      const int32_t st = (F.err & (MAP_ERR_LM_SYNC | MAP_ERR_STACK_WAIT)) ? LOAM_ERR_SYNC : LOAM_ERR_CAPACITY;
+      const int32_t st = (F.err & (MAP_ERR_LM_SYNC | MAP_ERR_STACK_WAIT | VH_ERR_SPIN)) ? LOAM_ERR_SYNC : LOAM_ERR_CAPACITY;
       if (status == LOAM_OK || st == LOAM_ERR_SYNC) status = st;
     }
   }
@@ -2889,6 +2902,24 @@ static int32_t mapper_replay(loam_mapper* h, const FrameRec& R, const std::vecto
 }
 
 // a pending frame at the front of the queue is enqueued (its predecessor has been waited for)
+// a failed frame finished by loam_mapper_solve_async (see loam_mapper::held_rc); a hand-off
+// error outranks a capacity one, the first of equal rank is kept
+static void hold_status(loam_mapper* h, int32_t rc) {
+  if (rc == LOAM_OK) return;
+  if (h->held_rc == LOAM_OK || (rc == LOAM_ERR_SYNC && h->held_rc != LOAM_ERR_SYNC)) {
+    h->held_rc = rc;
+    h->held_msg = loam_last_error();
+  }
+}
+static int32_t take_held(loam_mapper* h) {
+  if (h->held_rc == LOAM_OK) return LOAM_OK;
+  set_error("an earlier frame, finished by loam_mapper_solve_async, failed (" +
+            std::string(h->held_rc == LOAM_ERR_SYNC ? "LOAM_ERR_SYNC" : "LOAM_ERR_CAPACITY") + "): " + h->held_msg);
+  h->held_rc = LOAM_OK;
+  h->held_msg.clear();
+  return LOAM_ERR_EARLIER;
+}
+
 static int32_t launch_front(loam_mapper* h) {
   if (h->q.empty() || !h->q.front().pending) return LOAM_OK;
   FrameRec P = std::move(h->q.front());
@@ -2897,7 +2928,11 @@ static int32_t launch_front(loam_mapper* h) {
   for (int s = 0; s < h->B; ++s)
     if (P.active[s]) run.push_back(s);
   FrameRec R;
-  TRY(enqueue_saved(h, P, run, R));
+  const int32_t rc = enqueue_saved(h, P, run, R);
+  if (rc != LOAM_OK) {  // the pending frame is dropped, not run: say so
+    set_error("a queued frame was dropped, not run: " + std::string(loam_last_error()));
+    return rc;
+  }
   R.behind = P.behind;
   if (R.seq) h->q.push_front(std::move(R));
   return LOAM_OK;
@@ -2962,16 +2997,26 @@ static bool chain_ok(const loam_mapper* h) {
 // pending with its inputs and stack taken, and enqueued once its predecessor has been waited for.
 // loam_mapper_wait always finishes the oldest frame, so frame f + 1 can be given before frame f
 // is waited for, whichever way it runs.
+static int32_t solve_async_impl(loam_mapper* h);
 int32_t loam_mapper_solve_async(loam_mapper* h) {
+  const int32_t rc = solve_async_impl(h);
+  // a sharded rank whose HIP runtime fails here may never reach the frame's collectives: the
+  // others then fail theirs at once (in-process groups) instead of waiting out the transport's
+  // timeout.  (Argument, state and capacity errors are the same on every rank: identical inputs.)
+  if (rc == LOAM_ERR_HIP && h && h->comm) comm_abort(h->comm);
+  return rc;
+}
+static int32_t solve_async_impl(loam_mapper* h) {
   if (!h) return LOAM_ERR_ARG;
   LOAM_HIP(hipSetDevice(h->dev));
-  // a third frame first finishes the oldest; that frame's own status (a capacity or hand-off
-  // error, committed as computed) is returned after the new frame is enqueued, so the caller's
-  // input is never left behind.  A HIP or argument error stops here.
-  int32_t older = LOAM_OK;
+  // a third frame first finishes the oldest.  A non-OK return means the new frame was NOT
+  // enqueued (a HIP / argument / state error here, or one of its own enqueue); the oldest
+  // frame's own failure (a capacity or hand-off error, committed as computed) is held for the
+  // next loam_mapper_wait / _solve, which return it as LOAM_ERR_EARLIER.
   if (h->q.size() >= 2) {
-    older = finish_oldest(h);
+    const int32_t older = finish_oldest(h);
     if (older == LOAM_ERR_HIP || older == LOAM_ERR_ARG || older == LOAM_ERR_STATE) return older;
+    hold_status(h, older);
   }
   TRY(launch_front(h));
   FrameRec R;
@@ -3008,26 +3053,27 @@ int32_t loam_mapper_solve_async(loam_mapper* h) {
       H.in_ready = false;
       H.stk_launched = false;
     }
-    if (!any) return older;
+    if (!any) return LOAM_OK;
     R.seq = 1;  // (a real sequence number when it is enqueued)
     h->spar ^= 1;
   }
   R.behind = behind;
   if (R.seq) h->q.push_back(std::move(R));
-  return older;
+  return LOAM_OK;
 }
 
 int32_t loam_mapper_wait(loam_mapper* h) {
   if (!h) return LOAM_ERR_ARG;
-  if (h->q.empty()) return LOAM_OK;
+  if (h->q.empty()) return take_held(h);
   LOAM_HIP(hipSetDevice(h->dev));
-  return finish_oldest(h);  // (a pending oldest frame is enqueued first)
+  TRY(finish_oldest(h));  // (a pending oldest frame is enqueued first)
+  return take_held(h);
 }
 
 int32_t loam_mapper_solve(loam_mapper* h) {
   TRY(loam_mapper_solve_async(h));
   SETTLE(h);
-  return LOAM_OK;
+  return take_held(h);
 }
 
 int32_t loam_mapper_debug_counters(loam_mapper* h, uint64_t* out, int32_t n, int32_t reset) {

@@ -386,6 +386,7 @@ int32_t loam_voxel_grid_pcl(int32_t device, const float* in, int32_t n, float le
   int32_t rc = ensure_device(device);
   if (rc != LOAM_OK) return rc;
   LOAM_HIP(hipSetDevice(device));
+  vh_spin_limit_from_env();
   if (n <= VH_MAX_N) {
     DevBuf din, dout, drk, dhl, dhv, dfp, didx, dcnt, derr;
     const size_t m = std::max(n, 1);
@@ -422,6 +423,10 @@ int32_t loam_voxel_grid_pcl(int32_t device, const float* in, int32_t n, float le
     int err = 0;
     LOAM_HIP(hipMemcpy(&cnt, dcnt.p, sizeof(uint32_t), hipMemcpyDeviceToHost));
     LOAM_HIP(hipMemcpy(&err, derr.p, sizeof(int), hipMemcpyDeviceToHost));
+    if (err & VH_ERR_SPIN) {
+      set_error("loam_voxel_grid_pcl: sort: a wave's wait for a listed subtree ran out (err " + std::to_string(err) + ")");
+      return LOAM_ERR_SYNC;
+    }
     if (err) {
       set_error("loam_voxel_grid_pcl: capacity (unique voxels or sort lists)");
       return LOAM_ERR_CAPACITY;

@@ -828,6 +828,7 @@ void sr_free(loam_scanreg* h) {
 extern "C" {
 
 int32_t loam_scanreg_create(const loam_params* p, int32_t device, loam_scanreg** out) {
+  vh_spin_limit_from_env();
   if (!out) return LOAM_ERR_ARG;
   *out = nullptr;
   int32_t rc = ensure_device(device);
@@ -963,10 +964,13 @@ static int32_t sr_finish(loam_scanreg* h) {
   h->D.xyz = h->pending_xyz;
   h->D.stride = h->pending_stride;
   if (h->hf.err) {
+    const int e = h->hf.err;
     set_error(std::string("loam_scanreg_input: ") +
-              ((h->hf.err & SR_ERR_SORT) ? "std::sort emulation level list overflow" : "ring or sector larger than the LDS capacity") +
-              " (err " + std::to_string(h->hf.err) + ")");
-    return LOAM_ERR_CAPACITY;
+              ((e & VH_ERR_SPIN) ? "ring VoxelGrid sort: a wave's wait for a listed subtree ran out"
+               : (e & SR_ERR_SORT) ? "std::sort emulation level list overflow"
+                                   : "ring or sector larger than the LDS capacity") +
+              " (err " + std::to_string(e) + ")");
+    return (e & VH_ERR_SPIN) ? LOAM_ERR_SYNC : LOAM_ERR_CAPACITY;
   }
   return LOAM_OK;
 }

@@ -31,6 +31,8 @@
 // l_k < r_k  <=>  k <= #(right stops right of l_k), so only r_1 .. r_{(m-1)/2} are listed (u16,
 // a segment [lo, hi) owns Bs[lo/2 ..)), and every read of the segment precedes every write.
 #pragma once
+#include <cstdlib>
+
 #include "stdsort.h"
 #include "voxel.h"
 
@@ -47,7 +49,27 @@ constexpr int VH_WAVE_W = VH_LIFO + 64;  // per wave: LIFO + the dup check's key
 constexpr int VH_SMALL = 32;      // hot voxels up to this many members: summed by one thread
 constexpr int VH_REG = 8;         // hot voxels up to 64 * VH_REG members: rank-sorted by a wave
 constexpr uint32_t VH_HOT = 0x8000u;
-constexpr int VH_ERR_ROOTS = 16, VH_ERR_LIST = 32;
+// error bits (above the mapper's MAP_ERR_* and scan registration's SR_ERR_*, which share the
+// flag words these are or-ed into): a list overflow (cannot happen), a drain wait that ran out
+constexpr int VH_ERR_ROOTS = 1 << 12, VH_ERR_LIST = 1 << 13, VH_ERR_SPIN = 1 << 14;
+constexpr int VH_ERR_ANY = VH_ERR_ROOTS | VH_ERR_LIST | VH_ERR_SPIN;
+
+// The drain's bounded wait (vh_drain): spins of a wave whose claimed list entry is not listed yet
+// while some listed subtree is unfinished.  2^24 spins of s_sleep 1 (~seconds) cannot run out
+// while the workgroup makes progress; when it does, the subtree that entry would have held is
+// left unsorted, so the filter flags VH_ERR_SPIN (-> LOAM_ERR_SYNC) instead of a silently wrong
+// centroid.  LOAM_VH_SPIN_LIMIT (environment, read once per process by vh_spin_limit_from_env)
+// lowers it: tests/test_gpu_vh_spin.py sets 0 to show the flag reaches the caller.
+static __device__ uint32_t vh_spin_limit_g = 1u << 24;
+static inline void vh_spin_limit_from_env() {
+  static bool done = false;
+  if (done) return;
+  done = true;
+  if (const char* e = getenv("LOAM_VH_SPIN_LIMIT")) {
+    const uint32_t v = (uint32_t)strtoul(e, nullptr, 10);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(vh_spin_limit_g), &v, sizeof(v));
+  }
+}
 
 struct VhLess {
   __device__ bool operator()(uint32_t a, uint32_t b) const { return (a >> 16) < (b >> 16); }
@@ -537,7 +559,11 @@ __device__ inline void vh_drain(const VhLds& L) {
         item = it;
         break;
       }
-      if (pend == 0 || spins > (1u << 24)) break;  // (bounded: cannot run out)
+      if (pend == 0) break;
+      if (spins >= vh_spin_limit_g) {  // ran out: the entry's subtree may stay unsorted
+        if (lane == 0) atomicOr(&C->err, VH_ERR_SPIN);
+        break;
+      }
       __builtin_amdgcn_s_sleep(1);
     }
     if (!item) break;

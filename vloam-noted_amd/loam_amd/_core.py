@@ -19,7 +19,7 @@ vp = ctypes.c_void_p
 
 LOAM_OK = 0
 ERRORS = {-1: "LOAM_ERR_ARG", -2: "LOAM_ERR_HIP", -3: "LOAM_ERR_CAPACITY", -4: "LOAM_ERR_STATE",
-          -5: "LOAM_ERR_NODEVICE"}
+          -5: "LOAM_ERR_NODEVICE", -6: "LOAM_ERR_SYNC", -7: "LOAM_ERR_EARLIER"}
 
 
 class LoamError(RuntimeError):
