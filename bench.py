@@ -106,6 +106,25 @@ def drift_priors(seed, n, q_gt, t_gt):
     return q, t
 
 
+def scanreg_bytes(n_in):
+    """scan registration's algorithmic bytes per frame: 16 B per raw point read,
+    4 B of curvature and 4 B of label written per point"""
+    return 24.0 * n_in
+
+
+def odometry_bytes(counts, st):
+    """scan-to-scan odometry's algorithmic bytes per frame: the last clouds read
+    once into the cell tables (16 B per point); per outer round the sharp + flat queries (16 B each)
+    and every LM pass over the factor records (the initial evaluation plus one per iteration; 60 B
+    per edge record, 44 B per plane record, as the mapper's LM family counts them)"""
+    n_sharp, n_flat = int(counts[0]), int(counts[2])
+    b = 16.0 * (st.n_corner_last + st.n_surf_last)
+    for r in range(2):
+        b += 16.0 * (n_sharp + n_flat)
+        b += (st.lm[r].iterations + 1) * (60.0 * st.corner_num[r] + 44.0 * st.surf_num[r])
+    return b
+
+
 def make_frames(seed, n_frames, n_az, device, raw_frames=(), prior="odometry"):
     """raw scans (threads) -> HIP ScanRegistration -> HIP LaserOdometry -> features in HBM
     (torch tensors, plus host copies for the CPU legs) + the odometry pose (the mapping prior,
@@ -120,7 +139,8 @@ def make_frames(seed, n_frames, n_az, device, raw_frames=(), prior="odometry"):
     sr = ScanRegistration(device=device)
     od = BatchOdometry(1, device=device)
     frames = []
-    stage_ms = {"scan_registration": [], "odometry": [], "odometry_iters": []}
+    stage_ms = {"scan_registration": [], "odometry": [], "odometry_iters": [],
+                "scan_registration_bytes": [], "odometry_bytes": []}
     chunk = 64
     with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4)) as ex:
         for c0 in range(0, n_frames, chunk):
@@ -135,6 +155,8 @@ def make_frames(seed, n_frames, n_az, device, raw_frames=(), prior="odometry"):
                 stage_ms["scan_registration"].append(sr.ms)
                 stage_ms["odometry"].append(ost.ms)
                 stage_ms["odometry_iters"].append(ost.lm[0].iterations + ost.lm[1].iterations)
+                stage_ms["scan_registration_bytes"].append(scanreg_bytes(len(xyz)))
+                stage_ms["odometry_bytes"].append(odometry_bytes(counts, ost))
                 corner = sr.cloud(2)  # cornerPointsLessSharp -> laserCloudCornerLast
                 surf = sr.cloud(4)    # surfPointsLessFlat   -> laserCloudSurfLast
                 frames.append(dict(corner=torch.from_numpy(corner).to(f"cuda:{device}"),
@@ -823,9 +845,10 @@ def main():
         u_rate = uit / (time.perf_counter() - t0)
         um.close()
         res = {"streams": n_streams, "steps": steps, "unsharded": round(u_rate, 1),
-               "transport": "loam_comm_create_local: ranks as threads on one GPU, each collective staged and "
-                            "summed on the ranks' own HIP streams, ordered by events (threads meet only when they "
-                            "enqueue it)"}
+               "transport": "loam_comm_create_local: ranks as threads on one GPU; the submap sizes, 5-NN "
+                            "candidates and poses staged and summed on the ranks' own HIP streams, ordered by "
+                            "events (threads meet only when they enqueue them); every LM pass's normal equations "
+                            "meet inside the persistent LM round (peer slots and flags, lm.h)"}
         for R in (2, 3):
             comms = Comm.local_group(R, local)
             times, iters, errs = [0.0] * R, [0] * R, []
@@ -995,6 +1018,14 @@ def main():
                 continue
             e = {"gpu_ms_per_frame": round(float(g.mean()), 4), "gpu_frames": int(len(g)),
                  "gpu_frames_per_s": round(1e3 / float(g.mean()), 1)}
+            # the stage against the HBM roofline: its algorithmic bytes per frame / its device time
+            # per frame (every kernel of the stage, one stream: latency bound)
+            bpf = float(np.mean(stage_ms[name + "_bytes"][sl]))
+            ach = bpf / (float(g.mean()) * 1e-3) / 1e9
+            e["roofline"] = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(ach / HBM_PEAK_GBS, 6), "algorithmic_bytes_per_frame": round(bpf, 1),
+                             "traffic": None, "bytes": ("24 B per raw point" if name == "scan_registration" else
+                                                         "last clouds + queries + LM passes x records")}
             if name == "odometry":
                 it = float(np.sum(stage_ms["odometry_iters"][sl]))
                 e["gpu_lm_iters_per_s"] = round(it / (float(g.sum()) * 1e-3), 1)

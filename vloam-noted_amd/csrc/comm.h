@@ -32,6 +32,18 @@ int32_t comm_allgather(loam_comm* c, const void* d_send, void* d_recv, int64_t b
 // ranks fail their next collective at once instead of waiting out the timeout (no-op otherwise:
 // RCCL and callback transports own their failure handling)
 void comm_abort(loam_comm* c);
+// device memory every rank of the group sees at the same address (ranks of one process on one
+// device, loam_comm_create_local): the first caller allocates it zeroed, every rank asks for the
+// same size.  LOAM_ERR_STATE for transports without one (RCCL, callbacks)
+int32_t comm_peer_buffer(loam_comm* c, size_t bytes, void** dev);
+// ONE launch for every rank of an in-process group (ranks whose kernels must wait for each other
+// on the device: separate launches could sit behind each other in one hardware queue, the HIP
+// streams of a process sharing GPU_MAX_HW_QUEUES queues).  Each rank hands its argument blob and
+// its stream; rank 0's stream waits for every rank's stream, rank 0 calls fn(blobs, nrank, its
+// stream, user), and every other rank's stream then waits for that launch.  The host threads meet
+// twice (bounded; LOAM_ERR_SYNC when the group is broken).
+typedef void (*comm_group_launch_fn)(const void* const* blobs, int nrank, hipStream_t st, void* user);
+int32_t comm_group_launch(loam_comm* c, const void* blob, hipStream_t st, comm_group_launch_fn fn, void* user);
 
 // 4 m voxel-aligned ownership blocks: voxel v = floor(p / leaf) as PCL computes it
 // (floorf(p * (1/leaf)), voxel.h); block = floor(v / bv) with bv voxels per block edge, so a

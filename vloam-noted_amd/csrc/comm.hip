@@ -103,6 +103,11 @@ struct LocalGroup {
   hipEvent_t evB[2][LOAM_LOCAL_MAX_RANKS] = {};
   bool usedB[2][LOAM_LOCAL_MAX_RANKS] = {};
 
+  void* peer = nullptr;  // comm_peer_buffer
+  size_t peer_bytes = 0;
+  const void* blobs[LOAM_LOCAL_MAX_RANKS] = {};  // comm_group_launch
+  hipEvent_t ev_pre[LOAM_LOCAL_MAX_RANKS] = {};
+  hipEvent_t ev_post = nullptr;
   bool broken = false;
   // false: a rank did not arrive within the timeout (it failed or stopped); the group is broken
   // and every later collective fails at once instead of hanging
@@ -131,6 +136,21 @@ struct LocalGroup {
     cv.notify_all();
   }
 };
+
+static void local_group_free_events(LocalGroup& G) {
+  for (int p = 0; p < 2; ++p)
+    for (int r = 0; r < LOAM_LOCAL_MAX_RANKS; ++r) {
+      if (G.evA[p][r]) (void)hipEventDestroy(G.evA[p][r]);
+      if (G.evB[p][r]) (void)hipEventDestroy(G.evB[p][r]);
+      G.evA[p][r] = G.evB[p][r] = nullptr;
+    }
+  for (int r = 0; r < LOAM_LOCAL_MAX_RANKS; ++r) {
+    if (G.ev_pre[r]) (void)hipEventDestroy(G.ev_pre[r]);
+    G.ev_pre[r] = nullptr;
+  }
+  if (G.ev_post) (void)hipEventDestroy(G.ev_post);
+  G.ev_post = nullptr;
+}
 
 struct LocalSum {
   const void* src[LOAM_LOCAL_MAX_RANKS];
@@ -211,6 +231,63 @@ static int32_t local_allgather(loam_comm* c, const void* d_send, void* d_recv, i
 
 void comm_abort(loam_comm* c) {
   if (c && c->kind == 2 && c->local) c->local->break_group();
+}
+
+int32_t comm_group_launch(loam_comm* c, const void* blob, hipStream_t st, comm_group_launch_fn fn, void* user) {
+  if (!c || c->kind != 2 || !c->local || !fn) return LOAM_ERR_STATE;
+  LocalGroup& G = *c->local;
+  const int r = c->rank;
+  int32_t rc = LOAM_OK;
+  if (hipEventRecord(G.ev_pre[r], st) != hipSuccess) rc = LOAM_ERR_HIP;
+  G.blobs[r] = blob;  // (read by rank 0 before the second meeting; the caller's, valid until then)
+  if (rc != LOAM_OK) {
+    G.break_group();
+    set_error("local comm: group launch: hipEventRecord failed");
+    return rc;
+  }
+  if (!G.barrier()) {
+    set_error("local comm: a rank did not reach the group launch (group broken)");
+    return LOAM_ERR_SYNC;
+  }
+  if (r == 0) {
+    for (int q = 1; q < G.size && rc == LOAM_OK; ++q)
+      if (hipStreamWaitEvent(st, G.ev_pre[q], 0) != hipSuccess) rc = LOAM_ERR_HIP;
+    if (rc == LOAM_OK) {
+      fn(G.blobs, G.size, st, user);
+      if (hipGetLastError() != hipSuccess || hipEventRecord(G.ev_post, st) != hipSuccess) rc = LOAM_ERR_HIP;
+    }
+    if (rc != LOAM_OK) {
+      G.break_group();
+      set_error("local comm: group launch failed");
+      return rc;
+    }
+  }
+  if (!G.barrier()) {  // rank 0 recorded ev_post
+    set_error("local comm: the group launch's rank 0 failed (group broken)");
+    return LOAM_ERR_SYNC;
+  }
+  if (r != 0) LOAM_HIP(hipStreamWaitEvent(st, G.ev_post, 0));
+  return LOAM_OK;
+}
+
+int32_t comm_peer_buffer(loam_comm* c, size_t bytes, void** dev) {
+  if (!c || !dev || c->kind != 2 || !c->local) return LOAM_ERR_STATE;
+  LocalGroup& G = *c->local;
+  std::lock_guard<std::mutex> lk(G.mu);
+  if (!G.peer) {
+    LOAM_HIP(hipSetDevice(G.device));
+    LOAM_HIP(hipMalloc(&G.peer, bytes));
+    // zeroed and finished before any rank's kernels (which run on non-blocking streams, not
+    // ordered behind the null stream): the memory may be a freed group's, flags and all
+    LOAM_HIP(hipMemset(G.peer, 0, bytes));
+    LOAM_HIP(hipDeviceSynchronize());
+    G.peer_bytes = bytes;
+  } else if (G.peer_bytes != bytes) {
+    set_error("local comm: ranks asked for peer buffers of different sizes");
+    return LOAM_ERR_ARG;
+  }
+  *dev = G.peer;
+  return LOAM_OK;
 }
 
 int32_t comm_allreduce(loam_comm* c, void* d_buf, int64_t count, int32_t dtype, hipStream_t st) {
@@ -345,19 +422,18 @@ int32_t loam_comm_create_local(int32_t size, int32_t device, loam_comm** out) {
   G->size = size;
   G->device = device;
   G->alive = size;
-  for (int p = 0; p < 2; ++p)
-    for (int r = 0; r < size; ++r)
-      if (hipEventCreateWithFlags(&G->evA[p][r], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&G->evB[p][r], hipEventDisableTiming) != hipSuccess) {
-        for (int pp = 0; pp < 2; ++pp)  // the events created so far, then the group
-          for (int rr = 0; rr < size; ++rr) {
-            if (G->evA[pp][rr]) (void)hipEventDestroy(G->evA[pp][rr]);
-            if (G->evB[pp][rr]) (void)hipEventDestroy(G->evB[pp][rr]);
-          }
-        delete G;
-        loam::set_error("loam_comm_create_local: hipEventCreate failed");
-        return LOAM_ERR_HIP;
-      }
+  bool ok = hipEventCreateWithFlags(&G->ev_post, hipEventDisableTiming) == hipSuccess;
+  for (int r = 0; r < size && ok; ++r) ok = hipEventCreateWithFlags(&G->ev_pre[r], hipEventDisableTiming) == hipSuccess;
+  for (int p = 0; p < 2 && ok; ++p)
+    for (int r = 0; r < size && ok; ++r)
+      ok = hipEventCreateWithFlags(&G->evA[p][r], hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&G->evB[p][r], hipEventDisableTiming) == hipSuccess;
+  if (!ok) {  // the events created so far, then the group
+    loam::local_group_free_events(*G);
+    delete G;
+    loam::set_error("loam_comm_create_local: hipEventCreate failed");
+    return LOAM_ERR_HIP;
+  }
   for (int r = 0; r < size; ++r) {
     auto* c = new loam_comm;
     c->rank = r;
@@ -386,11 +462,10 @@ int32_t loam_comm_destroy(loam_comm* c) {
       (void)hipSetDevice(G->device);
       (void)hipDeviceSynchronize();
       for (int p = 0; p < 2; ++p)
-        for (int r = 0; r < G->size; ++r) {
+        for (int r = 0; r < G->size; ++r)
           if (G->stage[p][r]) (void)hipFree(G->stage[p][r]);
-          if (G->evA[p][r]) (void)hipEventDestroy(G->evA[p][r]);
-          if (G->evB[p][r]) (void)hipEventDestroy(G->evB[p][r]);
-        }
+      loam::local_group_free_events(*G);
+      if (G->peer) (void)hipFree(G->peer);
       delete G;
     }
     delete c;

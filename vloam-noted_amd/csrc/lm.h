@@ -590,15 +590,17 @@ __device__ inline void lm_acquire() {
 
 constexpr int LM_MAX_PASSES = 8;          // a round needs <= 1 + max_num_iterations = 5
 constexpr uint32_t LM_SPIN_LIMIT = 1u << 21;
+constexpr uint32_t LM_PEER_SPIN_LIMIT = 1u << 24;  // the cross-rank wait: other ranks' kernels
+                                                   // start after their own earlier kernels
 // sync words per solve, zeroed before the launch: [1] generation (pass + 1 of the published
 // evaluation point), [2] its status, [4 + p] claims of pass p's shares 1.. (share 0 is the
 // leader's), [4 + LM_MAX_PASSES + p] shares 1.. of pass p completed
 constexpr int LM_SYNC_WORDS = 4 + 2 * LM_MAX_PASSES;
 
-__device__ inline bool lm_spin_ge(uint32_t* w, uint32_t target) {
+__device__ inline bool lm_spin_ge(uint32_t* w, uint32_t target, uint32_t limit = LM_SPIN_LIMIT) {
   for (uint32_t spins = 0;; ++spins) {
     if (__hip_atomic_load(w, RLX_AGENT) >= target) return true;
-    if (spins >= LM_SPIN_LIMIT) return false;
+    if (spins >= limit) return false;
     __builtin_amdgcn_s_sleep(2);
   }
 }
@@ -620,13 +622,22 @@ struct LmJob {
   int err_code;
   unsigned long long* prof = nullptr;  // optional cycles: [0] leader eval, [1] leader wait,
                                        // [2] reduce + step, [3] passes, [4] member wait for x
+  // one solve sharded over nrank ranks whose kernels run at once (loam_comm_create_local): this
+  // rank evaluates shares rank * G .. of nrank * G; per pass its leader stores the rank's sums in
+  // its slot of peer ([nrank][LM_MAX_PASSES][LM_NACC], shared by the ranks), raises its flag
+  // peer_flag[rank] to flag_base + pass + 1 and, once every rank's flag is there, sums the slots
+  // in rank order: the same bits, hence the same step, on every rank
+  int rank = 0, nrank = 1;
+  double* peer = nullptr;
+  uint32_t* peer_flag = nullptr;
+  uint32_t flag_base = 0;
 };
 
 // share c of pass `pass` at X -> part[c], then counted complete (release)
 template <int kThreads>
 __device__ inline void lm_share(const LmJob& J, const double* X, int c, int G, int pass, double* bsum) {
   const int tid = threadIdx.x;
-  lm_eval_sum<kThreads>(J.R, J.nrec, X, c, G, bsum);
+  lm_eval_sum<kThreads>(J.R, J.nrec, X, J.rank * G + c, J.nrank * G, bsum);
   if (tid < LM_NACC) lm_part_store(&J.part[(size_t)c * LM_NACC + tid], bsum[tid]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -724,14 +735,14 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
     // LDS word written in such a region and read through readfirstlane, so the control flow
     // around barriers is uniform whatever the compiler does with the regions.  A share's
     // completion (release) and the next claim are one thread-0 region.
-    lm_eval_sum<kThreads>(J.R, J.nrec, X, 0, G, bsum0, J.prof ? J.prof + 5 : nullptr);
+    lm_eval_sum<kThreads>(J.R, J.nrec, X, J.rank * G, J.nrank * G, bsum0, J.prof ? J.prof + 5 : nullptr);
     if (G > 1) {
       if (tid == 0) sshare = 1 + (int)__hip_atomic_fetch_add(&sync[4 + pass], 1u, RLX_AGENT);
       __syncthreads();
       while (true) {
         const int c = __builtin_amdgcn_readfirstlane(sshare);
         if (c >= G) break;
-        lm_eval_sum<kThreads>(J.R, J.nrec, X, c, G, bsum);
+        lm_eval_sum<kThreads>(J.R, J.nrec, X, J.rank * G + c, J.nrank * G, bsum);
         if (tid < LM_NACC) lm_part_store(&J.part[(size_t)c * LM_NACC + tid], bsum[tid]);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // every thread has read sshare and stored its part
@@ -786,7 +797,35 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (lane == 0) {
+      if (J.nrank > 1) {  // this rank's sums to its slot, then every rank's, in rank order
+        const uint32_t want = J.flag_base + (uint32_t)pass + 1u;
+        double* mine = J.peer + ((size_t)J.rank * LM_MAX_PASSES + pass) * LM_NACC;
+        if (lane < LM_NACC) lm_part_store(&mine[lane], sred[lane]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+          lm_release();
+          __hip_atomic_store(&J.peer_flag[J.rank], want, RLX_AGENT);
+        }
+        const bool ok = lane >= J.nrank || lm_spin_ge(&J.peer_flag[lane], want, LM_PEER_SPIN_LIMIT);
+        if (__ballot(!ok) != 0ull) {  // a rank did not come: this rank's LM stops here
+          if (lane == 0) {
+            atomicOr(J.err, J.err_code);
+            sstat = -1;
+          }
+        } else {
+          lm_acquire();
+          if (lane < LM_NACC) {
+            double v = lm_part_load(&J.peer[(size_t)pass * LM_NACC + lane]);
+            for (int r = 1; r < J.nrank; ++r) v += lm_part_load(&J.peer[((size_t)r * LM_MAX_PASSES + pass) * LM_NACC + lane]);
+            sred[lane] = v;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      if (lane == 0 && __builtin_amdgcn_readfirstlane(sstat) != -1) {
         const unsigned long long ts = J.prof ? __builtin_readcyclecounter() : 0ull;
         LmState L = ls;  // registers for the dependent chain
         lm_step(L, sred);
@@ -796,10 +835,19 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
     }
     __syncthreads();
     if (tid == 0 && J.prof) atomicAdd(&J.prof[2], __builtin_readcyclecounter() - t0);
+    if (__builtin_amdgcn_readfirstlane(sstat) == -1) {  // (the cross-rank wait ran out)
+      aborted = true;
+      break;
+    }
   }
   if (aborted && tid == 0) {  // stop this stream's LM where it is (best so far)
     ls.term = 6;
     ls.status = LM_DONE;
+    if (G > 1) {  // members waiting for a next pass leave now
+      __hip_atomic_store(&sync[2], (uint32_t)LM_DONE, RLX_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(&sync[1], (uint32_t)LM_MAX_PASSES + 1u, RLX_AGENT);
+    }
   }
   __syncthreads();
   if (ls.status == LM_DONE && tid < 7 && J.best_out) J.best_out[tid] = ls.best[tid];

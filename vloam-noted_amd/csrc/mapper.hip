@@ -188,6 +188,11 @@ struct MapperDev {
   float4* nn_xyz;        // [5][B][2*max_in] merged neighbours (k_geom input in sharded mode)
   double* pose_x;        // [nrank][B][8] every rank's optimised pose (agreement check)
   double* lm_red;        // [B][LM_NACC] this rank's normal-equation sums, then the all-reduced
+  // in-process ranks (loam_comm_create_local): the persistent LM's cross-rank slots, shared by the
+  // ranks (comm_peer_buffer): [2 frame parities][B][2 rounds][nrank][LM_MAX_PASSES][LM_NACC] and
+  // the flags [B][2 rounds][nrank] (lm.h LmJob)
+  double* lm_peer = nullptr;
+  uint32_t* lm_peer_flag = nullptr;
   // few streams: the stack VoxelGrid of a (stream, map) split over stack_k workgroups by voxel
   // idx range (k_stack_part + k_stack_cat), else one workgroup (k_stack_ds)
   int stack_k = 0;
@@ -1222,6 +1227,86 @@ __global__ void __launch_bounds__(LM_THREADS) k_lm_round(MapperDev D, int round,
   lm_round_device<LM_THREADS>(J, g, G);
 }
 
+// The LM round of every rank of an in-process sharded group in ONE launch (comm_group_launch):
+// the ranks' leaders wait for each other's per-pass sums (peer slots, lm.h), which separate
+// launches could not do safely (two streams' kernels may share a hardware queue, one behind the
+// other).  What k_lm_round reads of each rank's MapperDev:
+struct LmRankArgs {
+  StreamFrame* fr;
+  const int* r_type;
+  const float *r_px, *r_py, *r_pz;
+  const double* r_a[3];
+  const double* r_b[3];
+  double* partials;
+  uint32_t* lm_sync;
+  double* lm_xpub;
+  unsigned long long* pdbg;
+  int max_in, max_chunks, B, s0;
+};
+struct LmGroupArgs {
+  LmRankArgs r[LOAM_LOCAL_MAX_RANKS];
+  double* peer;        // MapperDev::lm_peer (the group's)
+  uint32_t* peer_flag;
+  int nrank;
+};
+// blocks: the R x Bp leaders first (rank-major, so every leader is dispatched before any member),
+// then each rank's members; a stream's blocks are congruent mod 8 (one XCD) as in k_lm_round
+__global__ void __launch_bounds__(LM_THREADS) k_lm_group(LmGroupArgs A, int round, int G) {
+  const int R = A.nrank, Bp = lm_padded(A.r[0].B);
+  int b = blockIdx.x, rank, sl, g;
+  if (b < R * Bp) {
+    rank = b / Bp;
+    sl = b % Bp;
+    g = 0;
+  } else {
+    b -= R * Bp;
+    const int per = Bp * (G - 1);
+    rank = b / per;
+    sl = (b % per) % Bp;
+    g = 1 + (b % per) / Bp;
+  }
+  const LmRankArgs& a = A.r[rank];
+  if (sl >= a.B) return;
+  const int s = a.s0 + sl;
+  StreamFrame& F = a.fr[s];
+  if (!F.active) return;
+  const size_t rb = (size_t)s * 2 * a.max_in;
+  LmJob J;
+  J.S = &F.lm[round];
+  J.R = LmRecView{a.r_type + rb, a.r_px + rb, a.r_py + rb, a.r_pz + rb, a.r_a[0] + rb, a.r_a[1] + rb,
+                  a.r_a[2] + rb, a.r_b[0] + rb, a.r_b[1] + rb, a.r_b[2] + rb};
+  J.nrec = F.nc_stack + F.ns_stack;
+  J.part = a.partials + (size_t)s * a.max_chunks * LM_NACC;
+  J.sync = a.lm_sync + ((size_t)s * 2 + round) * LM_SYNC_WORDS;
+  J.xpub = a.lm_xpub + ((size_t)s * 2 + round) * 8;
+  J.best_out = F.pose;
+  J.err = &F.err;
+  J.err_code = MAP_ERR_LM_SYNC;
+  J.prof = a.pdbg ? a.pdbg + 17 : nullptr;
+  J.rank = rank;
+  J.nrank = R;
+  const size_t sr = (size_t)s * 2 + round;
+  J.peer = A.peer + (((size_t)(F.epoch & 1u) * a.B * 2 + sr) * R) * LM_MAX_PASSES * LM_NACC;
+  J.peer_flag = A.peer_flag + sr * R;
+  J.flag_base = F.epoch * (uint32_t)LM_MAX_PASSES;
+  lm_round_device<LM_THREADS>(J, g, G);
+}
+
+struct LmGroupCtx {
+  int round, G;
+  double* peer;
+  uint32_t* peer_flag;
+};
+static void lm_group_launch(const void* const* blobs, int nrank, hipStream_t st, void* user) {
+  const LmGroupCtx& C = *static_cast<const LmGroupCtx*>(user);
+  LmGroupArgs A{};
+  for (int r = 0; r < nrank; ++r) A.r[r] = *static_cast<const LmRankArgs*>(blobs[r]);
+  A.peer = C.peer;
+  A.peer_flag = C.peer_flag;
+  A.nrank = nrank;
+  k_lm_group<<<nrank * lm_padded(A.r[0].B) * C.G, LM_THREADS, 0, st>>>(A, C.round, C.G);
+}
+
 // sharded: every rank stores points with the same pose, so after the LM every rank adopts
 // rank 0's (they are equal when the all-reduce is bit-identical on every rank, as RCCL's and
 // the Python transports are); a rank that differed counts it in debug counter 40
@@ -2024,9 +2109,11 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     const bool allow = !(env && env[0] == '0');
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
       h->n_cu = cus;
-    // sharded over several ranks: the per-pass all-reduce needs the two-kernel path; at one
-    // rank every collective is the identity and the round stays one persistent launch
-    if (allow && (!comm || comm->size == 1) &&
+    // sharded over several ranks: ranks of one process (loam_comm_create_local) meet inside the
+    // persistent round (peer slots, lm.h); other transports all-reduce between two kernels per
+    // pass.  At one rank every collective is the identity and the round stays one launch.
+    const bool peer = comm && comm->size > 1 && comm->kind == 2;
+    if (allow && (!comm || comm->size == 1 || peer) &&
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_lm_round, LM_THREADS, 0) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess) {
       // 256 threads x 256 VGPRs: exactly one block per CU; the API can over-report by one
@@ -2035,9 +2122,22 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
       const int cap = occ * cus;
       // 16 at one stream: LM pass 26.5k -> 24.9k cycles once the leader loads the share partials
       // 8 at a time (4 / 8 / 12 / 16: 30.8k / 26.5k / 25.6k / 24.9k, tools/dbg_lm.py)
-      h->lm_G = std::min(LM_EBLK, std::min(16, cap / n_streams));
+      // (with peer ranks on this device every rank's round must fit at once: a leader waits for
+      // the other ranks' leaders)
+      h->lm_G = std::min(LM_EBLK, std::min(16, cap / (peer ? lm_padded(n_streams) * comm->size : n_streams)));
       const char* genv = std::getenv("LOAM_LM_G");  // measurement override
       if (genv && std::atoi(genv) > 0) h->lm_G = std::min(LM_EBLK, std::atoi(genv));
+      if (peer && h->lm_G > 0) {
+        const size_t nd = (size_t)2 * n_streams * 2 * comm->size * LM_MAX_PASSES * LM_NACC;
+        void* pb = nullptr;
+        if (comm_peer_buffer(comm, nd * sizeof(double) + (size_t)n_streams * 2 * comm->size * sizeof(uint32_t), &pb) ==
+            LOAM_OK) {
+          D.lm_peer = static_cast<double*>(pb);
+          D.lm_peer_flag = reinterpret_cast<uint32_t*>(D.lm_peer + nd);
+        } else {
+          h->lm_G = 0;  // the two-kernel path
+        }
+      }
     }
   }
   D.pcl_order = h->P.exact_voxel_order ? 1 : 0;
@@ -2683,7 +2783,15 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
     }
     LAUNCH(FAM_CORR, k_geom<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round));
     if (h->lm_G > 0) {
-      LAUNCH(FAM_LM, k_lm_round<<<lm_padded(B) * h->lm_G, LM_THREADS, 0, st>>>(D, round, h->lm_G));
+      if (D.lm_peer) {  // in-process ranks: one launch for every rank's round (k_lm_group)
+        LmRankArgs a{D.fr, D.r_type, D.r_px, D.r_py, D.r_pz, {D.r_a[0], D.r_a[1], D.r_a[2]},
+                     {D.r_b[0], D.r_b[1], D.r_b[2]}, D.partials, D.lm_sync, D.lm_xpub, D.pdbg,
+                     D.max_in, D.max_chunks, B, D.s0};
+        LmGroupCtx ctx{round, h->lm_G, D.lm_peer, D.lm_peer_flag};
+        LAUNCH(FAM_LM, TRY(comm_group_launch(h->comm, &a, st, lm_group_launch, &ctx)));
+      } else {
+        LAUNCH(FAM_LM, k_lm_round<<<lm_padded(B) * h->lm_G, LM_THREADS, 0, st>>>(D, round, h->lm_G));
+      }
     } else {
       for (int it = 0; it < 5; ++it) {  // iteration 0 + max_num_iterations = 4 candidates
         // sharded: evaluation + this rank's sums (last workgroup), then per Ceres iteration the
