@@ -1516,6 +1516,9 @@ __global__ void __launch_bounds__(VX_THREADS) k_insert_bucket(MapperDev D) {
 // the merge path (a fixed-point cube plus a few new points, voxel.h vx_merge_fixed_point) or
 // the full filter in a VX_THREADS workgroup with the whole LDS, then the cube's cell index.
 // ---------------------------------------------------------------------------------------
+#ifndef REVOX_PROF_MIN_N
+#define REVOX_PROF_MIN_N 0  // diagnostics builds: phase counters of the items of at least this many points only
+#endif
 template <bool PCL>
 __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube, int append, uint32_t* lds) {
   constexpr int LW = VX_LDS_WORDS;
@@ -1525,6 +1528,7 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
   uint32_t* tok = D.stable_tok + sm_index(s, m) * NCUBE + cube;
   uint2* tab = D.cube_tab + sm_index(s, m) * NCUBE;
   const uint2 cv = tab[cube];
+  if (cv.y + n_new < (uint32_t)REVOX_PROF_MIN_N) D.pdbg = nullptr;
   float4* ar = arena_base(D, s, m, F.arena_active[m]);
   VoxSeg S;
   S.src0 = ar + cv.x;
@@ -2802,7 +2806,10 @@ static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
       }
     }
   }
-  if (D.sharded) {  // pose agreement across ranks before anything is stored (k_pose_adopt)
+  // pose agreement across ranks before anything is stored (k_pose_adopt); the group LM round
+  // (in-process ranks) leaves every rank with the same bits by construction: every rank steps on
+  // the same peer slots summed in the same order
+  if (D.sharded && !(multi && D.lm_peer && h->lm_G > 0)) {
     LAUNCH(FAM_OTHER, k_pose_publish<<<B, 64, 0, st>>>(D));
     if (multi)
       TRY(comm_allgather(h->comm, D.pose_x + (size_t)D.rank * B * 8, D.pose_x, (int64_t)B * 8 * sizeof(double), st));
