@@ -352,6 +352,36 @@ def pose_errors(gpu, cpu):
             "frames": int(len(dt))}
 
 
+def scanreg_batched_stage(seed, device, n_az, frames=64, reps=5):
+    """BASELINE configs[1] as throughput: `frames` synthetic 64 x n_az scans resident in HBM
+    through one batched ScanRegistration launch sequence (loam_scanreg_input_batch: every kernel
+    runs the frames in grid rows), the device time of a launch (HIP events on the handle's
+    stream), median of `reps`; bytes as the per-frame roofline (24 B per raw point)"""
+    import torch
+    from loam_amd import synth
+    from loam_amd.scanreg import ScanRegistrationBatch
+    raws = [synth.frame(seed, 1000 + f, n_az)[0] for f in range(frames)]
+    dev = [torch.from_numpy(np.ascontiguousarray(r, dtype=np.float32)).to(f"cuda:{device}") for r in raws]
+    ptrs = [t.data_ptr() for t in dev]
+    ns = [len(r) for r in raws]
+    b = ScanRegistrationBatch(frames, device=device)
+    b.input_batch_device(ptrs, ns, stride=3)  # warm-up
+    times = []
+    for _ in range(reps):
+        b.input_batch_device(ptrs, ns, stride=3)
+        times.append(b.ms)
+    b.close()
+    ms = float(np.median(times))
+    byts = scanreg_bytes(float(np.sum(ns)))
+    ach = byts / (ms * 1e-3) / 1e9
+    return {"frames_per_launch": frames, "launch_ms": round(ms, 4), "frames_per_s": round(frames / (ms * 1e-3), 1),
+            "ms_per_frame": round(ms / frames, 5),
+            "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_launch": round(byts, 1),
+                         "traffic": None},
+            "mode": "loam_scanreg_create_batch / loam_scanreg_input_batch: the scans in HBM, one launch sequence"}
+
+
 def depth_stage(seed, device, n_frames=64, n_queries=2800, n_az=2000, with_cpu=True):
     """VO depth association (point_cloud_util.cpp:183-487): one stream
     per frame (device time of projectPointCloud + downsamplePointCloud) and n_frames streams in
@@ -1036,6 +1066,8 @@ def main():
                 if name == "odometry":
                     e["cpu_lm_iters_per_s"] = round(cpu_st["odometry_iters"] / (cpu_st[name] * 1e-3), 1)
             stages[name] = e
+        if world == 1 and "scan_registration" in stages:
+            stages["scan_registration"]["batched"] = scanreg_batched_stage(args.seed, local, args.n_az)
         if not args.no_depth and world == 1:
             stages["depth_association"] = depth_stage(args.seed, local, with_cpu=not args.no_cpu)
             stages["vo_solve"] = vo_stage(args.seed, local, with_cpu=not args.no_cpu)

@@ -134,6 +134,18 @@ int32_t loam_scanreg_device_ptr(loam_scanreg* h, int32_t which, const float** pt
 int32_t loam_scanreg_curvature(loam_scanreg* h, float* curv, int32_t* label, int32_t cap);
 /* device time of the last input (ms) */
 double loam_scanreg_ms(loam_scanreg* h);
+/* Batched ScanRegistration: up to max_frames independent scans per launch sequence (every kernel
+ * runs frame f in grid row f), for throughput on many streams or sensors.  A batch handle also
+ * takes every single-frame call above (frame 0).  loam_scanreg_input_batch runs n_frames scans
+ * (xyz[f]: host or, with on_device != 0, device pointers as integers; n[f] points each, stride
+ * floats per point) and waits; each frame's clouds are then read by frame index.  Results are
+ * bit-identical to one loam_scanreg_input per scan. */
+int32_t loam_scanreg_create_batch(const loam_params* p, int32_t device, int32_t max_frames, loam_scanreg** out);
+int32_t loam_scanreg_input_batch(loam_scanreg* h, int32_t n_frames, const uint64_t* xyz, const int32_t* n,
+                                 int32_t stride, int32_t on_device);
+int32_t loam_scanreg_frame_counts(loam_scanreg* h, int32_t frame, int32_t* counts5);
+int32_t loam_scanreg_frame_device_ptr(loam_scanreg* h, int32_t frame, int32_t which, const float** ptr);
+int32_t loam_scanreg_frame_copy(loam_scanreg* h, int32_t frame, int32_t which, float* out, int32_t cap);
 /* cumulative device cycle counters of scan registration, summed over rings and frames unless
  * "max": the per-ring PCL-order VoxelGrid (k_sr_ringvox): [0] cycles of the sort emulation
  * (libstdc++ introsort) for the voxels of 3+ members, [1] of their centroids, [2] rings that had

@@ -151,3 +151,33 @@ def test_async_pinned_ingest_and_overlap():
             sr.input_async(frames[f + 1])  # next frame's copy + kernels overlap this solve
         m.solve()
     sr.wait()
+
+
+def test_batched_frames_match_single():
+    """loam_scanreg_input_batch: scans of different sizes and shapes (quantized with tied
+    curvatures, column-major with per-laser offsets, a tiny one, an empty one) in one launch
+    sequence, each frame's five clouds bit-identical to the single-frame handle's, twice in a row
+    (the second batch smaller: the frames past it must not leak into the counts)"""
+    from loam_amd.scanreg import ScanRegistrationBatch
+    clouds = [synth.frame(1, 0)[0], synth.frame(6, 3, flags=synth.QUANTIZE)[0],
+              synth.frame(9, 40, flags=synth.COLUMN_MAJOR | synth.LASER_AZ)[0], synth.frame(4, 3, n_az=64)[0],
+              np.zeros((0, 3), np.float32), synth.frame(2, 13)[0]]
+    single = ScanRegistration()
+    want = []
+    for c in clouds:
+        single.input(c)
+        want.append(single.output())
+    b = ScanRegistrationBatch(8)
+    b.input_batch(clouds)
+    for f, w in enumerate(want):
+        assert list(b.counts(f)) == [len(x) for x in w], f
+        for k in range(5):
+            _same_points(b.cloud(f, k), w[k])
+    b.input_batch(clouds[2:4])
+    for f, w in enumerate(want[2:4]):
+        for k in range(5):
+            _same_points(b.cloud(f, k), w[k])
+    with pytest.raises(Exception):
+        b.counts(3)  # past the last launch's frames
+    b.close()
+    single.close()

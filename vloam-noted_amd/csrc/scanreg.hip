@@ -61,6 +61,7 @@ struct SrFrame {
 
 struct SrDev {
   int cap;  // max input points
+  int n_in;  // this frame's input points (k_sr_init)
   int n_scans;
   float min_range;
   int stride;
@@ -114,7 +115,9 @@ __device__ inline int sr_scan_id(float x, float y, float z, int n_scans) {
 
 // the frame record's initial state, written on the device (a pageable host-to-device copy of it
 // cost the stream a staging round trip per frame)
-__global__ void __launch_bounds__(256) k_sr_init(SrFrame* F, int n_in) {
+__global__ void __launch_bounds__(256) k_sr_init(const SrDev* __restrict__ Ds) {
+  SrFrame* F = Ds[blockIdx.y].fr;
+  const int n_in = Ds[blockIdx.y].n_in;
   uint32_t* w = reinterpret_cast<uint32_t*>(F);
   for (int k = threadIdx.x; k < (int)(sizeof(SrFrame) / 4); k += 256) w[k] = 0u;
   __syncthreads();
@@ -128,7 +131,8 @@ __global__ void __launch_bounds__(256) k_sr_init(SrFrame* F, int n_in) {
 
 // one point per thread; every block leaves its first / last valid index in blk_aux (one
 // contended device-scope atomic per block or wave cost ~100 us per frame)
-__global__ void __launch_bounds__(SR_BLOCK) k_sr_valid(SrDev D, int nblocks) {
+__global__ void __launch_bounds__(SR_BLOCK) k_sr_valid(const SrDev* __restrict__ Ds, int nblocks) {
+  const SrDev D = Ds[blockIdx.y];  // this launch's frame y (loam_scanreg_input_batch)
   __shared__ int wf[SR_BLOCK / 64], wl[SR_BLOCK / 64];
   SrFrame& F = *D.fr;
   const float thr2 = D.min_range * D.min_range;
@@ -165,7 +169,8 @@ __device__ inline float sr_ori_branch1(float ori, float startOri) {
 }
 
 // per raw point: ring (or -1), branch-1 latch test; per-block ring histogram
-__global__ void __launch_bounds__(SR_BLOCK) k_sr_ring(SrDev D, int nblocks) {
+__global__ void __launch_bounds__(SR_BLOCK) k_sr_ring(const SrDev* __restrict__ Ds, int nblocks) {
+  const SrDev D = Ds[blockIdx.y];  // this launch's frame y (loam_scanreg_input_batch)
   __shared__ int hist[SR_MAX_RINGS];
   SrFrame& F = *D.fr;
   for (int r = threadIdx.x; r < SR_MAX_RINGS; r += SR_BLOCK) hist[r] = 0;
@@ -198,7 +203,8 @@ __global__ void __launch_bounds__(SR_BLOCK) k_sr_ring(SrDev D, int nblocks) {
   for (int r = threadIdx.x; r < SR_MAX_RINGS; r += SR_BLOCK) D.blk_hist[r * nblocks + blockIdx.x] = hist[r];
 }
 
-__global__ void __launch_bounds__(1024) k_sr_oris(SrDev D, int nblocks) {
+__global__ void __launch_bounds__(1024) k_sr_oris(const SrDev* __restrict__ Ds, int nblocks) {
+  const SrDev D = Ds[blockIdx.y];  // this launch's frame y (loam_scanreg_input_batch)
   __shared__ int wf[16], wl[16];
   SrFrame& F = *D.fr;
   int f = 0x7FFFFFFF, l = -1;
@@ -236,7 +242,8 @@ __global__ void __launch_bounds__(1024) k_sr_oris(SrDev D, int nblocks) {
 }
 
 // exclusive scan of blk_hist in ring-major order (one 1024-thread workgroup)
-__global__ void __launch_bounds__(1024) k_sr_ring_scan(SrDev D, int nblocks) {
+__global__ void __launch_bounds__(1024) k_sr_ring_scan(const SrDev* __restrict__ Ds, int nblocks) {
+  const SrDev D = Ds[blockIdx.y];  // this launch's frame y (loam_scanreg_input_batch)
   __shared__ uint32_t ws[VX_WAVES + 1];
   __shared__ int ring_tot[SR_MAX_RINGS];
   __shared__ int wl[16];
@@ -328,7 +335,8 @@ __global__ void __launch_bounds__(1024) k_sr_ring_scan(SrDev D, int nblocks) {
 }
 
 // stable scatter: rank within the block by wave peeling, intensity = scanID + 0.1 * relTime
-__global__ void __launch_bounds__(SR_BLOCK) k_sr_scatter(SrDev D, int nblocks) {
+__global__ void __launch_bounds__(SR_BLOCK) k_sr_scatter(const SrDev* __restrict__ Ds, int nblocks) {
+  const SrDev D = Ds[blockIdx.y];  // this launch's frame y (loam_scanreg_input_batch)
   __shared__ int wcnt[SR_BLOCK / 64][SR_MAX_RINGS];
   const SrFrame& F = *D.fr;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
@@ -368,7 +376,8 @@ __global__ void __launch_bounds__(SR_BLOCK) k_sr_scatter(SrDev D, int nblocks) {
   D.cloud[pos] = make_float4(x, y, z, intensity);
 }
 
-__global__ void k_sr_curv(SrDev D) {
+__global__ void k_sr_curv(const SrDev* __restrict__ Ds) {
+  const SrDev D = Ds[blockIdx.y];
   const SrFrame& F = *D.fr;
   const int n = F.n_cloud;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -566,7 +575,8 @@ __device__ inline void sr_greedy(SrDev& D, int r, int base, const uint64_t* K, i
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(SrDev D) {
+__global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(const SrDev* __restrict__ Ds) {
+  SrDev D = Ds[blockIdx.y];
   __shared__ uint64_t keys[6 * SR_WSORT_MAX];  // 48 KiB: the 6 sorted sectors
   __shared__ uint8_t picked[SR_RING_CAP];
   __shared__ int8_t lab[SR_RING_CAP];
@@ -727,7 +737,8 @@ __device__ __noinline__ void sr_ringvox(const VoxSeg& S, int n, int* err, unsign
   }
 }
 
-__global__ void __launch_bounds__(SRV_THREADS) k_sr_ringvox(SrDev D) {
+__global__ void __launch_bounds__(SRV_THREADS) k_sr_ringvox(const SrDev* __restrict__ Ds) {
+  const SrDev D = Ds[blockIdx.y];
   const int r = blockIdx.x;
   SrFrame& F = *D.fr;
   const int base = F.ring_off[r];
@@ -751,7 +762,8 @@ __global__ void __launch_bounds__(SRV_THREADS) k_sr_ringvox(SrDev D) {
 }
 
 // concatenation of the per-ring outputs in ring order
-__global__ void k_sr_gather(SrDev D) {
+__global__ void k_sr_gather(const SrDev* __restrict__ Ds) {
+  const SrDev D = Ds[blockIdx.y];
   const int r = blockIdx.x;
   SrFrame& F = *D.fr;
   int o1 = 0, o2 = 0, o3 = 0, o4 = 0;
@@ -789,11 +801,20 @@ struct loam_scanreg {
   int dev = 0;
   hipStream_t st = nullptr;
   hipEvent_t ev[2] = {nullptr, nullptr};
+  // frames per launch sequence (loam_scanreg_create_batch; 1 for loam_scanreg_create): every
+  // per-frame buffer exists nb times, Dv[f] points at frame f's; D is frame 0's (the single-frame
+  // calls)
+  int nb = 1;
+  std::vector<SrDev> Dv;
   SrDev D{};
-  SrFrame hf{};
-  float* d_in = nullptr;
+  SrDev* d_Ds = nullptr;      // [nb] the launch's frame views (kernel argument arrays)
+  SrDev* h_Ds = nullptr;      // [nb] page-locked staging of d_Ds
+  int nf = 0;                 // frames of the last launch
+  std::vector<SrFrame> hfv;   // [nb] their records after the wait
+  SrFrame hf{};               // frame 0's
+  float* d_in = nullptr;      // [nb][cap][4] staging of host input
   float* h_pinned = nullptr;  // loam_scanreg_host_buffer: page-locked ingest buffer (cap x 4 floats)
-  SrFrame* hf_pinned = nullptr;  // D2H target of the frame record (page-locked: the copy stays async)
+  SrFrame* hf_pinned = nullptr;  // [nb] D2H target of the frame records (page-locked: the copy stays async)
   int pending = 0;            // loam_scanreg_input_async launched, loam_scanreg_wait not yet called
   int pending_stride = 4;
   const float* pending_xyz = nullptr;
@@ -817,6 +838,7 @@ void sr_free(loam_scanreg* h) {
   if (h->st) (void)hipStreamSynchronize(h->st);  // an input_async still in flight
   if (h->h_pinned) (void)hipHostFree(h->h_pinned);
   if (h->hf_pinned) (void)hipHostFree(h->hf_pinned);
+  if (h->h_Ds) (void)hipHostFree(h->h_Ds);
   for (void* p : h->allocs) (void)hipFree(p);
   h->allocs.clear();
   for (auto& e : h->ev)
@@ -828,8 +850,12 @@ void sr_free(loam_scanreg* h) {
 extern "C" {
 
 int32_t loam_scanreg_create(const loam_params* p, int32_t device, loam_scanreg** out) {
+  return loam_scanreg_create_batch(p, device, 1, out);
+}
+
+int32_t loam_scanreg_create_batch(const loam_params* p, int32_t device, int32_t max_frames, loam_scanreg** out) {
   vh_spin_limit_from_env();
-  if (!out) return LOAM_ERR_ARG;
+  if (!out || max_frames < 1) return LOAM_ERR_ARG;
   *out = nullptr;
   int32_t rc = ensure_device(device);
   if (rc != LOAM_OK) return rc;
@@ -842,6 +868,10 @@ int32_t loam_scanreg_create(const loam_params* p, int32_t device, loam_scanreg**
     return LOAM_ERR_ARG;
   }
   h->dev = device;
+  h->nb = max_frames;
+  const int nb = max_frames;
+  h->Dv.assign(nb, SrDev{});
+  h->hfv.assign(nb, SrFrame{});
   const int cap = h->P.max_input_points;
   SrDev& D = h->D;
   D.cap = cap;
@@ -856,38 +886,58 @@ int32_t loam_scanreg_create(const loam_params* p, int32_t device, loam_scanreg**
   if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess) return fail(LOAM_ERR_HIP);
   for (auto& e : h->ev)
     if (hipEventCreate(&e) != hipSuccess) return fail(LOAM_ERR_HIP);
-#define SRA(ptr, n) \
-  if ((rc = sralloc(h, &(ptr), (n))) != LOAM_OK) return fail(rc)
-  SRA(h->d_in, (size_t)cap * 4);
-  SRA(D.fr, 1);
-  SRA(D.ring_of, cap);
-  SRA(D.blk_hist, (size_t)SR_MAX_RINGS * nblocks);
-  SRA(D.blk_off, (size_t)SR_MAX_RINGS * nblocks);
-  SRA(D.blk_aux, (size_t)3 * nblocks);
-  SRA(D.cloud, cap);
-  SRA(D.curv, cap);
-  SRA(D.label, cap);
-  SRA(D.ring_sharp, SR_MAX_RINGS * 6 * SR_SHARP);
-  SRA(D.ring_less_sharp, SR_MAX_RINGS * 6 * SR_LESS_SHARP);
-  SRA(D.ring_flat, SR_MAX_RINGS * 6 * SR_FLAT);
-  SRA(D.less_flat_scan, cap);
-  SRA(D.less_flat_ds, cap);
-  SRA(D.vx_pts, cap);
-  SRA(D.vx_idx, cap);
-  for (int k = 1; k < 5; ++k) SRA(D.out[k], cap);
-  SRA(D.ss_e, cap);
-  SRA(D.ss_a, cap);
-  SRA(D.ss_b, cap);
-  SRA(D.ss_s, cap);
-  SRA(D.ss_seg, (size_t)SR_MAX_RINGS * 6 * SR_SS_GSEG);
-  SRA(D.dbg, LOAM_SR_DEBUG_COUNTERS);
+  // every per-frame buffer: one allocation of nb copies, frame f's at f * n
+#define SRA(field, n)                                                      \
+  do {                                                                     \
+    const size_t n_ = (n);                                                 \
+    if ((rc = sralloc(h, &D.field, n_ * nb)) != LOAM_OK) return fail(rc);  \
+    for (int f = 0; f < nb; ++f) h->Dv[f].field = D.field + f * n_;        \
+  } while (0)
+  if ((rc = sralloc(h, &h->d_in, (size_t)cap * 4 * nb)) != LOAM_OK) return fail(rc);
+  SRA(fr, 1);
+  SRA(ring_of, cap);
+  SRA(blk_hist, (size_t)SR_MAX_RINGS * nblocks);
+  SRA(blk_off, (size_t)SR_MAX_RINGS * nblocks);
+  SRA(blk_aux, (size_t)3 * nblocks);
+  SRA(cloud, cap);
+  SRA(curv, cap);
+  SRA(label, cap);
+  SRA(ring_sharp, SR_MAX_RINGS * 6 * SR_SHARP);
+  SRA(ring_less_sharp, SR_MAX_RINGS * 6 * SR_LESS_SHARP);
+  SRA(ring_flat, SR_MAX_RINGS * 6 * SR_FLAT);
+  SRA(less_flat_scan, cap);
+  SRA(less_flat_ds, cap);
+  SRA(vx_pts, cap);
+  SRA(vx_idx, cap);
+  for (int k = 1; k < 5; ++k) SRA(out[k], cap);
+  SRA(ss_e, cap);
+  SRA(ss_a, cap);
+  SRA(ss_b, cap);
+  SRA(ss_s, cap);
+  SRA(ss_seg, (size_t)SR_MAX_RINGS * 6 * SR_SS_GSEG);
+  if ((rc = sralloc(h, &D.dbg, LOAM_SR_DEBUG_COUNTERS)) != LOAM_OK) return fail(rc);  // shared by the frames
   {
     const char* penv = std::getenv("LOAM_PHASE_COUNTERS");
     D.pdbg = (penv && std::atoi(penv) > 0) ? D.dbg : nullptr;
   }
 #undef SRA
+  if ((rc = sralloc(h, &h->d_Ds, nb)) != LOAM_OK) return fail(rc);
+  if (hipHostMalloc(reinterpret_cast<void**>(&h->h_Ds), sizeof(SrDev) * nb, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&h->hf_pinned), sizeof(SrFrame) * nb, hipHostMallocDefault) != hipSuccess)
+    return fail(LOAM_ERR_HIP);
   D.out[0] = D.cloud;
   D.sort_ind = nullptr;
+  for (int f = 0; f < nb; ++f) {  // the scalars and the shared pointers
+    SrDev& V = h->Dv[f];
+    V.cap = D.cap;
+    V.n_scans = D.n_scans;
+    V.min_range = D.min_range;
+    V.dbg = D.dbg;
+    V.pdbg = D.pdbg;
+    V.out[0] = V.cloud;
+    V.sort_ind = nullptr;
+  }
+  h->Dv[0] = D;
   if (hipStreamSynchronize(h->st) != hipSuccess) return fail(LOAM_ERR_HIP);
   *out = h;
   return LOAM_OK;
@@ -903,55 +953,77 @@ int32_t loam_scanreg_destroy(loam_scanreg* h) {
 
 static int32_t sr_finish(loam_scanreg* h);
 
-// enqueue one frame (H2D when host memory, then every kernel and the D2H of the frame
-// record) on the handle's stream; sr_finish waits for it
-static int32_t sr_launch(loam_scanreg* h, const float* xyz, int32_t n, int32_t stride, bool on_device) {
-  if (!h || n < 0 || (n > 0 && !xyz) || stride < 3) {
+// enqueue nf frames (H2D when host memory, then every kernel, frame f in grid row y = f, and the
+// D2H of the frame records) on the handle's stream; sr_finish waits for them
+static int32_t sr_launch_frames(loam_scanreg* h, int nf, const float* const* xyz, const int32_t* n, int32_t stride,
+                                bool on_device) {
+  if (!h || nf < 1 || nf > h->nb || !xyz || !n || stride < 3) {
     set_error("loam_scanreg_input: bad arguments");
     return LOAM_ERR_ARG;
   }
-  if (n > h->D.cap) {
-    set_error("loam_scanreg_input: more points than max_input_points");
-    return LOAM_ERR_CAPACITY;
-  }
-  LOAM_HIP(hipSetDevice(h->dev));
-  hipStream_t st = h->st;
-  SrDev D = h->D;
-  D.stride = stride;
-  if (on_device) {
-    D.xyz = xyz;
-  } else {
-    if (stride != 4 && (size_t)n * stride > (size_t)h->D.cap * 4) {
-      set_error("loam_scanreg_input: stride too large for the staging buffer");
+  int nmax = 0;
+  for (int f = 0; f < nf; ++f) {
+    if (n[f] < 0 || (n[f] > 0 && !xyz[f])) {
+      set_error("loam_scanreg_input: bad arguments");
+      return LOAM_ERR_ARG;
+    }
+    if (n[f] > h->D.cap) {
+      set_error("loam_scanreg_input: more points than max_input_points");
       return LOAM_ERR_CAPACITY;
     }
-    if (n) LOAM_HIP(hipMemcpyAsync(h->d_in, xyz, sizeof(float) * (size_t)n * stride, hipMemcpyHostToDevice, st));
-    D.xyz = h->d_in;
+    nmax = std::max(nmax, (int)n[f]);
   }
+  if (!on_device && stride != 4)
+    for (int f = 0; f < nf; ++f)
+      if ((size_t)n[f] * stride > (size_t)h->D.cap * 4) {
+        set_error("loam_scanreg_input: stride too large for the staging buffer");
+        return LOAM_ERR_CAPACITY;
+      }
+  LOAM_HIP(hipSetDevice(h->dev));
+  hipStream_t st = h->st;
+  for (int f = 0; f < nf; ++f) {  // (the previous launch's copy of h_Ds is done: sr_finish came first)
+    SrDev D = h->Dv[f];
+    D.stride = stride;
+    D.n_in = n[f];
+    if (on_device) {
+      D.xyz = xyz[f];
+    } else {
+      float* stage = h->d_in + (size_t)f * h->D.cap * 4;
+      if (n[f]) LOAM_HIP(hipMemcpyAsync(stage, xyz[f], sizeof(float) * (size_t)n[f] * stride, hipMemcpyHostToDevice, st));
+      D.xyz = stage;
+    }
+    h->h_Ds[f] = D;
+  }
+  LOAM_HIP(hipMemcpyAsync(h->d_Ds, h->h_Ds, sizeof(SrDev) * nf, hipMemcpyHostToDevice, st));
   static_assert(sizeof(SrFrame) % 4 == 0, "k_sr_init writes the record by words");
   LOAM_HIP(hipEventRecord(h->ev[0], st));
-  k_sr_init<<<1, 256, 0, st>>>(D.fr, n);
-  const int nblocks = std::max(1, (n + SR_BLOCK - 1) / SR_BLOCK);
-  if (n > 0) {
-    k_sr_valid<<<nblocks, SR_BLOCK, 0, st>>>(D, nblocks);
-    k_sr_oris<<<1, 1024, 0, st>>>(D, nblocks);
-    k_sr_ring<<<nblocks, SR_BLOCK, 0, st>>>(D, nblocks);
-    k_sr_ring_scan<<<1, 1024, 0, st>>>(D, nblocks);
-    k_sr_scatter<<<nblocks, SR_BLOCK, 0, st>>>(D, nblocks);
-    k_sr_curv<<<std::min(nblocks, 1024), SR_BLOCK, 0, st>>>(D);
-    k_sr_select<<<SR_MAX_RINGS, SR_SEL_THREADS, 0, st>>>(D);
-    k_sr_ringvox<<<SR_MAX_RINGS, SRV_THREADS, 0, st>>>(D);
-    k_sr_gather<<<SR_MAX_RINGS, 256, 0, st>>>(D);
+  const SrDev* Ds = h->d_Ds;
+  k_sr_init<<<dim3(1, nf), 256, 0, st>>>(Ds);
+  const int nblocks = std::max(1, (nmax + SR_BLOCK - 1) / SR_BLOCK);
+  if (nmax > 0) {
+    k_sr_valid<<<dim3(nblocks, nf), SR_BLOCK, 0, st>>>(Ds, nblocks);
+    k_sr_oris<<<dim3(1, nf), 1024, 0, st>>>(Ds, nblocks);
+    k_sr_ring<<<dim3(nblocks, nf), SR_BLOCK, 0, st>>>(Ds, nblocks);
+    k_sr_ring_scan<<<dim3(1, nf), 1024, 0, st>>>(Ds, nblocks);
+    k_sr_scatter<<<dim3(nblocks, nf), SR_BLOCK, 0, st>>>(Ds, nblocks);
+    k_sr_curv<<<dim3(std::min(nblocks, 1024), nf), SR_BLOCK, 0, st>>>(Ds);
+    k_sr_select<<<dim3(SR_MAX_RINGS, nf), SR_SEL_THREADS, 0, st>>>(Ds);
+    k_sr_ringvox<<<dim3(SR_MAX_RINGS, nf), SRV_THREADS, 0, st>>>(Ds);
+    k_sr_gather<<<dim3(SR_MAX_RINGS, nf), 256, 0, st>>>(Ds);
     LOAM_HIP(hipGetLastError());
   }
   LOAM_HIP(hipEventRecord(h->ev[1], st));
-  if (!h->hf_pinned)
-    LOAM_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->hf_pinned), sizeof(SrFrame), hipHostMallocDefault));
-  LOAM_HIP(hipMemcpyAsync(h->hf_pinned, D.fr, sizeof(SrFrame), hipMemcpyDeviceToHost, st));
+  LOAM_HIP(hipMemcpyAsync(h->hf_pinned, h->Dv[0].fr, sizeof(SrFrame) * nf, hipMemcpyDeviceToHost, st));
   h->pending = 1;
-  h->pending_xyz = D.xyz;
+  h->nf = nf;
+  h->pending_xyz = h->h_Ds[0].xyz;
   h->pending_stride = stride;
   return LOAM_OK;
+}
+
+static int32_t sr_launch(loam_scanreg* h, const float* xyz, int32_t n, int32_t stride, bool on_device) {
+  if (!h) return LOAM_ERR_ARG;
+  return sr_launch_frames(h, 1, &xyz, &n, stride, on_device);
 }
 
 static int32_t sr_finish(loam_scanreg* h) {
@@ -959,13 +1031,19 @@ static int32_t sr_finish(loam_scanreg* h) {
   h->pending = 0;
   LOAM_HIP(hipSetDevice(h->dev));
   LOAM_HIP(hipStreamSynchronize(h->st));
-  h->hf = *h->hf_pinned;
+  for (int f = 0; f < h->nf; ++f) h->hfv[f] = h->hf_pinned[f];
+  h->hf = h->hfv[0];
   LOAM_HIP(hipEventElapsedTime(&h->ms, h->ev[0], h->ev[1]));
   h->D.xyz = h->pending_xyz;
   h->D.stride = h->pending_stride;
-  if (h->hf.err) {
-    const int e = h->hf.err;
-    set_error(std::string("loam_scanreg_input: ") +
+  int e = 0, ef = 0;
+  for (int f = 0; f < h->nf && !e; ++f)
+    if (h->hfv[f].err) {
+      e = h->hfv[f].err;
+      ef = f;
+    }
+  if (e) {
+    set_error(std::string("loam_scanreg_input: frame ") + std::to_string(ef) + ": " +
               ((e & VH_ERR_SPIN) ? "ring VoxelGrid sort: a wave's wait for a listed subtree ran out"
                : (e & SR_ERR_SORT) ? "std::sort emulation level list overflow"
                                    : "ring or sector larger than the LDS capacity") +
@@ -1052,6 +1130,57 @@ int32_t loam_scanreg_curvature(loam_scanreg* h, float* curv, int32_t* label, int
 }
 
 double loam_scanreg_ms(loam_scanreg* h) { return h ? (double)h->ms : 0.0; }
+
+int32_t loam_scanreg_input_batch(loam_scanreg* h, int32_t n_frames, const uint64_t* xyz, const int32_t* n,
+                                 int32_t stride, int32_t on_device) {
+  if (!h || n_frames < 1 || n_frames > h->nb || !xyz || !n) {
+    set_error("loam_scanreg_input_batch: bad arguments");
+    return LOAM_ERR_ARG;
+  }
+  if (h->pending) TRY(sr_finish(h));
+  std::vector<const float*> p(n_frames);
+  for (int f = 0; f < n_frames; ++f) p[f] = reinterpret_cast<const float*>(xyz[f]);
+  TRY(sr_launch_frames(h, n_frames, p.data(), n, stride, on_device != 0));
+  return sr_finish(h);
+}
+
+static int32_t sr_frame_ok(loam_scanreg* h, int32_t frame) {
+  if (!h || frame < 0) return LOAM_ERR_ARG;
+  TRY(sr_finish(h));  // an input_async in flight completes first
+  if (frame >= std::max(h->nf, 1)) {
+    set_error("loam_scanreg: frame index past the last launch's frames");
+    return LOAM_ERR_ARG;
+  }
+  return LOAM_OK;
+}
+
+int32_t loam_scanreg_frame_counts(loam_scanreg* h, int32_t frame, int32_t* counts) {
+  if (!counts) return LOAM_ERR_ARG;
+  TRY(sr_frame_ok(h, frame));
+  const SrFrame& F = h->hfv[frame];
+  for (int k = 0; k < 5; ++k) counts[k] = F.n_in > 0 ? F.out_n[k] : 0;
+  return LOAM_OK;
+}
+
+int32_t loam_scanreg_frame_device_ptr(loam_scanreg* h, int32_t frame, int32_t which, const float** ptr) {
+  if (which < 0 || which > 4 || !ptr) return LOAM_ERR_ARG;
+  TRY(sr_frame_ok(h, frame));
+  *ptr = reinterpret_cast<const float*>(h->Dv[frame].out[which]);
+  return h->hfv[frame].n_in > 0 ? h->hfv[frame].out_n[which] : 0;
+}
+
+int32_t loam_scanreg_frame_copy(loam_scanreg* h, int32_t frame, int32_t which, float* out, int32_t cap) {
+  if (which < 0 || which > 4 || (cap > 0 && !out)) return LOAM_ERR_ARG;
+  TRY(sr_frame_ok(h, frame));
+  LOAM_HIP(hipSetDevice(h->dev));
+  const int n = h->hfv[frame].n_in > 0 ? h->hfv[frame].out_n[which] : 0;
+  if (n > cap) {
+    set_error("loam_scanreg_frame_copy: output buffer too small");
+    return LOAM_ERR_CAPACITY;
+  }
+  if (n) LOAM_HIP(hipMemcpy(out, h->Dv[frame].out[which], sizeof(float4) * n, hipMemcpyDeviceToHost));
+  return n;
+}
 
 int32_t loam_scanreg_debug_counters(loam_scanreg* h, uint64_t* out, int32_t n, int32_t reset) {
   if (!h || !out || n < 0) return set_error("loam_scanreg_debug_counters: bad argument"), LOAM_ERR_ARG;

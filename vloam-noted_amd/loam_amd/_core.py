@@ -85,6 +85,11 @@ SIGNATURES = {
     "loam_scanreg_curvature": (c_i32, [vp, vp, vp, c_i32]),
     "loam_scanreg_ms": (c_d, [vp]),
     "loam_scanreg_debug_counters": (c_i32, [vp, vp, c_i32, c_i32]),
+    "loam_scanreg_create_batch": (c_i32, [ctypes.POINTER(Params), c_i32, c_i32, ctypes.POINTER(vp)]),
+    "loam_scanreg_input_batch": (c_i32, [vp, c_i32, vp, vp, c_i32, c_i32]),
+    "loam_scanreg_frame_counts": (c_i32, [vp, c_i32, vp]),
+    "loam_scanreg_frame_device_ptr": (c_i32, [vp, c_i32, c_i32, ctypes.POINTER(vp)]),
+    "loam_scanreg_frame_copy": (c_i32, [vp, c_i32, c_i32, vp, c_i32]),
     "loam_odometry_create": (c_i32, [ctypes.POINTER(Params), c_i32, c_i32, ctypes.POINTER(vp)]),
     "loam_odometry_destroy": (c_i32, [vp]),
     "loam_odometry_reset": (c_i32, [vp]),

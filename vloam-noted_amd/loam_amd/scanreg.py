@@ -108,3 +108,61 @@ class ScanRegistration:
         out = np.zeros(24, np.uint64)
         check(lib().loam_scanreg_debug_counters(self.h, ptr(out), 24, int(reset)))
         return out
+
+
+class ScanRegistrationBatch:
+    """Up to ``max_frames`` independent scans per launch sequence (loam_scanreg_create_batch):
+    ``input_batch(clouds)`` runs them together; ``cloud(frame, which)`` / ``device_ptr(frame,
+    which)`` read frame ``frame``'s clouds.  Bit-identical to one ScanRegistration per scan."""
+
+    def __init__(self, max_frames, device=0, params=None, **param_overrides):
+        self.params = params if params is not None else _core.default_params(**param_overrides)
+        self.max_frames = max_frames
+        h = ctypes.c_void_p()
+        check(lib().loam_scanreg_create_batch(ctypes.byref(self.params), device, int(max_frames), ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().loam_scanreg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def input_batch(self, clouds):
+        """clouds: host (n, >= 3) float32 arrays (same stride), one per frame"""
+        arrs = [np.ascontiguousarray(c, dtype=np.float32) for c in clouds]
+        stride = arrs[0].shape[1] if arrs and arrs[0].ndim == 2 else 4
+        ptrs = np.array([a.ctypes.data for a in arrs], dtype=np.uint64)
+        ns = np.array([len(a) for a in arrs], dtype=np.int32)
+        check(lib().loam_scanreg_input_batch(self.h, len(arrs), ptr(ptrs), ptr(ns), int(stride), 0))
+
+    def input_batch_device(self, ptrs, counts, stride=4):
+        """device pointers (integers) and point counts, one per frame"""
+        p = np.ascontiguousarray(ptrs, dtype=np.uint64)
+        n = np.ascontiguousarray(counts, dtype=np.int32)
+        check(lib().loam_scanreg_input_batch(self.h, len(p), ptr(p), ptr(n), int(stride), 1))
+
+    def counts(self, frame):
+        c = np.zeros(5, dtype=np.int32)
+        check(lib().loam_scanreg_frame_counts(self.h, int(frame), ptr(c)))
+        return c
+
+    def cloud(self, frame, which):
+        n = int(self.counts(frame)[which])
+        out = np.empty((n, 4), dtype=np.float32)
+        check(lib().loam_scanreg_frame_copy(self.h, int(frame), int(which), ptr(out), n))
+        return out
+
+    def device_ptr(self, frame, which):
+        p = ctypes.c_void_p()
+        n = check(lib().loam_scanreg_frame_device_ptr(self.h, int(frame), int(which), ctypes.byref(p)))
+        return p.value, n
+
+    @property
+    def ms(self):
+        return lib().loam_scanreg_ms(self.h)
