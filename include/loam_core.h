@@ -147,17 +147,18 @@ int32_t loam_scanreg_frame_counts(loam_scanreg* h, int32_t frame, int32_t* count
 int32_t loam_scanreg_frame_device_ptr(loam_scanreg* h, int32_t frame, int32_t which, const float** ptr);
 int32_t loam_scanreg_frame_copy(loam_scanreg* h, int32_t frame, int32_t which, float* out, int32_t cap);
 /* cumulative device cycle counters of scan registration, summed over rings and frames unless
- * "max": the per-ring PCL-order VoxelGrid (k_sr_ringvox): [0] cycles of the sort emulation
+ * "max": the per-ring PCL-order VoxelGrid (k_sr_ring_features' second phase): [0] cycles of the sort emulation
  * (libstdc++ introsort) for the voxels of 3+ members, [1] of their centroids, [2] rings that had
  * such a voxel, [3] max cycles of one ring, [4] cycles of the input-order filter, [5] points,
  * [6] max points of one ring, [7] max elements heap-sorted in one ring, [8] elements heap-sorted
  * at the depth limit, [9..12] cycles of the sort's setup, workgroup levels, wave subtrees and
- * positions; the feature selection (k_sr_select): [13] cycles of the sector sorts, [14] of the
+ * positions; the feature selection (its first phase): [13] cycles of the sector sorts, [14] of the
  * greedy picks, [15] max cycles of one ring, [19] / [20] max of one ring's sector sorts / greedy
  * picks; [16] the slowest VoxelGrid ring: its cycles << 32 | heap-sorted elements << 16 | points,
- * [18] its cycles << 32 | its cycles after the input-order filter.  reset = 1 zeroes them
- * after the copy.  Counted only in a handle created with LOAM_PHASE_COUNTERS=1 in the
- * environment. */
+ * [18] its cycles << 32 | its cycles after the input-order filter.  Counted only in a handle
+ * created with LOAM_PHASE_COUNTERS=1 in the environment.  Always counted: [21] sectors whose
+ * greedy picks were rerun with the flags inherited from the sector before, [22] rings whose
+ * sectors ran concurrently.  reset = 1 zeroes them after the copy. */
 #define LOAM_SR_DEBUG_COUNTERS 24
 int32_t loam_scanreg_debug_counters(loam_scanreg* h, uint64_t* out, int32_t n, int32_t reset);
 

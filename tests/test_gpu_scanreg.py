@@ -181,3 +181,18 @@ def test_batched_frames_match_single():
         b.counts(3)  # past the last launch's frames
     b.close()
     single.close()
+
+
+def test_concurrent_sectors_and_reruns():
+    """the six sectors of a ring pick concurrently and a sector is rerun where the flags inherited
+    from the sector before hit one of its first-5-point picks (scanreg.hip sr_greedy_ring; the
+    rule itself: tests/test_sr_conc_rule.py): the frames here exercise both, bit-exact"""
+    gpu = ScanRegistration()
+    gpu.debug_counters(reset=True)
+    for seed, f, flags in [(1, 0, 0), (6, 3, synth.QUANTIZE), (9, 4, synth.COLUMN_MAJOR | synth.LASER_AZ)]:
+        xyz, _ = synth.frame(seed, f, 2000, flags=flags)
+        _check_frame(xyz, gpu)
+    c = gpu.debug_counters()
+    assert c[22] > 100, list(c)  # rings with concurrent sectors
+    assert c[21] > 10, list(c)   # sector reruns
+    gpu.close()

@@ -11,11 +11,12 @@
 //                   offsets = laserCloudScans concatenation (:308-315)
 //   k_sr_scatter    stable scatter into the ring-major cloud, intensity = scanID + 0.1*relTime
 //   k_sr_curv       11-tap curvature over the concatenated cloud (:323-346), crossing rings
-//   k_sr_select     one workgroup per ring: the 6 sectors sorted by curvature at once (one wave
-//                   per sector, register bitonic), then the greedy sharp / lessSharp / flat
-//                   picks with +-5 neighbour suppression (:352-493): one wave runs the
-//                   (inherently sequential) greedy scan with 64-wide ballots, all in LDS
-//   k_sr_ringvox    VoxelGrid 0.2 m of each ring's lessFlat candidates (:497-503), in PCL's
+//   k_sr_ring_features  one workgroup per ring, two phases in one 160 KiB LDS:
+//                   selection: the 6 sectors sorted by curvature at once (one wave per sector,
+//                   register bitonic), then the greedy sharp / lessSharp / flat picks with +-5
+//                   neighbour suppression (:352-493), one wave per sector with 64-wide ballots,
+//                   sectors concurrently and a rerun where a border's inherited flags matter;
+//                   then VoxelGrid 0.2 m of the ring's lessFlat candidates (:497-503), in PCL's
 //                   summation order (voxel.h + voxel_hot.h: std::sort's order only where a
 //                   voxel has 3+ members)
 //   k_sr_gather     concatenation of the per-ring outputs in ring order
@@ -89,7 +90,7 @@ struct SrDev {
   uint32_t* ss_b;
   uint64_t* ss_s;
   int* ss_seg;  // [ring][2][3 * SR_SS_GSEG] level lists of the long-sector path (one sector of a ring at a time;
-               // every ring's workgroup has its own area: k_sr_select runs the rings concurrently)
+               // every ring's workgroup has its own area: the rings run concurrently)
   unsigned long long* dbg;  // [LOAM_SR_DEBUG_COUNTERS] (loam_scanreg_debug_counters)
   unsigned long long* pdbg;  // dbg when LOAM_PHASE_COUNTERS=1 at create, else null (no cycle counting)
 };
@@ -459,7 +460,6 @@ __device__ inline void sr_wave_sort(const float* curv, int sp, int len, uint64_t
   for (int e = 0; e < E; ++e) out[e * 64 + lane] = v[e];
 }
 
-constexpr int SR_SEL_THREADS = 512;
 constexpr int SR_WSORT_MAX = 1024;  // register sort (one wave per sector) up to this length
 constexpr int SR_SS_LDS = 512;      // tied sectors re-sorted in LDS up to this length (else global)
 constexpr int SR_SS_SEG = SR_WSORT_MAX / 17 + 2;  // level list of one wave-sorted sector
@@ -498,15 +498,28 @@ __device__ inline void sr_exact_sector(const SrDev& D, int sp, int len, uint64_t
   ss_wave_fence();
 }
 
+// One sector's picks (LDS), in pick order, and what the sector's run leaves at its borders.
+struct SrSect {
+  int sh[SR_SHARP], ls[SR_LESS_SHARP], fl[SR_FLAT];
+  int nsh, nls, nfl;
+  uint32_t spill;  // (concurrent runs) suppression past the sector's end: bit b = ring index hi + 1 + b
+  uint32_t head;   // picks among the sector's first 5 points: bit b = ring index lo + b
+};
+
 // sharp / lessSharp (descending curvature, :371-431) and flat (ascending, :439-483) picks of
-// one sector from its sorted keys K[0, len): one wave.  A window of 64 sorted candidates is
-// loaded with its picked flags and each candidate's suppression chains (sr_chain); a pick then
-// costs no LDS read: the candidates its suppression covers (cloud index within the chains) drop
-// out of the window's mask by one ballot, and picked[] is written for the later windows and
-// sectors.  The reference's next candidate is the first unpicked one behind the pick.
+// one sector [lo, hi] (ring-local) from its sorted keys K[0, len): one wave.  A window of 64
+// sorted candidates is loaded with its picked flags and each candidate's suppression chains
+// (sr_chain); a pick then costs no LDS read: the candidates its suppression covers (cloud index
+// within the chains) drop out of the window's mask by one ballot, and picked[] is written for
+// the later windows.  The reference's next candidate is the first unpicked one behind the pick.
+// conc (the sectors of a ring run concurrently, sr_greedy_ring): picked[] is written only inside
+// [lo, hi]; suppression past hi goes to `spill` instead, suppression before lo is dropped (the
+// sectors before are done with their picks in the reference's order, and lessFlat reads labels,
+// not picked flags).
 template <bool SHARP>
-__device__ inline void sr_greedy_pass(SrDev& D, int r, int base, const uint64_t* K, int len, uint8_t* picked,
-                                      int8_t* lab, const uint8_t* gapok, int& nsh, int& nls, int& nfl) {
+__device__ inline void sr_greedy_pass(int base, int lo, int hi, bool conc, const uint64_t* K, int len,
+                                      uint8_t* picked, int8_t* lab, const uint8_t* gapok, SrSect& S, int& nsh,
+                                      int& nls, int& nfl, uint32_t& spill, uint32_t& head) {
   const int lane = threadIdx.x & 63;
   int count = 0;
   for (int w = 0; w < len; w += 64) {
@@ -532,27 +545,33 @@ __device__ inline void sr_greedy_pass(SrDev& D, int r, int base, const uint64_t*
       const int pind = __builtin_amdgcn_readlane(ind, fc) - base;
       const int pf = __builtin_amdgcn_readlane(nf, fc), pb = __builtin_amdgcn_readlane(nb, fc);
       count++;
+      if (SHARP && count > SR_LESS_SHARP) return;
+      if (pind - lo < 5) head |= 1u << (pind - lo);  // (the 4th flat pick too: it is a pick)
       if (SHARP) {
-        if (count > SR_LESS_SHARP) return;
         if (lane == 0) {
           if (count <= SR_SHARP) {
             lab[pind] = 2;
-            D.ring_sharp[r * 6 * SR_SHARP + nsh++] = pind + base;
+            S.sh[nsh] = pind + base;
           } else {
             lab[pind] = 1;
           }
-          D.ring_less_sharp[r * 6 * SR_LESS_SHARP + nls++] = pind + base;
+          S.ls[nls] = pind + base;
         }
+        nsh += count <= SR_SHARP;
+        nls++;
       } else {
         if (lane == 0) {
           lab[pind] = -1;
-          D.ring_flat[r * 6 * SR_FLAT + nfl++] = pind + base;
+          S.fl[nfl] = pind + base;
         }
+        nfl++;
         if (count >= SR_FLAT) return;
       }
       if (lane == 0) picked[pind] = 1;
-      if (lane < pf) picked[pind + 1 + lane] = 1;
-      else if (lane >= 5 && lane - 5 < pb) picked[pind - (lane - 4)] = 1;
+      const int q = lane < pf ? pind + 1 + lane : (lane >= 5 && lane - 5 < pb) ? pind - (lane - 4) : -1;
+      if (q >= 0 && (!conc || (q >= lo && q <= hi))) picked[q] = 1;
+      if (conc && pind + pf > hi)
+        for (int l = hi + 1 - pind; l <= pf; ++l) spill |= 1u << (pind + l - hi - 1);
       const int rel = ind - base;
       avail &= ~__ballot(rel >= pind - pb && rel <= pind + pf);  // the pick and its suppressed neighbours
     }
@@ -563,44 +582,134 @@ __device__ inline void sr_greedy_pass(SrDev& D, int r, int base, const uint64_t*
   }
 }
 
-__device__ inline void sr_greedy(SrDev& D, int r, int base, const uint64_t* K, int len, uint8_t* picked,
-                                 int8_t* lab, const uint8_t* gapok, int& nsh, int& nls, int& nfl) {
-  sr_greedy_pass<true>(D, r, base, K, len, picked, lab, gapok, nsh, nls, nfl);
+// one sector's two passes (sharp first, :371-431, then flat, :439-483) on one wave; the counts,
+// spill and head go to S
+__device__ inline void sr_greedy_sector(int base, int lo, int hi, bool conc, const uint64_t* K, int len,
+                                        uint8_t* picked, int8_t* lab, const uint8_t* gapok, SrSect& S) {
+  int nsh = 0, nls = 0, nfl = 0;
+  uint32_t spill = 0, head = 0;
+  sr_greedy_pass<true>(base, lo, hi, conc, K, len, picked, lab, gapok, S, nsh, nls, nfl, spill, head);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  sr_greedy_pass<false>(D, r, base, K, len, picked, lab, gapok, nsh, nls, nfl);
+  sr_greedy_pass<false>(base, lo, hi, conc, K, len, picked, lab, gapok, S, nsh, nls, nfl, spill, head);
+  if ((threadIdx.x & 63) == 0) {
+    S.nsh = nsh;
+    S.nls = nls;
+    S.nfl = nfl;
+    S.spill = spill;
+    S.head = head;
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(const SrDev* __restrict__ Ds) {
-  SrDev D = Ds[blockIdx.y];
-  __shared__ uint64_t keys[6 * SR_WSORT_MAX];  // 48 KiB: the 6 sorted sectors
-  __shared__ uint8_t picked[SR_RING_CAP];
-  __shared__ int8_t lab[SR_RING_CAP];
-  __shared__ uint8_t gapok[SR_RING_CAP];
-  __shared__ uint32_t ws[SR_SEL_THREADS / 64];
-  __shared__ uint64_t ssE[6][SR_SS_LDS];  // exact re-sort of tied sectors (one wave each)
-  __shared__ uint32_t ssA[6][SR_SS_LDS], ssB[6][SR_SS_LDS];
-  __shared__ int ssSeg[6][2][3 * SR_SS_SEG];
-  __shared__ SsLevels ssLev[6];
-  const int r = blockIdx.x;
+constexpr int SR_CONC_MIN = 8;  // sectors run concurrently when each holds at least this many points
+
+// The six sectors' greedy picks, concurrently (one wave each), in the reference's sequential
+// result.  The reference runs sector j after sector j - 1, so the only state sector j inherits is
+// the picked flags that j - 1's last picks spread into j's first (at most 5) points.  Sector j ran
+// without them; its picks are still the reference's unless it picked one of those points (a flag
+// on a point the run never picked changes no availability test the run's choices depended on).
+// Wave 0 then walks the borders in order and reruns such a sector with the inherited flags (its
+// own spill can change, so the next border is checked against the rerun's).
+__device__ inline void sr_greedy_ring(int base, const int* lo, const int* hi, const uint64_t* keys, const int* len,
+                                      uint8_t* picked, int8_t* lab, const uint8_t* gapok, SrSect* sect,
+                                      unsigned long long* dbg) {
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (wid < 6) sr_greedy_sector(base, lo[wid], hi[wid], true, keys + wid * SR_WSORT_MAX, len[wid], picked, lab, gapok,
+                                sect[wid]);
+  __syncthreads();
+  if (wid == 0) {
+    for (int j = 1; j < 6; ++j) {
+      const uint32_t inh = sect[j - 1].spill;
+      if (!(inh & sect[j].head)) continue;
+      for (int k = lo[j] + lane; k <= hi[j]; k += 64) {
+        picked[k] = (k - lo[j] < 5 && ((inh >> (k - lo[j])) & 1u)) ? 1 : 0;
+        lab[k] = 0;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      sr_greedy_sector(base, lo[j], hi[j], true, keys + j * SR_WSORT_MAX, len[j], picked, lab, gapok, sect[j]);
+      if (lane == 0 && dbg) atomicAdd(dbg + 21, 1ull);  // (debug counter 21: sector reruns)
+    }
+  }
+  __syncthreads();
+}
+
+// LDS of one ring's feature selection (carved from the ring workgroup's 160 KiB)
+struct SrSelLds {
+  uint64_t* keys;    // [6][SR_WSORT_MAX] the sorted sectors
+  uint64_t* ssE;     // [6][SR_SS_LDS] exact re-sort of tied sectors (one wave each)
+  uint32_t* ssA;     // [6][SR_SS_LDS]
+  uint32_t* ssB;     // [6][SR_SS_LDS]
+  uint8_t* picked;   // [SR_RING_CAP]
+  int8_t* lab;       // [SR_RING_CAP]
+  uint8_t* gapok;    // [SR_RING_CAP]
+  int* ssSeg;        // [6][2][3 * SR_SS_SEG]
+  SsLevels* ssLev;   // [6]
+  SrSect* sect;      // [6]
+  uint32_t* ws;      // [VX_WAVES]
+};
+
+constexpr size_t sr_align16(size_t b) { return (b + 15) & ~(size_t)15; }
+constexpr size_t SR_SEL_LDS_BYTES =
+    sr_align16(6 * SR_WSORT_MAX * 8) + sr_align16(6 * SR_SS_LDS * 8) + 2 * sr_align16(6 * SR_SS_LDS * 4) +
+    3 * sr_align16(SR_RING_CAP) + sr_align16(6 * 2 * 3 * SR_SS_SEG * 4) + sr_align16(6 * sizeof(SsLevels)) +
+    sr_align16(6 * sizeof(SrSect)) + sr_align16(VX_WAVES * 4);
+static_assert(SR_SEL_LDS_BYTES <= (size_t)VX_LDS_WORDS * 4, "the ring's selection fits the workgroup's LDS");
+
+__device__ inline SrSelLds sr_sel_carve(uint32_t* lds) {
+  uint8_t* p = reinterpret_cast<uint8_t*>(lds);
+  SrSelLds L;
+  auto take = [&p](size_t b) {
+    uint8_t* q = p;
+    p += sr_align16(b);
+    return q;
+  };
+  L.keys = reinterpret_cast<uint64_t*>(take(6 * SR_WSORT_MAX * 8));
+  L.ssE = reinterpret_cast<uint64_t*>(take(6 * SR_SS_LDS * 8));
+  L.ssA = reinterpret_cast<uint32_t*>(take(6 * SR_SS_LDS * 4));
+  L.ssB = reinterpret_cast<uint32_t*>(take(6 * SR_SS_LDS * 4));
+  L.picked = take(SR_RING_CAP);
+  L.lab = reinterpret_cast<int8_t*>(take(SR_RING_CAP));
+  L.gapok = take(SR_RING_CAP);
+  L.ssSeg = reinterpret_cast<int*>(take(6 * 2 * 3 * SR_SS_SEG * 4));
+  L.ssLev = reinterpret_cast<SsLevels*>(take(6 * sizeof(SsLevels)));
+  L.sect = reinterpret_cast<SrSect*>(take(6 * sizeof(SrSect)));
+  L.ws = reinterpret_cast<uint32_t*>(take(VX_WAVES * 4));
+  return L;
+}
+
+// Feature selection of ring r (:352-493) by the whole workgroup (NT threads): the 6 sectors
+// sorted by curvature at once (one wave per sector, register bitonic; a sector with tied
+// curvatures re-sorted in libstdc++'s order), the greedy picks (sr_greedy_ring), the ring's pick
+// lists and labels, and its lessFlat candidates compacted in index order into the ring's region
+// of less_flat_scan.  Returns their number (0 for a ring too short to select from).
+template <int NT>
+__device__ inline int sr_select_ring(const SrDev& D, int r, const SrSelLds& M) {
   SrFrame& F = *D.fr;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int base = F.ring_off[r], n = F.ring_cnt[r];
   const int s = base + 5, e = base + n - 6;
-  if (tid == 0) {
-    F.n_sharp[r] = F.n_less_sharp[r] = F.n_flat[r] = F.n_less_flat_scan[r] = 0;
+  if (e - s < 6) {  // :355-356
+    if (tid == 0) F.n_sharp[r] = F.n_less_sharp[r] = F.n_flat[r] = F.n_less_flat_scan[r] = 0;
+    return 0;
   }
-  if (e - s < 6) return;  // :355-356
   if (n > SR_RING_CAP) {
-    if (tid == 0) atomicOr(&F.err, SR_ERR_RING);
-    return;
+    if (tid == 0) {
+      F.n_sharp[r] = F.n_less_sharp[r] = F.n_flat[r] = F.n_less_flat_scan[r] = 0;
+      atomicOr(&F.err, SR_ERR_RING);
+    }
+    return 0;
   }
+  uint64_t* keys = M.keys;
+  uint8_t* picked = M.picked;
+  int8_t* lab = M.lab;
   const float4* L = D.cloud;
-  for (int k = tid; k < n; k += SR_SEL_THREADS) {
+  for (int k = tid; k < n; k += NT) {
     picked[k] = 0;
     lab[k] = 0;
     uint8_t ok = 0;
@@ -609,67 +718,81 @@ __global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(const SrDev* __res
       const float dX = b.x - a.x, dY = b.y - a.y, dZ = b.z - a.z;
       ok = (dX * dX + dY * dY + dZ * dZ > 0.05) ? 0 : 1;
     }
-    gapok[k] = ok;
+    M.gapok[k] = ok;
   }
   // sectors (:361-365); with all 6 short enough, wave j sorts sector j in registers
-  int sp[6], len[6], maxlen = 0;
+  int sp[6], len[6], lo[6], hi[6], maxlen = 0, minlen = 1 << 30;
 #pragma unroll
   for (int j = 0; j < 6; j++) {
     sp[j] = s + (e - s) * j / 6;
     len[j] = (s + (e - s) * (j + 1) / 6 - 1) - sp[j] + 1;
+    lo[j] = sp[j] - base;
+    hi[j] = lo[j] + len[j] - 1;
     maxlen = max(maxlen, len[j]);
+    minlen = min(minlen, len[j]);
   }
   const bool fast = maxlen <= SR_WSORT_MAX;
   unsigned long long* prof = D.pdbg;  // (diagnostics: [13] sector sorts, [14] greedy, [15] slowest ring)
   const unsigned long long t0 = prof ? __builtin_readcyclecounter() : 0ull;
   if (!fast && maxlen > 6 * SR_WSORT_MAX) {
-    if (tid == 0) atomicOr(&F.err, SR_ERR_RING);
-    return;
+    if (tid == 0) {
+      F.n_sharp[r] = F.n_less_sharp[r] = F.n_flat[r] = F.n_less_flat_scan[r] = 0;
+      atomicOr(&F.err, SR_ERR_RING);
+    }
+    return 0;
   }
   if (fast && wid < 6) {
-    if (maxlen <= 512) sr_wave_sort<8>(D.curv, sp[wid], len[wid], keys + wid * SR_WSORT_MAX);
-    else sr_wave_sort<16>(D.curv, sp[wid], len[wid], keys + wid * SR_WSORT_MAX);
-    sr_exact_sector(D, sp[wid], len[wid], keys + wid * SR_WSORT_MAX, ssE[wid], ssA[wid], ssB[wid], &ssLev[wid],
-                    ssSeg[wid][0], ssSeg[wid][1], SR_SS_SEG);
+    uint64_t* K = keys + wid * SR_WSORT_MAX;
+    if (maxlen <= 512) sr_wave_sort<8>(D.curv, sp[wid], len[wid], K);
+    else sr_wave_sort<16>(D.curv, sp[wid], len[wid], K);
+    sr_exact_sector(D, sp[wid], len[wid], K, M.ssE + wid * SR_SS_LDS, M.ssA + wid * SR_SS_LDS,
+                    M.ssB + wid * SR_SS_LDS, &M.ssLev[wid], M.ssSeg + wid * 6 * SR_SS_SEG,
+                    M.ssSeg + wid * 6 * SR_SS_SEG + 3 * SR_SS_SEG, SR_SS_SEG);
   }
   __syncthreads();
   const unsigned long long t1 = prof ? __builtin_readcyclecounter() : 0ull;
-  int nsh = 0, nls = 0, nfl = 0;  // valid in wave 0
-  for (int j = 0; j < 6; j++) {
-    const uint64_t* K = keys + j * SR_WSORT_MAX;
-    if (!fast) {  // long sectors: block bitonic in LDS, one sector at a time
-      K = keys;
-      int pad = 1;
-      while (pad < len[j]) pad <<= 1;
-      for (int k = tid; k < pad; k += SR_SEL_THREADS)
-        keys[k] = k < len[j] ? (((uint64_t)__float_as_uint(D.curv[sp[j] + k]) << 32) | (uint32_t)(sp[j] + k))
-                             : 0xFFFFFFFFFFFFFFFFull;
-      __syncthreads();
-      for (int kk = 2; kk <= pad; kk <<= 1) {
-        for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-          for (int i = tid; i < pad; i += SR_SEL_THREADS) {
-            const int ixj = i ^ jj;
-            if (ixj > i) {
-              const uint64_t a = keys[i], b = keys[ixj];
-              const bool asc = (i & kk) == 0;
-              if ((a > b) == asc) {
-                keys[i] = b;
-                keys[ixj] = a;
+  if (fast && minlen >= SR_CONC_MIN) {
+    sr_greedy_ring(base, lo, hi, keys, len, picked, lab, M.gapok, M.sect, D.dbg);
+    if (tid == 0 && D.dbg) atomicAdd(D.dbg + 22, 1ull);  // (debug counter 22: rings with concurrent sectors)
+  } else {
+    // sequential sectors (a ring with a sector over SR_WSORT_MAX points, or one shorter than
+    // SR_CONC_MIN): every suppression flag written where the reference writes it
+    for (int j = 0; j < 6; j++) {
+      const uint64_t* K = keys + j * SR_WSORT_MAX;
+      if (!fast) {  // long sectors: block bitonic in LDS, one sector at a time
+        K = keys;
+        int pad = 1;
+        while (pad < len[j]) pad <<= 1;
+        for (int k = tid; k < pad; k += NT)
+          keys[k] = k < len[j] ? (((uint64_t)__float_as_uint(D.curv[sp[j] + k]) << 32) | (uint32_t)(sp[j] + k))
+                               : 0xFFFFFFFFFFFFFFFFull;
+        __syncthreads();
+        for (int kk = 2; kk <= pad; kk <<= 1) {
+          for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+            for (int i = tid; i < pad; i += NT) {
+              const int ixj = i ^ jj;
+              if (ixj > i) {
+                const uint64_t a = keys[i], b = keys[ixj];
+                const bool asc = (i & kk) == 0;
+                if ((a > b) == asc) {
+                  keys[i] = b;
+                  keys[ixj] = a;
+                }
               }
             }
+            __syncthreads();
           }
-          __syncthreads();
         }
+        if (wid == 0)
+          sr_exact_sector(D, sp[j], len[j], keys, nullptr, nullptr, nullptr, &M.ssLev[0],
+                          D.ss_seg + r * 6 * SR_SS_GSEG, D.ss_seg + r * 6 * SR_SS_GSEG + 3 * SR_SS_GSEG, SR_SS_GSEG);
+        __syncthreads();
       }
-      if (wid == 0)
-        sr_exact_sector(D, sp[j], len[j], keys, nullptr, nullptr, nullptr, &ssLev[0], D.ss_seg + r * 6 * SR_SS_GSEG,
-                        D.ss_seg + r * 6 * SR_SS_GSEG + 3 * SR_SS_GSEG, SR_SS_GSEG);
-      __syncthreads();
+      if (wid == 0) sr_greedy_sector(base, lo[j], hi[j], false, K, len[j], picked, lab, M.gapok, M.sect[j]);
+      if (!fast) __syncthreads();
     }
-    if (wid == 0) sr_greedy(D, r, base, K, len[j], picked, lab, gapok, nsh, nls, nfl);
-    if (!fast) __syncthreads();
+    __syncthreads();
   }
-  __syncthreads();
   if (prof && tid == 0) {
     const unsigned long long t2 = __builtin_readcyclecounter();
     atomicAdd(prof + 13, t1 - t0);
@@ -678,71 +801,59 @@ __global__ void __launch_bounds__(SR_SEL_THREADS) k_sr_select(const SrDev* __res
     atomicMax(prof + 19, t1 - t0);
     atomicMax(prof + 20, t2 - t1);
   }
+  // the ring's pick lists, sectors in order (the reference appends them sector by sector)
+  if (wid == 0) {
+    int osh = 0, ols = 0, ofl = 0;
+    for (int j = 0; j < 6; ++j) {
+      const SrSect& S = M.sect[j];
+      if (lane < S.nsh) D.ring_sharp[r * 6 * SR_SHARP + osh + lane] = S.sh[lane];
+      if (lane < S.nls) D.ring_less_sharp[r * 6 * SR_LESS_SHARP + ols + lane] = S.ls[lane];
+      if (lane < S.nfl) D.ring_flat[r * 6 * SR_FLAT + ofl + lane] = S.fl[lane];
+      osh += S.nsh;
+      ols += S.nls;
+      ofl += S.nfl;
+    }
+    if (lane == 0) {
+      F.n_sharp[r] = osh;
+      F.n_less_sharp[r] = ols;
+      F.n_flat[r] = ofl;
+    }
+  }
   // lessFlat candidates: label <= 0 in index order (:486-493) over [s, e), the 6 sectors
   // back to back; stable block compaction
   int nlf = 0;
-  for (int c = s; c < e; c += SR_SEL_THREADS) {
+  for (int c = s; c < e; c += NT) {
     const int k = c + tid;
     const bool pred = k < e && lab[k - base] <= 0;
     const uint64_t bal = __ballot(pred);
     const uint32_t pre = __popcll(bal & lanemask_lt());
-    if (lane == 0) ws[wid] = __popcll(bal);
+    if (lane == 0) M.ws[wid] = __popcll(bal);
     __syncthreads();
     uint32_t off = 0, tot = 0;
-    for (int w = 0; w < SR_SEL_THREADS / 64; ++w) {
-      if (w < wid) off += ws[w];
-      tot += ws[w];
+    for (int w = 0; w < NT / 64; ++w) {
+      if (w < wid) off += M.ws[w];
+      tot += M.ws[w];
     }
     if (pred) D.less_flat_scan[base + nlf + off + pre] = L[k];
     nlf += tot;
     __syncthreads();
   }
-  for (int k = tid; k < n; k += SR_SEL_THREADS) D.label[base + k] = lab[k];
-  if (tid == 0) {
-    F.n_sharp[r] = nsh;
-    F.n_less_sharp[r] = nls;
-    F.n_flat[r] = nfl;
-    F.n_less_flat_scan[r] = nlf;
-  }
+  for (int k = tid; k < n; k += NT) D.label[base + k] = lab[k];
+  if (tid == 0) F.n_less_flat_scan[r] = nlf;
+  return nlf;
 }
 
 // PCL VoxelGrid of one ring's lessFlat candidates (scan_registration.cpp:497-501) in PCL's
-// summation order, one workgroup per ring: the input-order filter (voxel.h) sums every voxel of at
-// most 2 members (order-free) and records the others, then voxel_hot.h runs the pruned std::sort
-// emulation in LDS and sums those voxels in its order.  Scratch: the ring's region of the
-// sector sort's arrays (k_sr_select is done with them).
+// summation order: the input-order filter (voxel.h) sums every voxel of at most 2 members
+// (order-free) and records the others, then voxel_hot.h runs the pruned std::sort emulation in
+// LDS and sums those voxels in its order.  Scratch: the ring's region of the sector sort's
+// arrays (the ring's selection is done with them).
 constexpr int SRV_THREADS = VX_THREADS;
 static_assert(SR_RING_CAP <= VH_MAX_N, "a ring's lessFlat cloud fits the LDS emulation");
 
-// (a separate function holding the LDS: the ROCm 7.2 compiler crashes in InstCombine when the
-// filter is inlined into the kernel; declared here, the array keeps its LDS address space)
-__device__ __noinline__ void sr_ringvox(const VoxSeg& S, int n, int* err, unsigned long long* prof) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
-  const unsigned long long t0 = __builtin_readcyclecounter();
-  voxel_segment(S, lds);
-  const unsigned long long t1 = __builtin_readcyclecounter();
-  const int heap_el = vh_fixup<SRV_THREADS>(VxSrc{S.src0, n, nullptr}, n, S.out, S.hot, lds, VX_LDS_WORDS - 256,
-                                            *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192), nullptr, err,
-                                            prof, prof ? prof + 8 : nullptr);
-  if (prof && threadIdx.x == 0) {  // (diagnostics: include/loam_core.h LOAM_SR_DEBUG_COUNTERS)
-    const unsigned long long t2 = __builtin_readcyclecounter();
-    atomicAdd(prof + 4, t1 - t0);
-    atomicAdd(prof + 5, (unsigned long long)n);
-    atomicMax(prof + 6, (unsigned long long)n);
-    atomicMax(prof + 7, (unsigned long long)heap_el);
-    // the slowest ring: its cycles in the high bits, then its heap-sorted elements and points
-    atomicMax(prof + 3, t2 - t0);
-    atomicMax(prof + 16, ((t2 - t0) << 32) | ((unsigned long long)heap_el << 16) | (unsigned long long)n);
-    atomicMax(prof + 18, ((t2 - t0) << 32) | (t2 - t1));
-  }
-}
-
-__global__ void __launch_bounds__(SRV_THREADS) k_sr_ringvox(const SrDev* __restrict__ Ds) {
-  const SrDev D = Ds[blockIdx.y];
-  const int r = blockIdx.x;
+__device__ inline void sr_ringvox(const SrDev& D, int r, int n, uint32_t* lds) {
   SrFrame& F = *D.fr;
   const int base = F.ring_off[r];
-  const int n = F.n_less_flat_scan[r];
   VoxSeg S{};
   S.src0 = D.less_flat_scan + base;
   S.n0 = n;
@@ -758,7 +869,42 @@ __global__ void __launch_bounds__(SRV_THREADS) k_sr_ringvox(const SrDev* __restr
   S.hot.hv = S.hot.hl + n;  // 3 words per hot voxel, at most n / 3 of them: within the ring's 2 n
   S.hot.fpos = reinterpret_cast<uint32_t*>(D.ss_s + base);
   S.hot.cap_h = (uint32_t)n / 3;
-  sr_ringvox(S, n, &F.err, D.pdbg);
+  unsigned long long* prof = D.pdbg;
+  const unsigned long long t0 = __builtin_readcyclecounter();
+  voxel_segment(S, lds);
+  const unsigned long long t1 = __builtin_readcyclecounter();
+  const int heap_el = vh_fixup<SRV_THREADS>(VxSrc{S.src0, n, nullptr}, n, S.out, S.hot, lds, VX_LDS_WORDS - 256,
+                                            *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192), nullptr, &F.err,
+                                            prof, prof ? prof + 8 : nullptr);
+  if (prof && threadIdx.x == 0) {  // (diagnostics: include/loam_core.h LOAM_SR_DEBUG_COUNTERS)
+    const unsigned long long t2 = __builtin_readcyclecounter();
+    atomicAdd(prof + 4, t1 - t0);
+    atomicAdd(prof + 5, (unsigned long long)n);
+    atomicMax(prof + 6, (unsigned long long)n);
+    atomicMax(prof + 7, (unsigned long long)heap_el);
+    // the slowest ring: its cycles in the high bits, then its heap-sorted elements and points
+    atomicMax(prof + 3, t2 - t0);
+    atomicMax(prof + 16, ((t2 - t0) << 32) | ((unsigned long long)heap_el << 16) | (unsigned long long)n);
+    atomicMax(prof + 18, ((t2 - t0) << 32) | (t2 - t1));
+  }
+}
+
+// A ring's selection and then its lessFlat VoxelGrid in one workgroup: the ring's VoxelGrid
+// starts when its own picks are done, not when the slowest ring's are, and both phases share
+// the 160 KiB.  (A separate function holding the LDS: the ROCm 7.2 compiler crashes in
+// InstCombine when the filter is inlined into the kernel; declared here, the array keeps its LDS
+// address space.)
+__device__ __noinline__ void sr_ring_features(const SrDev* __restrict__ Ds) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
+  const SrDev D = Ds[blockIdx.y];
+  const int r = blockIdx.x;
+  const int nlf = sr_select_ring<SRV_THREADS>(D, r, sr_sel_carve(lds));
+  __syncthreads();  // (the ring's lessFlat points were written by this workgroup: same CU)
+  sr_ringvox(D, r, nlf, lds);
+}
+
+__global__ void __launch_bounds__(SRV_THREADS) k_sr_ring_features(const SrDev* __restrict__ Ds) {
+  sr_ring_features(Ds);
 }
 
 // concatenation of the per-ring outputs in ring order
@@ -1007,8 +1153,7 @@ static int32_t sr_launch_frames(loam_scanreg* h, int nf, const float* const* xyz
     k_sr_ring_scan<<<dim3(1, nf), 1024, 0, st>>>(Ds, nblocks);
     k_sr_scatter<<<dim3(nblocks, nf), SR_BLOCK, 0, st>>>(Ds, nblocks);
     k_sr_curv<<<dim3(std::min(nblocks, 1024), nf), SR_BLOCK, 0, st>>>(Ds);
-    k_sr_select<<<dim3(SR_MAX_RINGS, nf), SR_SEL_THREADS, 0, st>>>(Ds);
-    k_sr_ringvox<<<dim3(SR_MAX_RINGS, nf), SRV_THREADS, 0, st>>>(Ds);
+    k_sr_ring_features<<<dim3(SR_MAX_RINGS, nf), SRV_THREADS, 0, st>>>(Ds);
     k_sr_gather<<<dim3(SR_MAX_RINGS, nf), 256, 0, st>>>(Ds);
     LOAM_HIP(hipGetLastError());
   }
