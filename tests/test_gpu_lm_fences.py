@@ -5,9 +5,14 @@ workgroups with agent-scope atomic stores, a `vmcnt(0)` drain and relaxed polls:
 gfx950 by how its L2 / write-through path behaves, not by the HIP memory model.
 `libloam_core_fences.so` is the same source built with LM_HANDOFF_FENCES=1 (release / acquire
 fences, cdna_hip_programming.md §6 Guideline 16).  Both run the same free-running frames on
-several streams (persistent LM, hand-offs every pass) and must agree bit for bit: a stale read
-in the fence-free build would change a pose.
+one stream (16 workgroups per solve: the most hand-offs per pass) and on four, and must agree bit
+for bit in every pose and in every LM summary (steps, accepted / invalid steps, termination and the
+initial / final cost as float64 bits): a stale read of a partial sum or of the evaluation point
+in the fence-free build would change a cost even where the pose survived.  The evidence stays
+empirical: this checks the hardware behaviour the fence-free build relies on, on
+these frames.
 """
+import inspect
 import json
 import os
 import subprocess
@@ -23,9 +28,21 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FENCES = os.path.join(ROOT, "vloam-noted_amd", "loam_amd", "_lib", "libloam_core_fences.so")
-N_STREAMS = 4
 
-CHILD = r"""
+
+def summary(m, n_streams):
+    """poses and LM summaries of every stream, costs as float64 bit patterns"""
+    out = []
+    for s in range(n_streams):
+        st = m.stats(s)
+        lm = [[l.iterations, l.successful, l.invalid, l.termination,
+               int(np.float64(l.initial_cost).view(np.uint64)), int(np.float64(l.final_cost).view(np.uint64))]
+              for l in st.lm]
+        out.append([np.concatenate(m.pose(s)).view(np.uint64).tolist(), lm])
+    return out
+
+
+CHILD_MAIN = r"""
 import json, sys
 import numpy as np
 sys.path.insert(0, sys.argv[2])
@@ -39,9 +56,10 @@ for f in range(n_frames):
         k = (f + 3 * s) % n_frames
         m.input(s, d[f"c{k}"], d[f"s{k}"], d[f"q{k}"], d[f"t{k}"])
     m.solve()
-    out.append([np.concatenate(m.pose(s)).tolist() for s in range(n_streams)])
+    out.append(summary(m, n_streams))
 print(json.dumps(out))
 """
+CHILD = "import numpy as np\n" + inspect.getsource(summary) + CHILD_MAIN
 
 
 def _run(m, d, n_frames, n_streams):
@@ -51,15 +69,16 @@ def _run(m, d, n_frames, n_streams):
             k = (f + 3 * s) % n_frames
             m.input(s, d[f"c{k}"], d[f"s{k}"], d[f"q{k}"], d[f"t{k}"])
         m.solve()
-        out.append([np.concatenate(m.pose(s)).tolist() for s in range(n_streams)])
+        out.append(summary(m, n_streams))
     return out
 
 
-def test_fence_free_handoff_matches_fenced_build(tmp_path):
+@pytest.mark.parametrize("n_streams", [1, 4])
+def test_fence_free_handoff_matches_fenced_build(tmp_path, n_streams):
     if not os.path.exists(FENCES):
         pytest.fail(f"{FENCES} missing: run make -C vloam-noted_amd")
-    seq = run_sequence(seed=5, n_frames=10)
-    d = {"n_frames": np.int64(len(seq)), "n_streams": np.int64(N_STREAMS)}
+    seq = run_sequence(seed=5, n_frames=16)
+    d = {"n_frames": np.int64(len(seq)), "n_streams": np.int64(n_streams)}
     for k, rec in enumerate(seq):
         d[f"c{k}"], d[f"s{k}"] = rec["corner"], rec["surf"]
         d[f"q{k}"], d[f"t{k}"] = rec["q_wodom"], rec["t_wodom"]
@@ -70,5 +89,5 @@ def test_fence_free_handoff_matches_fenced_build(tmp_path):
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     fenced = json.loads(r.stdout.strip().splitlines()[-1])
-    plain = _run(BatchMapper(N_STREAMS), dict(np.load(path)), len(seq), N_STREAMS)
-    assert np.array_equal(np.array(plain), np.array(fenced))
+    plain = _run(BatchMapper(n_streams), dict(np.load(path)), len(seq), n_streams)
+    assert plain == fenced
