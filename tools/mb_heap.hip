@@ -1,6 +1,7 @@
 // Microbenchmark: libstdc++ heap sort (__make_heap + __sort_heap) of one LDS segment per wave, in
 // the two device formulations of stdsort.h / voxel_hot.h: one lane (ss_heap_sort) and the wave
-// (vh_heap_sort_wave: scalar path codes over 5-level look-aheads).  Checks the permutations
+// (vh_heap_sort_wave: scalar path codes over 5-level look-aheads), and the pipelined pops
+// (vh_sort_heap_pipe).  Checks the permutations
 // agree; prints cycles per element.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I../include -I../vloam-noted_amd/csrc tools/mb_heap.hip -o /tmp/mb_heap
 #include <hip/hip_runtime.h>
@@ -89,11 +90,21 @@ __global__ void __launch_bounds__(1024) k_heap(const uint32_t* in, uint32_t* out
   } else if (MODE == 1) {
     vh_heap_sort_wave(S, 0, len);
     ss_wave_fence();
-  } else {
+  } else if (MODE == 2) {
     if (len >= 2) {
       mb_make_heap_wave(S, 0, len);
       mb_sort_heap_wave(S, 0, len);
     }
+    ss_wave_fence();
+  } else if (MODE == 3) {  // the pipelined pops (vh_sort_heap_pipe)
+    if (len >= 2) {
+      vh_make_heap_wave(S, 0, len);
+      ss_wave_fence();
+      vh_sort_heap_pipe(S, 0, len);
+    }
+    ss_wave_fence();
+  } else {  // __make_heap alone
+    if (len >= 2) vh_make_heap_wave(S, 0, len);
     ss_wave_fence();
   }
   const unsigned long long t1 = __builtin_readcyclecounter();
@@ -114,26 +125,30 @@ int main() {
       uint32_t *din, *dout;
       unsigned long long* dc;
       hipMalloc(&din, h.size() * 4);
-      hipMalloc(&dout, h.size() * 4 * 3);
-      hipMalloc(&dc, 8 * 3);
+      hipMalloc(&dout, h.size() * 4 * 5);
+      hipMalloc(&dc, 8 * 5);
       hipMemcpy(din, h.data(), h.size() * 4, hipMemcpyHostToDevice);
-      hipMemset(dc, 0, 24);
+      hipMemset(dc, 0, 40);
       k_heap<0><<<blocks, 64 * waves>>>(din, dout, len, dc);
       k_heap<1><<<blocks, 64 * waves>>>(din, dout + h.size(), len, dc + 1);
       k_heap<2><<<blocks, 64 * waves>>>(din, dout + 2 * h.size(), len, dc + 2);
+      k_heap<3><<<blocks, 64 * waves>>>(din, dout + 3 * h.size(), len, dc + 3);
+      k_heap<4><<<blocks, 64 * waves>>>(din, dout + 4 * h.size(), len, dc + 4);
       if (hipDeviceSynchronize() != hipSuccess) {
         printf("kernel error\n");
         return 1;
       }
-      std::vector<uint32_t> o(h.size() * 3);
-      unsigned long long c[3];
+      std::vector<uint32_t> o(h.size() * 5);
+      unsigned long long c[5];
       hipMemcpy(o.data(), dout, o.size() * 4, hipMemcpyDeviceToHost);
-      hipMemcpy(c, dc, 24, hipMemcpyDeviceToHost);
+      hipMemcpy(c, dc, 40, hipMemcpyDeviceToHost);
       const bool ok = std::equal(o.begin(), o.begin() + h.size(), o.begin() + h.size()) &&
-                      std::equal(o.begin(), o.begin() + h.size(), o.begin() + 2 * h.size());
-      printf("waves/CU %2d len %5d: cycles/element one-lane %.0f wave %.0f variant %.0f  (%s)\n", waves, len,
+                      std::equal(o.begin(), o.begin() + h.size(), o.begin() + 2 * h.size()) &&
+                      std::equal(o.begin(), o.begin() + h.size(), o.begin() + 3 * h.size());
+      printf("waves/CU %2d len %5d: cycles/element one-lane %.0f wave %.0f variant %.0f pipelined %.0f"
+             " (make_heap alone %.0f)  (%s)\n", waves, len,
              (double)c[0] / segs / len, (double)c[1] / segs / len, (double)c[2] / segs / len,
-             ok ? "same permutation" : "DIFFERS");
+             (double)c[3] / segs / len, (double)c[4] / segs / len, ok ? "same permutation" : "DIFFERS");
       if (!ok) return 1;
       hipFree(din);
       hipFree(dout);

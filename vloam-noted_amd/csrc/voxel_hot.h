@@ -316,10 +316,109 @@ __device__ inline void vh_sort_heap_wave(uint32_t* E, int lo, int hi) {
   }
 }
 
+// compiler-only ordering of one wave's LDS accesses: the LDS executes a wave's instructions in
+// order, so a lane's read in the next round sees another lane's write of this one
+__device__ inline void vh_lds_order() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_wave_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// one round of every sifting pop (n != 0: its heap size, 0 once its sift ended) from the hole's
+// children a, b (c1 = 2 h + 1, loaded at min(c1, npops - 1)): the larger one (right unless
+// right < left) moves up while it is not less than v, else v is put and the sift ends
+__device__ inline void vh_pipe_move(uint32_t* Eb, int& h, int& n, uint32_t v, int c1, uint32_t a, uint32_t b) {
+  const bool right = c1 + 1 < n && (b >> 16) >= (a >> 16);
+  const uint32_t cv = right ? b : a;
+  const bool go = c1 < n && (cv >> 16) >= (v >> 16);
+  if (n != 0) Eb[h] = go ? cv : v;
+  h = go ? c1 + (right ? 1 : 0) : h;
+  n = go ? n : 0;
+}
+__device__ inline void vh_pipe_step(uint32_t* Eb, int npops, int& h, int& n, uint32_t v) {
+  const int c1 = 2 * h + 1;
+  const int ca = min(c1, npops - 1);
+  const uint32_t a = Eb[ca], b = Eb[ca + 1];
+  vh_pipe_move(Eb, h, n, v, c1, a, b);
+}
+
+// __sort_heap on the heap E[lo, hi), one wave, pops pipelined (tools/heap_pipe_model.py checks
+// the schedule against libstdc++'s sequential pops).  A __pop_heap (hole to a leaf along the
+// larger children, then __push_heap of the tail value v) is the same as a top-down sift of v: the
+// larger child moves up while it is not less than v.  Top-down, pops overlap: each in-flight pop
+// (one per lane, lanes 0..15 in pop order mod 16) advances one level per round (reads its hole's
+// children, writes its hole), so a pop at depth d reads depth d + 1 and writes depth d.  A new pop
+// starts when every unfinished older pop is at least two levels deep and none of them can still
+// end at the tail position L the new pop takes v from: one whose hole is an ancestor of L (or L)
+// ends there only by moving E[L] up, i.e. if E[L] is not less than its v.  A start is considered
+// every second round (the two-level spacing makes that the rate anyway): round A reads E[L], the
+// root and its children with the holes' children (one LDS latency), decides a start and moves;
+// round B moves.  A pop's output (its old root to its tail position) is written by its lane when
+// the slot starts its next pop, 2 S >= D + 1 rounds later, when every older pop has finished
+// (older pops may read that position as a child), or after the last rounds.  ~2.4 rounds per pop
+// and ~100 instructions per two rounds: the wave is issue-bound (a variant that precomputed both
+// next addresses to shorten the dependent chain issued more and ran slower).
+__device__ inline void vh_sort_heap_pipe(uint32_t* E, int lo, int hi) {
+  const int lane = threadIdx.x & 63;
+  const int len = hi - lo;
+  const int npops = len - 1;
+  if (npops < 1) return;
+  const int D = 31 - __clz(len);  // depth of the deepest node (<= 14: len <= VH_MAX_N)
+  constexpr int S = 16;
+  int h = 0, n = 0, L = -1;
+  uint32_t v = 0, top = 0;
+  uint32_t* const Eb = E + lo;
+  const int cr = min(1, npops - 1);  // the root's children, loaded at cr, cr + 1
+  int tail = 0;  // pops started (wave-uniform)
+  while (tail < npops) {
+    // ---- round A
+    const int Ln = npops - tail;
+    const uint32_t eln = Eb[Ln], e0 = Eb[0], r1 = Eb[cr], r2 = Eb[cr + 1];
+    int c1 = 2 * h + 1;
+    const int ca = min(c1, npops - 1);
+    uint32_t a = Eb[ca], b = Eb[ca + 1];
+    const int k = __clz(h + 1) - __clz(Ln + 1);  // depth of Ln minus the hole's
+    const bool blocks = n != 0 && (h < 3 || (k >= 0 && ((Ln + 1) >> k) == h + 1 && (eln >> 16) >= (v >> 16)));
+    const bool can = __ballot(blocks) == 0ull;
+    const bool start = can && lane == (tail & (S - 1));
+    tail += can ? 1 : 0;
+    if (start && L >= 0) Eb[L] = top;  // the slot's previous pop
+    if (start) {
+      v = eln;
+      top = e0;
+      h = 0;
+      n = Ln;
+      L = Ln;
+      c1 = 1;
+      a = r1;
+      b = r2;
+    }
+    vh_pipe_move(Eb, h, n, v, c1, a, b);
+    vh_lds_order();
+    // ---- round B
+    vh_pipe_step(Eb, npops, h, n, v);
+    vh_lds_order();
+  }
+  for (int r = 0; r < D + 1; ++r) {  // the last pops' sifts
+    vh_pipe_step(Eb, npops, h, n, v);
+    vh_lds_order();
+  }
+  if (lane < S && L >= 0) Eb[L] = top;
+  vh_lds_order();
+}
+
+// (tools/mb_heap.hip, one wave per CU: 1227 -> 958 cycles per element at 1024 elements, 1786 ->
+// 1148 with 16 waves per CU; below ~128 elements the look-ahead pops are as fast)
+constexpr int VH_PIPE_MIN = 192;
 __device__ inline void vh_heap_sort_wave(uint32_t* E, int lo, int hi) {
   if (hi - lo < 2) return;
   vh_make_heap_wave(E, lo, hi);
-  vh_sort_heap_wave(E, lo, hi);
+  if (hi - lo >= VH_PIPE_MIN) {
+    ss_wave_fence();
+    vh_sort_heap_pipe(E, lo, hi);
+  } else {
+    vh_sort_heap_wave(E, lo, hi);
+  }
 }
 
 // A depth-limit segment on one wave: heap-sorted literally when two members of one hot voxel lie
