@@ -1,16 +1,15 @@
-"""Model of the pipelined __sort_heap of voxel_hot.h (vh_sort_heap_pipe), checked on the CPU
-against libstdc++'s sequential __sort_heap (restated: __pop_heap = hole to a leaf along the larger
-children, right unless right < left, then __push_heap).
+"""Model of the pipelined __sort_heap of voxel_hot.h (vh_sort_heap_pipe), lane by lane, checked
+on the CPU against libstdc++'s sequential __sort_heap (restated: __pop_heap = hole to a leaf along
+the larger children, right unless right < left, then __push_heap).
 
 A pop of libstdc++'s __sort_heap is the same as a top-down sift of its value v from the root: the
 larger child moves up while it is not less than v (ties keep descending), and v lands at the first
 node whose larger child is less than it (or at a leaf).  Top-down, pops pipeline: every in-flight
-pop advances one level per round, a pop starts when every older one is at least two levels deep
-(a pop at depth d reads depth d + 1 and writes depth d), and when no older pop can still end at the
-tail position the new pop takes its v from (an older pop whose hole is an ancestor of it or the
-node itself).  A pop's output write (the old root to its tail position) waits until every older
-pop has finished (older pops may still read that position as a child): a pop takes at most D + 1
-rounds (D: the heap's depth), so the lane writes it in the pop's (D + 1)-th round.
+pop advances one level per round; a start is considered every second round (round A, then round
+B) and happens when every unfinished older pop is at least two levels deep (a pop at depth d reads
+depth d + 1 and writes depth d) and none can still end at the tail position L the new pop takes v
+from (hole an ancestor of L, or L, and E[L] not less than its v).  A pop's output (the old root to
+L) is written when its slot (16, round robin) starts its next pop, or after the last rounds.
 
     python tools/heap_pipe_model.py [trials]"""
 import random
@@ -89,62 +88,60 @@ def anc_or_eq(x, y):
 
 
 def pipe_sort_heap(E, S=16):
-    """the schedule of vh_sort_heap_pipe, lane by lane; returns (array, rounds, stall rounds)"""
+    """vh_sort_heap_pipe's schedule; returns (array, rounds)"""
     E = list(E)
-    len_ = len(E)
-    npops = len_ - 1
-    D = len_.bit_length() - 1
-    lanes = [dict(act=False, done=True, h=0, dep=0, n=0, L=0, age=0, v=0, top=0) for _ in range(S)]
-    tail = rounds = stalls = 0
-    while True:
-        start = -1
-        if tail < npops:
-            Ln = npops - tail
-            blk = any(p["act"] and not p["done"] and (p["dep"] < 2 or anc_or_eq(p["h"], Ln)) for p in lanes)
-            busy = lanes[tail % S]["act"]
-            if not blk and not busy:
-                start = tail % S
-                lanes[start].update(act=True, done=False, h=0, dep=0, n=Ln, L=Ln, age=0)
-                tail += 1
-            else:
-                stalls += 1
-        elif not any(p["act"] for p in lanes):
-            break
-        rounds += 1
+    npops = len(E) - 1
+    if npops < 1:
+        return E, 0
+    D = len(E).bit_length() - 1
+    lanes = [dict(h=0, n=0, L=-1, v=0, top=0) for _ in range(S)]
+    tail = rounds = 0
+
+    def step():
         reads = []
-        for i, p in enumerate(lanes):  # reads of the round
-            st = p["act"] and not p["done"]
+        for p in lanes:
             c1 = 2 * p["h"] + 1
-            a = E[c1] if st and c1 < p["n"] else 0
-            b = E[c1 + 1] if st and c1 + 1 < p["n"] else 0
-            if i == start:
-                p["v"], p["top"] = E[p["L"]], E[0]
-            reads.append((st, c1, a, b))
-        for p, (st, c1, a, b) in zip(lanes, reads):  # writes
-            if not st:
-                continue
-            h1, h2 = c1 < p["n"], c1 + 1 < p["n"]
-            right = h2 and not key(b) < key(a)
+            ca = min(c1, npops - 1)
+            reads.append((c1, E[ca], E[ca + 1]))
+        for p, (c1, a, b) in zip(lanes, reads):
+            n = p["n"]
+            right = c1 + 1 < n and key(b) >= key(a)
             cv = b if right else a
-            go = h1 and not key(cv) < key(p["v"])
-            E[p["h"]] = cv if go else p["v"]
+            go = c1 < n and key(cv) >= key(p["v"])
+            if n != 0:
+                E[p["h"]] = cv if go else p["v"]
             if go:
-                p["h"], p["dep"] = c1 + (1 if right else 0), p["dep"] + 1
+                p["h"] = c1 + (1 if right else 0)
             else:
-                p["done"] = True
-        for p in lanes:  # outputs
-            if p["act"]:
-                p["age"] += 1
-                if p["age"] == D + 1:
-                    E[p["L"]] = p["top"]
-                    p["act"] = False
-    return E, rounds, stalls
+                p["n"] = 0
+
+    while tail < npops:
+        Ln = npops - tail
+        eln = E[Ln]
+        blk = any(p["n"] != 0 and (p["h"] < 3 or (anc_or_eq(p["h"], Ln) and key(eln) >= key(p["v"])))
+                  for p in lanes)
+        if not blk:
+            p = lanes[tail % S]
+            if p["L"] >= 0:
+                E[p["L"]] = p["top"]
+            p.update(v=E[Ln], top=E[0], h=0, n=Ln, L=Ln)
+            tail += 1
+        step()  # round A (the new pop moves in it too)
+        step()  # round B
+        rounds += 2
+    for _ in range(D + 1):
+        step()
+        rounds += 1
+    for p in lanes:
+        if p["L"] >= 0:
+            E[p["L"]] = p["top"]
+    return E, rounds
 
 
 def main():
     trials = int(sys.argv[1]) if len(sys.argv) > 1 else 300
     rnd = random.Random(5)
-    tot_pops = tot_rounds = tot_stalls = 0
+    tot_pops = tot_rounds = 0
     for t in range(trials):
         n = rnd.choice([2, 3, 4, 5, 17, 64, 100, 395, 512, 928, 1024, 1500])
         nk = rnd.choice([1, 2, 3, 8, max(1, n // 10), n])
@@ -152,13 +149,11 @@ def main():
         E = [(k << 16) | i for i, k in enumerate(keys)]
         H = make_heap(E)
         want = seq_sort_heap(H)
-        got, rounds, stalls = pipe_sort_heap(H)
+        got, rounds = pipe_sort_heap(H)
         assert got == want, (t, n, nk)
         tot_pops += n - 1
         tot_rounds += rounds
-        tot_stalls += stalls
-    print(f"{trials} heaps: pipelined order == libstdc++ __sort_heap; {tot_rounds / tot_pops:.2f} rounds per pop, "
-          f"{tot_stalls / tot_pops:.3f} stall rounds per pop")
+    print(f"{trials} heaps: pipelined order == libstdc++ __sort_heap; {tot_rounds / tot_pops:.2f} rounds per pop")
 
 
 if __name__ == "__main__":
