@@ -827,9 +827,10 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
       }
       if (lane == 0 && __builtin_amdgcn_readfirstlane(sstat) != -1) {
         const unsigned long long ts = J.prof ? __builtin_readcyclecounter() : 0ull;
-        LmState L = ls;  // registers for the dependent chain
-        lm_step(L, sred);
-        ls = L;
+        // the step works on the LDS state in place: a register copy of the whole state (~140
+        // VGPRs) spilled into AGPRs beside the solve's temporaries (tools/mb_lmstep2.hip: 5.7k ->
+        // 4.8k cycles per step)
+        lm_step(ls, sred);
         if (J.prof) atomicAdd(&J.prof[-2], __builtin_readcyclecounter() - ts);  // [15]: the step alone
       }
     }
