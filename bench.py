@@ -1048,6 +1048,14 @@ def main():
                 continue
             e = {"gpu_ms_per_frame": round(float(g.mean()), 4), "gpu_frames": int(len(g)),
                  "gpu_frames_per_s": round(1e3 / float(g.mean()), 1)}
+            ga = np.array(stage_ms[name][10:], dtype=np.float64)
+            if cpu_st is not None and len(ga):
+                # the frames above are the cpu_baseline's (a 20-frame sample); every frame after
+                # the first 10 of the sequence, for the distribution (per-frame time varies with
+                # the scene: the nearest ring's sort for scan registration)
+                e["gpu_all_frames"] = {"ms_per_frame": round(float(ga.mean()), 4), "frames": int(len(ga)),
+                                       "median_ms": round(float(np.median(ga)), 4),
+                                       "p90_ms": round(float(np.percentile(ga, 90)), 4)}
             # the stage against the HBM roofline: its algorithmic bytes per frame / its device time
             # per frame (every kernel of the stage, one stream: latency bound)
             bpf = float(np.mean(stage_ms[name + "_bytes"][sl]))

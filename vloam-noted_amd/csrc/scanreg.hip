@@ -891,10 +891,9 @@ __device__ inline void sr_ringvox(const SrDev& D, int r, int n, uint32_t* lds) {
 
 // A ring's selection and then its lessFlat VoxelGrid in one workgroup: the ring's VoxelGrid
 // starts when its own picks are done, not when the slowest ring's are, and both phases share
-// the 160 KiB.  (A separate function holding the LDS: the ROCm 7.2 compiler crashes in
-// InstCombine when the filter is inlined into the kernel; declared here, the array keeps its LDS
-// address space.)
-__device__ __noinline__ void sr_ring_features(const SrDev* __restrict__ Ds) {
+// the 160 KiB.  Inlined into the kernel (as a called function its frame spilled 464 B per lane
+// to scratch; 84 inlined).
+__device__ __attribute__((always_inline)) inline void sr_ring_features(const SrDev* __restrict__ Ds) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[VX_LDS_WORDS];
   const SrDev D = Ds[blockIdx.y];
   const int r = blockIdx.x;

@@ -1149,7 +1149,7 @@ __device__ inline bool vh_centroids(const PF& P, float4* out, const VxHot& H, co
 // wave subtrees, positions).  Returns the elements heap-sorted at the depth limit (0 without a
 // hot voxel; diagnostics).
 template <int NT, typename PF>
-__device__ inline int vh_fixup(const PF& P, int n, float4* out, const VxHot& H, uint32_t* lds, uint32_t lds_words,
+__device__ __attribute__((always_inline)) inline int vh_fixup(const PF& P, int n, float4* out, const VxHot& H, uint32_t* lds, uint32_t lds_words,
                                 VxMisc& M, uint32_t* stable_out, int* err, unsigned long long* prof = nullptr,
                                 unsigned long long* sprof = nullptr, unsigned long long* dprof = nullptr) {
   __syncthreads();
