@@ -634,7 +634,7 @@ def pipelined_chain(scans, device, n_frames, timed):
 
 def _pmc_file():
     """the newest committed PMC traffic summary (tools/pmc_traffic.py -> profiles/rN_pmc_traffic.json)"""
-    for r in (4, 3, 2):
+    for r in (5, 4, 3, 2):
         path = os.path.join(ROOT, "profiles", f"r{r}_pmc_traffic.json")
         if os.path.exists(path):
             return path
