@@ -633,3 +633,42 @@ def test_async_capacity_error_is_held_for_wait(seq):
     # every frame ran exactly once: the final pose is the blocking solve's
     assert pose(m) == want[-1]
     m.close()
+
+
+def test_exact_refilter_of_a_cube_over_lds(seq):
+    """PCL's order for a window cube of more than VH_MAX_N (30720) points: set through the API it
+    is not a VoxelGrid fixed point, so the reference re-filters it (laser_mapping.cpp:795-808) and
+    the exact mode sorts it in global memory (k_revox_big, its own kernel).  The same frame through
+    the oracle from the same state: equal poses within the solve tolerance, equal maps."""
+    import loam_oracle as O
+    from helpers import snapshot
+    rec = seq[SNAP[0]]
+    before = dict(rec["before"])
+    surf = dict(before["surf"])
+    cube = max(surf, key=lambda c: len(surf[c]))
+    pts = surf[cube]
+    lo, hi = pts[:, :3].min(0), pts[:, :3].max(0)
+    rng = np.random.default_rng(3)
+    n = 36000  # > VH_MAX_N with the cube's own points; 5 cm quantization: many voxels of 3+ members
+    extra = np.round(rng.uniform(lo, hi, (n, 3)) * 20) / 20
+    surf[cube] = np.concatenate([pts, np.c_[extra, rng.uniform(0, 64, n)].astype(np.float32)])
+    before["surf"] = surf
+    assert len(surf[cube]) > 30720
+    ref = O.LaserMapping()
+    ref.set_state(before["cen"], before["q"], before["t"])
+    for which, key in ((0, "corner"), (1, "surf")):
+        for c, p in before[key].items():
+            ref.set_cube(which, c, p)
+    ref.input(rec["corner"], rec["surf"], None, rec["q_wodom"], rec["t_wodom"])
+    ref.solve()
+    after = snapshot(ref)
+    m = BatchMapper(1, exact_voxel_order=1, max_submap_points=400000)
+    load_state(m, 0, before)
+    m.input(0, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+    m.solve()
+    q, t = m.pose(0)
+    qr, tr = ref.pose()
+    assert np.linalg.norm(t - tr) < 1e-4 and quat_angle(q, qr) < 1e-4
+    _check_map(m, 0, after)
+    assert len(after["surf"][cube]) < len(surf[cube])  # the re-filter merged the duplicates
+    m.close()
