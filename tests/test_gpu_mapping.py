@@ -153,7 +153,7 @@ def test_many_streams_exact_order(seq):
 
 
 @pytest.mark.parametrize("exact", [1, 0])
-@pytest.mark.parametrize("n_corner,n_surf", [(3000, 9000), (20000, 70000)])
+@pytest.mark.parametrize("n_corner,n_surf", [(3000, 9000), (20000, 70000), (6000, 36000)])
 def test_stack_voxelgrid_bit_exact(n_corner, n_surf, exact):
     """CornerStack / SurfStack (laser_mapping.cpp:492-500) bit for bit against the oracle
     VoxelGrid: exact_voxel_order = 1 in PCL's order; 0 in input order (single-pass and grouped,
@@ -635,11 +635,13 @@ def test_async_capacity_error_is_held_for_wait(seq):
     m.close()
 
 
-def test_exact_refilter_of_a_cube_over_lds(seq):
+@pytest.mark.parametrize("target", [35000, 46000])
+def test_exact_refilter_of_a_cube_over_lds(seq, target):
     """PCL's order for a window cube of more than VH_MAX_N (30720) points: set through the API it
-    is not a VoxelGrid fixed point, so the reference re-filters it (laser_mapping.cpp:795-808) and
-    the exact mode sorts it in global memory (k_revox_big, its own kernel).  The same frame through
-    the oracle from the same state: equal poses within the solve tolerance, equal maps."""
+    is not a VoxelGrid fixed point, so the reference re-filters it (laser_mapping.cpp:795-808).  Up
+    to VH_BIG_N (40000) the first partition runs in global memory and the parts in LDS
+    (voxel_hot.h vh_sort_big); above it the whole sort runs in global memory.  The same frame
+    through the oracle from the same state: equal poses within the solve tolerance, equal maps."""
     import loam_oracle as O
     from helpers import snapshot
     rec = seq[SNAP[0]]
@@ -649,7 +651,7 @@ def test_exact_refilter_of_a_cube_over_lds(seq):
     pts = surf[cube]
     lo, hi = pts[:, :3].min(0), pts[:, :3].max(0)
     rng = np.random.default_rng(3)
-    n = 36000  # > VH_MAX_N with the cube's own points; 5 cm quantization: many voxels of 3+ members
+    n = target - len(pts)  # the cube's points in all; 5 cm quantization: many voxels of 3+ members
     extra = np.round(rng.uniform(lo, hi, (n, 3)) * 20) / 20
     surf[cube] = np.concatenate([pts, np.c_[extra, rng.uniform(0, 64, n)].astype(np.float32)])
     before["surf"] = surf

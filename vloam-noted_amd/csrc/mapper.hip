@@ -342,6 +342,7 @@ __device__ inline VxHot map_hot(const MapperDev& D, size_t sm, uint32_t so, uint
   H.hl = reinterpret_cast<uint32_t*>(D.pe + b);
   H.hv = H.hl + n;
   H.cap_h = n / 3 + 1;
+  H.w = D.ps + b;  // (sorts of VH_MAX_N .. VH_BIG_N points: vh_sort_big)
   return H;
 }
 
@@ -357,14 +358,10 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
   if (!I.active) return;
   const size_t sm = sm_index(s, m);
   int* err = &D.stk_err[s];
-  if (PCL && I.n[m] > VH_MAX_N) {  // PCL's order, the sort in global memory
-    VxPclOut O;
-    O.out = D.stack[m] + (size_t)s * D.max_in;
-    O.cap = D.max_in;
-    O.res_cnt = reinterpret_cast<uint32_t*>(&D.stk_n[2 * s + m]);
-    map_voxel_pcl(D, sm, mp_stack_offset(D), VxPtrSrc{I.p[m]}, I.n[m], D.leaf[m], O, lds, err);
-    return;
-  }
+  // PCL's order above VH_BIG_N points (or when vh_fixup cannot split the sort for the LDS): the
+  // whole sort in global memory
+  bool global = PCL && I.n[m] > VH_BIG_N;
+  if (!global) {
   VoxSeg S;
   S.src1 = nullptr;
   S.tag1 = nullptr;
@@ -388,9 +385,19 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_ds(MapperDev D) {
   if (PCL) S.hot = map_hot(D, sm, mp_stack_offset(D), (uint32_t)I.n[m]);
   voxel_segment(S, lds);
   if (PCL) {  // PCL's summation order for the voxels of 3+ members (voxel_hot.h)
-    vh_fixup<VX_THREADS>(VxSrc{I.p[m], I.n[m], nullptr}, I.n[m], S.out, S.hot, lds, VX_LDS_WORDS - 256,
-                         *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192), nullptr, err, D.pdbg ? D.pdbg + 54 : nullptr,
-                         D.pdbg ? D.pdbg + 77 : nullptr);
+    const int he = vh_fixup<VX_THREADS>(VxSrc{I.p[m], I.n[m], nullptr}, I.n[m], S.out, S.hot, lds, VX_LDS_WORDS - 256,
+                                        *reinterpret_cast<VxMisc*>(lds + VX_LDS_WORDS - 192), nullptr, err,
+                                        D.pdbg ? D.pdbg + 54 : nullptr, D.pdbg ? D.pdbg + 77 : nullptr);
+    global = he < 0;  // (over VH_MAX_N: the first partition left a part too large for the LDS)
+    __syncthreads();
+  }
+  }
+  if (PCL && global) {
+    VxPclOut O;
+    O.out = D.stack[m] + (size_t)s * D.max_in;
+    O.cap = D.max_in;
+    O.res_cnt = reinterpret_cast<uint32_t*>(&D.stk_n[2 * s + m]);
+    map_voxel_pcl(D, sm, mp_stack_offset(D), VxPtrSrc{I.p[m]}, I.n[m], D.leaf[m], O, lds, err);
   }
 }
 
@@ -1564,7 +1571,8 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
     __syncthreads();
     const uint32_t so = *sb;
     __syncthreads();
-    if (n <= (uint32_t)VH_MAX_N) {
+    bool global = n > (uint32_t)VH_BIG_N;
+    if (!global) {
       // the input-order filter sums every voxel of at most 2 members (order-free) and records the
       // others, then voxel_hot.h sums those in std::sort's order
       if ((size_t)so + n + MP_SLACK > mp_cube_scratch(D)) {
@@ -1577,11 +1585,16 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
         }
         if (!merged) voxel_segment(S, lds);
         const VxSrc P{ar + cv.x, (int)cv.y, D.ins_sorted + sm_index(s, m) * D.max_in + i0};
-        vh_fixup<VX_THREADS>(P, (int)n, ar, S.hot, lds, LW - 256, *reinterpret_cast<VxMisc*>(lds + LW - 192), tok,
-                             &F.err, D.pdbg ? D.pdbg + 50 : nullptr, D.pdbg ? D.pdbg + 72 : nullptr,
-                             D.pdbg ? D.pdbg + 82 : nullptr);
+        const int he = vh_fixup<VX_THREADS>(P, (int)n, ar, S.hot, lds, LW - 256, *reinterpret_cast<VxMisc*>(lds + LW - 192),
+                                            tok, &F.err, D.pdbg ? D.pdbg + 50 : nullptr,
+                                            D.pdbg ? D.pdbg + 72 : nullptr, D.pdbg ? D.pdbg + 82 : nullptr);
+        // (over VH_MAX_N, a part too large for the LDS after the first partition: the global
+        // sort below writes the cube again, at a new arena offset)
+        global = he < 0;
+        __syncthreads();
       }
-    } else {  // the whole std::sort emulated in global memory (voxel_pcl.h)
+    }
+    if (global) {  // the whole std::sort emulated in global memory (voxel_pcl.h)
       VxPclOut O;
       O.out = ar;
       O.tail = &F.arena_tail[m];

@@ -42,6 +42,7 @@ struct VxHot {
   uint32_t* hv;    // [3 * cap_h] per hot voxel: output slot, list start, member count
   uint32_t* fpos;  // [n] per hot point: its position after the emulated sort (voxel_hot.h)
   uint32_t cap_h;
+  uint64_t* w = nullptr;  // [n] optional: scratch of the sorts over VH_MAX_N points (voxel_hot.h vh_sort_big)
 };
 
 struct VoxSeg {

@@ -914,9 +914,13 @@ __device__ inline void vh_depth_limit_wg(const VhLds& L, int n, int lo, int hi) 
 // H.fpos[i] for every hot point i.  *err |= VH_ERR_ROOTS on a list overflow (cannot happen).
 // prof (optional, diagnostics): [0] elements heap-sorted literally; [1..4] cycles of the setup, the
 // workgroup partitions (and depth-limit segments), the wave subtrees, the positions
+// part (vh_sort_big): the n elements are a part of a larger sort, W[0 .. n) (slot << 32 | hot << 31 |
+// point), whose depth budget is d0 and whose first position is pos0 (the point ids in E are then
+// local: k, with W[k] holding the point)
 template <int NT>
 __device__ inline int vh_sort(uint32_t* lds, int n, const VxHot& H, int* err, unsigned long long* prof = nullptr,
-                               unsigned long long* dprof = nullptr) {
+                               unsigned long long* dprof = nullptr, const uint64_t* part = nullptr, int d0 = -1,
+                               uint32_t pos0 = 0) {
   const int tid = threadIdx.x;
   unsigned long long tp = __builtin_readcyclecounter(), t_drain = 0;
   const VhLds L = vh_layout<NT>(lds, n);
@@ -924,7 +928,15 @@ __device__ inline int vh_sort(uint32_t* lds, int n, const VxHot& H, int* err, un
   for (int i0 = tid; i0 < n; i0 += 8 * NT) {  // 8 loads in flight per thread
     uint32_t r[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) r[u] = i0 + u * NT < n ? H.rk[i0 + u * NT] : 0u;
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * NT;
+      if (part) {
+        const uint64_t w = i < n ? part[i] : 0ull;
+        r[u] = ((uint32_t)(w >> 32) << 1) | (uint32_t)((w >> 31) & 1ull);
+      } else {
+        r[u] = i < n ? H.rk[i] : 0u;
+      }
+    }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int i = i0 + u * NT;
@@ -933,7 +945,7 @@ __device__ inline int vh_sort(uint32_t* lds, int n, const VxHot& H, int* err, un
   }
   for (int i = tid; i < VH_ROOTS; i += NT) L.roots[i] = 0u;
   __syncthreads();  // (the entries are zero until listed: tid 0 lists below)
-  const int D0 = n > 1 ? 2 * (31 - __clz(n)) : 0;  // 2 * __lg(n)
+  const int D0 = d0 >= 0 ? d0 : n > 1 ? 2 * (31 - __clz(n)) : 0;  // 2 * __lg(n)
   if (tid == 0) {
     C->nbig[0] = C->nbig[1] = 0;
     C->nroot = C->root_take = 0;
@@ -1009,15 +1021,89 @@ __device__ inline int vh_sort(uint32_t* lds, int n, const VxHot& H, int* err, un
   if (tid == 0 && prof) atomicAdd(prof, (unsigned long long)heap_el);
   for (int q = tid; q < n; q += NT) {
     const uint32_t e = L.E[q];
-    if (e & VH_HOT) H.fpos[e & 0x7FFFu] = (uint32_t)q;
+    if (e & VH_HOT) {
+      const uint32_t k = e & 0x7FFFu;
+      H.fpos[part ? (uint32_t)part[k] & 0x7FFFFFFFu : k] = pos0 + (uint32_t)q;
+    }
   }
   __syncthreads();
   vx_phase(prof ? prof + 4 : nullptr, 0, &tp);
   return heap_el;
 }
 
+// Sorts of more than VH_MAX_N points (up to VH_BIG_N; the LDS holds only VH_MAX_N): libstdc++'s
+// first partition of the whole array runs in global memory (H.w: slot << 32 | hot << 31 | point),
+// exactly: __move_median_to_first(first, first + 1, mid, last - 1), then __unguarded_partition with
+// the k-th left stop (key not below the pivot, ascending) swapped with the k-th right stop (not
+// above, descending) while l_k < r_k, cut = min(l_{S+1}, r_S) (the rank form of the scanning
+// loop); each part then runs the LDS emulation with depth budget 2 lg n - 1 (vh_fixup).  Stop
+// positions: H.rk (consumed when W is built) and H.fpos (written only after the partition).
+// Returns the cut, or -1 when a part is still over VH_MAX_N (the caller then sorts in global
+// memory).  All NT threads.
+constexpr int VH_BIG_N = 40000;  // hot member lists of vh_centroids fit the LDS (n + 64 words)
+template <int NT>
+__device__ inline int vh_big_partition(uint32_t* ws, int n, const VxHot& H) {
+  const int tid = threadIdx.x;
+  uint64_t* W = H.w;
+  uint32_t* Lp = H.rk;
+  uint32_t* Rp = H.fpos;
+  for (int i = tid; i < n; i += NT) {
+    const uint32_t r = H.rk[i];
+    W[i] = ((uint64_t)(r >> 1) << 32) | ((uint64_t)(r & 1u) << 31) | (uint64_t)i;
+  }
+  __syncthreads();
+  if (tid == 0) {  // the median of positions 1, n / 2, n - 1 to position 0
+    const int a = 1, b = n / 2, c = n - 1;
+    const uint64_t wa = W[a], wb = W[b], wc = W[c];
+    const uint32_t ka = (uint32_t)(wa >> 32), kb = (uint32_t)(wb >> 32), kc = (uint32_t)(wc >> 32);
+    int m;
+    if (ka < kb) m = kb < kc ? b : (ka < kc ? c : a);
+    else m = ka < kc ? a : (kb < kc ? c : b);
+    const uint64_t w0 = W[0], wm = m == a ? wa : (m == b ? wb : wc);
+    W[0] = wm;
+    W[m] = w0;
+  }
+  __syncthreads();
+  const uint32_t p = (uint32_t)(W[0] >> 32);
+  // stops of positions 1 .. n - 1: thread t owns [1 + t C, 1 + (t + 1) C)
+  const int C = (n - 1 + NT - 1) / NT;
+  const int b0 = 1 + tid * C, b1 = min(n, b0 + C);
+  uint32_t cl = 0, cr = 0;
+  for (int i = b0; i < b1; ++i) {
+    const uint32_t k = (uint32_t)(W[i] >> 32);
+    cl += k < p ? 0u : 1u;
+    cr += p < k ? 0u : 1u;
+  }
+  uint32_t totl, totr;
+  const uint32_t pl = vx_block_scan_t<NT>(cl, ws, &totl);
+  const uint32_t pr = vx_block_scan_t<NT>(cr, ws, &totr);
+  {
+    uint32_t jl = pl, jr = totr - pr;  // (descending rank of the chunk's last right stop) + 1
+    for (int i = b0; i < b1; ++i) {
+      const uint32_t k = (uint32_t)(W[i] >> 32);
+      if (!(k < p)) Lp[jl++] = (uint32_t)i;
+      if (!(p < k)) Rp[--jr] = (uint32_t)i;
+    }
+  }
+  __syncthreads();
+  uint32_t sc = 0;  // pairs l_k < r_k (a prefix of k)
+  const uint32_t kmax = min(totl, totr);
+  for (uint32_t k = tid; k < kmax; k += NT) sc += Lp[k] < Rp[k] ? 1u : 0u;
+  uint32_t S;
+  (void)vx_block_scan_t<NT>(sc, ws, &S);
+  for (uint32_t k = tid; k < S; k += NT) {
+    const uint32_t a = Lp[k], b = Rp[k];
+    const uint64_t wa = W[a], wb = W[b];
+    W[a] = wb;
+    W[b] = wa;
+  }
+  const int cut = (int)min(S < totl ? Lp[S] : (uint32_t)n, S >= 1 ? Rp[S - 1] : (uint32_t)n);
+  __syncthreads();
+  return (cut > VH_MAX_N || n - cut > VH_MAX_N) ? -1 : cut;
+}
+
 // Phase 3: every hot voxel's centroid from its members in position order -> out[slot].  The
-// members' (position << 15 | point) go to LDS (lds[0 .. list length)), each voxel's run is
+// members' (position << 16 | point) go to LDS (lds[0 .. list length)), each voxel's run is
 // sorted (one thread up to VH_SMALL members, else one wave by rank), then summed in that order
 // from 0 in float (PCL's CentroidPoint), divided by (float)count.  Returns whether some centroid
 // left its voxel (then the filter's output is not a VoxelGrid fixed point).  All NT threads;
@@ -1029,7 +1115,7 @@ __device__ inline bool vh_centroids(const PF& P, float4* out, const VxHot& H, co
   const uint32_t nh = min(M.hot_n, H.cap_h), nl = M.hot_l;
   uint32_t* Lh = lds;
   uint32_t* big = lds + nl;  // the voxels left to the waves
-  if (nl + 64 > lds_words) {  // cannot happen: nl <= n <= VH_MAX_N
+  if (nl + 64 > lds_words) {  // cannot happen: nl <= n <= VH_BIG_N
     if (tid == 0) atomicOr(err, VH_ERR_LIST);
     return true;
   }
@@ -1042,7 +1128,7 @@ __device__ inline bool vh_centroids(const PF& P, float4* out, const VxHot& H, co
     for (int u = 0; u < 8; ++u) fp[u] = j0 + u * NT < nl ? H.fpos[ii[u]] : 0u;
 #pragma unroll
     for (int u = 0; u < 8; ++u)
-      if (j0 + u * NT < nl) Lh[j0 + u * NT] = (fp[u] << 15) | ii[u];
+      if (j0 + u * NT < nl) Lh[j0 + u * NT] = (fp[u] << 16) | ii[u];
   }
   if (tid == 0) {
     M.nbig = 0;
@@ -1077,14 +1163,14 @@ __device__ inline bool vh_centroids(const PF& P, float4* out, const VxHot& H, co
       float4 pp[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (a + u < cnt) pp[u] = P(Lh[st + a + u] & 0x7FFFu);
+        if (a + u < cnt) pp[u] = P(Lh[st + a + u] & 0xFFFFu);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (a + u < cnt) {
           sx += pp[u].x; sy += pp[u].y; sz += pp[u].z; si += pp[u].w;
         }
     }
-    finish(slot, sx, sy, sz, si, cnt, Lh[st] & 0x7FFFu);
+    finish(slot, sx, sy, sz, si, cnt, Lh[st] & 0xFFFFu);
   }
   __syncthreads();
   const uint32_t nbig = min(M.nbig, big_cap);
@@ -1124,7 +1210,7 @@ __device__ inline bool vh_centroids(const PF& P, float4* out, const VxHot& H, co
     float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;  // every lane keeps the same running sum
     for (uint32_t a = 0; a < cnt; a += 64) {
       float4 pp = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (a + lane < cnt) pp = P(Lh[st + a + lane] & 0x7FFFu);
+      if (a + lane < cnt) pp = P(Lh[st + a + lane] & 0xFFFFu);
       const uint32_t mm = min(64u, cnt - a);
       for (uint32_t l = 0; l < mm; ++l) {
         sx += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pp.x), (int)l));
@@ -1133,7 +1219,7 @@ __device__ inline bool vh_centroids(const PF& P, float4* out, const VxHot& H, co
         si += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pp.w), (int)l));
       }
     }
-    if (lane == 0) finish(slot, sx, sy, sz, si, cnt, Lh[st] & 0x7FFFu);
+    if (lane == 0) finish(slot, sx, sy, sz, si, cnt, Lh[st] & 0xFFFFu);
   }
   if (moved) M.moved = 1;
   __syncthreads();
@@ -1147,7 +1233,8 @@ __device__ inline bool vh_centroids(const PF& P, float4* out, const VxHot& H, co
 // prof (optional, diagnostics): [0] cycles of the emulated sort, [1] of the hot centroids, [2]
 // filters with a hot voxel; sprof: vh_sort's (literal heap elements, setup, workgroup levels,
 // wave subtrees, positions).  Returns the elements heap-sorted at the depth limit (0 without a
-// hot voxel; diagnostics).
+// hot voxel; diagnostics), or -1 when n > VH_MAX_N and the first partition left a part over
+// VH_MAX_N (vh_sort_big: nothing written; the caller sorts in global memory).
 template <int NT, typename PF>
 __device__ __attribute__((always_inline)) inline int vh_fixup(const PF& P, int n, float4* out, const VxHot& H, uint32_t* lds, uint32_t lds_words,
                                 VxMisc& M, uint32_t* stable_out, int* err, unsigned long long* prof = nullptr,
@@ -1157,7 +1244,37 @@ __device__ __attribute__((always_inline)) inline int vh_fixup(const PF& P, int n
   const VxGeom g = M.g;
   float4* o = out + M.sbase[1];
   const unsigned long long t0 = __builtin_readcyclecounter();
-  const int heap_el = vh_sort<NT>(lds, n, H, err, sprof, dprof);
+  int heap_el = 0;
+  // the whole sort, or (more than VH_MAX_N points: callers pass at most VH_BIG_N, with H.w) the two
+  // parts of its first partition; one call site of vh_sort (inlined)
+  int nparts = 1, cut = n, d0 = -1;
+  const uint64_t* W = nullptr;
+  if (n > VH_MAX_N) {
+    cut = vh_big_partition<NT>(lds, n, H);
+    if (cut < 0) return -1;
+    nparts = 2;
+    W = H.w;
+    d0 = 2 * (31 - __clz(n)) - 1;
+  }
+  for (int q = 0; q < nparts; ++q) {
+    const int lo = q ? cut : 0, len = q ? n - cut : cut;
+    bool run = true;
+    if (W) {  // a part of at most 16 elements, or with fewer than two hot ones, keeps its positions
+      uint32_t nh = 0;
+      for (int i = threadIdx.x; i < len; i += NT) nh += (uint32_t)(W[lo + i] >> 31) & 1u;
+      uint32_t tot;
+      (void)vx_block_scan_t<NT>(nh, lds, &tot);
+      run = len > SS_THRESHOLD && tot >= 2;
+      if (!run) {
+        for (int i = threadIdx.x; i < len; i += NT) {
+          const uint64_t w = W[lo + i];
+          if ((w >> 31) & 1ull) H.fpos[(uint32_t)w & 0x7FFFFFFFu] = (uint32_t)(lo + i);
+        }
+        __syncthreads();
+      }
+    }
+    if (run) heap_el += vh_sort<NT>(lds, len, H, err, sprof, dprof, W ? W + lo : nullptr, d0, (uint32_t)lo);
+  }
   const unsigned long long t1 = __builtin_readcyclecounter();
   const bool mv = vh_centroids<NT>(P, o, H, g, lds, lds_words, M, err);
   if (mv && threadIdx.x == 0 && stable_out) *stable_out = 0u;
