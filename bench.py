@@ -751,6 +751,8 @@ def main():
             if not args.no_prof:
                 m.set_profiling(True)
             m.reset_kernel_times()
+            if os.environ.get("BENCH_DEBUG_COUNTERS"):
+                m.debug_counters(reset=True)  # the timed steps only
         barrier()
         t0 = time.perf_counter()
         if args.pipelined and H == 1:

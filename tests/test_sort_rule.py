@@ -35,7 +35,8 @@ def _adjust(E, first, hole, length, value):
     E[first + hole] = value
 
 
-def _heap_sort(E, lo, hi):
+def _heap_sort(E, lo, hi, pops=None):
+    """__make_heap + __sort_heap on E[lo, hi); pops: only the first that many pops"""
     n = hi - lo
     if n >= 2:
         parent = (n - 2) // 2
@@ -45,7 +46,8 @@ def _heap_sort(E, lo, hi):
                 break
             parent -= 1
     last = hi
-    while last - lo > 1:
+    end = lo + 1 if pops is None else max(lo + 1, hi - pops)
+    while last > end:
         last -= 1
         v = E[last]
         E[last] = E[lo]
@@ -169,7 +171,9 @@ def test_depth_limit_rule_keeps_pcl_centroids(n_old, n_single, n_pair):
 # final segment.  So the device
 #   * does not partition a segment holding fewer than two hot elements (no hot voxel can have two
 #     members inside it, so nothing below it can reorder a hot voxel);
-#   * heap-sorts a depth-limit segment literally only when two members of one hot voxel lie in it;
+#   * heap-sorts a depth-limit segment literally only when two members of one hot voxel lie in it,
+#     and stops once every element with a key not less than the smallest shared hot key is popped
+#     (voxel_hot.h vh_pops_needed: pops go in descending key order, what is left is never read);
 #   * skips the final insertion sort, and sums each hot voxel in its members' position order.
 # The restatement below does that and must give std::sort's centroids bit for bit.
 # ---------------------------------------------------------------------------------------------
@@ -216,8 +220,11 @@ def _hot_pruned_positions(pairs, hot):
             continue
         if d == 0:
             if len(set(hk)) < len(hk):
-                _heap_sort(E, lo, hi)
+                kmin = min(k for k in set(hk) if hk.count(k) > 1)
+                pops = sum(1 for k, _ in E[lo:hi] if k >= kmin)
+                _heap_sort(E, lo, hi, pops)
                 stats["heap"] += 1
+                stats["pops_saved"] = stats.get("pops_saved", 0) + (hi - lo - 1) - min(pops, hi - lo - 1)
             else:
                 stats["heap_skipped"] += 1
             continue

@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(1024) k_heap(const uint32_t* in, uint32_t* out
     if (lane == 0) ss_heap_sort(S, 0, len, VhLess{});
     ss_wave_fence();
   } else if (MODE == 1) {
-    vh_heap_sort_wave(S, 0, len);
+    vh_heap_sort_wave(S, 0, len, len);
     ss_wave_fence();
   } else if (MODE == 2) {
     if (len >= 2) {
@@ -100,7 +100,7 @@ __global__ void __launch_bounds__(1024) k_heap(const uint32_t* in, uint32_t* out
     if (len >= 2) {
       vh_make_heap_wave(S, 0, len);
       ss_wave_fence();
-      vh_sort_heap_pipe(S, 0, len);
+      vh_sort_heap_pipe(S, 0, len, len);
     }
     ss_wave_fence();
   } else {  // __make_heap alone

@@ -268,13 +268,14 @@ __device__ inline void vh_make_heap_wave(uint32_t* E, int lo, int hi) {
   }
 }
 
-// __sort_heap on the heap E[lo, hi) in LDS, one wave
-__device__ inline void vh_sort_heap_wave(uint32_t* E, int lo, int hi) {
+// __sort_heap on the heap E[lo, hi) in LDS, one wave: its first `pops` pops (the rest of the heap
+// is then left as a heap)
+__device__ inline void vh_sort_heap_wave(uint32_t* E, int lo, int hi, int pops) {
   const int lane = threadIdx.x & 63;
   const VhLess less;
   // lane l < 62 of a look-ahead: depth lj = 1 .. 5 below the hole, index lt in that depth
   const int lj = 31 - __clz(lane + 2), lt = lane + 2 - (1 << lj);
-  for (int last = hi - 1; last > lo; --last) {
+  for (int last = hi - 1; last > hi - 1 - pops; --last) {
     const int n = last - lo;
     const uint32_t v = E[last], top = E[lo];
     const int lim = (n - 1) / 2;
@@ -358,11 +359,12 @@ __device__ inline void vh_pipe_step(uint32_t* Eb, int npops, int& h, int& n, uin
 // (older pops may read that position as a child), or after the last rounds.  ~2.4 rounds per pop
 // and ~100 instructions per two rounds: the wave is issue-bound (a variant that precomputed both
 // next addresses to shorten the dependent chain issued more and ran slower).
-__device__ inline void vh_sort_heap_pipe(uint32_t* E, int lo, int hi) {
+__device__ inline void vh_sort_heap_pipe(uint32_t* E, int lo, int hi, int pops) {
   const int lane = threadIdx.x & 63;
   const int len = hi - lo;
   const int npops = len - 1;
-  if (npops < 1) return;
+  const int todo = min(pops, npops);  // the pops made (the first ones of __sort_heap)
+  if (todo < 1) return;
   const int D = 31 - __clz(len);  // depth of the deepest node (<= 14: len <= VH_MAX_N)
   constexpr int S = 16;
   int h = 0, n = 0, L = -1;
@@ -370,7 +372,7 @@ __device__ inline void vh_sort_heap_pipe(uint32_t* E, int lo, int hi) {
   uint32_t* const Eb = E + lo;
   const int cr = min(1, npops - 1);  // the root's children, loaded at cr, cr + 1
   int tail = 0;  // pops started (wave-uniform)
-  while (tail < npops) {
+  while (tail < todo) {
     // ---- round A
     const int Ln = npops - tail;
     const uint32_t eln = Eb[Ln], e0 = Eb[0], r1 = Eb[cr], r2 = Eb[cr + 1];
@@ -410,15 +412,33 @@ __device__ inline void vh_sort_heap_pipe(uint32_t* E, int lo, int hi) {
 // (tools/mb_heap.hip, one wave per CU: 1227 -> 958 cycles per element at 1024 elements, 1786 ->
 // 1148 with 16 waves per CU; below ~128 elements the look-ahead pops are as fast)
 constexpr int VH_PIPE_MIN = 192;
-__device__ inline void vh_heap_sort_wave(uint32_t* E, int lo, int hi) {
+// __make_heap, then the first `pops` pops of __sort_heap (at most hi - lo - 1: all of them)
+__device__ inline void vh_heap_sort_wave(uint32_t* E, int lo, int hi, int pops) {
   if (hi - lo < 2) return;
+  pops = min(pops, hi - lo - 1);
   vh_make_heap_wave(E, lo, hi);
   if (hi - lo >= VH_PIPE_MIN) {
     ss_wave_fence();
-    vh_sort_heap_pipe(E, lo, hi);
+    vh_sort_heap_pipe(E, lo, hi, pops);
   } else {
-    vh_sort_heap_wave(E, lo, hi);
+    vh_sort_heap_wave(E, lo, hi, pops);
   }
+}
+
+// The pops a depth-limit heap sort needs: __sort_heap pops in descending key order, so once every
+// element with a key not less than kmin (the smallest key two hot members of the segment share)
+// is popped, the order among the members of each hot voxel in the segment is final; the elements
+// left in the heap all have smaller keys, and their order inside the segment is never read (a hot
+// point's position is compared only with its own voxel's members, and those of its voxel outside
+// the segment lie outside it).  One wave; the count of E[lo, hi) with key >= kmin.
+__device__ inline int vh_pops_needed(const uint32_t* E, int lo, int hi, uint32_t kmin) {
+  const int lane = threadIdx.x & 63;
+  int c = 0;
+  for (int c0 = lo; c0 < hi; c0 += 64) {
+    const int i = c0 + lane;
+    c += __popcll(__ballot(i < hi && (E[i] >> 16) >= kmin));
+  }
+  return c;
 }
 
 // A depth-limit segment on one wave: heap-sorted literally when two members of one hot voxel lie
@@ -428,6 +448,7 @@ __device__ inline void vh_depth_limit_wave(uint32_t* E, int lo, int hi, uint32_t
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   int nh = 0;
   bool dup = false;
+  uint32_t kmin = 0;  // the smallest shared hot key (0: not known, every pop)
   for (int c0 = lo; c0 < hi; c0 += 64) {
     const int i = c0 + lane;
     const uint32_t e = i < hi ? E[i] : 0u;
@@ -446,11 +467,13 @@ __device__ inline void vh_depth_limit_wave(uint32_t* E, int lo, int hi, uint32_t
     bool d = false;
     for (int j = 0; j < nh; ++j) d |= lane < nh && j != lane && kb[j] == mine;
     dup = __ballot(d) != 0ull;
+    kmin = (uint32_t)wave_min_i(d ? (int)mine : 0x7FFFFFFF);
   }
   if (!dup) return;
   ss_wave_fence();
-  if (lane == 0) atomicAdd(heap_el, hi - lo);
-  vh_heap_sort_wave(E, lo, hi);
+  const int pops = kmin ? vh_pops_needed(E, lo, hi, kmin) : hi - lo;
+  if (lane == 0) atomicAdd(heap_el, pops);
+  vh_heap_sort_wave(E, lo, hi, pops);
 }
 
 // position of the k-th highest / lowest set bit of m (k >= 1, at least k bits set), per lane
@@ -891,21 +914,24 @@ __device__ inline void vh_depth_limit_wg(const VhLds& L, int n, int lo, int hi) 
   uint32_t* bm = reinterpret_cast<uint32_t*>(L.Bs);
   const int nw = (n >> 5) + 1;  // slot < n
   for (int w = tid; w < nw; w += NT) bm[w] = 0u;
-  if (tid == 0) L.C->dup = 0;
+  if (tid == 0) L.C->dup = 0x7FFFFFFF;  // the smallest shared hot key (none)
   __syncthreads();
-  bool d = false;
+  int kd = 0x7FFFFFFF;
   for (int i = lo + tid; i < hi; i += NT) {
     const uint32_t e = L.E[i];
     if (e & VH_HOT) {
       const uint32_t s = e >> 16, bit = 1u << (s & 31u);
-      d |= (atomicOr(&bm[s >> 5], bit) & bit) != 0u;
+      if ((atomicOr(&bm[s >> 5], bit) & bit) != 0u) kd = min(kd, (int)s);  // its second member seen
     }
   }
-  if (__ballot(d) != 0ull && (tid & 63) == 0) L.C->dup = 1;
+  kd = wave_min_i(kd);
+  if (kd != 0x7FFFFFFF && (tid & 63) == 0) atomicMin(&L.C->dup, kd);
   __syncthreads();
-  if (L.C->dup && tid < 64) {
-    if (tid == 0) L.C->heap_el += hi - lo;
-    vh_heap_sort_wave(L.E, lo, hi);
+  const int kmin = L.C->dup;
+  if (kmin != 0x7FFFFFFF && tid < 64) {
+    const int pops = vh_pops_needed(L.E, lo, hi, (uint32_t)kmin);
+    if (tid == 0) L.C->heap_el += pops;
+    vh_heap_sort_wave(L.E, lo, hi, pops);
   }
   __syncthreads();
 }
