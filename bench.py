@@ -80,8 +80,12 @@ def parse():
     ap.add_argument("--shard-streams", type=int, default=32,
                     help="streams of the sharded leg (every stream split over all ranks; 0: skip the leg)")
     ap.add_argument("--pipelined", action="store_true",
-                    help="one handle: the timed steps queue step k + 1's input and stack VoxelGrid while step k is "
-                         "in flight (loam_mapper_solve_async; for kernel traces of the single-stream mode)")
+                    help="(the default for the timed steps; kept for older command lines)")
+    ap.add_argument("--blocking", action="store_true",
+                    help="timed steps one after the other (loam_mapper_solve): step k + 1's input and stack "
+                         "VoxelGrid only after step k has finished.  Default: pipelined, each handle queues step "
+                         "k + 1 (its stack VoxelGrid runs beside step k) before waiting for step k "
+                         "(loam_mapper_solve_async)")
     ap.add_argument("--no-exact-leg", action="store_true",
                     help="skip the second (exact_voxel_order = 1) measurement of the same workload")
     ap.add_argument("--shard", action="store_true",
@@ -201,7 +205,7 @@ def run_steps(mapper, plan, first, count, poses=None):
     return iters
 
 
-def run_steps_pipelined(mapper, plan, first, count):
+def run_steps_pipelined(mapper, plan, first, count, poses=None):
     """count solveMapping steps, each enqueued behind the one in flight (loam_mapper_solve_async
     queues it on the device, its records prepared there: include/loam_core.h) before that one is
     waited for: the same results as run_steps, frame after frame, without the host round trip
@@ -214,22 +218,28 @@ def run_steps_pipelined(mapper, plan, first, count):
             mapper.input_device_batch(*plan[k])
             mapper.solve_async()  # queued behind frame k - 1
         mapper.wait()  # frame k - 1
-        iters += mapper.total_iterations()
+        iters += mapper.total_iterations()  # (results: frame k - 1, the newest finished)
+        if poses is not None:
+            poses.append(mapper.pose(0))
     return iters
 
 
-def run_handles(mappers, plans, first, count, poses=None):
-    """run_steps on every handle, one host thread each (ctypes releases the GIL in the
-    library calls): one handle's host work overlaps the others' kernels"""
+def run_handles(mappers, plans, first, count, poses=None, pipelined=False):
+    """run_steps (or run_steps_pipelined) on every handle, one host thread each (ctypes releases
+    the GIL in the library calls): one handle's host work overlaps the others' kernels"""
+    if pipelined:
+        run_one = lambda h: run_steps_pipelined(mappers[h], plans[h], first, count, poses if h == 0 else None)  # noqa: E731
+    else:
+        run_one = lambda h: run_steps(mappers[h], plans[h], first, count, poses if h == 0 else None)  # noqa: E731
     if len(mappers) == 1:
-        return run_steps(mappers[0], plans[0], first, count, poses)
+        return run_one(0)
     import threading
     out = [0] * len(mappers)
     errs = []
 
     def work(h):
         try:
-            out[h] = run_steps(mappers[h], plans[h], first, count, poses if h == 0 else None)
+            out[h] = run_one(h)
         except Exception as e:  # surfaced after the join
             errs.append(e)
 
@@ -755,10 +765,7 @@ def main():
                 m.debug_counters(reset=True)  # the timed steps only
         barrier()
         t0 = time.perf_counter()
-        if args.pipelined and H == 1:
-            it = run_steps_pipelined(mappers[0], plans[0], pre, K)
-        else:
-            it = run_handles(mappers, plans, pre, K, poses)
+        it = run_handles(mappers, plans, pre, K, poses, pipelined=not args.blocking)
         barrier()
         secs = time.perf_counter() - t0
         fam = {}
@@ -1020,7 +1027,10 @@ def main():
                                        f"5-NN candidates per round, all-reduce of the normal equations per LM "
                                        f"iteration" if args.shard else
                                        f"{world} GPU x {B} independent streams"
-                                       + (f" ({H} handles x {Bh}, one host thread each)" if H > 1 else ""))},
+                                       + (f" ({H} handles x {Bh}, one host thread each)" if H > 1 else "")),
+                       "steps": ("blocking: one after the other" if args.blocking else
+                                 "pipelined: each handle queues step k + 1 (its stack VoxelGrid runs beside step k) "
+                                 "before waiting for step k")},
             "lm_iterations": int(iters_all),
             "kernel_ms_per_step": {k: round(v["ms"] / K, 4) for k, v in kt.items()},
             "roofline": roofline,

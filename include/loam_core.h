@@ -255,7 +255,8 @@ int32_t loam_mapper_solve(loam_mapper* h);
  * waited for; one the device finds recentering or due for an arena compaction is deferred and
  * run again on the host-prepared path (loam_map_stats.queued / .rerun say which happened).
  * Otherwise (other handles) frame f + 1's stack VoxelGrids (:492-500) run beside f and the rest
- * after it.  loam_mapper_prefetch queues the stack VoxelGrids of given inputs early.
+ * is enqueued by the _wait that finishes f, before it returns.  loam_mapper_prefetch queues the
+ * stack VoxelGrids of given inputs early.
  * The results are those of the sequential loam_mapper_solve, bit for bit; only the order in time
  * changes.  loam_mapper_pose / _stats / _stats_all / _total_iterations / _get_state report the
  * newest frame waited for (a frame enqueued with nothing before it in the queue is waited for by
@@ -271,7 +272,7 @@ int32_t loam_mapper_solve(loam_mapper* h);
  * is dropped, and the call that tried returns that error with "dropped" in loam_last_error. */
 int32_t loam_mapper_solve_async(loam_mapper* h);
 int32_t loam_mapper_wait(loam_mapper* h);
-/* queue the stack VoxelGrids of every stream's pending input now (no-op with profiling on) */
+/* queue the stack VoxelGrids of every stream's pending input now */
 int32_t loam_mapper_prefetch(loam_mapper* h);
 /* pose after solveMapping: q_w_curr (xyzw), t_w_curr (laser_mapping.cpp:826-832) */
 int32_t loam_mapper_pose(loam_mapper* h, int32_t stream, double* q_w, double* t_w);

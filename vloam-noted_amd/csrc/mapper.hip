@@ -2564,7 +2564,6 @@ static int32_t launch_stacks(loam_mapper* h) {
 int32_t loam_mapper_prefetch(loam_mapper* h) {
   if (!h) return LOAM_ERR_ARG;
   LOAM_HIP(hipSetDevice(h->dev));
-  if (h->prof) return LOAM_OK;  // with profiling, stacks are timed inside their frame
   return launch_stacks(h);
 }
 
@@ -2599,7 +2598,6 @@ static void capture_frame(loam_mapper* h, const MapperDev& D, int fpar, hipStrea
 // flight, whose results the host does not have yet: the device prepares the stream records
 // (k_frame_prep) from what that frame left, and only the graph path runs.
 static int32_t mapper_enqueue(loam_mapper* h, bool chained, FrameRec& R) {
-  h->ev_fam.clear();
   MapperDev& D = h->D;
   const int B = h->B;
   TRY(launch_stacks(h));  // inputs not prefetched
@@ -2878,12 +2876,24 @@ static int32_t mapper_finish_rec(loam_mapper* h, const FrameRec& R, bool replay)
     h->mirror_seq = R.seq;
   }
   if (h->prof) {
+    // the launches timed so far whose stop event has passed: this frame's, and perhaps a queued
+    // frame's stack VoxelGrid (launched beside this one); the others stay listed for a later frame
+    size_t kept = 0;
     for (size_t k = 0; k < h->ev_fam.size(); ++k) {
+      const hipError_t q = hipEventQuery(h->ev_pool[2 * k + 1]);
+      if (q == hipErrorNotReady) {
+        std::swap(h->ev_pool[2 * kept], h->ev_pool[2 * k]);
+        std::swap(h->ev_pool[2 * kept + 1], h->ev_pool[2 * k + 1]);
+        h->ev_fam[kept++] = h->ev_fam[k];
+        continue;
+      }
+      LOAM_HIP(q);
       float ms = 0;
       LOAM_HIP(hipEventElapsedTime(&ms, h->ev_pool[2 * k], h->ev_pool[2 * k + 1]));
       h->fam_ms[h->ev_fam[k]] += ms;
       h->fam_launches[h->ev_fam[k]]++;
     }
+    h->ev_fam.resize(kept);
     // algorithmic bytes (DESIGN.md "Kernels"): what each family must read / write
     for (int s = 0; s < B; ++s) {
       const StreamFrame& F = FO[s];
@@ -3195,6 +3205,9 @@ int32_t loam_mapper_wait(loam_mapper* h) {
   if (h->q.empty()) return take_held(h);
   LOAM_HIP(hipSetDevice(h->dev));
   TRY(finish_oldest(h));  // (a pending oldest frame is enqueued first)
+  // a frame waiting behind the finished one (its stack VoxelGrid already queued) is enqueued now,
+  // so the device works on it while the host returns and gives the next input
+  TRY(launch_front(h));
   return take_held(h);
 }
 
@@ -3218,6 +3231,7 @@ int32_t loam_mapper_set_profiling(loam_mapper* h, int32_t enable) {
   SETTLE(h);
   if (!h) return LOAM_ERR_ARG;
   h->prof = enable != 0;
+  h->ev_fam.clear();  // (settled: every timed launch has been read)
   return LOAM_OK;
 }
 
