@@ -42,7 +42,7 @@ constexpr int VH_BIG = 1024;      // longer segments: partitioned by the workgro
 constexpr int VH_MAX_N = 30720;   // LDS-resident emulation up to this many points (30 per thread)
 constexpr int VH_CHUNK = VH_MAX_N / VX_THREADS;  // positions per thread of a workgroup partition
 constexpr int VH_ROOTS = 512;     // wave subtrees listed per drain
-constexpr int VH_SHARE = 96;      // a wave lists the larger part of a partition when longer (others may take it)
+constexpr int VH_SHARE = 96;      // a wave lists the larger part of a partition when longer and it has the smaller part to do
 constexpr int VH_BIGC = 32;       // workgroup segments of one level (segments > VH_BIG are disjoint: <= 30)
 constexpr int VH_LIFO = 8;        // wave-local pending parts (smaller part first: depth <= 6)
 constexpr int VH_WAVE_W = VH_LIFO + 64;  // per wave: LIFO + the dup check's keys
@@ -615,26 +615,32 @@ __device__ inline void vh_wave_subtree(uint32_t* E, uint16_t* Bs, uint32_t root,
           const bool left_small = l0 <= l1;
           const int sl = left_small ? lo : cut, sn = left_small ? l0 : l1;  // smaller part: now
           const int bl_ = left_small ? cut : lo, bn = left_small ? l1 : l0;  // larger: pending
-          if (bn > SS_THRESHOLD) {
-            int s = VH_ROOTS;
-            if (bn > VH_SHARE && lane == 0 && __hip_atomic_load(&C->nroot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < VH_ROOTS - 64) {
-              // listed for any wave: counted pending before it is visible
-              s = atomicAdd(&C->nroot, 1);
-              if (s < VH_ROOTS) {
-                atomicAdd(&C->pending, 1);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __hip_atomic_store(&roots[s], vh_pack(bl_, bn, d - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (sn > SS_THRESHOLD) {  // the smaller part now, the larger one listed or kept
+            if (bn > SS_THRESHOLD) {
+              int s = VH_ROOTS;
+              if (bn > VH_SHARE && lane == 0 &&
+                  __hip_atomic_load(&C->nroot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < VH_ROOTS - 64) {
+                // listed for any wave: counted pending before it is visible
+                s = atomicAdd(&C->nroot, 1);
+                if (s < VH_ROOTS) {
+                  atomicAdd(&C->pending, 1);
+                  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                  __hip_atomic_store(&roots[s], vh_pack(bl_, bn, d - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
               }
+              s = __builtin_amdgcn_readfirstlane(s);
+              if (s >= VH_ROOTS) {  // kept by this wave
+                if (lane == 0 && top < VH_LIFO) stk[top] = vh_pack(bl_, bn, d - 1);
+                ++top;  // (overflow impossible: each kept part is larger than the current one)
+              }
+              ss_wave_fence();
             }
-            s = __builtin_amdgcn_readfirstlane(s);
-            if (s >= VH_ROOTS) {  // kept by this wave
-              if (lane == 0 && top < VH_LIFO) stk[top] = vh_pack(bl_, bn, d - 1);
-              ++top;  // (overflow impossible: each kept part is larger than the current one)
-            }
-            ss_wave_fence();
-          }
-          if (sn > SS_THRESHOLD) {
             cur = vh_pack(sl, sn, d - 1);
+            next = false;
+          } else if (bn > SS_THRESHOLD) {
+            // a degenerate partition (the smaller part needs nothing): the chain goes on on this
+            // wave, with no round trip through the list or the LIFO
+            cur = vh_pack(bl_, bn, d - 1);
             next = false;
           }
         }
