@@ -577,6 +577,54 @@ def test_split_prefetch_matches_blocking(seq, exact, n_streams):
     assert got == want
 
 
+@pytest.mark.parametrize("exact", [0, 1])
+def test_pipelined_frames_with_profiling(seq, exact):
+    """bench.py's timed steps: each frame given and enqueued (loam_mapper_solve_async) before the
+    previous one is waited for, with per-launch HIP events on.  At 8 streams (no hipGraph chain)
+    the queued frame's stack VoxelGrid runs beside the frame in flight and the rest is enqueued by
+    the wait that finishes it; a launch whose events have not passed when a frame is finished
+    (that stack VoxelGrid) stays listed for a later frame instead of failing the read.  Poses and
+    counts equal the blocking solve's; every family is timed, the stack's once per frame."""
+    n_streams = 8
+
+    def row(m, s):
+        st = m.stats(s)
+        q, t = m.pose(s)
+        return (q.tobytes(), t.tobytes(), st.corner_stack, st.surf_stack, tuple(st.corner_num), tuple(st.surf_num),
+                st.lm[0].iterations, st.lm[1].iterations)
+
+    def give(m, f):
+        for s in range(n_streams):
+            rec = seq[f + s % 4]
+            m.input(s, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+
+    n = len(seq) - 3
+    ref = BatchMapper(n_streams, exact_voxel_order=exact)
+    want = []
+    for f in range(n):
+        give(ref, f)
+        ref.solve()
+        want.append([row(ref, s) for s in range(n_streams)])
+    ref.close()
+    m = BatchMapper(n_streams, exact_voxel_order=exact)
+    m.set_profiling(True)
+    got = []
+    give(m, 0)
+    m.solve_async()
+    for f in range(1, n + 1):
+        if f < n:
+            give(m, f)
+            m.solve_async()  # its stack VoxelGrid beside frame f - 1
+        m.wait()             # frame f - 1 (and frame f enqueued)
+        got.append([row(m, s) for s in range(n_streams)])
+    kt = m.kernel_times()
+    m.close()
+    assert got == want
+    assert kt["stack_voxelgrid"]["launches"] == n, kt["stack_voxelgrid"]
+    assert kt["correspondence"]["launches"] > 0 and kt["cube_revoxel"]["launches"] > 0
+    assert all(v["ms"] >= 0.0 for v in kt.values())
+
+
 def test_async_capacity_error_is_held_for_wait(seq):
     """loam_mapper_solve_async returns OK exactly when it enqueued its frame.  With two frames in
     the queue it first finishes the oldest; when that one fails (here: its submap exceeds
