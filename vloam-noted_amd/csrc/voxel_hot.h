@@ -357,7 +357,8 @@ __device__ inline void vh_pipe_step(uint32_t* Eb, int npops, int& h, int& n, uin
 // round B moves.  A pop's output (its old root to its tail position) is written by its lane when
 // the slot starts its next pop, 2 S >= D + 1 rounds later, when every older pop has finished
 // (older pops may read that position as a child), or after the last rounds.  ~2.4 rounds per pop
-// and ~100 instructions per two rounds: the wave is issue-bound (a variant that precomputed both
+// and ~100 instructions per two rounds (the start and block tests bitwise: 964 -> 888 cycles a pop,
+// profiles/r5_mb_heap_branchfree.txt): the wave is issue-bound (a variant that precomputed both
 // next addresses to shorten the dependent chain issued more and ran slower).
 __device__ inline void vh_sort_heap_pipe(uint32_t* E, int lo, int hi, int pops) {
   const int lane = threadIdx.x & 63;
@@ -380,21 +381,21 @@ __device__ inline void vh_sort_heap_pipe(uint32_t* E, int lo, int hi, int pops) 
     const int ca = min(c1, npops - 1);
     uint32_t a = Eb[ca], b = Eb[ca + 1];
     const int k = __clz(h + 1) - __clz(Ln + 1);  // depth of Ln minus the hole's
-    const bool blocks = n != 0 && (h < 3 || (k >= 0 && ((Ln + 1) >> k) == h + 1 && (eln >> 16) >= (v >> 16)));
+    // (bitwise, not short-circuit: straight-line compares instead of nested exec branches)
+    const bool anc = (k >= 0) & (((Ln + 1) >> (k & 31)) == h + 1);
+    const bool blocks = (n != 0) & ((h < 3) | (anc & ((eln >> 16) >= (v >> 16))));
     const bool can = __ballot(blocks) == 0ull;
-    const bool start = can && lane == (tail & (S - 1));
+    const bool start = can & (lane == (tail & (S - 1)));
     tail += can ? 1 : 0;
     if (start && L >= 0) Eb[L] = top;  // the slot's previous pop
-    if (start) {
-      v = eln;
-      top = e0;
-      h = 0;
-      n = Ln;
-      L = Ln;
-      c1 = 1;
-      a = r1;
-      b = r2;
-    }
+    v = start ? eln : v;
+    top = start ? e0 : top;
+    h = start ? 0 : h;
+    n = start ? Ln : n;
+    L = start ? Ln : L;
+    c1 = start ? 1 : c1;
+    a = start ? r1 : a;
+    b = start ? r2 : b;
     vh_pipe_move(Eb, h, n, v, c1, a, b);
     vh_lds_order();
     // ---- round B
