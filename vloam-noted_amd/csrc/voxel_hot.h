@@ -168,13 +168,12 @@ __device__ inline int vh_partition_wave_u(uint32_t* E, uint16_t* Bs, int lo, int
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = b0 + u;
-      if (u < c && i < hi) {
-        const uint32_t x = i == mm ? elo : e[u];
-        const uint32_t k = x >> 16;
-        ml |= (k < p ? 0u : 1u) << u;
-        mr |= (p < k ? 0u : 1u) << u;
-        nh += (x & VH_HOT) ? 1u : 0u;
-      }
+      const uint32_t x = i == mm ? elo : e[u];
+      const uint32_t in = (u < c && i < hi) ? 1u : 0u;
+      const uint32_t k = x >> 16;
+      ml |= (in & (k < p ? 0u : 1u)) << u;
+      mr |= (in & (p < k ? 0u : 1u)) << u;
+      nh += in & ((x & VH_HOT) ? 1u : 0u);
     }
   }
   if (dpp_wave_sum_u(nh) + ((pe & VH_HOT) ? 1u : 0u) < 2u) return -1;
@@ -191,39 +190,52 @@ __device__ inline int vh_partition_wave_u(uint32_t* E, uint16_t* Bs, int lo, int
   const int m = hi - lo, KB = (m - 1) / 2, bb = lo >> 1;
   uint32_t S = 0;
   {
+    // (bitwise counts: straight-line code, only the Bs stores predicated)
     int kl = (int)(off & 0xFFFFu), t = 1 + (int)(off >> 16);  // t: ascending right-stop index
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const bool isl = (ml >> u) & 1u, isr = (mr >> u) & 1u;
-      if (isl) {
-        ++kl;
-        S += kl <= nr - (t + (isr ? 1 : 0)) ? 1u : 0u;
-      }
-      if (isr) {
-        if (nr - t <= KB) Bs[bb + nr - t - 1] = (uint16_t)(b0 + u);
-        ++t;
-      }
+      const int isl = (int)((ml >> u) & 1u), isr = (int)((mr >> u) & 1u);
+      kl += isl;
+      S += (uint32_t)(isl & (kl <= nr - (t + isr) ? 1 : 0));
+      if (isr & (nr - t <= KB ? 1 : 0)) Bs[bb + nr - t - 1] = (uint16_t)(b0 + u);
+      t += isr;
     }
     if (lane == 0 && nr <= KB) Bs[bb + nr - 1] = (uint16_t)lo;
   }
   S = dpp_wave_sum_u(S);
   ss_wave_fence();
   // the swaps (each pair (l_k, r_k), k <= S, read and written by the lane of l_k alone: l_k < cut
-  // <= r_k, no position is in two pairs) and l_{S+1}
+  // <= r_k, no position is in two pairs) and l_{S+1}, four of a lane's positions at a time: their
+  // r_k at once, then E[r_k] and E[l_k] at once (two LDS latencies per four, not two per one),
+  // then the writes (later groups read other pairs' positions only)
   int lK = 0x7FFFFFFF;
   {
     int kl = (int)(off & 0xFFFFu);
+    constexpr int G = U < 4 ? U : 4;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if ((ml >> u) & 1u) {
-        ++kl;
-        if (kl <= (int)S) {
-          const int y = Bs[bb + kl - 1];
-          const uint32_t tv = E[y];
-          E[y] = E[b0 + u];
-          E[b0 + u] = tv;
+    for (int u0 = 0; u0 < U; u0 += G) {
+      int y[G];
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        const int isl = (int)((ml >> (u0 + j)) & 1u);
+        kl += isl;
+        const bool sw = isl && kl <= (int)S;
+        y[j] = (int)Bs[sw ? bb + kl - 1 : bb] | (sw ? 0 : 0x10000);  // (bit 16: no swap)
+        lK = (isl && kl == (int)S + 1) ? b0 + u0 + j : lK;
+      }
+      uint32_t tv[G], lv[G];
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        tv[j] = E[y[j] & 0xFFFF];
+        lv[j] = E[(y[j] & 0x10000) ? b0 : b0 + u0 + j];
+      }
+      ss_wave_fence();
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        if (!(y[j] & 0x10000)) {
+          E[y[j]] = lv[j];
+          E[b0 + u0 + j] = tv[j];
         }
-        if (kl == (int)S + 1) lK = b0 + u;
       }
     }
   }
