@@ -163,8 +163,12 @@ def make_frames(seed, n_frames, n_az, device, raw_frames=(), prior="odometry"):
                 stage_ms["odometry_bytes"].append(odometry_bytes(counts, ost))
                 corner = sr.cloud(2)  # cornerPointsLessSharp -> laserCloudCornerLast
                 surf = sr.cloud(4)    # surfPointsLessFlat   -> laserCloudSurfLast
-                frames.append(dict(corner=torch.from_numpy(corner).to(f"cuda:{device}"),
-                                   surf=torch.from_numpy(surf).to(f"cuda:{device}"),
+                dev = f"cuda:{device}"
+                frames.append(dict(corner=torch.from_numpy(corner).to(dev),
+                                   surf=torch.from_numpy(surf).to(dev),
+                                   # the sharp / flat queries too: the batched odometry stage
+                                   sharp=torch.from_numpy(sr.cloud(1)).to(dev),
+                                   flat=torch.from_numpy(sr.cloud(3)).to(dev),
                                    corner_h=corner, surf_h=surf,
                                    gt=gt, q=q, t=t, raw=xyz if c0 + k in raw_frames else None))
     sr.close()
@@ -390,6 +394,56 @@ def scanreg_batched_stage(seed, device, n_az, frames=64, reps=5):
                          "frac": round(ach / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_launch": round(byts, 1),
                          "traffic": None},
             "mode": "loam_scanreg_create_batch / loam_scanreg_input_batch: the scans in HBM, one launch sequence"}
+
+
+def odometry_batched_stage(frames, device, streams=64, steps=10, warmup=3, spacing=4):
+    """BASELINE configs[2] as throughput: `streams` independent LaserOdometry streams in one
+    handle (BatchOdometry, every kernel of a solve covers all of them), stream b fed frames
+    b*spacing, b*spacing + 1, ... of the sequence (features resident in HBM from the HIP
+    ScanRegistration); the first frame of each stream only primes its last clouds, then `warmup`
+    untimed and `steps` timed solves.  Device time per solve from the handle's HIP events
+    (loam_odom_stats.ms: the whole launch sequence), wall time around the host calls too; bytes as
+    the one-stream roofline (odometry_bytes), summed over the streams of a launch"""
+    import torch
+    from loam_amd.odometry import BatchOdometry
+    need = (streams - 1) * spacing + warmup + steps + 1
+    if need > len(frames):
+        return {"error": f"needs {need} frames, {len(frames)} built"}
+    od = BatchOdometry(streams, device=device)
+    ms, byts, iters = [], [], 0
+    t_wall = 0.0
+    for k in range(warmup + steps + 1):
+        for b in range(streams):
+            f = frames[b * spacing + k]
+            cl = (f["sharp"], f["corner"], f["flat"], f["surf"])
+            od.input_device(b, [c.data_ptr() for c in cl], [len(c) for c in cl])
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        od.solve()
+        dt = time.perf_counter() - t0
+        if k <= warmup:
+            continue
+        t_wall += dt
+        ms.append(od.stats(0).ms)
+        for b in range(streams):
+            f = frames[b * spacing + k]
+            st = od.stats(b)
+            iters += st.lm[0].iterations + st.lm[1].iterations
+            byts.append(odometry_bytes((len(f["sharp"]), len(f["corner"]), len(f["flat"]), len(f["surf"])), st))
+    od.close()
+    dev_s = float(np.sum(ms)) * 1e-3
+    bpl = float(np.sum(byts)) / steps
+    ach = bpl / (dev_s / steps) / 1e9
+    return {"streams_per_launch": streams, "steps": steps, "launch_ms": round(1e3 * dev_s / steps, 4),
+            "frames_per_s": round(streams * steps / dev_s, 1), "ms_per_frame": round(1e3 * dev_s / (streams * steps), 5),
+            "lm_iters_per_s": round(iters / dev_s, 1),
+            "wall_frames_per_s": round(streams * steps / t_wall, 1),
+            "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_launch": round(bpl, 1),
+                         "traffic": None},
+            "mode": f"BatchOdometry of {streams} streams (loam_odometry_solve: 2 x (k_od_corr -> k_od_lm) -> "
+                    f"k_od_build over every stream per launch), stream b on frames b*{spacing} + k; device time "
+                    f"from the handle's HIP events, wall time around the blocking solve beside it"}
 
 
 def depth_stage(seed, device, n_frames=64, n_queries=2800, n_az=2000, with_cpu=True):
@@ -1088,6 +1142,8 @@ def main():
             stages[name] = e
         if world == 1 and "scan_registration" in stages:
             stages["scan_registration"]["batched"] = scanreg_batched_stage(args.seed, local, args.n_az)
+        if world == 1 and "odometry" in stages:
+            stages["odometry"]["batched"] = odometry_batched_stage(frames, local)
         if not args.no_depth and world == 1:
             stages["depth_association"] = depth_stage(args.seed, local, with_cpu=not args.no_cpu)
             stages["vo_solve"] = vo_stage(args.seed, local, with_cpu=not args.no_cpu)

@@ -174,3 +174,93 @@ def test_rccl_one_rank(seq, unsharded):
         assert np.linalg.norm(t - tr) < 1e-7 and quat_angle(q, qr) < 1e-7
     m.close()
     c.close()
+
+
+def test_device_group_mappers_in_turn(seq, unsharded):
+    """two sharded mappers created one after the other on the same Comm.local_group: the group's
+    LM peer buffer is re-bound (zeroed) for the second, whose epochs count from 1 again (before,
+    the first mapper's larger flags let the second's leaders sum stale peer slots: ADVICE r5)"""
+    ref, _ = unsharded
+
+    def body(rank, comm):
+        out = []
+        for n in (N_FRAMES, 6):
+            m = BatchMapper(1, comm=comm)
+            poses = []
+            for rec in seq[:n]:
+                m.input(0, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+                m.solve()
+                poses.append((m.pose(0), _stat_tuple(m.stats(0))))
+            m.close()
+            out.append(poses)
+        return out
+
+    res = _run_ranks(2, body, "device")
+    for run in range(2):
+        for f, ((qr, tr), sr) in enumerate(ref[:len(res[0][run])]):
+            (q0, t0), s0 = res[0][run][f]
+            (q1, t1), s1 = res[1][run][f]
+            assert np.array_equal(q0, q1) and np.array_equal(t0, t1), (run, f)
+            assert s0 == sr and s1 == sr, (run, f)
+            assert np.linalg.norm(t0 - tr) < 1e-6 and quat_angle(q0, qr) < 1e-6, (run, f)
+
+
+def test_device_group_beside_a_busy_handle(seq, unsharded):
+    """a 2-rank in-process group (persistent group LM: its leaders wait for each other inside one
+    launch) solving while an unsharded 8-stream handle runs its own frames on the same GPU from a
+    third thread: the group's leaders are dispatched whatever the other handle holds (its kernels
+    end on their own), and both give the unsharded results bit for bit"""
+    ref, _ = unsharded
+    comms = Comm.local_group(2)
+    res, errs = [None] * 3, []
+    start = threading.Barrier(3)
+
+    def ranks(r):
+        try:
+            m = BatchMapper(1, comm=comms[r])
+            start.wait()
+            out = []
+            for rec in seq:
+                m.input(0, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+                m.solve()
+                out.append((m.pose(0), _stat_tuple(m.stats(0))))
+            m.close()
+            res[r] = out
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            start.abort()
+
+    def busy():
+        try:
+            m = BatchMapper(8)
+            start.wait()
+            out = []
+            for rec in seq:
+                for s in range(8):
+                    m.input(s, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+                m.solve()
+                out.append([(m.pose(s), _stat_tuple(m.stats(s))) for s in range(8)])
+            m.close()
+            res[2] = out
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            start.abort()
+
+    th = [threading.Thread(target=ranks, args=(r,)) for r in range(2)] + [threading.Thread(target=busy)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    for c in comms:
+        c.close()
+    if errs:
+        raise errs[0]
+    assert all(not t.is_alive() for t in th)
+    for f, ((qr, tr), sr) in enumerate(ref):
+        (q0, t0), s0 = res[0][f]
+        (q1, t1), s1 = res[1][f]
+        assert np.array_equal(q0, q1) and np.array_equal(t0, t1), f
+        assert s0 == sr, (f, s0, sr)
+        assert np.linalg.norm(t0 - tr) < 1e-6 and quat_angle(q0, qr) < 1e-6, f
+        for (q, t), st in res[2][f]:  # the busy handle's streams: the unsharded mapper's bits
+            assert st == sr and np.array_equal(q, qr) and np.array_equal(t, tr), f

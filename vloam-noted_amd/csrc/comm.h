@@ -33,9 +33,15 @@ int32_t comm_allgather(loam_comm* c, const void* d_send, void* d_recv, int64_t b
 // RCCL and callback transports own their failure handling)
 void comm_abort(loam_comm* c);
 // device memory every rank of the group sees at the same address (ranks of one process on one
-// device, loam_comm_create_local): the first caller allocates it zeroed, every rank asks for the
-// same size.  LOAM_ERR_STATE for transports without one (RCCL, callbacks)
-int32_t comm_peer_buffer(loam_comm* c, size_t bytes, void** dev);
+// device, loam_comm_create_local), bound by every rank's mapper at once (its creation: the host
+// threads meet twice, bounded): zeroed at each binding, every rank asks for the same size.
+// LOAM_ERR_STATE for transports without one (RCCL, callbacks) and while a rank's earlier mapper
+// still holds it (released by comm_peer_release when that mapper is destroyed).  `leaders`: the
+// group LM's leader workgroups (one per rank and padded stream), reserved against `capacity` (LM
+// workgroups the device holds at once) together with every group bound in this process:
+// LOAM_ERR_CAPACITY when they would not all fit at once
+int32_t comm_peer_buffer(loam_comm* c, size_t bytes, int leaders, int capacity, void** dev);
+void comm_peer_release(loam_comm* c);
 // ONE launch for every rank of an in-process group (ranks whose kernels must wait for each other
 // on the device: separate launches could sit behind each other in one hardware queue, the HIP
 // streams of a process sharing GPU_MAX_HW_QUEUES queues).  Each rank hands its argument blob and

@@ -105,6 +105,10 @@ struct LocalGroup {
 
   void* peer = nullptr;  // comm_peer_buffer
   size_t peer_bytes = 0;
+  size_t peer_req[LOAM_LOCAL_MAX_RANKS] = {};     // this binding's requested size, per rank
+  bool peer_bound[LOAM_LOCAL_MAX_RANKS] = {};     // a live mapper of rank r holds the buffer
+  int32_t peer_rc = LOAM_OK;                      // rank 0's decision for the current binding
+  int peer_leaders = 0;                           // LM leaders this binding reserved on the device
   const void* blobs[LOAM_LOCAL_MAX_RANKS] = {};  // comm_group_launch
   hipEvent_t ev_pre[LOAM_LOCAL_MAX_RANKS] = {};
   hipEvent_t ev_post = nullptr;
@@ -121,12 +125,14 @@ struct LocalGroup {
       cv.notify_all();
       return true;
     }
-    if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return generation != g || broken; }) || broken) {
-      broken = true;
-      cv.notify_all();
-      return false;
-    }
-    return true;
+    const bool woke = cv.wait_for(lk, std::chrono::seconds(120), [&] { return generation != g || broken; });
+    // the barrier completed (every rank arrived) even if a rank broke the group just after it,
+    // e.g. by leaving once its last collective was done: that collective succeeded
+    if (generation != g) return true;
+    (void)woke;  // timed out, or broken before every rank arrived
+    broken = true;
+    cv.notify_all();
+    return false;
   }
   // a rank that fails between or inside collectives (or leaves the group) breaks it at once:
   // the other ranks' barriers return false now instead of after their 120 s timeout
@@ -270,24 +276,105 @@ int32_t comm_group_launch(loam_comm* c, const void* blob, hipStream_t st, comm_g
   return LOAM_OK;
 }
 
-int32_t comm_peer_buffer(loam_comm* c, size_t bytes, void** dev) {
+// Leaders of the persistent group LM rounds (k_lm_group) reserved per device, process-wide: a
+// leader waits for the other ranks' leaders of its launch, which are dispatched after it, so the
+// leaders of every group bound at once in this process must fit the device together (one
+// 256-thread LM workgroup per CU).  Kernels that end on their own (other handles' kernels, this
+// handle's stack VoxelGrids) only delay a leader's dispatch; a binding whose leaders would not fit
+// beside the groups already bound fails (LOAM_ERR_CAPACITY: the two-kernel LM path instead).
+static std::mutex g_lead_mu;
+static int g_lead_reserved[64] = {};
+
+int32_t comm_peer_buffer(loam_comm* c, size_t bytes, int leaders, int capacity, void** dev) {
   if (!c || !dev || c->kind != 2 || !c->local) return LOAM_ERR_STATE;
   LocalGroup& G = *c->local;
-  std::lock_guard<std::mutex> lk(G.mu);
-  if (!G.peer) {
-    LOAM_HIP(hipSetDevice(G.device));
-    LOAM_HIP(hipMalloc(&G.peer, bytes));
-    // zeroed and finished before any rank's kernels (which run on non-blocking streams, not
-    // ordered behind the null stream): the memory may be a freed group's, flags and all
-    LOAM_HIP(hipMemset(G.peer, 0, bytes));
-    LOAM_HIP(hipDeviceSynchronize());
-    G.peer_bytes = bytes;
-  } else if (G.peer_bytes != bytes) {
-    set_error("local comm: ranks asked for peer buffers of different sizes");
-    return LOAM_ERR_ARG;
+  const int r = c->rank;
+  {
+    std::lock_guard<std::mutex> lk(G.mu);
+    G.peer_req[r] = bytes;
+  }
+  // every rank binds (a sharded mapper is created on every rank); then rank 0 (re)allocates and
+  // zeroes the buffer, flags and all, while no rank's kernels use it: the flags hold
+  // epoch * LM_MAX_PASSES + pass + 1 of the mapper that used them last, and a new mapper counts
+  // its epochs from 1 again.  A rank whose earlier mapper still holds the buffer makes
+  // the binding fail on every rank alike (the mappers then take the two-kernel LM path)
+  if (!G.barrier()) {
+    set_error("local comm: a rank did not reach the peer-buffer binding (group broken)");
+    return LOAM_ERR_SYNC;
+  }
+  if (r == 0) {
+    std::lock_guard<std::mutex> lk(G.mu);
+    int32_t rc = LOAM_OK;
+    for (int q = 0; q < G.size; ++q) {
+      if (G.peer_req[q] != bytes) rc = LOAM_ERR_ARG;
+      if (G.peer_bound[q] && rc == LOAM_OK) rc = LOAM_ERR_STATE;
+    }
+    if (rc == LOAM_OK && G.peer && G.peer_bytes != bytes) {
+      if (hipSetDevice(G.device) != hipSuccess || hipDeviceSynchronize() != hipSuccess || hipFree(G.peer) != hipSuccess)
+        rc = LOAM_ERR_HIP;
+      G.peer = nullptr;
+      G.peer_bytes = 0;
+    }
+    if (rc == LOAM_OK && !G.peer) {
+      if (hipSetDevice(G.device) != hipSuccess || hipMalloc(&G.peer, bytes) != hipSuccess) {
+        G.peer = nullptr;
+        rc = LOAM_ERR_HIP;
+      } else {
+        G.peer_bytes = bytes;
+      }
+    }
+    // zeroed and finished before any rank's kernels (non-blocking streams are not ordered behind
+    // the null stream); the device synchronize also waits out any kernel of an earlier mapper
+    if (rc == LOAM_OK && (hipSetDevice(G.device) != hipSuccess || hipMemset(G.peer, 0, bytes) != hipSuccess ||
+                          hipDeviceSynchronize() != hipSuccess))
+      rc = LOAM_ERR_HIP;
+    if (rc == LOAM_OK) {
+      std::lock_guard<std::mutex> lk2(g_lead_mu);
+      const int d = G.device & 63;
+      if (leaders <= 0 || g_lead_reserved[d] + leaders > capacity) {
+        rc = LOAM_ERR_CAPACITY;
+      } else {
+        g_lead_reserved[d] += leaders;
+        G.peer_leaders = leaders;
+      }
+    }
+    if (rc == LOAM_OK)
+      for (int q = 0; q < G.size; ++q) G.peer_bound[q] = true;
+    G.peer_rc = rc;
+  }
+  if (!G.barrier()) {
+    set_error("local comm: the peer-buffer binding's rank 0 did not return (group broken)");
+    return LOAM_ERR_SYNC;
+  }
+  int32_t rc;
+  {
+    std::lock_guard<std::mutex> lk(G.mu);
+    rc = G.peer_rc;
+  }
+  if (rc != LOAM_OK) {
+    set_error(rc == LOAM_ERR_STATE      ? "local comm: a rank's earlier mapper still holds the group's LM peer buffer"
+              : rc == LOAM_ERR_ARG      ? "local comm: ranks asked for peer buffers of different sizes"
+              : rc == LOAM_ERR_CAPACITY ? "local comm: the group LM's leaders do not fit the device beside the "
+                                          "groups already bound"
+                                        : "local comm: peer buffer allocation failed");
+    return rc;
   }
   *dev = G.peer;
   return LOAM_OK;
+}
+
+void comm_peer_release(loam_comm* c) {
+  if (!c || c->kind != 2 || !c->local) return;
+  LocalGroup& G = *c->local;
+  std::lock_guard<std::mutex> lk(G.mu);
+  G.peer_bound[c->rank] = false;
+  bool any = false;
+  for (int q = 0; q < G.size; ++q) any |= G.peer_bound[q];
+  if (!any && G.peer_leaders > 0) {  // the group's last mapper: its leaders leave the device budget
+    std::lock_guard<std::mutex> lk2(g_lead_mu);
+    g_lead_reserved[G.device & 63] -= G.peer_leaders;
+    G.peer_leaders = 0;
+  }
 }
 
 int32_t comm_allreduce(loam_comm* c, void* d_buf, int64_t count, int32_t dtype, hipStream_t st) {

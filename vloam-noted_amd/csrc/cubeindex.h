@@ -92,25 +92,35 @@ __device__ inline bool cube_index_build(const float4* pts, uint32_t n, const int
       const uint32_t i = tid + k * nthreads;
       sr[k] = i < n ? ci_local_key(pts[i], corner) : CI_EMPTY;
     }
+    // a cube's points come in VoxelGrid order (z, y, x rows), so neighbouring lanes often share a
+    // cell: each run of equal keys in a wave takes its ranks with one table update by its first
+    // lane (the order of points within a cell is free: kNN ties go by cube position, k_knn)
+    const int lane = tid & 63;
+    const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes <= this one
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      if (sr[k] == CI_EMPTY) continue;
       const uint32_t key = sr[k];
-      uint32_t h = ci_hash(key, mask);
-      uint32_t rank;
-      while (true) {
-        const uint32_t old = atomicCAS(&lent[h], CI_EMPTY, key | (1u << 18));
-        if (old == CI_EMPTY) {
-          rank = 0;
-          break;
+      const uint32_t prev = (uint32_t)__shfl_up((int)key, 1, 64);
+      const uint64_t heads = __ballot(lane == 0 || prev != key);
+      const int head = 63 - __clzll(heads & le);  // this lane's run starts here
+      uint32_t base = 0;
+      if (key != CI_EMPTY && head == lane) {
+        const uint64_t after = heads & ~le;
+        const uint32_t run = (uint32_t)((after ? __ffsll((long long)after) - 1 : 64) - lane);
+        uint32_t h = ci_hash(key, mask);
+        while (true) {
+          const uint32_t old = atomicCAS(&lent[h], CI_EMPTY, key | (run << 18));
+          if (old == CI_EMPTY) break;
+          if ((old & CI_KEY_MASK) == key) {
+            base = atomicAdd(&lent[h], run << 18) >> 18;
+            break;
+          }
+          h = (h + 1) & mask;
         }
-        if ((old & CI_KEY_MASK) == key) {
-          rank = atomicAdd(&lent[h], 1u << 18) >> 18;
-          break;
-        }
-        h = (h + 1) & mask;
+        base |= h << 15;  // slot < 2^15, rank < n <= 2^14
       }
-      sr[k] = (h << 15) | rank;  // slot < 2^15, rank < n <= 2^14
+      const uint32_t hb = (uint32_t)__shfl((int)base, head, 64);
+      sr[k] = key == CI_EMPTY ? CI_EMPTY : hb + (uint32_t)(lane - head);
     }
     __syncthreads();
     if (prof && tid == 0) atomicAdd(prof, __builtin_readcyclecounter());  // minus the start below

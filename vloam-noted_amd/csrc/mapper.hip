@@ -1572,6 +1572,7 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
     const uint32_t so = *sb;
     __syncthreads();
     bool global = n > (uint32_t)VH_BIG_N;
+    uint32_t reuse_off = 0xFFFFFFFFu, reuse_cnt = 0;
     if (!global) {
       // the input-order filter sums every voxel of at most 2 members (order-free) and records the
       // others, then voxel_hot.h sums those in std::sort's order
@@ -1589,13 +1590,21 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
                                             tok, &F.err, D.pdbg ? D.pdbg + 50 : nullptr,
                                             D.pdbg ? D.pdbg + 72 : nullptr, D.pdbg ? D.pdbg + 82 : nullptr);
         // (over VH_MAX_N, a part too large for the LDS after the first partition: the global
-        // sort below writes the cube again, at a new arena offset)
+        // sort below writes the cube again, into the block the filter above allocated for it:
+        // the same voxels, so the same count)
         global = he < 0;
         __syncthreads();
+        if (global) {
+          const uint2 v = tab[cube];  // (thread 0 wrote it inside the filter, before the barrier)
+          reuse_off = v.x;
+          reuse_cnt = v.y;
+        }
       }
     }
     if (global) {  // the whole std::sort emulated in global memory (voxel_pcl.h)
       VxPclOut O;
+      O.reuse_off = reuse_off;
+      O.reuse_cnt = reuse_cnt;
       O.out = ar;
       O.tail = &F.arena_tail[m];
       O.cap = D.map_cap;
@@ -2020,6 +2029,11 @@ uint32_t next_pow2(uint32_t v) {
 }
 
 void free_all(loam_mapper* h) {
+  if (h->D.lm_peer && h->comm) {  // the group's LM peer buffer (kernels done: the caller synchronized)
+    comm_peer_release(h->comm);
+    h->D.lm_peer = nullptr;
+    h->D.lm_peer_flag = nullptr;
+  }
   for (void* p : h->allocs) (void)hipFree(p);
   h->allocs.clear();
   if (h->d_pub) (void)hipFree(h->d_pub);
@@ -2093,6 +2107,7 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   *out = nullptr;
   TRY(ensure_device(device));
   LOAM_HIP(hipSetDevice(device));
+  vh_spin_limit_from_env(device);
   auto* h = new loam_mapper;
   if (p) h->P = *p; else loam_params_default(&h->P);
   h->dev = device;
@@ -2147,8 +2162,10 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
       if (peer && h->lm_G > 0) {
         const size_t nd = (size_t)2 * n_streams * 2 * comm->size * LM_MAX_PASSES * LM_NACC;
         void* pb = nullptr;
-        if (comm_peer_buffer(comm, nd * sizeof(double) + (size_t)n_streams * 2 * comm->size * sizeof(uint32_t), &pb) ==
-            LOAM_OK) {
+        // the leaders (R x Bp) reserved against the device's LM capacity with every other group of
+        // this process: all of them must fit at once (comm.hip); else the two-kernel path
+        if (comm_peer_buffer(comm, nd * sizeof(double) + (size_t)n_streams * 2 * comm->size * sizeof(uint32_t),
+                             lm_padded(n_streams) * comm->size, cap, &pb) == LOAM_OK) {
           D.lm_peer = static_cast<double*>(pb);
           D.lm_peer_flag = reinterpret_cast<uint32_t*>(D.lm_peer + nd);
         } else {
@@ -2322,13 +2339,11 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
 }
 
 int32_t loam_mapper_create(const loam_params* p, int32_t device, int32_t n_streams, loam_mapper** out) {
-  vh_spin_limit_from_env();
   return mapper_create(p, device, n_streams, nullptr, out);
 }
 
 int32_t loam_mapper_create_sharded(const loam_params* p, int32_t device, int32_t n_streams, loam_comm* comm,
                                    loam_mapper** out) {
-  vh_spin_limit_from_env();
   if (!comm) {
     set_error("loam_mapper_create_sharded: null comm");
     return LOAM_ERR_ARG;
@@ -2366,6 +2381,7 @@ int32_t loam_mapper_destroy(loam_mapper* h) {
   if (!h) return LOAM_ERR_ARG;
   (void)hipSetDevice(h->dev);
   while (!h->q.empty()) (void)finish_oldest(h);
+  (void)hipStreamSynchronize(h->st);
   (void)hipStreamSynchronize(h->st2);
   free_all(h);
   delete h;
@@ -2470,15 +2486,25 @@ static hipError_t prof_begin(loam_mapper* h, int fam, hipEvent_t* stop, hipStrea
   *stop = h->ev_pool[k + 1];
   return hipEventRecord(h->ev_pool[k], st);
 }
-static hipError_t prof_end(loam_mapper* h, hipEvent_t stop, hipStream_t st) {
-  return (h->prof && stop) ? hipEventRecord(stop, st) : hipSuccess;
-}
-#define LAUNCH_ON(stream, fam, ...)                   \
-  do {                                                \
-    hipEvent_t stop_;                                 \
-    LOAM_HIP(prof_begin(h, (fam), &stop_, (stream))); \
-    __VA_ARGS__;                                      \
-    LOAM_HIP(prof_end(h, stop_, (stream)));           \
+// the stop event of a timed launch: recorded by end(), or, when the launch body returns early (a
+// TRY inside it), by the destructor, so no listed (start, stop) pair is left without its stop
+struct ProfStop {
+  hipEvent_t ev = nullptr;
+  hipStream_t st = nullptr;
+  hipError_t end() {
+    const hipError_t e = ev ? hipEventRecord(ev, st) : hipSuccess;
+    ev = nullptr;
+    return e;
+  }
+  ~ProfStop() { (void)end(); }
+};
+#define LAUNCH_ON(stream, fam, ...)                     \
+  do {                                                  \
+    ProfStop stop_;                                     \
+    stop_.st = (stream);                                \
+    LOAM_HIP(prof_begin(h, (fam), &stop_.ev, (stream))); \
+    __VA_ARGS__;                                        \
+    LOAM_HIP(stop_.end());                              \
   } while (0)
 #define LAUNCH(fam, ...) LAUNCH_ON(h->st, fam, __VA_ARGS__)
 
@@ -2887,9 +2913,13 @@ static int32_t mapper_finish_rec(loam_mapper* h, const FrameRec& R, bool replay)
         h->ev_fam[kept++] = h->ev_fam[k];
         continue;
       }
-      LOAM_HIP(q);
+      // a pair that cannot be timed (a launch whose enqueue failed between its events) is
+      // dropped from the list, not an error of this frame
       float ms = 0;
-      LOAM_HIP(hipEventElapsedTime(&ms, h->ev_pool[2 * k], h->ev_pool[2 * k + 1]));
+      if (q != hipSuccess || hipEventElapsedTime(&ms, h->ev_pool[2 * k], h->ev_pool[2 * k + 1]) != hipSuccess) {
+        (void)hipGetLastError();
+        continue;
+      }
       h->fam_ms[h->ev_fam[k]] += ms;
       h->fam_launches[h->ev_fam[k]]++;
     }

@@ -386,7 +386,7 @@ int32_t loam_voxel_grid_pcl(int32_t device, const float* in, int32_t n, float le
   int32_t rc = ensure_device(device);
   if (rc != LOAM_OK) return rc;
   LOAM_HIP(hipSetDevice(device));
-  vh_spin_limit_from_env();
+  vh_spin_limit_from_env(device);
   if (n <= VH_MAX_N) {
     DevBuf din, dout, drk, dhl, dhv, dfp, didx, dcnt, derr;
     const size_t m = std::max(n, 1);

@@ -999,12 +999,12 @@ int32_t loam_scanreg_create(const loam_params* p, int32_t device, loam_scanreg**
 }
 
 int32_t loam_scanreg_create_batch(const loam_params* p, int32_t device, int32_t max_frames, loam_scanreg** out) {
-  vh_spin_limit_from_env();
   if (!out || max_frames < 1) return LOAM_ERR_ARG;
   *out = nullptr;
   int32_t rc = ensure_device(device);
   if (rc != LOAM_OK) return rc;
   LOAM_HIP(hipSetDevice(device));
+  vh_spin_limit_from_env(device);
   auto* h = new loam_scanreg;
   if (p) h->P = *p; else loam_params_default(&h->P);
   if (h->P.scan_line != 16 && h->P.scan_line != 32 && h->P.scan_line != 64) {

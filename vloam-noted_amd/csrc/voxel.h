@@ -892,7 +892,17 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
       if (tid + u * NT < n0) acc(cc[u]);
-    for (uint32_t k = tid + U * NT; k < n0; k += NT) acc(C[k]);
+    // C points past the register-held ones: 4 loads in flight per step (one at a time, each pass
+    // over a large cube's remainder was a chain of memory round trips)
+    for (uint32_t k = tid + U * NT; k < n0; k += 4 * NT) {
+      float4 p[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (k + u * NT < n0) p[u] = C[k + u * NT];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (k + u * NT < n0) acc(p[u]);
+    }
 #pragma unroll
     for (int u = 0; u < UA; ++u)
       if (tid + u * NT < n1) acc(aa[u]);
@@ -969,9 +979,17 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
       if (cl[u] != NONE) hit[cl[u]] = (int)k;
     }
   }
-  for (uint32_t k = tid + U * NT; k < n0; k += NT) {
-    const uint32_t h = lookup(vx_key(g, C[k]));
-    if (h != NONE) hit[h] = (int)k;
+  for (uint32_t k = tid + U * NT; k < n0; k += 4 * NT) {
+    float4 p[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (k + u * NT < n0) p[u] = C[k + u * NT];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (k + u * NT < n0) {
+        const uint32_t h = lookup(vx_key(g, p[u]));
+        if (h != NONE) hit[h] = (int)(k + u * NT);
+      }
   }
   __syncthreads();
   vx_phase(S.prof, 1, &tp);
@@ -1082,10 +1100,17 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
 #pragma unroll
   for (int u = 0; u < U; ++u)
     if (tid + u * NT < n0) emit(tid + u * NT, cc[u], ck[u], cl[u]);
-  for (uint32_t k = tid + U * NT; k < n0; k += NT) {
-    const float4 c = C[k];
-    const uint32_t key = vx_key(g, c);
-    emit(k, c, key, lookup(key));
+  for (uint32_t k = tid + U * NT; k < n0; k += 4 * NT) {
+    float4 p[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (k + u * NT < n0) p[u] = C[k + u * NT];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (k + u * NT < n0) {
+        const uint32_t key = vx_key(g, p[u]);
+        emit(k + u * NT, p[u], key, lookup(key));
+      }
   }
   __syncthreads();
   // C points below new-only voxel r: inclusive prefix of cbelow (Dn + 1 entries)

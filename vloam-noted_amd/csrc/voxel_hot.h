@@ -32,6 +32,7 @@
 // a segment [lo, hi) owns Bs[lo/2 ..)), and every read of the segment precedes every write.
 #pragma once
 #include <cstdlib>
+#include <mutex>
 
 #include "stdsort.h"
 #include "voxel.h"
@@ -58,17 +59,20 @@ constexpr int VH_ERR_ANY = VH_ERR_ROOTS | VH_ERR_LIST | VH_ERR_SPIN;
 // while some listed subtree is unfinished.  2^24 spins of s_sleep 1 (~seconds) cannot run out
 // while the workgroup makes progress; when it does, the subtree that entry would have held is
 // left unsorted, so the filter flags VH_ERR_SPIN (-> LOAM_ERR_SYNC) instead of a silently wrong
-// centroid.  LOAM_VH_SPIN_LIMIT (environment, read once per process by vh_spin_limit_from_env)
-// lowers it: tests/test_gpu_vh_spin.py sets 0 to show the flag reaches the caller.
+// centroid.  LOAM_VH_SPIN_LIMIT (environment) lowers it: tests/test_gpu_vh_spin.py sets 0 to show
+// the flag reaches the caller.  vh_spin_limit_from_env(device) writes it once per device of this
+// translation unit's code object; the caller has made `device` current (hipMemcpyToSymbol writes
+// the current device's copy), and handles created from several threads serialise on the mutex.
 static __device__ uint32_t vh_spin_limit_g = 1u << 24;
-static inline void vh_spin_limit_from_env() {
-  static bool done = false;
-  if (done) return;
-  done = true;
-  if (const char* e = getenv("LOAM_VH_SPIN_LIMIT")) {
-    const uint32_t v = (uint32_t)strtoul(e, nullptr, 10);
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(vh_spin_limit_g), &v, sizeof(v));
-  }
+static inline void vh_spin_limit_from_env(int device) {
+  const char* e = getenv("LOAM_VH_SPIN_LIMIT");
+  if (!e || device < 0 || device >= 64) return;
+  static std::mutex mu;
+  static uint64_t done = 0;  // bit d: device d written
+  std::lock_guard<std::mutex> lk(mu);
+  if ((done >> device) & 1ull) return;
+  const uint32_t v = (uint32_t)strtoul(e, nullptr, 10);
+  if (hipMemcpyToSymbol(HIP_SYMBOL(vh_spin_limit_g), &v, sizeof(v)) == hipSuccess) done |= 1ull << device;
 }
 
 struct VhLess {

@@ -69,6 +69,9 @@ struct VxPclOut {
   uint32_t* res_off = nullptr;
   uint32_t* res_cnt = nullptr;
   uint32_t* stable_out = nullptr;
+  // a block an earlier filter of the same points already allocated (the mapper's fall-back from
+  // the LDS emulation, mapper.hip): reused when the output fits it, instead of a second block
+  uint32_t reuse_off = 0xFFFFFFFFu, reuse_cnt = 0;
 };
 
 // All NT threads call it.  P(i): the i-th input point (i < n).  ws: >= NT / 64 + 1 words of
@@ -84,6 +87,7 @@ __device__ inline void voxel_grid_pcl(const PF& P, int n, float leaf, const VxPc
     if (O.stable_out) *O.stable_out = fixed ? base + 1 : 0u;
   };
   auto alloc = [&](uint32_t cnt) {  // thread 0; 0xFFFFFFFF: no room
+    if (O.reuse_off != 0xFFFFFFFFu && cnt <= O.reuse_cnt) return O.reuse_off;
     uint32_t b = O.tail ? atomicAdd(O.tail, cnt) : 0u;
     if (b + cnt > O.cap) {
       atomicOr(err, VX_ERR_OUTPUT);
