@@ -186,13 +186,14 @@ def make_frames(seed, n_frames, n_az, device, raw_frames=(), prior="odometry"):
 def step_inputs(frames, streams, stride, k, first=0):
     """batched input arrays for step k (stream b consumes frame b*stride + k); streams
     first .. first + streams - 1 of the run, numbered from 0 in their handle"""
+    from loam_amd.mapping import BatchMapper
     fs = [frames[(first + b) * stride + k] for b in range(streams)]
-    return (np.arange(streams, dtype=np.int32),
-            np.array([f["corner"].data_ptr() for f in fs], dtype=np.uint64),
-            np.array([len(f["corner"]) for f in fs], dtype=np.int32),
-            np.array([f["surf"].data_ptr() for f in fs], dtype=np.uint64),
-            np.array([len(f["surf"]) for f in fs], dtype=np.int32),
-            np.array([f["q"] for f in fs]), np.array([f["t"] for f in fs]))
+    return BatchMapper.batch_args(np.arange(streams, dtype=np.int32),
+                                  np.array([f["corner"].data_ptr() for f in fs], dtype=np.uint64),
+                                  np.array([len(f["corner"]) for f in fs], dtype=np.int32),
+                                  np.array([f["surf"].data_ptr() for f in fs], dtype=np.uint64),
+                                  np.array([len(f["surf"]) for f in fs], dtype=np.int32),
+                                  np.array([f["q"] for f in fs]), np.array([f["t"] for f in fs]))
 
 
 def run_steps(mapper, plan, first, count, poses=None):
@@ -201,7 +202,7 @@ def run_steps(mapper, plan, first, count, poses=None):
     the solve already copied back)"""
     iters = 0
     for k in range(first, first + count):
-        mapper.input_device_batch(*plan[k])
+        mapper.input_device_batch_args(plan[k])
         mapper.solve()
         iters += mapper.total_iterations()
         if poses is not None:
@@ -215,11 +216,11 @@ def run_steps_pipelined(mapper, plan, first, count, poses=None):
     waited for: the same results as run_steps, frame after frame, without the host round trip
     between frames"""
     iters = 0
-    mapper.input_device_batch(*plan[first])
+    mapper.input_device_batch_args(plan[first])
     mapper.solve_async()
     for k in range(first + 1, first + count + 1):
         if k < first + count:
-            mapper.input_device_batch(*plan[k])
+            mapper.input_device_batch_args(plan[k])
             mapper.solve_async()  # queued behind frame k - 1
         mapper.wait()  # frame k - 1
         iters += mapper.total_iterations()  # (results: frame k - 1, the newest finished)
@@ -888,17 +889,65 @@ def main():
         finally:
             os.dup2(saved, 1)
             os.close(saved)
-        sm = BatchMapper(Bs, device=local, max_map_points=args.map_points, comm=scomm)
         splan = [step_inputs(sframes, Bs, args.stride, k) for k in range(pre + K)]
-        run_steps(sm, splan, 0, pre)
-        barrier()
-        t0 = time.perf_counter()
-        sit = run_steps(sm, splan, pre, K)
-        barrier()
-        sdt = time.perf_counter() - t0
-        sm.close()
+
+        def sharded_run(two_kernel):
+            """map building untimed, then K timed steps of the sharded handle.  Default: the LM
+            schedule the library picks (one persistent round per outer round; across processes
+            the per-iteration sums meet in IPC-mapped peer buffers, loam_mapper_lm_path 3), its
+            cross-rank wait bounded to ~1 s (LOAM_PEER_SPIN_LIMIT) so that a transport that never
+            delivers ends in LOAM_ERR_SYNC, counted, not in a hang.  two_kernel: the LM forced to
+            eval -> all-reduce -> step launches per pass (LOAM_LM_PERSISTENT=0, read at create).
+            Every rank solves every frame whatever an earlier one returned (the collectives stay
+            matched); the failures are summed over the ranks"""
+            env = {"LOAM_LM_PERSISTENT": "0"} if two_kernel else {"LOAM_PEER_SPIN_LIMIT": str(1 << 20)}
+            saved_env = {k: os.environ.get(k) for k in env}
+            os.environ.update(env)
+            try:
+                sm = BatchMapper(Bs, device=local, max_map_points=args.map_points, comm=scomm)
+            finally:
+                for k, v in saved_env.items():
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
+            path = sm.lm_path()
+            errs = {"n": 0, "last": None}
+
+            def steps(first, count):
+                it = 0
+                for k in range(first, first + count):
+                    sm.input_device_batch_args(splan[k])
+                    try:
+                        sm.solve()
+                        it += sm.total_iterations()
+                    except Exception as e:  # noqa: BLE001 - counted, reported in the line
+                        errs["n"] += 1
+                        errs["last"] = repr(e)[:300]
+                return it
+
+            steps(0, pre)
+            barrier()
+            t0 = time.perf_counter()
+            it = steps(pre, K)
+            barrier()
+            dt = time.perf_counter() - t0
+            sm.close()
+            nerr = errs["n"]
+            if world > 1:
+                t = torch.tensor([nerr], dtype=torch.int64, device=f"cuda:{local}")
+                dist.all_reduce(t)
+                nerr = int(t.item())
+            return it, dt, {"lm_path": path, "failed_solves": nerr, "last_error": errs["last"]}
+
+        sit, sdt, sinfo = sharded_run(False)
+        # the per-iteration cost a multi-rank RCCL group pays without the peer buffers (10 eval /
+        # all-reduce / step launch triples per frame), measured here at this world size (at one
+        # rank the all-reduce is RCCL's one-rank identity on the stream)
+        tit, tdt, tinfo = sharded_run(True)
         scomm.close()
         sit_all, sdt_max = aggregate(sit, sdt, world, f"cuda:{local}")
+        tit_all, tdt_max = aggregate(tit, tdt, world, f"cuda:{local}")
         # the same streams and frames through an unsharded handle on this GPU (the reference
         # point of the sharding overhead at one rank)
         um = BatchMapper(Bs, device=local, max_map_points=args.map_points)
@@ -914,7 +963,17 @@ def main():
                 "ms_per_step": round(1e3 * sdt_max / K, 4), "streams": Bs, "ranks": world, "scaling": "strong",
                 "frames_per_step": Bs, "unsharded_same_streams": round(uit / udt, 3),
                 "sharded_over_unsharded": round((sit_all / world / sdt_max) / (uit / udt), 4),
-                "transport": "RCCL" if world > 1 else "one rank: every collective is the identity",
+                **sinfo,
+                "two_kernel_lm": {"value": round(tit_all / world / tdt_max, 3),
+                                  "ms_per_step": round(1e3 * tdt_max / K, 4),
+                                  "over_persistent": round((tit_all / tdt_max) / (sit_all / sdt_max), 4),
+                                  **tinfo,
+                                  "mode": "the same sharded handle with LOAM_LM_PERSISTENT=0: per LM pass "
+                                          "k_lm_eval -> RCCL all-reduce (29 f64 per stream) -> k_lm_step, the "
+                                          "schedule of RCCL groups of more than one rank"},
+                "transport": ("RCCL (5-NN all-gather, submap sizes, pose agreement); the LM's per-iteration "
+                              "sums in IPC-mapped peer buffers when lm_path is 3" if world > 1 else
+                              "one rank: every collective is the identity"),
                 "mode": "every stream split over all ranks (block-owned map shards, per-round 5-NN all-gather, "
                         "per-LM-iteration normal-equation all-reduce); iterations counted once per stream",
                 "thread_ranks": thread_ranks}
@@ -928,7 +987,7 @@ def main():
         handle on the same streams and frames"""
         import threading
         from loam_amd.comm import Comm
-        plan = [tuple(a[:n_streams] for a in step) for step in splan[:pre + steps]]
+        plan = [BatchMapper.batch_args(*(a[:n_streams] for a in step[-1])) for step in splan[:pre + steps]]
         um = BatchMapper(n_streams, device=local, max_map_points=args.map_points)
         run_steps(um, plan, 0, pre)
         torch.cuda.synchronize(local)

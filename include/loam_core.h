@@ -307,6 +307,14 @@ int32_t loam_mapper_stats(loam_mapper* h, int32_t stream, loam_map_stats* st);
 int32_t loam_mapper_debug_counters(loam_mapper* h, uint64_t* out, int32_t n, int32_t reset);
 /* sum over the streams solved by the last loam_mapper_solve of their LM iterations (both rounds) */
 int64_t loam_mapper_total_iterations(loam_mapper* h);
+/* the LM schedule the handle runs (decided at create; laser_mapping.cpp:709-717 either way):
+ * 0 two launches per Ceres iteration (k_lm_eval, then k_lm_step; sharded over several ranks the
+ *   normal equations are all-reduced between them), 1 one persistent launch per outer round
+ *   (k_lm_round), 2 the in-process group's round (k_lm_group: every rank of a
+ *   loam_comm_create_local group in one launch), 3 the persistent round of ranks in separate
+ *   processes, their per-iteration sums meeting in IPC-mapped peer buffers (RCCL / callback comms;
+ *   LOAM_PEER_LM=0 at create keeps 0) */
+int32_t loam_mapper_lm_path(loam_mapper* h);
 /* stats of streams 0..n-1 */
 int32_t loam_mapper_stats_all(loam_mapper* h, loam_map_stats* out, int32_t n);
 

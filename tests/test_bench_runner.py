@@ -18,7 +18,7 @@ class QueueMapper:
         self.offset = offset
         self.calls = []
 
-    def input_device_batch(self, *plan):
+    def input_device_batch_args(self, plan):
         self.given = plan[0]
 
     def solve_async(self):

@@ -722,3 +722,43 @@ def test_exact_refilter_of_a_cube_over_lds(seq, target):
     _check_map(m, 0, after)
     assert len(after["surf"][cube]) < len(surf[cube])  # the re-filter merged the duplicates
     m.close()
+
+
+@pytest.mark.parametrize("exact", [1, 0])
+def test_cube_content_outside_its_bounds(seq, exact):
+    """content set through the API need not lie in its cube: a merge of such a cube keys its
+    voxels from the cube's corner only while every point lies in the cube's key box
+    (VoxSeg::anchored), else it takes the full filter.  The centre cube (which every frame's
+    insertion reaches) holds extra points 600 m above it (no query comes near them: a kNN of the
+    cube's cell index, which keys cells inside the cube, and the oracle's KD-tree agree); three
+    frames from that state against the oracle from the same state: poses, counts and (PCL order)
+    maps as the oracle's"""
+    import loam_oracle as O
+    rec = seq[7]
+    state = {k: (dict(v) if isinstance(v, dict) else v) for k, v in rec["before"].items()}
+    c = rec["stats"].center
+    cube = int(c[0] + 21 * c[1] + 441 * c[2])
+    for key in ("corner", "surf"):
+        pts = state[key].get(cube)
+        assert pts is not None and len(pts) > 100
+        far = pts[: len(pts) // 3].copy()
+        far[:, 2] += 600.0
+        state[key][cube] = np.concatenate([pts, far])
+    ref = O.LaserMapping()
+    ref.set_state(state["cen"], state["q"], state["t"])
+    for which, key in ((0, "corner"), (1, "surf")):
+        for cb, pts in state[key].items():
+            ref.set_cube(which, cb, pts)
+    m = BatchMapper(1, exact_voxel_order=exact)
+    load_state(m, 0, state)
+    for f in (7, 8, 9):
+        r = seq[f]
+        ref.input(r["corner"], r["surf"], None, r["q_wodom"], r["t_wodom"])
+        ref.solve()
+        m.input(0, r["corner"], r["surf"], r["q_wodom"], r["t_wodom"])
+        m.solve()
+        _check_frame(m, 0, dict(pose=ref.pose(), stats=ref.stats()))
+    if exact:  # (points within a few ulps: the insertion poses differ by ~1e-9, Cholesky vs QR)
+        _check_map(m, 0, {"corner": ref.cubes(0), "surf": ref.cubes(1)})
+        assert len(m.cubes(0, 1)[cube]) == len(ref.cubes(1)[cube])
+    m.close()

@@ -34,3 +34,4 @@ def test_std_sort_permutation_model(tmp_path):
     r = _build_run(tmp_path, "stdsort_model.cpp")
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout
+

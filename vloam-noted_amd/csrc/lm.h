@@ -21,6 +21,8 @@
 // cost AND its normal equations (used only if the step is accepted), so an iteration costs
 // exactly one pass over the correspondences.
 #pragma once
+#include <cstdlib>
+#include <mutex>
 #include <type_traits>
 #include "common.h"
 #include "device_math.h"
@@ -592,6 +594,20 @@ constexpr int LM_MAX_PASSES = 8;          // a round needs <= 1 + max_num_iterat
 constexpr uint32_t LM_SPIN_LIMIT = 1u << 21;
 constexpr uint32_t LM_PEER_SPIN_LIMIT = 1u << 24;  // the cross-rank wait: other ranks' kernels
                                                    // start after their own earlier kernels
+// the cross-rank wait's bound as the kernels read it: LOAM_PEER_SPIN_LIMIT (environment, written
+// per device when a mapper is created there) lowers it, so that tests can show an exhausted wait
+// reaching the caller as LOAM_ERR_SYNC (tests/test_gpu_shard_mp.py)
+static __device__ uint32_t lm_peer_spin_limit_g = LM_PEER_SPIN_LIMIT;
+static inline void lm_peer_spin_limit_from_env(int device) {
+  const char* e = getenv("LOAM_PEER_SPIN_LIMIT");
+  if (!e || device < 0 || device >= 64) return;
+  static std::mutex mu;
+  static uint64_t done = 0;
+  std::lock_guard<std::mutex> lk(mu);
+  if ((done >> device) & 1ull) return;
+  const uint32_t v = (uint32_t)strtoul(e, nullptr, 10);
+  if (hipMemcpyToSymbol(HIP_SYMBOL(lm_peer_spin_limit_g), &v, sizeof(v)) == hipSuccess) done |= 1ull << device;
+}
 // sync words per solve, zeroed before the launch: [1] generation (pass + 1 of the published
 // evaluation point), [2] its status, [4 + p] claims of pass p's shares 1.. (share 0 is the
 // leader's), [4 + LM_MAX_PASSES + p] shares 1.. of pass p completed
@@ -600,6 +616,24 @@ constexpr int LM_SYNC_WORDS = 4 + 2 * LM_MAX_PASSES;
 __device__ inline bool lm_spin_ge(uint32_t* w, uint32_t target, uint32_t limit = LM_SPIN_LIMIT) {
   for (uint32_t spins = 0;; ++spins) {
     if (__hip_atomic_load(w, RLX_AGENT) >= target) return true;
+    if (spins >= limit) return false;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// the cross-process exchange (LmJob::ipc): peer buffers another process (perhaps another GPU over
+// xGMI) reads, so every access is a system-scope atomic (written through / read past every cache
+// on the way), data and flags alike, in either build
+#define RLX_SYS __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM
+__device__ inline void lm_sys_store(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v), RLX_SYS);
+}
+__device__ inline double lm_sys_load(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), RLX_SYS));
+}
+__device__ inline bool lm_spin_ge_sys(uint32_t* w, uint32_t target, uint32_t limit) {
+  for (uint32_t spins = 0;; ++spins) {
+    if (__hip_atomic_load(w, RLX_SYS) >= target) return true;
     if (spins >= limit) return false;
     __builtin_amdgcn_s_sleep(2);
   }
@@ -631,6 +665,12 @@ struct LmJob {
   double* peer = nullptr;
   uint32_t* peer_flag = nullptr;
   uint32_t flag_base = 0;
+  // ranks in separate processes (loam_comm kinds 0 / 1, each rank's launch on its own stream): each
+  // rank owns a buffer the others map through IPC handles; ipc[r] is rank r's slot base (double*),
+  // ipc[nrank + r] its flag base (uint32_t*), as this process maps them; this solve's slots start
+  // ipc_slot_off doubles in ([LM_MAX_PASSES][LM_NACC]), its flag ipc_flag_off words in
+  const unsigned long long* ipc = nullptr;
+  size_t ipc_slot_off = 0, ipc_flag_off = 0;
 };
 
 // share c of pass `pass` at X -> part[c], then counted complete (release)
@@ -797,7 +837,39 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (J.nrank > 1) {  // this rank's sums to its slot, then every rank's, in rank order
+      if (J.nrank > 1 && J.ipc) {  // ranks of other processes: their IPC-mapped buffers
+        const uint32_t want = J.flag_base + (uint32_t)pass + 1u;
+        const size_t so = J.ipc_slot_off + (size_t)pass * LM_NACC;
+        double* mine = reinterpret_cast<double*>(J.ipc[J.rank]) + so;
+        if (lane < LM_NACC) lm_sys_store(&mine[lane], sred[lane]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+#if LM_HANDOFF_FENCES
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the memory model's recipe
+#endif
+          __hip_atomic_store(reinterpret_cast<uint32_t*>(J.ipc[J.nrank + J.rank]) + J.ipc_flag_off, want, RLX_SYS);
+        }
+        const bool ok = lane >= J.nrank ||
+                        lm_spin_ge_sys(reinterpret_cast<uint32_t*>(J.ipc[J.nrank + lane]) + J.ipc_flag_off, want,
+                                       lm_peer_spin_limit_g);
+        if (__ballot(!ok) != 0ull) {
+          if (lane == 0) {
+            atomicOr(J.err, J.err_code);
+            sstat = -1;
+          }
+        } else if (lane < LM_NACC) {
+#if LM_HANDOFF_FENCES
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#endif
+          double v = lm_sys_load(reinterpret_cast<const double*>(J.ipc[0]) + so + lane);
+          for (int r = 1; r < J.nrank; ++r) v += lm_sys_load(reinterpret_cast<const double*>(J.ipc[r]) + so + lane);
+          sred[lane] = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      } else if (J.nrank > 1) {  // this rank's sums to its slot, then every rank's, in rank order
         const uint32_t want = J.flag_base + (uint32_t)pass + 1u;
         double* mine = J.peer + ((size_t)J.rank * LM_MAX_PASSES + pass) * LM_NACC;
         if (lane < LM_NACC) lm_part_store(&mine[lane], sred[lane]);
@@ -807,7 +879,7 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
           lm_release();
           __hip_atomic_store(&J.peer_flag[J.rank], want, RLX_AGENT);
         }
-        const bool ok = lane >= J.nrank || lm_spin_ge(&J.peer_flag[lane], want, LM_PEER_SPIN_LIMIT);
+        const bool ok = lane >= J.nrank || lm_spin_ge(&J.peer_flag[lane], want, lm_peer_spin_limit_g);
         if (__ballot(!ok) != 0ull) {  // a rank did not come: this rank's LM stops here
           if (lane == 0) {
             atomicOr(J.err, J.err_code);
@@ -829,7 +901,8 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
         const unsigned long long ts = J.prof ? __builtin_readcyclecounter() : 0ull;
         // the step works on the LDS state in place: a register copy of the whole state (~140
         // VGPRs) spilled into AGPRs beside the solve's temporaries (tools/mb_lmstep2.hip: 5.7k ->
-        // 4.8k cycles per step)
+        // 4.8k cycles per step; in the kernel 7.4k against 9.9k for a copy of the fields a step
+        // touches, taken once and written back once, profiles/r6_lm_step_regs.txt)
         lm_step(ls, sred);
         if (J.prof) atomicAdd(&J.prof[-2], __builtin_readcyclecounter() - ts);  // [15]: the step alone
       }

@@ -193,6 +193,11 @@ struct MapperDev {
   // the flags [B][2 rounds][nrank] (lm.h LmJob)
   double* lm_peer = nullptr;
   uint32_t* lm_peer_flag = nullptr;
+  // ranks in separate processes (RCCL / callback comms): every rank's LM peer buffer as this
+  // process maps it (ipc_peer_setup): [r] slot base, [nrank + r] flag base; each buffer holds
+  // [2 frame parities][ipc_B][2 rounds][LM_MAX_PASSES][LM_NACC] f64, then flags [ipc_B][2 rounds]
+  const unsigned long long* ipc_tab = nullptr;
+  int ipc_B = 0;
   // few streams: the stack VoxelGrid of a (stream, map) split over stack_k workgroups by voxel
   // idx range (k_stack_part + k_stack_cat), else one workgroup (k_stack_ds)
   int stack_k = 0;
@@ -443,7 +448,13 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_part(MapperDev D) {
   auto blo = [&](uint32_t b) { return (uint32_t)(((unsigned long long)b * V + VX_NB - 1) / VX_NB); };
   for (int b = tid; b < VX_NB; b += VX_THREADS) hist[b] = 0;
   __syncthreads();
-  for (uint32_t i = tid; i < N; i += VX_THREADS) atomicAdd(&hist[bucket(vx_key(g, P(i)))], 1u);
+  for (uint32_t i0 = tid; i0 < N; i0 += VX_UNROLL * VX_THREADS) {  // loads in flight together
+    uint32_t kk4[VX_UNROLL];
+    vx_keys4(g, P, N, i0, kk4);
+#pragma unroll
+    for (int u = 0; u < VX_UNROLL; ++u)
+      if (kk4[u] != VX_EMPTY) atomicAdd(&hist[bucket(kk4[u])], 1u);
+  }
   __syncthreads();
   // range r starts at the first bucket whose points-before count reaches r N / K: a block scan
   // of the histogram (two buckets per thread) and a test at every bucket
@@ -1231,6 +1242,14 @@ __global__ void __launch_bounds__(LM_THREADS) k_lm_round(MapperDev D, int round,
   J.err = &F.err;
   J.err_code = MAP_ERR_LM_SYNC;
   J.prof = D.pdbg ? D.pdbg + 17 : nullptr;
+  if (D.ipc_tab) {  // ranks in other processes: the per-pass sums meet in their mapped buffers
+    J.rank = D.rank;
+    J.nrank = D.nrank;
+    J.ipc = D.ipc_tab;
+    J.ipc_slot_off = (((size_t)(F.epoch & 1u) * D.ipc_B + s) * 2 + round) * LM_MAX_PASSES * LM_NACC;
+    J.ipc_flag_off = (size_t)s * 2 + round;
+    J.flag_base = F.epoch * (uint32_t)LM_MAX_PASSES;
+  }
   lm_round_device<LM_THREADS>(J, g, G);
 }
 
@@ -1558,6 +1577,8 @@ __device__ inline void revox_item(MapperDev& D, int s, int m, int slot, int cube
   S.scratch_cap = D.scratch_cap;
   S.err = &F.err;
   S.prof = D.pdbg ? D.pdbg + 11 : nullptr;  // merge phases: dbg[11..14]
+  S.anchored = 1;  // a merge keys the voxels from the cube's corner (VoxSeg::anchored)
+  cube_corner(cube, F.cen, S.anchor);
   bool merged = false;
   const unsigned long long t0 = __builtin_readcyclecounter();
   const bool fixed = n_new > 0 && n_new <= VX_MERGE_CAP && cv.y > 0 && *tok == cv.x + 1;
@@ -1967,6 +1988,9 @@ struct loam_mapper {
   // the window that receive points; a write past the capacity is reported (err flags)
   uint32_t compact_at = 0;
   int lm_G = 0;  // workgroups per stream of k_lm_round (0: two-kernel path k_lm_eval / k_lm_step)
+  bool want_ipc = false;            // cross-process ranks: set up the IPC peer buffers at create
+  void* ipc_own = nullptr;          // this rank's LM peer buffer (ipc_peer_setup)
+  std::vector<void*> ipc_open;      // the other ranks' buffers, mapped from their IPC handles
   int knn_cs = 0;     // k_knn: 8 lanes per query splitting the cells (handles of <= 4 streams), else 0
                       // (one lane per query)
   loam_comm* comm = nullptr;  // sharded mode (loam_mapper_create_sharded)
@@ -2034,6 +2058,11 @@ void free_all(loam_mapper* h) {
     h->D.lm_peer = nullptr;
     h->D.lm_peer_flag = nullptr;
   }
+  for (void* p : h->ipc_open) (void)hipIpcCloseMemHandle(p);
+  h->ipc_open.clear();
+  if (h->ipc_own) (void)hipFree(h->ipc_own);
+  h->ipc_own = nullptr;
+  h->D.ipc_tab = nullptr;
   for (void* p : h->allocs) (void)hipFree(p);
   h->allocs.clear();
   if (h->d_pub) (void)hipFree(h->d_pub);
@@ -2098,6 +2127,107 @@ int32_t check_stream(loam_mapper* h, int32_t s) {
 
 extern "C" {
 
+// The persistent LM across processes (the peer one-shot reduce instead of an RCCL
+// all-reduce per LM iteration): every rank allocates its LM peer buffer, exports it as an IPC handle,
+// the handles travel through the comm's own all-gather, and every rank maps the others'.  All ranks
+// take the same decision (each one's outcome is all-gathered): on any failure every rank keeps the
+// two-kernel path.  Returns LOAM_OK with D.ipc_tab set, or LOAM_OK without it (fall back), or the
+// comm's error.
+static int32_t ipc_peer_setup(loam_mapper* h) {
+  loam_comm* c = h->comm;
+  MapperDev& D = h->D;
+  const int R = c->size, me = c->rank;
+  const size_t B = h->B, nslot = 2 * B * 2 * LM_MAX_PASSES * LM_NACC;
+  const size_t bytes = nslot * sizeof(double) + B * 2 * sizeof(uint32_t);
+  struct Msg {
+    hipIpcMemHandle_t hdl;
+    int32_t ok, pad;
+  };
+  static_assert(sizeof(Msg) % 8 == 0, "exchange record");
+  Msg mine{};
+  void* buf = nullptr;
+  // uncached device memory where the runtime offers it (its accesses bypass the caches of every
+  // agent, as RCCL's flags); else ordinary device memory (the accesses are system-scope atomics)
+  if (hipExtMallocWithFlags(&buf, bytes, hipDeviceMallocUncached) != hipSuccess) {
+    (void)hipGetLastError();
+    buf = nullptr;
+    if (hipMalloc(&buf, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      buf = nullptr;
+    }
+  }
+  mine.ok = buf && hipMemset(buf, 0, bytes) == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+            hipIpcGetMemHandle(&mine.hdl, buf) == hipSuccess;
+  if (!mine.ok) (void)hipGetLastError();
+  Msg* dsend = nullptr;
+  Msg* drecv = nullptr;
+  std::vector<Msg> all(R);
+  auto cleanup = [&] {
+    if (dsend) (void)hipFree(dsend);
+    if (drecv) (void)hipFree(drecv);
+    dsend = drecv = nullptr;
+  };
+  LOAM_HIP(hipMalloc(&dsend, sizeof(Msg)));
+  if (hipMalloc(&drecv, sizeof(Msg) * R) != hipSuccess) {
+    cleanup();
+    return LOAM_ERR_HIP;
+  }
+  auto exchange = [&]() -> int32_t {  // mine -> all (every rank's, in rank order)
+    if (hipMemcpy(dsend, &mine, sizeof(Msg), hipMemcpyHostToDevice) != hipSuccess) return LOAM_ERR_HIP;
+    TRY(comm_allgather(c, dsend, drecv, (int64_t)sizeof(Msg), h->st));
+    if (hipStreamSynchronize(h->st) != hipSuccess ||
+        hipMemcpy(all.data(), drecv, sizeof(Msg) * R, hipMemcpyDeviceToHost) != hipSuccess)
+      return LOAM_ERR_HIP;
+    return LOAM_OK;
+  };
+  int32_t rc = exchange();
+  bool ok = rc == LOAM_OK;
+  for (int r = 0; r < R && ok; ++r) ok = all[r].ok != 0;
+  std::vector<unsigned long long> tab(2 * (size_t)R, 0ull);
+  if (ok) {  // map the others' buffers; then agree that every rank mapped every buffer
+    for (int r = 0; r < R; ++r) {
+      void* p = buf;
+      if (r != me) {
+        p = nullptr;
+        if (hipIpcOpenMemHandle(&p, all[r].hdl, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+          (void)hipGetLastError();
+          p = nullptr;
+        } else {
+          h->ipc_open.push_back(p);
+        }
+      }
+      tab[r] = reinterpret_cast<unsigned long long>(p);
+      tab[R + r] = p ? reinterpret_cast<unsigned long long>(static_cast<char*>(p) + nslot * sizeof(double)) : 0ull;
+      if (!p) ok = false;
+    }
+    const hipIpcMemHandle_t keep = mine.hdl;
+    mine = Msg{};
+    mine.hdl = keep;
+    mine.ok = ok ? 1 : 0;
+    if (rc == LOAM_OK) rc = exchange();
+    ok = rc == LOAM_OK;
+    for (int r = 0; r < R && ok; ++r) ok = all[r].ok != 0;
+  }
+  cleanup();
+  if (!ok) {  // every rank arrives here alike: the two-kernel path
+    for (void* p : h->ipc_open) (void)hipIpcCloseMemHandle(p);
+    h->ipc_open.clear();
+    if (buf) (void)hipFree(buf);
+    return rc;
+  }
+  h->ipc_own = buf;
+  unsigned long long* dtab = nullptr;
+  const int32_t arc = dalloc(h, &dtab, tab.size());
+  if (arc != LOAM_OK) return arc;
+  // on the handle's stream, behind dalloc's zero fill there (a null-stream copy is not ordered
+  // after it: the fill could land last and leave null peer pointers)
+  LOAM_HIP(hipMemcpyAsync(dtab, tab.data(), sizeof(unsigned long long) * tab.size(), hipMemcpyHostToDevice, h->st));
+  LOAM_HIP(hipStreamSynchronize(h->st));
+  D.ipc_tab = dtab;
+  D.ipc_B = (int)B;
+  return LOAM_OK;
+}
+
 static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_streams, loam_comm* comm,
                              loam_mapper** out) {
   if (!out || n_streams <= 0) {
@@ -2108,6 +2238,7 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   TRY(ensure_device(device));
   LOAM_HIP(hipSetDevice(device));
   vh_spin_limit_from_env(device);
+  lm_peer_spin_limit_from_env(device);
   auto* h = new loam_mapper;
   if (p) h->P = *p; else loam_params_default(&h->P);
   h->dev = device;
@@ -2145,7 +2276,12 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     // persistent round (peer slots, lm.h); other transports all-reduce between two kernels per
     // pass.  At one rank every collective is the identity and the round stays one launch.
     const bool peer = comm && comm->size > 1 && comm->kind == 2;
-    if (allow && (!comm || comm->size == 1 || peer) &&
+    // ranks in separate processes: the same persistent round, meeting in IPC-mapped peer buffers
+    // (ipc_peer_setup, below, once the stream exists; LOAM_PEER_LM=0 keeps the two-kernel path)
+    const char* ienv = std::getenv("LOAM_PEER_LM");
+    const bool ipc = comm && comm->size > 1 && comm->kind != 2 && !(ienv && ienv[0] == '0');
+    h->want_ipc = false;
+    if (allow && (!comm || comm->size == 1 || peer || ipc) &&
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_lm_round, LM_THREADS, 0) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess) {
       // 256 threads x 256 VGPRs: exactly one block per CU; the API can over-report by one
@@ -2159,6 +2295,12 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
       h->lm_G = std::min(LM_EBLK, std::min(16, cap / (peer ? lm_padded(n_streams) * comm->size : n_streams)));
       const char* genv = std::getenv("LOAM_LM_G");  // measurement override
       if (genv && std::atoi(genv) > 0) h->lm_G = std::min(LM_EBLK, std::atoi(genv));
+      // cross-process ranks: every rank's leaders wait for each other; they fit even if every rank
+      // shared this device (the test's two processes on one GPU); the members are claimed (lm.h)
+      if (ipc && h->lm_G > 0) {
+        if (lm_padded(n_streams) * comm->size <= cap) h->want_ipc = true;
+        else h->lm_G = 0;
+      }
       if (peer && h->lm_G > 0) {
         const size_t nd = (size_t)2 * n_streams * 2 * comm->size * LM_MAX_PASSES * LM_NACC;
         void* pb = nullptr;
@@ -2334,6 +2476,10 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
     F.pose[3] = F.wodom[3] = F.wmap[3] = 1.0;
   }
   if (hipStreamSynchronize(h->st) != hipSuccess) return fail(LOAM_ERR_HIP);  // zero-fills done
+  if (h->want_ipc) {  // collective: every rank of the comm creates its mapper
+    if ((rc = ipc_peer_setup(h)) != LOAM_OK) return fail(rc);
+    if (!D.ipc_tab) h->lm_G = 0;  // some rank could not map the buffers: the two-kernel path
+  }
   *out = h;
   return LOAM_OK;
 }
@@ -2523,6 +2669,14 @@ int32_t loam_mapper_input_device_batch(loam_mapper* h, int32_t n, const int32_t*
     if (rc != LOAM_OK) return rc;
   }
   return LOAM_OK;
+}
+
+int32_t loam_mapper_lm_path(loam_mapper* h) {
+  if (!h) return LOAM_ERR_ARG;
+  if (h->lm_G <= 0) return 0;
+  if (h->D.lm_peer) return 2;
+  if (h->D.ipc_tab) return 3;
+  return 1;
 }
 
 int64_t loam_mapper_total_iterations(loam_mapper* h) {

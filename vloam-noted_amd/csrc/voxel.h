@@ -71,6 +71,13 @@ struct VoxSeg {
                                            // hash, sort + scan, member lists + centroids]
   VxHot hot{};  // exact order (hot.rk set): record the hot voxels instead of summing them (the
                 // stable token then covers the cold voxels only; voxel_hot.h)
+  // a map cube's merge (vx_merge_fixed_point): its lower corner in whole metres.  Every point of
+  // the cube lies within [corner, corner + 50] (laser_mapping.cpp:747-756), so the voxel keys can
+  // be taken relative to the corner's voxel instead of the points' bounding box: the same order
+  // (PCL's idx is lexicographic in (z, y, x) whatever its origin) without the bounding-box pass;
+  // a point outside the margin (content set through the API) falls back to the full filter
+  int anchored = 0;
+  int anchor[3] = {0, 0, 0};
 };
 
 // thread 0 adds the cycles since *t to prof[k] and restarts *t (phase counters; call after a barrier)
@@ -215,24 +222,47 @@ __device__ inline bool vx_centroids(const VxGeom& g, const VxSrc& P, uint32_t N,
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   unsigned long long tq = __builtin_readcyclecounter();
   bool moved = false;
-  float4 pn = make_float4(0.f, 0.f, 0.f, 0.f);
-  if ((uint32_t)tid < N) pn = P(tid);
-  for (uint32_t c = 0; c < N; c += VX_THREADS) {
-    const uint32_t i = c + tid;
-    const float4 p = pn;
-    if (i + VX_THREADS < N) pn = P(i + VX_THREADS);  // next chunk, in flight across the barrier
-    if (i < N) {
-      const uint32_t k = vx_key(g, p);
-      if (k >= klo && k < khi) {
-        uint32_t lo = 0, hi = U;  // lower_bound
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (ukey[mid] < k) lo = mid + 1; else hi = mid;
+  // four chunks per step: their loads and lower_bound searches in flight together; the list
+  // appends then go chunk by chunk, a barrier after each, so that every list holds its members
+  // chunk by chunk in input order (nearly sorted: the insertion sort below is cheap; with the
+  // four chunks' appends racing, the lists of the large voxels came out shuffled and their
+  // insertion sorts cost more than the whole pass, profiles/r6_stack_member_pass.txt)
+  constexpr int CH = 4;
+  for (uint32_t c = 0; c < N; c += CH * VX_THREADS) {
+    float4 p[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const uint32_t i = c + u * VX_THREADS + tid;
+      if (i < N) p[u] = P(i);
+    }
+    uint32_t kk[CH], lo[CH], hi[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const uint32_t i = c + u * VX_THREADS + tid;
+      kk[u] = i < N ? vx_key(g, p[u]) : 0u;
+      const bool in = i < N && kk[u] >= klo && kk[u] < khi;
+      lo[u] = 0;
+      hi[u] = in ? U : 0u;  // lower_bound (empty search: not in this range)
+    }
+    for (bool more = true; more;) {  // the four searches step together
+      more = false;
+#pragma unroll
+      for (int u = 0; u < CH; ++u)
+        if (lo[u] < hi[u]) {
+          const uint32_t mid = (lo[u] + hi[u]) >> 1;
+          if (ukey[mid] < kk[u]) lo[u] = mid + 1; else hi[u] = mid;
+          more |= lo[u] < hi[u];
         }
-        const uint32_t pos = uoff[lo] + atomicAdd(&ufill[lo], 1u);
+    }
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const uint32_t i = c + u * VX_THREADS + tid;
+      if (i < N && kk[u] >= klo && kk[u] < khi) {
+        const uint32_t pos = uoff[lo[u]] + atomicAdd(&ufill[lo[u]], 1u);
         members[pos] = (MT)i;
-        if (H) H->rk[i] = (rank0 + lo) << 1;  // the hot ones are re-marked below
+        if (H) H->rk[i] = (rank0 + lo[u]) << 1;  // the hot ones are re-marked below
       }
+      if (c + (u + 1) * VX_THREADS < N) __syncthreads();  // (uniform) chunk u's appends first
     }
     __syncthreads();
   }
@@ -882,7 +912,20 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
 #pragma unroll
   for (int u = 0; u < UA; ++u)
     if (tid + u * NT < n1) aa[u] = A[tid + u * NT];
-  {
+  VxGeom g;
+  int W = 0;  // anchored: voxels per axis of the key box
+  if (S.anchored) {  // keys from the cube's corner voxel (VoxSeg::anchored): no bounding-box pass
+    g.inv = 1.0f / S.leaf;
+    g.minbx = (int)floorf((float)S.anchor[0] * g.inv) - 1;
+    g.minby = (int)floorf((float)S.anchor[1] * g.inv) - 1;
+    g.minbz = (int)floorf((float)S.anchor[2] * g.inv) - 1;
+    W = (int)ceilf(50.0f * g.inv) + 3;  // the 50 m edge, one voxel of margin on each side, rounding
+    g.mul1 = W;
+    g.mul2 = W * W;
+    g.nvox = (unsigned long long)W * W * W;
+    g.overflow = 0;
+    if (tid == 0) M.g = g;  // (read after later barriers: the exact order's fix-up)
+  } else {
     float mnx = 3.402823466e38f, mny = 3.402823466e38f, mnz = 3.402823466e38f;
     float mxx = -3.402823466e38f, mxy = -3.402823466e38f, mxz = -3.402823466e38f;
     auto acc = [&](const float4& p) {
@@ -907,10 +950,18 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
     for (int u = 0; u < UA; ++u)
       if (tid + u * NT < n1) acc(aa[u]);
     vx_geometry_finish<NT>(mnx, mny, mnz, mxx, mxy, mxz, S.leaf, M);
+    g = M.g;
   }
-  const VxGeom g = M.g;
   vx_phase(S.prof, 0, &tp);
   if (g.overflow) return false;
+  // anchored keys are valid only inside the key box: checked for every point on the way (pass A)
+  int bad = 0;
+  auto outside = [&](const float4& p) -> int {
+    if (!W) return 0;
+    const int ix = (int)(floorf(p.x * g.inv) - (float)g.minbx), iy = (int)(floorf(p.y * g.inv) - (float)g.minby),
+              iz = (int)(floorf(p.z * g.inv) - (float)g.minbz);
+    return ((unsigned)ix >= (unsigned)W) | ((unsigned)iy >= (unsigned)W) | ((unsigned)iz >= (unsigned)W);
+  };
   uint32_t T = 64;
   while (T < 2 * n1) T <<= 1;
   const uint32_t mask = T - 1;
@@ -924,6 +975,7 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
     hcnt[h] = 0;
     hit[h] = -1;
   }
+  if (tid == 0) M.sfail = 0;  // the anchored key box check (pass A)
   __syncthreads();
   // 1. A's voxels: slot and rank of every new point
   uint32_t ar[UA];
@@ -931,6 +983,7 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
   for (int u = 0; u < UA; ++u) {
     ar[u] = NONE;
     if (tid + u * NT >= n1) continue;
+    bad |= outside(aa[u]);
     const uint32_t key = vx_key(g, aa[u]);
     uint32_t h = vx_slot(key, mask);
     while (true) {
@@ -974,6 +1027,7 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
     cl[u] = NONE;
     ck[u] = 0;
     if (k < n0) {
+      bad |= outside(cc[u]);
       ck[u] = vx_key(g, cc[u]);
       cl[u] = lookup(ck[u]);
       if (cl[u] != NONE) hit[cl[u]] = (int)k;
@@ -987,11 +1041,14 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       if (k + u * NT < n0) {
+        bad |= outside(p[u]);
         const uint32_t h = lookup(vx_key(g, p[u]));
         if (h != NONE) hit[h] = (int)(k + u * NT);
       }
   }
+  if (bad) atomicOr(&M.sfail, 1);
   __syncthreads();
+  if (W && __builtin_amdgcn_readfirstlane(M.sfail)) return false;  // a point outside the anchored key box: full filter
   vx_phase(S.prof, 1, &tp);
   // 4. the voxels holding A points only, listed then sorted by key
   uint32_t fmask = 0, cnt = 0;
@@ -1077,10 +1134,22 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
     }
     return lo;
   };
-  // 5. pass B: C point k goes to k + (new-only voxels before it); merged voxels re-averaged
-  auto emit = [&](uint32_t k, const float4& c, uint32_t key, uint32_t h) {
-    const uint32_t b = below(key);
-    atomicAdd(&cbelow[b], 1u);
+  // 5. pass B: C point k goes to k + (new-only voxels before it); merged voxels re-averaged.
+  // cbelow[b] counts the C points with b new-only voxels before them: C is in key order, so a
+  // wave's lanes (consecutive C points) mostly share b, and each run of equal b adds its length
+  // with one atomic by its first lane (lanes past n0 end every run).  All lanes of a wave call it.
+  const int lane = tid & 63;
+  auto count_below = [&](bool act, uint32_t b) {
+    const uint32_t bb = act ? b : 0xFFFFFFFFu;
+    const uint32_t prev = (uint32_t)__shfl_up((int)bb, 1, 64);
+    const uint64_t starts = __ballot(!act || lane == 0 || prev != bb);
+    if (act && ((starts >> lane) & 1ull)) {
+      const uint64_t after = lane == 63 ? 0ull : starts & (~0ull << (lane + 1));
+      const uint32_t run = (uint32_t)((after ? __ffsll((long long)after) - 1 : 64) - lane);
+      atomicAdd(&cbelow[b], run);
+    }
+  };
+  auto emit = [&](uint32_t k, const float4& c, uint32_t key, uint32_t h, uint32_t b) {
     float4 v = c;
     if (h != NONE) {
       if constexpr (HOT) {
@@ -1098,19 +1167,27 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
     out[k + b] = v;
   };
 #pragma unroll
-  for (int u = 0; u < U; ++u)
-    if (tid + u * NT < n0) emit(tid + u * NT, cc[u], ck[u], cl[u]);
-  for (uint32_t k = tid + U * NT; k < n0; k += 4 * NT) {
+  for (int u = 0; u < U; ++u) {
+    const bool act = tid + u * NT < n0;
+    const uint32_t b = act ? below(ck[u]) : 0u;
+    count_below(act, b);
+    if (act) emit(tid + u * NT, cc[u], ck[u], cl[u], b);
+  }
+  // (a wave-uniform loop: count_below needs every lane of the wave)
+  for (uint32_t kb = (uint32_t)(tid & ~63) + U * NT; kb < n0; kb += 4 * NT) {
+    const uint32_t k = kb + lane;
     float4 p[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       if (k + u * NT < n0) p[u] = C[k + u * NT];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (k + u * NT < n0) {
-        const uint32_t key = vx_key(g, p[u]);
-        emit(k + u * NT, p[u], key, lookup(key));
-      }
+    for (int u = 0; u < 4; ++u) {
+      const bool act = k + u * NT < n0;
+      const uint32_t key = act ? vx_key(g, p[u]) : 0u;
+      const uint32_t b = act ? below(key) : 0u;
+      count_below(act, b);
+      if (act) emit(k + u * NT, p[u], key, lookup(key), b);
+    }
   }
   __syncthreads();
   // C points below new-only voxel r: inclusive prefix of cbelow (Dn + 1 entries)

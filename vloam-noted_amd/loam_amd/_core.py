@@ -109,6 +109,7 @@ SIGNATURES = {
     "loam_mapper_input_device_batch": (c_i32, [vp, c_i32, vp, vp, vp, vp, vp, vp, vp]),
     "loam_mapper_stats_all": (c_i32, [vp, vp, c_i32]),
     "loam_mapper_total_iterations": (ctypes.c_int64, [vp]),
+    "loam_mapper_lm_path": (c_i32, [vp]),
     "loam_mapper_solve": (c_i32, [vp]),
     "loam_mapper_solve_async": (c_i32, [vp]),
     "loam_mapper_wait": (c_i32, [vp]),
@@ -170,6 +171,8 @@ def lib():
             raise LoamError(-5, f"{LIB_PATH} not built (run __graft_entry__.build())")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("LOAM_CORE_LIB") and not hasattr(L, name):
+                continue  # an A/B build of an older tree: entry points added since stay unbound
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

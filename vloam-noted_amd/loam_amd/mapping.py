@@ -83,6 +83,22 @@ class BatchMapper:
         check(lib().loam_mapper_input_device_batch(self.h, len(st), ptr(st), ptr(cp), ptr(cn), ptr(sp),
                                                    ptr(sn), ptr(q), ptr(t)))
 
+    @staticmethod
+    def batch_args(streams, corner_ptrs, n_corner, surf_ptrs, n_surf, q_wodom, t_wodom):
+        """input_device_batch's arrays made contiguous once, with their addresses: a tuple for
+        input_device_batch_args (frame loops that replay prepared inputs skip the per-call numpy
+        conversions; the arrays are kept alive in the tuple)"""
+        arrs = (np.ascontiguousarray(streams, dtype=np.int32), np.ascontiguousarray(corner_ptrs, dtype=np.uint64),
+                np.ascontiguousarray(n_corner, dtype=np.int32), np.ascontiguousarray(surf_ptrs, dtype=np.uint64),
+                np.ascontiguousarray(n_surf, dtype=np.int32),
+                np.ascontiguousarray(q_wodom, dtype=np.float64).reshape(-1, 4),
+                np.ascontiguousarray(t_wodom, dtype=np.float64).reshape(-1, 3))
+        return (len(arrs[0]),) + tuple(ptr(a) for a in arrs) + (arrs,)
+
+    def input_device_batch_args(self, args):
+        """input_device_batch from batch_args' tuple"""
+        check(lib().loam_mapper_input_device_batch(self.h, *args[:8]))
+
     def stack(self, stream, which):
         """laserCloudCornerStack (0) / laserCloudSurfStack (1) of the last solve, (n, 4) float32"""
         n = check(lib().loam_mapper_stack_copy(self.h, stream, which, None, 0))
@@ -90,6 +106,11 @@ class BatchMapper:
         if n:
             check(lib().loam_mapper_stack_copy(self.h, stream, which, ptr(out), n))
         return out
+
+    def lm_path(self):
+        """the LM schedule of this handle: 0 two launches per iteration, 1 persistent round, 2 in-process
+        group round, 3 persistent round with cross-process IPC peer slots (loam_mapper_lm_path)"""
+        return check(lib().loam_mapper_lm_path(self.h))
 
     def total_iterations(self):
         """sum of the LM iterations of every stream in the last solve"""
