@@ -300,7 +300,9 @@ int32_t loam_mapper_stats(loam_mapper* h, int32_t stream, loam_map_stats* st);
  * [62] its launches, [63] of them frames prepared on the device, [64..65] PCL-order VoxelGrid
  * (exact_voxel_order = 1) sorts in global memory: cycles of their own levels, cubes / stacks
  * ([11..14] / [42..45] hold the rest), [66..67] cube sorts' depth-limit segments and their
- * elements, [68..69] the same for stack sorts.
+ * elements, [68..69] the same for stack sorts, [91] the few-stream stack VoxelGrid's (k_stack_part)
+ * histogram and range cuts ([42..45] then hold its bounding box, hash, sort + scan, member lists +
+ * centroids, summed over its parts).
  * The cycle counters (all but [40], [41], [48], [49]; [52], [56], [66..69], [72], [77], [82..86], [90] count) run only in a handle created with the
  * environment variable LOAM_PHASE_COUNTERS=1 (they cost atomics in the kernels); else they stay 0. */
 #define LOAM_DEBUG_COUNTERS 96

@@ -1,5 +1,6 @@
-"""Tile kNN phase cycles of a one-stream mapper (debug counters 50..56) over 40 frames
-after 120 map-building frames of the synthetic street (GPU scan registration + odometry)."""
+"""Few-stream stack VoxelGrid (k_stack_part, laser_mapping.cpp:492-500) phase cycles of a
+one-stream mapper over 40 frames after 120 map-building frames of the synthetic street (GPU scan
+registration + odometry): debug counters 42..47 and 91, per part (K = 8 parts per (frame, map))."""
 import os
 os.environ.setdefault("LOAM_PHASE_COUNTERS", "1")  # the handles below count phase cycles
 import sys
@@ -14,6 +15,7 @@ from loam_amd.odometry import BatchOdometry  # noqa: E402
 from loam_amd.scanreg import ScanRegistration  # noqa: E402
 
 sr, od, mp = ScanRegistration(), BatchOdometry(1), BatchMapper(1)
+sizes = []
 for f in range(160):
     xyz, _ = synth.frame(1, f, 2000)
     sr.input(xyz)
@@ -21,12 +23,16 @@ for f in range(160):
     od.input(0, c[1], c[2], c[3], c[4])
     od.solve()
     q, t, _, _, skip = od.output(0)
-    mp.input(0, od.last_cloud(0, 0), od.last_cloud(0, 1), q, t)
+    cn, sn = od.last_cloud(0, 0), od.last_cloud(0, 1)
+    mp.input(0, cn, sn, q, t)
     if f == 120:
         mp.debug_counters(reset=True)
+    if f >= 120:
+        sizes.append((len(cn), len(sn)))
     mp.solve()
 c = mp.debug_counters().astype(np.float64)
-tiles = max(c[55], 1)
-print(f"tiles {c[55]:.0f}, queries/tile {c[56] / tiles:.1f}, staged points/tile {c[57] / tiles:.1f}; cycles per tile: "
-      f"record + queries {c[50] / tiles:.0f}, probes + cell starts {c[51] / tiles:.0f}, staging {c[52] / tiles:.0f}, "
-      f"search {c[53] / tiles:.0f}, results {c[54] / tiles:.0f}")
+parts = 40 * 2 * 8
+print(f"stack inputs (corner, surf) mean {np.mean(sizes, axis=0).round(0).tolist()}")
+print(f"k_stack_part per part: bbox {c[42] / parts:.0f} histogram+cuts {c[91] / parts:.0f} hash {c[43] / parts:.0f} "
+      f"sort+scan {c[44] / parts:.0f} members+centroids {c[45] / parts:.0f} (member lists {c[46] / parts:.0f}, "
+      f"per-voxel sums {c[47] / parts:.0f})")

@@ -609,9 +609,19 @@ static inline void lm_peer_spin_limit_from_env(int device) {
   if (hipMemcpyToSymbol(HIP_SYMBOL(lm_peer_spin_limit_g), &v, sizeof(v)) == hipSuccess) done |= 1ull << device;
 }
 // sync words per solve, zeroed before the launch: [1] generation (pass + 1 of the published
-// evaluation point), [2] its status, [4 + p] claims of pass p's shares 1.. (share 0 is the
-// leader's), [4 + LM_MAX_PASSES + p] shares 1.. of pass p completed
+// evaluation point; past LM_MAX_PASSES once the round has ended), [4 + p] claims of pass p's
+// shares 1.. (share 0 is the leader's), [4 + LM_MAX_PASSES + p] shares 1.. of pass p completed
 constexpr int LM_SYNC_WORDS = 4 + 2 * LM_MAX_PASSES;
+
+// the polled word once it reaches target (>= 1), or 0 when the wait runs out
+__device__ inline uint32_t lm_spin_val(uint32_t* w, uint32_t target, uint32_t limit = LM_SPIN_LIMIT) {
+  for (uint32_t spins = 0;; ++spins) {
+    const uint32_t v = __hip_atomic_load(w, RLX_AGENT);
+    if (v >= target) return v;
+    if (spins >= limit) return 0u;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
 
 __device__ inline bool lm_spin_ge(uint32_t* w, uint32_t target, uint32_t limit = LM_SPIN_LIMIT) {
   for (uint32_t spins = 0;; ++spins) {
@@ -707,19 +717,23 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
       if (tid == 0) {
         t0 = __builtin_readcyclecounter();
         int st = LM_DONE, c = G, p = 0;
-        if (lm_spin_ge(&sync[1], want)) {  // a member that waits too long just leaves
-          const uint32_t gen = __hip_atomic_load(&sync[1], RLX_AGENT);
+        // the generation as polled (0: the wait ran out, a member that waits too long just
+        // leaves); above LM_MAX_PASSES the round has ended
+        const uint32_t gen = lm_spin_val(&sync[1], want);
+        if (gen != 0u && gen <= (uint32_t)LM_MAX_PASSES) {
           lm_acquire();
-          st = (int)__hip_atomic_load(&sync[2], RLX_AGENT);
           p = (int)gen - 1;
-          if (st != LM_DONE && p < LM_MAX_PASSES) {
-            c = 1 + (int)__hip_atomic_fetch_add(&sync[4 + p], 1u, RLX_AGENT);
-            // a claimed share holds the leader in pass p: the published point is pass p's
-            if (c < G)
-              for (int i = 0; i < 7; ++i) sx[i] = __hip_atomic_load(&xpub[i], RLX_AGENT);
-          } else {
-            st = LM_DONE;
-          }
+          // the point's loads and the claim in flight together (one memory round trip): they are
+          // issued after the generation was seen, so the point is at least pass p's, and a claimed
+          // share holds the leader in pass p, so it is not yet a later one; with no share left
+          // the values are not used
+          double xv[7];
+#pragma unroll
+          for (int i = 0; i < 7; ++i) xv[i] = __hip_atomic_load(&xpub[i], RLX_AGENT);
+          c = 1 + (int)__hip_atomic_fetch_add(&sync[4 + p], 1u, RLX_AGENT);
+          if (c < G)
+            for (int i = 0; i < 7; ++i) sx[i] = xv[i];
+          st = LM_EVAL_CAND;  // (any status but LM_DONE)
         }
         sstat = st;
         sshare = c;
@@ -759,11 +773,12 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
       for (int i = 0; i < 7; ++i) sx[i] = ls.status == LM_EVAL_X ? ls.x[i] : ls.cand[i];
     }
     __syncthreads();
-    if (G > 1 && wid == 0) {  // publish: sc1 stores, drain, relaxed generation
+    if (G > 1 && wid == 0) {  // publish: sc1 stores, drain, relaxed generation (pass + 1, or
+                              // past LM_MAX_PASSES when the round has ended: the members leave)
       if (lane < 7) __hip_atomic_store(&xpub[lane], sx[lane], RLX_AGENT);
-      if (lane == 7) __hip_atomic_store(&sync[2], (uint32_t)sstat, RLX_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_store(&sync[1], (uint32_t)(pass + 1), RLX_AGENT);
+      if (lane == 0)
+        __hip_atomic_store(&sync[1], sstat == LM_DONE ? (uint32_t)LM_MAX_PASSES + 1u : (uint32_t)(pass + 1), RLX_AGENT);
     }
     if (__builtin_amdgcn_readfirstlane(sstat) == LM_DONE) break;
     if (tid == 0) t0 = __builtin_readcyclecounter();
@@ -917,11 +932,8 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
   if (aborted && tid == 0) {  // stop this stream's LM where it is (best so far)
     ls.term = 6;
     ls.status = LM_DONE;
-    if (G > 1) {  // members waiting for a next pass leave now
-      __hip_atomic_store(&sync[2], (uint32_t)LM_DONE, RLX_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (G > 1)  // members waiting for a next pass leave now
       __hip_atomic_store(&sync[1], (uint32_t)LM_MAX_PASSES + 1u, RLX_AGENT);
-    }
   }
   __syncthreads();
   if (ls.status == LM_DONE && tid < 7 && J.best_out) J.best_out[tid] = ls.best[tid];

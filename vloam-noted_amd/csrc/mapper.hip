@@ -433,7 +433,9 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_part(MapperDev D) {
     if (tid == 0) part[j] = make_uint2(0, 0);
     return;
   }
+  unsigned long long tp = __builtin_readcyclecounter();  // phase counters (diagnostics)
   vx_geometry(P, N, D.leaf[m], M);
+  vx_phase(D.pdbg ? D.pdbg + 42 : nullptr, 0, &tp);  // bounding box -> dbg[42] (summed over the K parts)
   const VxGeom g = M.g;
   if (g.overflow) {  // PCL: "Leaf size is too small" -> output = input (range 0 copies it)
     if (j == 0)
@@ -443,17 +445,36 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_part(MapperDev D) {
   }
   // idx histogram -> the ranges' bucket cuts by cumulative point count
   uint32_t* hist = lds + VX_HIST_WORD;
+  // bucket(k) = floor(k mulc / 2^32) with mulc = floor(2^32 VX_NB / V): monotone in k and below
+  // VX_NB for k < V, and a multiply instead of a 64-bit division per point (the histogram pass
+  // spent most of its cycles in the division); blo(b) = ceil(b 2^32 / mulc) is its exact inverse
+  // (the first key of bucket b), so the parts still cut the idx range at key boundaries
   const unsigned long long V = g.nvox;
-  auto bucket = [&](uint32_t k) { return (uint32_t)(((unsigned long long)k * VX_NB) / V); };
-  auto blo = [&](uint32_t b) { return (uint32_t)(((unsigned long long)b * V + VX_NB - 1) / VX_NB); };
+  const unsigned long long mulc = (((unsigned long long)VX_NB) << 32) / V;
+  auto bucket = [&](uint32_t k) { return (uint32_t)(((unsigned long long)k * mulc) >> 32); };
+  auto blo = [&](uint32_t b) { return (uint32_t)((((unsigned long long)b << 32) + mulc - 1) / mulc); };
   for (int b = tid; b < VX_NB; b += VX_THREADS) hist[b] = 0;
   __syncthreads();
-  for (uint32_t i0 = tid; i0 < N; i0 += VX_UNROLL * VX_THREADS) {  // loads in flight together
-    uint32_t kk4[VX_UNROLL];
-    vx_keys4(g, P, N, i0, kk4);
+  // loads in flight together; the scan's points come in ring order, so a wave's lanes (consecutive
+  // points) mostly fall in one bucket: each run of equal buckets adds its length with one LDS
+  // atomic by its first lane (same-address atomics of a wave serialise).  Wave-uniform loop.
+  {
+    const int lane = tid & 63;
+    const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+    for (uint32_t ib = (uint32_t)(tid & ~63); ib < N; ib += VX_UNROLL * VX_THREADS) {
+      uint32_t kk4[VX_UNROLL];
+      vx_keys4(g, P, N, ib + lane, kk4);
 #pragma unroll
-    for (int u = 0; u < VX_UNROLL; ++u)
-      if (kk4[u] != VX_EMPTY) atomicAdd(&hist[bucket(kk4[u])], 1u);
+      for (int u = 0; u < VX_UNROLL; ++u) {
+        const uint32_t bk = kk4[u] != VX_EMPTY ? bucket(kk4[u]) : 0xFFFFFFFFu;
+        const uint32_t prev = (uint32_t)__shfl_up((int)bk, 1, 64);
+        const uint64_t starts = __ballot(lane == 0 || prev != bk);
+        if (bk != 0xFFFFFFFFu && ((starts >> lane) & 1ull)) {
+          const uint64_t after = starts & ~le;
+          atomicAdd(&hist[bk], (uint32_t)((after ? __ffsll((long long)after) - 1 : 64) - lane));
+        }
+      }
+    }
   }
   __syncthreads();
   // range r starts at the first bucket whose points-before count reaches r N / K: a block scan
@@ -482,6 +503,7 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_part(MapperDev D) {
   __syncthreads();
   const uint32_t b0 = M.sbase[0], b1 = max(M.sbase[0], M.sbase[1]), base = (uint32_t)M.sfail;
   __syncthreads();  // vx_group reuses M
+  vx_phase(D.pdbg ? D.pdbg + 91 : nullptr, 0, &tp);  // histogram + range cuts -> dbg[91]
   if (b0 >= b1) {  // empty range
     if (tid == 0) part[j] = make_uint2(base, 0);
     return;
@@ -505,6 +527,7 @@ __global__ void __launch_bounds__(VX_THREADS) k_stack_part(MapperDev D) {
   S.scratch_tail = nullptr;
   S.scratch_cap = (uint32_t)D.max_in;
   S.err = &D.stk_err[s];
+  S.prof_seg = D.pdbg ? D.pdbg + 42 : nullptr;  // hash, sort + scan, members + centroids -> dbg[43..45]
   int moved = 0;
   const uint32_t klo = blo(b0), khi = b1 >= (uint32_t)VX_NB ? 0xFFFFFFFFu : blo(b1);
   const uint32_t U = vx_group(S, g, P, N, D.stk_idx + sm * D.max_in + base, klo, khi, base,
@@ -2320,6 +2343,8 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   // few streams: the input-order stack VoxelGrid over 8 workgroups per (stream, map)
   // (k_stack_part; 4 / 6 / 12 ranges measured slower)
   D.stack_k = (n_streams <= 4 && !D.pcl_order) ? 8 : 0;
+  if (const char* kenv = std::getenv("LOAM_STACK_K"))  // measurement override (parts per stack)
+    if (D.stack_k) D.stack_k = std::max(1, std::min(STACK_K_MAX, std::atoi(kenv)));
   D.leaf[0] = (float)h->P.mapping_line_resolution;
   D.leaf[1] = (float)h->P.mapping_plane_resolution;
   const size_t B = n_streams;
@@ -2404,8 +2429,13 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   for (int p = 0; p < 2; ++p) {
     ALLOC(h->stk_n_buf[p], B * 2);
     ALLOC(h->stk_err_buf[p], B);
-    ALLOC(h->sin_buf[p], B);
-    if (!h->hsin[p].assign(B, StackIn{})) return fail(LOAM_ERR_HIP);
+    // the stack inputs in page-locked host memory the stack kernels read in place (mapped): no
+    // H2D copy ahead of the stack VoxelGrid (it heads the blocking frame's critical path)
+    void* dp = nullptr;
+    if (!h->hsin[p].assign(B, StackIn{}, hipHostMallocMapped | hipHostMallocCoherent) ||
+        hipHostGetDevicePointer(&dp, h->hsin[p].data(), 0) != hipSuccess)
+      return fail(LOAM_ERR_HIP);
+    h->sin_buf[p] = static_cast<StackIn*>(dp);
   }
   D.sin = h->sin_buf[0];
   D.stk_n = h->stk_n_buf[0];
@@ -2703,7 +2733,7 @@ static int32_t launch_stacks(loam_mapper* h) {
   for (const FrameRec& R : h->q)  // that parity's stack buffers still belong to a frame in flight
     if (R.fpar == par) return LOAM_OK;
   bool any = false;
-  LOAM_HIP(hipEventSynchronize(h->ev_sin[par]));  // the last copy out of hsin[par] is done
+  LOAM_HIP(hipEventSynchronize(h->ev_sin[par]));  // the last stack kernels reading hsin[par] are done
   StackIn* in = h->hsin[par].data();
   for (int s = 0; s < B; ++s) {
     HostStream& H = h->hs[s];
@@ -2726,8 +2756,6 @@ static int32_t launch_stacks(loam_mapper* h) {
   D.stk_err = h->stk_err_buf[par];
   for (int m = 0; m < 2; ++m) D.stack[m] = h->stack_buf[par][m];
   hipStream_t s2 = h->st2;
-  LOAM_HIP(hipMemcpyAsync(h->sin_buf[par], in, sizeof(StackIn) * B, hipMemcpyHostToDevice, s2));
-  LOAM_HIP(hipEventRecord(h->ev_sin[par], s2));
   if (D.stack_k) {
     LAUNCH_ON(s2, FAM_STACK, k_stack_part<<<B * 2 * D.stack_k, VX_THREADS, 0, s2>>>(D));
     LAUNCH_ON(s2, FAM_STACK, k_stack_cat<<<B * 2, VX_THREADS, 0, s2>>>(D));
@@ -2737,6 +2765,7 @@ static int32_t launch_stacks(loam_mapper* h) {
   }
   k_stack_done<<<1, 64, 0, s2>>>(h->d_stk_ready + par, seq);
   LOAM_HIP(hipGetLastError());
+  LOAM_HIP(hipEventRecord(h->ev_sin[par], s2));  // (hsin[par] is read in place until here)
   LOAM_HIP(hipEventRecord(h->ev_stack, s2));
   return LOAM_OK;
 }

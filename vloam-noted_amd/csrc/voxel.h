@@ -220,6 +220,7 @@ __device__ inline bool vx_centroids(const VxGeom& g, const VxSrc& P, uint32_t N,
                                     unsigned long long* dprof = nullptr, const VxHot* H = nullptr,
                                     uint32_t rank0 = 0) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes <= this one
   unsigned long long tq = __builtin_readcyclecounter();
   bool moved = false;
   // four chunks per step: their loads and lower_bound searches in flight together; the list
@@ -256,11 +257,23 @@ __device__ inline bool vx_centroids(const VxGeom& g, const VxSrc& P, uint32_t N,
     }
 #pragma unroll
     for (int u = 0; u < CH; ++u) {
+      // a run of a wave's lanes in one voxel appends with one atomic by its first lane, its
+      // members in lane (input) order
       const uint32_t i = c + u * VX_THREADS + tid;
-      if (i < N && kk[u] >= klo && kk[u] < khi) {
-        const uint32_t pos = uoff[lo[u]] + atomicAdd(&ufill[lo[u]], 1u);
-        members[pos] = (MT)i;
-        if (H) H->rk[i] = (rank0 + lo[u]) << 1;  // the hot ones are re-marked below
+      const bool in = i < N && kk[u] >= klo && kk[u] < khi;
+      const uint32_t v = in ? lo[u] : 0xFFFFFFFFu;
+      const uint32_t prev = (uint32_t)__shfl_up((int)v, 1, 64);
+      const uint64_t starts = __ballot(lane == 0 || prev != v);
+      const int head = 63 - __clzll(starts & le);
+      uint32_t base = 0;
+      if (in && head == lane) {
+        const uint64_t after = starts & ~le;
+        base = atomicAdd(&ufill[v], (uint32_t)((after ? __ffsll((long long)after) - 1 : 64) - lane));
+      }
+      base = (uint32_t)__shfl((int)base, head, 64) + (uint32_t)(lane - head);
+      if (in) {
+        members[uoff[v] + base] = (MT)i;
+        if (H) H->rk[i] = (rank0 + v) << 1;  // the hot ones are re-marked below
       }
       if (c + (u + 1) * VX_THREADS < N) __syncthreads();  // (uniform) chunk u's appends first
     }
@@ -361,19 +374,28 @@ __device__ inline uint32_t vx_group(const VoxSeg& S, const VxGeom& g, const VxSr
     M.moved = 0;
   }
   __syncthreads();
-  for (uint32_t i0 = tid; i0 < N; i0 += VX_UNROLL * VX_THREADS) {
+  // points come in input order, in which neighbours mostly share a voxel (a scan ring, a cube's
+  // voxel rows): each run of equal keys among a wave's lanes counts its length with one insertion
+  // by its first lane (same-address LDS atomics of a wave serialise).  Wave-uniform loop.
+  const int lane_ = tid & 63;
+  const uint64_t le_ = lane_ == 63 ? ~0ull : ((2ull << lane_) - 1ull);
+  for (uint32_t ib = (uint32_t)(tid & ~63); ib < N; ib += VX_UNROLL * VX_THREADS) {
     uint32_t kk4[VX_UNROLL];
-    vx_keys4(g, P, N, i0, kk4);
+    vx_keys4(g, P, N, ib + lane_, kk4);
 #pragma unroll
     for (int u = 0; u < VX_UNROLL; ++u) {
-      const uint32_t k = kk4[u];
-      if (k < klo || k >= khi) continue;  // also skips i >= N (key VX_EMPTY)
+      const uint32_t k = (kk4[u] < klo || kk4[u] >= khi) ? VX_EMPTY : kk4[u];  // (i >= N: VX_EMPTY)
+      const uint32_t prev = (uint32_t)__shfl_up((int)k, 1, 64);
+      const uint64_t starts = __ballot(lane_ == 0 || prev != k);
+      if (k == VX_EMPTY || !((starts >> lane_) & 1ull)) continue;
+      const uint64_t after = starts & ~le_;
+      const uint32_t run = (uint32_t)((after ? __ffsll((long long)after) - 1 : 64) - lane_);
       uint32_t h = vx_hash(k);
       int probes = 0;
       while (true) {
         uint32_t old = atomicCAS(&hkey[h], VX_EMPTY, k);
         if (old == VX_EMPTY || old == k) {
-          atomicAdd(&hcnt[h], 1u);
+          atomicAdd(&hcnt[h], run);
           break;
         }
         h = (h + 1) & (VX_HASH - 1);
@@ -1080,6 +1102,22 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
   }
   uint32_t* cbelow = reinterpret_cast<uint32_t*>(srt + npad);  // Dn + 1 <= 2 npad words
   for (uint32_t r = tid; r <= Dn; r += NT) cbelow[r] = 0;
+  // a bucket directory over the new-only voxels' keys for below(): bucket b = (key - kmin) >> sh,
+  // bdir[b] the first voxel of a bucket >= b (bdir[MB] = Dn), so a lookup searches one bucket
+  // (~Dn / MB voxels) instead of all Dn (pass B looks up every C point)
+  constexpr int MB = 1024;
+  static_assert(RX + 4 * CAP + MB + 1 <= LW - 256, "merge LDS layout: bucket directory");
+  uint32_t* bdir = lds + RX + 4 * CAP;
+  const uint32_t kmin = Dn ? (uint32_t)(srt[0] >> 32) : 0u, kmax = Dn ? (uint32_t)(srt[Dn - 1] >> 32) : 0u;
+  int sh = 0;
+  while ((((uint64_t)kmax - kmin) >> sh) >= (uint64_t)MB) ++sh;  // every bucket < MB: bdir[b + 1] exists
+  for (uint32_t r = tid; r < Dn; r += NT) {
+    const int b = (int)(((uint32_t)(srt[r] >> 32) - kmin) >> sh);
+    const int bp = r ? (int)(((uint32_t)(srt[r - 1] >> 32) - kmin) >> sh) : -1;
+    for (int q = bp + 1; q <= b; ++q) bdir[q] = r;
+    if (r == Dn - 1)
+      for (int q = b + 1; q <= MB; ++q) bdir[q] = Dn;
+  }
   if (tid == 0) {
     M.moved = 0;
     M.hot_n = 0;
@@ -1125,9 +1163,12 @@ __device__ inline bool vx_merge_fixed_point(const VoxSeg& S, uint32_t* lds) {
     const float fn = (float)n;
     return make_float4(sx / fn, sy / fn, sz / fn, si / fn);
   };
-  // new-only voxels with key below `key`
+  // new-only voxels with key below `key` (the bucket of `key`, then a search inside it)
   auto below = [&](uint32_t key) -> uint32_t {
-    uint32_t lo = 0, hi = Dn;
+    if (Dn == 0 || key <= kmin) return 0u;
+    if (key > kmax) return Dn;
+    const uint32_t b = (key - kmin) >> sh;
+    uint32_t lo = bdir[b], hi = bdir[b + 1];
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
       if ((uint32_t)(srt[mid] >> 32) < key) lo = mid + 1; else hi = mid;
