@@ -220,7 +220,6 @@ __device__ inline bool vx_centroids(const VxGeom& g, const VxSrc& P, uint32_t N,
                                     unsigned long long* dprof = nullptr, const VxHot* H = nullptr,
                                     uint32_t rank0 = 0) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes <= this one
   unsigned long long tq = __builtin_readcyclecounter();
   bool moved = false;
   // four chunks per step: their loads and lower_bound searches in flight together; the list
@@ -257,23 +256,11 @@ __device__ inline bool vx_centroids(const VxGeom& g, const VxSrc& P, uint32_t N,
     }
 #pragma unroll
     for (int u = 0; u < CH; ++u) {
-      // a run of a wave's lanes in one voxel appends with one atomic by its first lane, its
-      // members in lane (input) order
       const uint32_t i = c + u * VX_THREADS + tid;
-      const bool in = i < N && kk[u] >= klo && kk[u] < khi;
-      const uint32_t v = in ? lo[u] : 0xFFFFFFFFu;
-      const uint32_t prev = (uint32_t)__shfl_up((int)v, 1, 64);
-      const uint64_t starts = __ballot(lane == 0 || prev != v);
-      const int head = 63 - __clzll(starts & le);
-      uint32_t base = 0;
-      if (in && head == lane) {
-        const uint64_t after = starts & ~le;
-        base = atomicAdd(&ufill[v], (uint32_t)((after ? __ffsll((long long)after) - 1 : 64) - lane));
-      }
-      base = (uint32_t)__shfl((int)base, head, 64) + (uint32_t)(lane - head);
-      if (in) {
-        members[uoff[v] + base] = (MT)i;
-        if (H) H->rk[i] = (rank0 + v) << 1;  // the hot ones are re-marked below
+      if (i < N && kk[u] >= klo && kk[u] < khi) {
+        const uint32_t pos = uoff[lo[u]] + atomicAdd(&ufill[lo[u]], 1u);
+        members[pos] = (MT)i;
+        if (H) H->rk[i] = (rank0 + lo[u]) << 1;  // the hot ones are re-marked below
       }
       if (c + (u + 1) * VX_THREADS < N) __syncthreads();  // (uniform) chunk u's appends first
     }
@@ -374,28 +361,19 @@ __device__ inline uint32_t vx_group(const VoxSeg& S, const VxGeom& g, const VxSr
     M.moved = 0;
   }
   __syncthreads();
-  // points come in input order, in which neighbours mostly share a voxel (a scan ring, a cube's
-  // voxel rows): each run of equal keys among a wave's lanes counts its length with one insertion
-  // by its first lane (same-address LDS atomics of a wave serialise).  Wave-uniform loop.
-  const int lane_ = tid & 63;
-  const uint64_t le_ = lane_ == 63 ? ~0ull : ((2ull << lane_) - 1ull);
-  for (uint32_t ib = (uint32_t)(tid & ~63); ib < N; ib += VX_UNROLL * VX_THREADS) {
+  for (uint32_t i0 = tid; i0 < N; i0 += VX_UNROLL * VX_THREADS) {
     uint32_t kk4[VX_UNROLL];
-    vx_keys4(g, P, N, ib + lane_, kk4);
+    vx_keys4(g, P, N, i0, kk4);
 #pragma unroll
     for (int u = 0; u < VX_UNROLL; ++u) {
-      const uint32_t k = (kk4[u] < klo || kk4[u] >= khi) ? VX_EMPTY : kk4[u];  // (i >= N: VX_EMPTY)
-      const uint32_t prev = (uint32_t)__shfl_up((int)k, 1, 64);
-      const uint64_t starts = __ballot(lane_ == 0 || prev != k);
-      if (k == VX_EMPTY || !((starts >> lane_) & 1ull)) continue;
-      const uint64_t after = starts & ~le_;
-      const uint32_t run = (uint32_t)((after ? __ffsll((long long)after) - 1 : 64) - lane_);
+      const uint32_t k = kk4[u];
+      if (k < klo || k >= khi) continue;  // also skips i >= N (key VX_EMPTY)
       uint32_t h = vx_hash(k);
       int probes = 0;
       while (true) {
         uint32_t old = atomicCAS(&hkey[h], VX_EMPTY, k);
         if (old == VX_EMPTY || old == k) {
-          atomicAdd(&hcnt[h], run);
+          atomicAdd(&hcnt[h], 1u);
           break;
         }
         h = (h + 1) & (VX_HASH - 1);
