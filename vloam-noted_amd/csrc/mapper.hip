@@ -2429,13 +2429,20 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   for (int p = 0; p < 2; ++p) {
     ALLOC(h->stk_n_buf[p], B * 2);
     ALLOC(h->stk_err_buf[p], B);
-    // the stack inputs in page-locked host memory the stack kernels read in place (mapped): no
-    // H2D copy ahead of the stack VoxelGrid (it heads the blocking frame's critical path)
-    void* dp = nullptr;
-    if (!h->hsin[p].assign(B, StackIn{}, hipHostMallocMapped | hipHostMallocCoherent) ||
-        hipHostGetDevicePointer(&dp, h->hsin[p].data(), 0) != hipSuccess)
-      return fail(LOAM_ERR_HIP);
-    h->sin_buf[p] = static_cast<StackIn*>(dp);
+    // few streams: the stack inputs in page-locked host memory the stack kernels read in place
+    // (mapped), no H2D copy ahead of the stack VoxelGrid, which heads the blocking frame's critical
+    // path; many streams: a device copy (256 workgroups reading host memory cost the stack family
+    // ~0.05 ms per step at B = 128, profiles/r6_member_chunks_ab.txt)
+    if (B <= 4) {
+      void* dp = nullptr;
+      if (!h->hsin[p].assign(B, StackIn{}, hipHostMallocMapped | hipHostMallocCoherent) ||
+          hipHostGetDevicePointer(&dp, h->hsin[p].data(), 0) != hipSuccess)
+        return fail(LOAM_ERR_HIP);
+      h->sin_buf[p] = static_cast<StackIn*>(dp);
+    } else {
+      ALLOC(h->sin_buf[p], B);
+      if (!h->hsin[p].assign(B, StackIn{})) return fail(LOAM_ERR_HIP);
+    }
   }
   D.sin = h->sin_buf[0];
   D.stk_n = h->stk_n_buf[0];
@@ -2733,7 +2740,7 @@ static int32_t launch_stacks(loam_mapper* h) {
   for (const FrameRec& R : h->q)  // that parity's stack buffers still belong to a frame in flight
     if (R.fpar == par) return LOAM_OK;
   bool any = false;
-  LOAM_HIP(hipEventSynchronize(h->ev_sin[par]));  // the last stack kernels reading hsin[par] are done
+  LOAM_HIP(hipEventSynchronize(h->ev_sin[par]));  // the last reads of hsin[par] are done
   StackIn* in = h->hsin[par].data();
   for (int s = 0; s < B; ++s) {
     HostStream& H = h->hs[s];
@@ -2756,6 +2763,7 @@ static int32_t launch_stacks(loam_mapper* h) {
   D.stk_err = h->stk_err_buf[par];
   for (int m = 0; m < 2; ++m) D.stack[m] = h->stack_buf[par][m];
   hipStream_t s2 = h->st2;
+  if (h->B > 4) LOAM_HIP(hipMemcpyAsync(h->sin_buf[par], in, sizeof(StackIn) * B, hipMemcpyHostToDevice, s2));
   if (D.stack_k) {
     LAUNCH_ON(s2, FAM_STACK, k_stack_part<<<B * 2 * D.stack_k, VX_THREADS, 0, s2>>>(D));
     LAUNCH_ON(s2, FAM_STACK, k_stack_cat<<<B * 2, VX_THREADS, 0, s2>>>(D));
@@ -2765,7 +2773,7 @@ static int32_t launch_stacks(loam_mapper* h) {
   }
   k_stack_done<<<1, 64, 0, s2>>>(h->d_stk_ready + par, seq);
   LOAM_HIP(hipGetLastError());
-  LOAM_HIP(hipEventRecord(h->ev_sin[par], s2));  // (hsin[par] is read in place until here)
+  LOAM_HIP(hipEventRecord(h->ev_sin[par], s2));  // (hsin[par] is read, in place or by the copy, until here)
   LOAM_HIP(hipEventRecord(h->ev_stack, s2));
   return LOAM_OK;
 }

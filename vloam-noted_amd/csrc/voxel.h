@@ -222,47 +222,30 @@ __device__ inline bool vx_centroids(const VxGeom& g, const VxSrc& P, uint32_t N,
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   unsigned long long tq = __builtin_readcyclecounter();
   bool moved = false;
-  // four chunks per step: their loads and lower_bound searches in flight together; the list
-  // appends then go chunk by chunk, a barrier after each, so that every list holds its members
-  // chunk by chunk in input order (nearly sorted: the insertion sort below is cheap; with the
-  // four chunks' appends racing, the lists of the large voxels came out shuffled and their
-  // insertion sorts cost more than the whole pass, profiles/r6_stack_member_pass.txt)
-  constexpr int CH = 4;
-  for (uint32_t c = 0; c < N; c += CH * VX_THREADS) {
-    float4 p[CH];
-#pragma unroll
-    for (int u = 0; u < CH; ++u) {
-      const uint32_t i = c + u * VX_THREADS + tid;
-      if (i < N) p[u] = P(i);
-    }
-    uint32_t kk[CH], lo[CH], hi[CH];
-#pragma unroll
-    for (int u = 0; u < CH; ++u) {
-      const uint32_t i = c + u * VX_THREADS + tid;
-      kk[u] = i < N ? vx_key(g, p[u]) : 0u;
-      const bool in = i < N && kk[u] >= klo && kk[u] < khi;
-      lo[u] = 0;
-      hi[u] = in ? U : 0u;  // lower_bound (empty search: not in this range)
-    }
-    for (bool more = true; more;) {  // the four searches step together
-      more = false;
-#pragma unroll
-      for (int u = 0; u < CH; ++u)
-        if (lo[u] < hi[u]) {
-          const uint32_t mid = (lo[u] + hi[u]) >> 1;
-          if (ukey[mid] < kk[u]) lo[u] = mid + 1; else hi[u] = mid;
-          more |= lo[u] < hi[u];
+  // one chunk per barrier (members of earlier chunks precede later ones, so each list is nearly
+  // sorted), the next chunk's point loaded before the barrier.  Measured and not kept: four chunks'
+  // loads and lower_bound searches per step, the appends chunk by chunk (the stack VoxelGrid
+  // 0.50 -> 0.57-0.62 ms per step at B = 128 and one-stream blocking frames 0.459 -> 0.470 ms,
+  // profiles/r6_member_chunks_ab.txt); with the four chunks' appends racing, the lists came out
+  // shuffled and their insertion sorts cost more than the pass (profiles/r6_stack_member_pass.txt)
+  float4 pn = make_float4(0.f, 0.f, 0.f, 0.f);
+  if ((uint32_t)tid < N) pn = P(tid);
+  for (uint32_t c = 0; c < N; c += VX_THREADS) {
+    const uint32_t i = c + tid;
+    const float4 p = pn;
+    if (i + VX_THREADS < N) pn = P(i + VX_THREADS);  // next chunk, in flight across the barrier
+    if (i < N) {
+      const uint32_t k = vx_key(g, p);
+      if (k >= klo && k < khi) {
+        uint32_t lo = 0, hi = U;  // lower_bound
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (ukey[mid] < k) lo = mid + 1; else hi = mid;
         }
-    }
-#pragma unroll
-    for (int u = 0; u < CH; ++u) {
-      const uint32_t i = c + u * VX_THREADS + tid;
-      if (i < N && kk[u] >= klo && kk[u] < khi) {
-        const uint32_t pos = uoff[lo[u]] + atomicAdd(&ufill[lo[u]], 1u);
+        const uint32_t pos = uoff[lo] + atomicAdd(&ufill[lo], 1u);
         members[pos] = (MT)i;
-        if (H) H->rk[i] = (rank0 + lo[u]) << 1;  // the hot ones are re-marked below
+        if (H) H->rk[i] = (rank0 + lo) << 1;  // the hot ones are re-marked below
       }
-      if (c + (u + 1) * VX_THREADS < N) __syncthreads();  // (uniform) chunk u's appends first
     }
     __syncthreads();
   }
