@@ -81,6 +81,9 @@ def parse():
                     help="streams of the sharded leg (every stream split over all ranks; 0: skip the leg)")
     ap.add_argument("--pipelined", action="store_true",
                     help="(the default for the timed steps; kept for older command lines)")
+    ap.add_argument("--pose-first", action="store_true",
+                    help="with --blocking: each step by loam_mapper_solve_pose (returns at the poses; the map "
+                         "update finishes beside the next step's stack VoxelGrid)")
     ap.add_argument("--blocking", action="store_true",
                     help="timed steps one after the other (loam_mapper_solve): step k + 1's input and stack "
                          "VoxelGrid only after step k has finished.  Default: pipelined, each handle queues step "
@@ -196,14 +199,18 @@ def step_inputs(frames, streams, stride, k, first=0):
                                   np.array([f["q"] for f in fs]), np.array([f["t"] for f in fs]))
 
 
-def run_steps(mapper, plan, first, count, poses=None):
+def run_steps(mapper, plan, first, count, poses=None, pose_first=False):
     """count solveMapping steps from the precomputed per-step input arrays; with `poses`, the
     pose of the handle's stream 0 after every step is appended (a host read of the records
-    the solve already copied back)"""
+    the solve already copied back).  pose_first: loam_mapper_solve_pose, which returns at the
+    frame's pose and finishes its map update beside the next frame"""
     iters = 0
     for k in range(first, first + count):
         mapper.input_device_batch_args(plan[k])
-        mapper.solve()
+        if pose_first:
+            mapper.solve_pose()
+        else:
+            mapper.solve()
         iters += mapper.total_iterations()
         if poses is not None:
             poses.append(mapper.pose(0))
@@ -229,13 +236,14 @@ def run_steps_pipelined(mapper, plan, first, count, poses=None):
     return iters
 
 
-def run_handles(mappers, plans, first, count, poses=None, pipelined=False):
+def run_handles(mappers, plans, first, count, poses=None, pipelined=False, pose_first=False):
     """run_steps (or run_steps_pipelined) on every handle, one host thread each (ctypes releases
     the GIL in the library calls): one handle's host work overlaps the others' kernels"""
     if pipelined:
         run_one = lambda h: run_steps_pipelined(mappers[h], plans[h], first, count, poses if h == 0 else None)  # noqa: E731
     else:
-        run_one = lambda h: run_steps(mappers[h], plans[h], first, count, poses if h == 0 else None)  # noqa: E731
+        run_one = lambda h: run_steps(mappers[h], plans[h], first, count, poses if h == 0 else None,  # noqa: E731
+                                      pose_first=pose_first)
     if len(mappers) == 1:
         return run_one(0)
     import threading
@@ -820,7 +828,7 @@ def main():
                 m.debug_counters(reset=True)  # the timed steps only
         barrier()
         t0 = time.perf_counter()
-        it = run_handles(mappers, plans, pre, K, poses, pipelined=not args.blocking)
+        it = run_handles(mappers, plans, pre, K, poses, pipelined=not args.blocking, pose_first=args.pose_first)
         barrier()
         secs = time.perf_counter() - t0
         fam = {}
@@ -1042,19 +1050,24 @@ def main():
         frame f is in flight (loam_mapper_solve_async / _prefetch / _wait, the same results);
         the blocking loam_mapper_solve beside it"""
         out = {}
-        for mode in ("pipelined", "blocking"):
+        for mode in ("pipelined", "blocking", "pose_first"):
             m1 = BatchMapper(1, device=local, exact_voxel_order=exact)
             plan1 = [step_inputs(frames, 1, args.stride, k) for k in range(pre + K)]
             run_steps(m1, plan1, 0, pre)
             torch.cuda.synchronize(local)
             t1 = time.perf_counter()
-            it1 = run_steps_pipelined(m1, plan1, pre, K) if mode == "pipelined" else run_steps(m1, plan1, pre, K)
-            torch.cuda.synchronize(local)
+            if mode == "pipelined":
+                it1 = run_steps_pipelined(m1, plan1, pre, K)
+            else:
+                it1 = run_steps(m1, plan1, pre, K, pose_first=mode == "pose_first")
+            torch.cuda.synchronize(local)  # (every stream of the device: the last map update too)
             d1 = time.perf_counter() - t1
             m1.close()
             out[mode] = {"value": it1 / d1, "ms_per_frame": 1e3 * d1 / K, "iterations": it1}
         return {**out["pipelined"], "blocking_value": out["blocking"]["value"],
-                "blocking_ms_per_frame": out["blocking"]["ms_per_frame"]}
+                "blocking_ms_per_frame": out["blocking"]["ms_per_frame"],
+                "pose_first_value": out["pose_first"]["value"],
+                "pose_first_ms_per_frame": out["pose_first"]["ms_per_frame"]}
 
     single = single_exact = None
     if not args.no_single_stream and rank == 0 and world == 1 and not args.shard:
@@ -1223,6 +1236,9 @@ def main():
             out["speedup_vs_cpu_whole_host_estimate"] = round(out["value"] / allc["whole_host_estimate"]["value"], 2)
             if single is not None:
                 out["single_stream"]["speedup_vs_cpu_baseline"] = round(single["value"] / cpu["value"], 2)
+                out["single_stream"]["blocking_speedup_vs_cpu_baseline"] = round(single["blocking_value"] / cpu["value"], 2)
+                out["single_stream"]["pose_first_speedup_vs_cpu_baseline"] = round(
+                    single["pose_first_value"] / cpu["value"], 2)
             if single_exact is not None:
                 out["single_stream_exact_voxel_order"]["speedup_vs_cpu_baseline"] = round(
                     single_exact["value"] / cpu["value"], 2)

@@ -272,6 +272,20 @@ int32_t loam_mapper_solve(loam_mapper* h);
  * is dropped, and the call that tried returns that error with "dropped" in loam_last_error. */
 int32_t loam_mapper_solve_async(loam_mapper* h);
 int32_t loam_mapper_wait(loam_mapper* h);
+/* loam_mapper_solve for a caller that needs the pose before the map update: it returns once the
+ * frame's optimisation is done (laser_mapping.cpp:516-736: the pose the node publishes as
+ * /aft_mapped_to_init, and the frame's stats), while the insertion and re-VoxelGrid of the cubes
+ * (:741-808) are still running on the device.  They finish beside the next frame's stack
+ * VoxelGrid (the next call queues that frame behind this one, as loam_mapper_solve_async does)
+ * or before any call that reads or changes the map (every call but _pose / _stats / _stats_all /
+ * _total_iterations / _get_state, which report this frame).  Same results as loam_mapper_solve,
+ * bit for bit.  Status: a failure found by the optimisation (or a deferred frame, run again on
+ * the host path) is returned by this call, after the whole frame; one of the map update
+ * (LOAM_ERR_CAPACITY) is returned as LOAM_ERR_EARLIER by the next solve / wait.  Frames that
+ * do not run as the handle's hipGraph (handles of more than 4 streams, sharded, profiling, a
+ * recentering or compaction ahead) are finished whole.  The first call switches the handle's
+ * frame sequence to one that also writes the records after the optimisation. */
+int32_t loam_mapper_solve_pose(loam_mapper* h);
 /* queue the stack VoxelGrids of every stream's pending input now */
 int32_t loam_mapper_prefetch(loam_mapper* h);
 /* pose after solveMapping: q_w_curr (xyzw), t_w_curr (laser_mapping.cpp:826-832) */

@@ -524,6 +524,54 @@ def test_chained_solve_matches_blocking(seq, n_streams, exact, defer_every, monk
         assert queued >= n - 2, queued  # every frame but the first ran queued behind another
 
 
+@pytest.mark.parametrize("n_streams,exact,defer_every", [(1, 0, 0), (1, 1, 0), (3, 0, 0), (1, 0, 3), (6, 0, 0)])
+def test_solve_pose_matches_blocking(seq, n_streams, exact, defer_every, monkeypatch):
+    """loam_mapper_solve_pose (include/loam_core.h): each call returns at the frame's poses, its
+    map update finishing beside the next frame; poses, counts and iterations after every frame,
+    then every cube of the final maps, equal the blocking loam_mapper_solve bit for bit.
+    defer_every > 0: frames the device defers are finished whole (run again on the host path);
+    6 streams: the handle does not run frames as a graph, every frame is finished whole."""
+    def row(m, s):
+        st = m.stats(s)
+        q, t = m.pose(s)
+        return (q.tobytes(), t.tobytes(), st.corner_stack, st.surf_stack, tuple(st.corner_num), tuple(st.surf_num),
+                st.lm[0].iterations, st.lm[1].iterations, tuple(st.center), st.valid_num, m.total_iterations())
+
+    def feed(m, f):
+        for s in range(n_streams):
+            rec = seq[f + s]
+            m.input(s, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+
+    def maps(m):
+        return [[m.cubes(s, w) for w in (0, 1)] for s in range(n_streams)]
+
+    n = len(seq) - n_streams + 1
+    ref = BatchMapper(n_streams, exact_voxel_order=exact)
+    want = []
+    for f in range(n):
+        feed(ref, f)
+        ref.solve()
+        want.append([row(ref, s) for s in range(n_streams)])
+    want_maps = maps(ref)
+    ref.close()
+    if defer_every:
+        monkeypatch.setenv("LOAM_DEFER_EVERY", str(defer_every))
+    m = BatchMapper(n_streams, exact_voxel_order=exact)
+    monkeypatch.delenv("LOAM_DEFER_EVERY", raising=False)
+    got = []
+    for f in range(n):
+        feed(m, f)
+        m.solve_pose()
+        got.append([row(m, s) for s in range(n_streams)])
+    got_maps = maps(m)  # (finishes the last frame's map update first)
+    m.close()
+    assert got == want
+    for gs, ws in zip(got_maps, want_maps):
+        for gc, wc in zip(gs, ws):
+            assert sorted(gc) == sorted(wc)
+            assert all(np.array_equal(gc[c], wc[c]) for c in wc)
+
+
 @pytest.mark.parametrize("exact", [0, 1])
 @pytest.mark.parametrize("n_streams", [2, 16])
 def test_split_prefetch_matches_blocking(seq, exact, n_streams):
@@ -681,6 +729,22 @@ def test_async_capacity_error_is_held_for_wait(seq):
     # every frame ran exactly once: the final pose is the blocking solve's
     assert pose(m) == want[-1]
     m.close()
+
+    # loam_mapper_solve_pose: a failure found before the map update (here the submap size) is
+    # returned by the call of its own frame, as by the blocking solve, with the same poses
+    m = BatchMapper(1, max_submap_points=cap)
+    got, got_fail = [], []
+    for rec in seq:
+        m.input(0, rec["corner"], rec["surf"], rec["q_wodom"], rec["t_wodom"])
+        try:
+            m.solve_pose()
+            got_fail.append(False)
+        except LoamError as e:
+            assert e.rc == -3, e
+            got_fail.append(True)
+        got.append(pose(m))
+    m.close()
+    assert got_fail == want_fail and got == want
 
 
 @pytest.mark.parametrize("target", [35000, 46000])

@@ -1969,6 +1969,7 @@ struct FrameRec {
   bool has_deferred = false;  // known (its records are back) to have deferred streams
   bool pending = false;       // not enqueued yet: inputs and stack taken, run on the host path later
   bool behind = false;        // solve_async was called with another frame in the queue
+  bool early_seen = false;    // its poses and stats were taken from the early records (loam_mapper_solve_pose)
   uint32_t epoch = 0;         // its frame number (the done word frame_out writes)
   int fpar = 0;
   uint64_t seq = 0;  // enqueue order (0: nothing was enqueued)
@@ -2039,6 +2040,13 @@ struct loam_mapper {
   PinnedArray<unsigned long long> done;  // [2 parities]
   unsigned long long* done_dev = nullptr;
   StreamFrame* hfo_dev[2] = {nullptr, nullptr};
+  // loam_mapper_solve_pose: graph-path frames also write their records after the second LM round
+  // (before the insertion and re-VoxelGrid) with their own done word
+  bool early = false;
+  PinnedArray<StreamFrame> hfo_early[2];
+  PinnedArray<unsigned long long> done_early;
+  StreamFrame* hfo_early_dev[2] = {nullptr, nullptr};
+  unsigned long long* done_early_dev = nullptr;
   uint32_t grow_max = 0;     // largest arena growth of one frame seen (compaction foresight)
   std::vector<std::array<uint32_t, 2>> last_tail;
   hipEvent_t ev_stack = nullptr;   // after the last stack launch (on st2)
@@ -2504,6 +2512,16 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
         hipHostGetDevicePointer(&dp, h->done.data(), 0) != hipSuccess)
       return fail(LOAM_ERR_HIP);
     h->done_dev = reinterpret_cast<unsigned long long*>(dp);
+    if (!h->done_early.assign(2, 0ull, hipHostMallocMapped | hipHostMallocCoherent) ||
+        hipHostGetDevicePointer(&dp, h->done_early.data(), 0) != hipSuccess)
+      return fail(LOAM_ERR_HIP);
+    h->done_early_dev = reinterpret_cast<unsigned long long*>(dp);
+    for (int p = 0; p < 2; ++p) {
+      if (!h->hfo_early[p].assign(B, StreamFrame{}, hipHostMallocMapped | hipHostMallocCoherent) ||
+          hipHostGetDevicePointer(&dp, h->hfo_early[p].data(), 0) != hipSuccess)
+        return fail(LOAM_ERR_HIP);
+      h->hfo_early_dev[p] = reinterpret_cast<StreamFrame*>(dp);
+    }
   }
   h->hs.assign(B, HostStream{});
   h->last_tail.assign(B, std::array<uint32_t, 2>{0u, 0u});
@@ -2552,12 +2570,12 @@ static bool chain_capable(const loam_mapper* h);
   } while (0)
 // the result calls (pose, stats, state, iterations) report the newest finished frame: they finish
 // the oldest frame in the queue unless it was given behind another (whose results they report)
-#define SETTLE_RESULTS(h)                                  \
-  do {                                                     \
-    if ((h) && !(h)->q.empty() && !(h)->q.front().behind) { \
-      LOAM_HIP(hipSetDevice((h)->dev));                    \
-      TRY(finish_oldest(h));                               \
-    }                                                      \
+#define SETTLE_RESULTS(h)                                                                   \
+  do {                                                                                      \
+    if ((h) && !(h)->q.empty() && !(h)->q.front().behind && !(h)->q.front().early_seen) { \
+      LOAM_HIP(hipSetDevice((h)->dev));                                                     \
+      TRY(finish_oldest(h));                                                                \
+    }                                                                                       \
   } while (0)
 
 int32_t loam_mapper_destroy(loam_mapper* h) {
@@ -2805,6 +2823,8 @@ static void capture_frame(loam_mapper* h, const MapperDev& D, int fpar, hipStrea
     k_geom<<<B * CORR_BLK, CORR_THREADS, 0, st>>>(D, round);
     k_lm_round<<<lm_padded(B) * h->lm_G, LM_THREADS, 0, st>>>(D, round, h->lm_G);
   }
+  // (loam_mapper_solve_pose) the final poses and the frame's stats are in the records now
+  if (h->early) k_frame_out<<<1, 256, 0, st>>>(D, h->hfo_early_dev[fpar], h->done_early_dev + fpar);
   k_insert_bucket<<<B * 2, VX_THREADS, 0, st>>>(D);
   launch_revox(h, D, st);
   k_frame_out<<<1, 256, 0, st>>>(D, h->hfo_dev[fpar], h->done_dev + fpar);
@@ -3058,14 +3078,14 @@ static int32_t mapper_replay(loam_mapper* h, const FrameRec& R, const std::vecto
 // a queued frame is done when frame_out has written its number to the done word of its parity
 // (the words only grow: a later frame of the same parity is not enqueued before this one is
 // finished).  The stream is polled for errors while waiting.
-static int32_t wait_done(loam_mapper* h, const FrameRec& R) {
-  const volatile unsigned long long* w = h->done.data() + R.fpar;
+static int32_t wait_word(loam_mapper* h, const unsigned long long* word, uint32_t epoch) {
+  const volatile unsigned long long* w = word;
   for (uint64_t spins = 0;; ++spins) {
-    if (__atomic_load_n(const_cast<const unsigned long long*>(w), __ATOMIC_ACQUIRE) >= R.epoch) return LOAM_OK;
+    if (__atomic_load_n(const_cast<const unsigned long long*>(w), __ATOMIC_ACQUIRE) >= epoch) return LOAM_OK;
     if ((spins & 1023) == 1023) {
       const hipError_t e = hipStreamQuery(h->st);
       if (e == hipSuccess) {  // the stream drained: the word must be there now
-        if (__atomic_load_n(const_cast<const unsigned long long*>(w), __ATOMIC_ACQUIRE) >= R.epoch) return LOAM_OK;
+        if (__atomic_load_n(const_cast<const unsigned long long*>(w), __ATOMIC_ACQUIRE) >= epoch) return LOAM_OK;
         set_error("loam_mapper: frame finished without its done word");
         return LOAM_ERR_HIP;
       }
@@ -3073,6 +3093,7 @@ static int32_t wait_done(loam_mapper* h, const FrameRec& R) {
     }
   }
 }
+static int32_t wait_done(loam_mapper* h, const FrameRec& R) { return wait_word(h, h->done.data() + R.fpar, R.epoch); }
 
 // the host side of one finished frame: transformUpdate (:147-151), stats, errors, timing.
 // replay: a deferred frame run again for some streams (the others keep what their frame gave).
@@ -3435,6 +3456,84 @@ int32_t loam_mapper_wait(loam_mapper* h) {
 int32_t loam_mapper_solve(loam_mapper* h) {
   TRY(loam_mapper_solve_async(h));
   SETTLE(h);
+  return take_held(h);
+}
+
+// the newest frame's poses and stats from its early records (written after the second LM round):
+// false when they cannot stand for the frame (a deferred stream, or an error flag already set),
+// then the caller finishes the frame whole
+static bool take_early(loam_mapper* h, FrameRec& R) {
+  const StreamFrame* FE = h->hfo_early[R.fpar].data();
+  for (int s = 0; s < h->B; ++s)
+    if (R.active[s] && (FE[s].deferred || FE[s].err)) return false;
+  for (int s = 0; s < h->B; ++s) {
+    const StreamFrame& F = FE[s];
+    HostStream& H = h->hs[s];
+    H.solved_last = R.active[s] && F.active;
+    if (!H.solved_last) continue;
+    for (int i = 0; i < 7; ++i) H.pose[i] = F.pose[i];
+    for (int i = 0; i < 4; ++i) H.q_wodom[i] = R.wodom[s][i];
+    for (int i = 0; i < 3; ++i) H.t_wodom[i] = R.wodom[s][4 + i];
+    host_transform_update(H);  // (the full finish repeats it on the same values)
+    loam_map_stats& S = H.st;
+    S.optimized = F.optimize;
+    S.corner_stack = F.nc_stack;
+    S.surf_stack = F.ns_stack;
+    S.corner_map = F.sub_n[0];
+    S.surf_map = F.sub_n[1];
+    for (int r = 0; r < 2; ++r) {
+      S.corner_num[r] = F.corner_num[r];
+      S.surf_num[r] = F.surf_num[r];
+      const LmState& L = F.lm[r];
+      S.lm[r].iterations = F.optimize ? L.iteration : 0;
+      S.lm[r].successful = L.successful;
+      S.lm[r].invalid = L.invalid;
+      S.lm[r].termination = L.term;
+      S.lm[r].initial_cost = L.initial_cost;
+      S.lm[r].final_cost = L.min_cost;
+    }
+    for (int a = 0; a < 3; ++a) {
+      S.center[a] = F.center[a];
+      H.cen[a] = F.cen[a];
+    }
+    S.valid_num = F.valid_num;
+    S.ms_total = 0;
+    S.ms_opt = 0;
+    S.queued = R.chained ? 1 : 0;
+    S.rerun = 0;
+  }
+  R.early_seen = true;
+  return true;
+}
+
+int32_t loam_mapper_solve_pose(loam_mapper* h) {
+  if (!h) return LOAM_ERR_ARG;
+  LOAM_HIP(hipSetDevice(h->dev));
+  if (!h->early) {  // the frames' sequences gain the early records: recapture the graphs
+    SETTLE(h);
+    for (auto& gp : h->gexec)
+      for (auto& g : gp)
+        if (g) {
+          (void)hipGraphExecDestroy(g);
+          g = nullptr;
+        }
+    h->early = true;
+  }
+  TRY(loam_mapper_solve_async(h));  // queued behind the previous frame, as the pipelined solves
+  while (h->q.size() > 1) {  // the previous frame: its insertion and re-VoxelGrid ran meanwhile
+    const int32_t older = finish_oldest(h);
+    if (older == LOAM_ERR_HIP || older == LOAM_ERR_ARG || older == LOAM_ERR_STATE) return older;
+    hold_status(h, older);
+  }
+  TRY(launch_front(h));  // (a frame kept pending behind it is enqueued now)
+  if (h->q.empty()) return take_held(h);
+  FrameRec& R = h->q.front();
+  bool early = R.graph && !R.pending;
+  if (early) TRY(wait_word(h, h->done_early.data() + R.fpar, R.epoch));
+  if (!early || !take_early(h, R)) {  // the frame whole: its status now
+    const int32_t rc = finish_oldest(h);
+    if (rc != LOAM_OK) return rc;
+  }
   return take_held(h);
 }
 

@@ -113,6 +113,7 @@ SIGNATURES = {
     "loam_mapper_solve": (c_i32, [vp]),
     "loam_mapper_solve_async": (c_i32, [vp]),
     "loam_mapper_wait": (c_i32, [vp]),
+    "loam_mapper_solve_pose": (c_i32, [vp]),
     "loam_mapper_prefetch": (c_i32, [vp]),
     "loam_mapper_debug_counters": (c_i32, [vp, vp, c_i32, c_i32]),
     "loam_mapper_pose": (c_i32, [vp, c_i32, vp, vp]),

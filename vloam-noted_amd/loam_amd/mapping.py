@@ -139,6 +139,11 @@ class BatchMapper:
         """finish the oldest frame in the queue; pose / stats / get_state then report it"""
         check(lib().loam_mapper_wait(self.h))
 
+    def solve_pose(self):
+        """solve() that returns at the frame's pose: the insertion and re-VoxelGrid of the cubes
+        finish beside the next frame (include/loam_core.h loam_mapper_solve_pose)"""
+        check(lib().loam_mapper_solve_pose(self.h))
+
     def prefetch(self):
         """queue the stack VoxelGrids of the pending inputs now, beside a frame in flight"""
         check(lib().loam_mapper_prefetch(self.h))
