@@ -161,6 +161,9 @@ class BatchMapper {
   // frame; an older frame it finished to make room that failed is reported by the next wait() /
   // solve() (LOAM_ERR_EARLIER), so a caller that re-submits on a throw never queues a frame twice.
   void solve_async() { check(loam_mapper_solve_async(h_)); }
+  // solve() that returns at the poses (loam_mapper_solve_pose): the map update of the frame
+  // finishes beside the next frame's stack VoxelGrid; same results, bit for bit
+  void solve_pose() { check(loam_mapper_solve_pose(h_)); }
   void wait() { check(loam_mapper_wait(h_)); }
   // queue the stack VoxelGrids of the inputs given so far (they run beside the frame in flight)
   void prefetch() { check(loam_mapper_prefetch(h_)); }
@@ -210,6 +213,10 @@ class LaserMapping {
     m_.input(0, corner_last, surf_last, q_wodom_curr, t_wodom_curr, skip_frame);
   }
   void solveMapping() { m_.solve(); }
+  // solveMapping that returns once q_w_curr / t_w_curr are final ("Pose first"):
+  // output() and stats() read at once; the cube insertion and re-VoxelGrid run on beside the
+  // next frame, and laserCloudMap() waits for them
+  void solveMappingPose() { m_.solve_pose(); }
   // solveMapping split so that the node publishes frame f - 1 while frame f runs (INTEGRATION.md,
   // "Pipelined mapping"): input(f); solveMappingAsync(); waitMapping() finishes f - 1, whose
   // output() / stats() / laserCloudMap() are then read.  Host clouds are copied at input().

@@ -81,10 +81,14 @@ static double pose_diff(const double q[4], const double t[3], const std::array<d
   return d;
 }
 
-// queued = false: each frame's solveMapping blocks (the reference's facade,
-// lidar_odometry_mapping.cpp:144-176); queued = true: frame f is enqueued with solveMappingAsync
-// and frame f - 1 is waited for and "published" after it (pipelined mapping)
-static int frames_through_the_shim(bool queued, const std::vector<std::array<double, 7>>& ref, int n_az) {
+// mode BLOCKING: each frame's solveMapping blocks (the reference's facade,
+// lidar_odometry_mapping.cpp:144-176); QUEUED: frame f is enqueued with solveMappingAsync and
+// frame f - 1 is waited for and "published" after it (pipelined mapping); POSE:
+// solveMappingPose, frame f published at once, its map update finishing beside frame f + 1
+enum ShimMode { BLOCKING, QUEUED, POSE };
+static int frames_through_the_shim(ShimMode mode, const std::vector<std::array<double, 7>>& ref, int n_az) {
+  const bool queued = mode == QUEUED;
+  static const char* const names[] = {"blocking", "queued", "pose"};
   loam_params p = loam_amd::default_params();
   p.exact_voxel_order = 1;  // free-running frames: PCL's VoxelGrid order, like the oracle
   loam_amd::ScanRegistration sr(p, 0);
@@ -101,7 +105,7 @@ static int frames_through_the_shim(bool queued, const std::vector<std::array<dou
     worst = std::fmax(worst, d);
     const loam_map_stats st = lm.stats();
     std::printf("%s frame %d: mapping t (%.4f %.4f %.4f), LM iterations %d + %d, |d| %.3e\n",
-                queued ? "queued" : "blocking", f, tm[0], tm[1], tm[2], st.lm[0].iterations, st.lm[1].iterations, d);
+                names[mode], f, tm[0], tm[1], tm[2], st.lm[0].iterations, st.lm[1].iterations, d);
   };
   for (int f = 0; f < nf; ++f) {
     const int n = synth_frame(23, f, n_az, 1.0, xyz.data(), gt);
@@ -114,8 +118,11 @@ static int frames_through_the_shim(bool queued, const std::vector<std::array<dou
     double q[4], t[3];
     const bool skip = lo.output(q, t);
     lm.input(lo.copy_last(0), lo.copy_last(1), q, t, skip);
-    if (!queued) {
+    if (mode == BLOCKING) {
       lm.solveMapping();
+      publish(f);
+    } else if (mode == POSE) {
+      lm.solveMappingPose();
       publish(f);
     } else {
       lm.solveMappingAsync();  // frame f, behind f - 1 on the device
@@ -163,7 +170,9 @@ int main(int argc, char** argv) {
   }
   const int n_az = 1000;
   const std::vector<std::array<double, 7>> ref = oracle_poses(6, n_az);
-  const int rc = frames_through_the_shim(false, ref, n_az);
-  if (rc) return rc;
-  return frames_through_the_shim(true, ref, n_az);
+  for (ShimMode mode : {BLOCKING, QUEUED, POSE}) {
+    const int rc = frames_through_the_shim(mode, ref, n_az);
+    if (rc) return rc;
+  }
+  return 0;
 }

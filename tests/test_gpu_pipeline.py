@@ -70,7 +70,8 @@ def test_cxx_shim_frames(tmp_path):
     """the header-only C++ shim (include/loam_core.hpp) driving six frames through
     ScanRegistration -> LaserOdometry -> LaserMapping with host clouds between the stages, as the
     reference nodes would (tests/cxx/shim_check.cpp), against the oracle pipeline: within 1e-4,
-    with the blocking solveMapping and with frames queued (solveMappingAsync / waitMapping)"""
+    with the blocking solveMapping, with frames queued (solveMappingAsync / waitMapping) and with
+    solveMappingPose"""
     import os
     import subprocess
     from conftest import ROOT
@@ -85,7 +86,7 @@ def test_cxx_shim_frames(tmp_path):
     r = subprocess.run([exe, "1"], capture_output=True, text=True, timeout=120)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "blocking frame 5" in r.stdout and "queued frame 5" in r.stdout
+    assert "blocking frame 5" in r.stdout and "queued frame 5" in r.stdout and "pose frame 5" in r.stdout
 
 
 def test_pipelined_chain_matches_sequential():
