@@ -2390,6 +2390,8 @@ static int32_t mapper_create(const loam_params* p, int32_t device, int32_t n_str
   // B = 128 it costs 1.2x (more lanes idle on pruned cells): one lane per query there
   h->knn_cs = n_streams <= 4 ? 8 : 0;
   D.knn_blk = n_streams <= 4 ? 4 * CORR_BLK : CORR_BLK;
+  if (const char* benv = std::getenv("LOAM_KNN_BLK"))  // measurement override (cell-split workgroups per stream)
+    if (h->knn_cs) D.knn_blk = std::max(1, std::min(64 * CORR_BLK, std::atoi(benv)));
   ALLOC(D.fr, B);
   for (int m = 0; m < 2; ++m) {
     ALLOC(D.in_pts[m], B * D.max_in);
