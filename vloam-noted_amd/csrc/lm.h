@@ -590,6 +590,9 @@ __device__ inline void lm_acquire() {
 #endif
 }
 
+#ifndef LM_RED_BATCH
+#define LM_RED_BATCH 16  // the leader's partial loads in flight per batch
+#endif
 constexpr int LM_MAX_PASSES = 8;          // a round needs <= 1 + max_num_iterations = 5
 constexpr uint32_t LM_SPIN_LIMIT = 1u << 21;
 constexpr uint32_t LM_PEER_SPIN_LIMIT = 1u << 24;  // the cross-rank wait: other ranks' kernels
@@ -837,14 +840,16 @@ __device__ inline void lm_round_device(const LmJob& J, int g, int G) {
     if (wid == 0) {
       // lane i sums accumulator i over the shares in order (G <= 32: one lane per
       // accumulator beats a shuffle tree per accumulator)
-      if (lane < LM_NACC) {  // loads 8 at a time in flight (the last batch too), added in share order
+      if (lane < LM_NACC) {  // loads LM_RED_BATCH at a time in flight (one batch up to G = 17),
+                             // added in share order
         double v = bsum0[lane];
-        for (int c = 1; c < G; c += 8) {
-          double q[8];
+        for (int c = 1; c < G; c += LM_RED_BATCH) {
+          double q[LM_RED_BATCH];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) q[u] = c + u < G ? lm_part_load(&part[(size_t)(c + u) * LM_NACC + lane]) : 0.0;
+          for (int u = 0; u < LM_RED_BATCH; ++u)
+            q[u] = c + u < G ? lm_part_load(&part[(size_t)(c + u) * LM_NACC + lane]) : 0.0;
 #pragma unroll
-          for (int u = 0; u < 8; ++u)
+          for (int u = 0; u < LM_RED_BATCH; ++u)
             if (c + u < G) v += q[u];
         }
         sred[lane] = v;
