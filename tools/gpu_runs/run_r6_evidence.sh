@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-6 evidence on the final code: kernel-trace stats of the default bench (B = 128, both legs),
-# one stream queued and blocking traces, then one PMC pass per counter (kernel trace only), then
+# one stream queued, blocking and pose-first traces, then one PMC pass per counter (kernel trace only), then
 # the phase counters (LM, re-VoxelGrid of the large items, few-stream stack VoxelGrid)
 cd "$(dirname "$0")/../.."
 R="$(pwd)"
@@ -11,6 +11,7 @@ cd /tmp && export TMPDIR=/tmp && \
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" $A > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof_bench.err" && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof1" -o run --output-format csv -- python3 "$R/bench.py" $B1 > "$R/gpurun_out/prof1_bench.json" 2> "$R/gpurun_out/prof1_bench.err" && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/profb" -o run --output-format csv -- python3 "$R/bench.py" $B1 --blocking > "$R/gpurun_out/profb_bench.json" 2> "$R/gpurun_out/profb_bench.err" && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/profp" -o run --output-format csv -- python3 "$R/bench.py" $B1 --blocking --pose-first > "$R/gpurun_out/profp_bench.json" 2> "$R/gpurun_out/profp_bench.err" && \
 timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$R/gpurun_out/pmc_fetch" -o run --output-format csv -- python3 "$R/bench.py" $A --no-exact-leg --no-prof --steps 5 > "$R/gpurun_out/pmc_fetch.json" 2> "$R/gpurun_out/pmc_fetch.err" && \
 timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$R/gpurun_out/pmc_write" -o run --output-format csv -- python3 "$R/bench.py" $A --no-exact-leg --no-prof --steps 5 > "$R/gpurun_out/pmc_write.json" 2> "$R/gpurun_out/pmc_write.err" && \
 cd "$R" && \
