@@ -3097,6 +3097,33 @@ static int32_t wait_word(loam_mapper* h, const unsigned long long* word, uint32_
 }
 static int32_t wait_done(loam_mapper* h, const FrameRec& R) { return wait_word(h, h->done.data() + R.fpar, R.epoch); }
 
+// a finished frame's stream record -> the stream's stats and cube-grid centre (what
+// loam_mapper_stats / _get_state report)
+static void frame_stats(const StreamFrame& F, HostStream& H) {
+  loam_map_stats& S = H.st;
+  S.optimized = F.optimize;
+  S.corner_stack = F.nc_stack;
+  S.surf_stack = F.ns_stack;
+  S.corner_map = F.sub_n[0];
+  S.surf_map = F.sub_n[1];
+  for (int r = 0; r < 2; ++r) {
+    S.corner_num[r] = F.corner_num[r];
+    S.surf_num[r] = F.surf_num[r];
+    const LmState& L = F.lm[r];
+    S.lm[r].iterations = F.optimize ? L.iteration : 0;
+    S.lm[r].successful = L.successful;
+    S.lm[r].invalid = L.invalid;
+    S.lm[r].termination = L.term;
+    S.lm[r].initial_cost = L.initial_cost;
+    S.lm[r].final_cost = L.min_cost;
+  }
+  for (int a = 0; a < 3; ++a) {
+    S.center[a] = F.center[a];
+    H.cen[a] = F.cen[a];
+  }
+  S.valid_num = F.valid_num;
+}
+
 // the host side of one finished frame: transformUpdate (:147-151), stats, errors, timing.
 // replay: a deferred frame run again for some streams (the others keep what their frame gave).
 static int32_t mapper_finish_rec(loam_mapper* h, const FrameRec& R, bool replay) {
@@ -3179,27 +3206,7 @@ static int32_t mapper_finish_rec(loam_mapper* h, const FrameRec& R, bool replay)
       h->last_tail[s][m] = F.arena_tail[m];
     }
     loam_map_stats& S = H.st;
-    S.optimized = F.optimize;
-    S.corner_stack = F.nc_stack;
-    S.surf_stack = F.ns_stack;
-    S.corner_map = F.sub_n[0];
-    S.surf_map = F.sub_n[1];
-    for (int r = 0; r < 2; ++r) {
-      S.corner_num[r] = F.corner_num[r];
-      S.surf_num[r] = F.surf_num[r];
-      const LmState& L = F.lm[r];
-      S.lm[r].iterations = F.optimize ? L.iteration : 0;
-      S.lm[r].successful = L.successful;
-      S.lm[r].invalid = L.invalid;
-      S.lm[r].termination = L.term;
-      S.lm[r].initial_cost = L.initial_cost;
-      S.lm[r].final_cost = L.min_cost;
-    }
-    for (int a = 0; a < 3; ++a) {
-      S.center[a] = F.center[a];
-      H.cen[a] = F.cen[a];
-    }
-    S.valid_num = F.valid_num;
+    frame_stats(F, H);
     S.ms_total = ms_total;
     S.ms_opt = ms_opt;
     S.queued = R.chained ? 1 : 0;
@@ -3478,27 +3485,7 @@ static bool take_early(loam_mapper* h, FrameRec& R) {
     for (int i = 0; i < 3; ++i) H.t_wodom[i] = R.wodom[s][4 + i];
     host_transform_update(H);  // (the full finish repeats it on the same values)
     loam_map_stats& S = H.st;
-    S.optimized = F.optimize;
-    S.corner_stack = F.nc_stack;
-    S.surf_stack = F.ns_stack;
-    S.corner_map = F.sub_n[0];
-    S.surf_map = F.sub_n[1];
-    for (int r = 0; r < 2; ++r) {
-      S.corner_num[r] = F.corner_num[r];
-      S.surf_num[r] = F.surf_num[r];
-      const LmState& L = F.lm[r];
-      S.lm[r].iterations = F.optimize ? L.iteration : 0;
-      S.lm[r].successful = L.successful;
-      S.lm[r].invalid = L.invalid;
-      S.lm[r].termination = L.term;
-      S.lm[r].initial_cost = L.initial_cost;
-      S.lm[r].final_cost = L.min_cost;
-    }
-    for (int a = 0; a < 3; ++a) {
-      S.center[a] = F.center[a];
-      H.cen[a] = F.cen[a];
-    }
-    S.valid_num = F.valid_num;
+    frame_stats(F, H);
     S.ms_total = 0;
     S.ms_opt = 0;
     S.queued = R.chained ? 1 : 0;
