@@ -1,5 +1,5 @@
 #!/bin/bash
-# cell-index hash updates batched: mapping parity tests, one-stream A/B against HEAD, re-VoxelGrid
+# cell-index build (hash batching, then load batching): mapping parity tests, one-stream A/B against HEAD, re-VoxelGrid
 # phase counters of both, B = 128 A/B
 cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
