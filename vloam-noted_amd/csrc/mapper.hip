@@ -1424,27 +1424,39 @@ __global__ void __launch_bounds__(VX_THREADS) k_insert_bucket(MapperDev D) {
     const int c0 = F.center[0], c1 = F.center[1], c2 = F.center[2];
     const int e0 = F.cen[0], e1 = F.cen[1], e2 = F.cen[2];
     const uint32_t epoch = F.epoch;
-    for (int i = tid; i < n; i += VX_THREADS) {
-      const float4 sel = to_map(X, D.stack[m][(size_t)s * D.max_in + i]);
-      const int ci = cube_of(sel.x, e0), cj = cube_of(sel.y, e1), ck = cube_of(sel.z, e2);
-      int tag = -1;
-      // sharded: only the owner of the point's 4 m block stores it (comm.h)
-      const bool mine = !D.sharded || shard_owner(sel.x, sel.y, sel.z, 1.0f / D.leaf[m], D.blk_v[m], D.nrank) == D.rank;
-      if (mine && ci >= 0 && ci < CW && cj >= 0 && cj < CH && ck >= 0 && ck < CD) {
-        tag = ci + CW * cj + CW * CH * ck;
-        const bool in_window = ci >= c0 - 2 && ci <= c0 + 2 && cj >= c1 - 2 && cj <= c1 + 2 && ck >= c2 - 1 && ck <= c2 + 1;
-        if (!in_window) {
-          uint32_t* fl = D.extra_flag + sm_index(s, m) * NCUBE + tag;
-          if (atomicExch(fl, epoch) != epoch) {
-            int e = atomicAdd(&F.extra_n[m], 1);
-            if (e < EXTRA_CAP) F.extra_list[m][e] = tag;
-            else atomicOr(&F.err, MAP_ERR_EXTRA);
+    // the stack points INS_LOADS at a time from a clamped index, all in flight before the first is
+    // transformed (a load per loop trip is one memory latency per trip)
+    constexpr int INS_LOADS = 4;
+    const float4* stk = D.stack[m] + (size_t)s * D.max_in;
+    for (int i0 = tid; i0 < n; i0 += INS_LOADS * VX_THREADS) {
+      float4 q[INS_LOADS];
+#pragma unroll
+      for (int u = 0; u < INS_LOADS; ++u) q[u] = stk[min(i0 + u * VX_THREADS, n - 1)];
+#pragma unroll
+      for (int u = 0; u < INS_LOADS; ++u) {
+        const int i = i0 + u * VX_THREADS;
+        if (i >= n) break;
+        const float4 sel = to_map(X, q[u]);
+        const int ci = cube_of(sel.x, e0), cj = cube_of(sel.y, e1), ck = cube_of(sel.z, e2);
+        int tag = -1;
+        // sharded: only the owner of the point's 4 m block stores it (comm.h)
+        const bool mine = !D.sharded || shard_owner(sel.x, sel.y, sel.z, 1.0f / D.leaf[m], D.blk_v[m], D.nrank) == D.rank;
+        if (mine && ci >= 0 && ci < CW && cj >= 0 && cj < CH && ck >= 0 && ck < CD) {
+          tag = ci + CW * cj + CW * CH * ck;
+          const bool in_window = ci >= c0 - 2 && ci <= c0 + 2 && cj >= c1 - 2 && cj <= c1 + 2 && ck >= c2 - 1 && ck <= c2 + 1;
+          if (!in_window) {
+            uint32_t* fl = D.extra_flag + sm_index(s, m) * NCUBE + tag;
+            if (atomicExch(fl, epoch) != epoch) {
+              int e = atomicAdd(&F.extra_n[m], 1);
+              if (e < EXTRA_CAP) F.extra_list[m][e] = tag;
+              else atomicOr(&F.err, MAP_ERR_EXTRA);
+            }
           }
         }
+        const size_t o = sm_index(s, m) * D.max_in + i;
+        D.ins_pts[o] = sel;
+        D.ins_tag[o] = tag;
       }
-      const size_t o = sm_index(s, m) * D.max_in + i;
-      D.ins_pts[o] = sel;
-      D.ins_tag[o] = tag;
     }
     __syncthreads();  // the points, tags and the out-of-window list, for the grouping below
   }
@@ -1508,9 +1520,18 @@ __global__ void __launch_bounds__(VX_THREADS) k_insert_bucket(MapperDev D) {
     if (lane == 63) off[INS_SLOTS] = x;
   }
   __syncthreads();
+  // software pipeline: the next chunk's tag and point are loaded while this chunk is grouped
+  int t_next = tid < n ? tag[tid] : -1;
+  float4 p_next = tid < n ? pts[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
   for (int c0 = 0; c0 < n; c0 += VX_THREADS) {
     const int i = c0 + tid;
-    const int t = i < n ? tag[i] : -1;
+    const int t = t_next;
+    const float4 p_cur = p_next;
+    t_next = -1;  // (past the end: no point)
+    if (i + VX_THREADS < n) {
+      t_next = tag[i + VX_THREADS];
+      p_next = pts[i + VX_THREADS];
+    }
     const int sl = t >= 0 ? cslot[t] : -1;
     for (int k = tid; k < VX_WAVES * INS_SLOTS; k += VX_THREADS) (&wcnt[0][0])[k] = 0;
     __syncthreads();
@@ -1541,7 +1562,7 @@ __global__ void __launch_bounds__(VX_THREADS) k_insert_bucket(MapperDev D) {
       base[tid] = acc;
     }
     __syncthreads();
-    if (sl >= 0) out[wcnt[wid][sl] + rank] = pts[i];
+    if (sl >= 0) out[wcnt[wid][sl] + rank] = p_cur;
     __syncthreads();
   }
   // this (stream, map)'s re-VoxelGrid items, listed by size class (k_revox takes the largest
