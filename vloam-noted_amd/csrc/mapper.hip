@@ -1130,17 +1130,12 @@ __global__ void __launch_bounds__(CORR_THREADS) k_geom(MapperDev D, int round) {
     const float4 po = D.stack[m][(size_t)s * D.max_in + qi];
     int type = 0;
     double a[3] = {0, 0, 0}, b[3] = {0, 0, 0};
-    // the five neighbour positions loaded together with the acceptance test's (k_knn writes all
-    // five, -1 when the query failed; sharded, k_nn_merge writes the first and nn_xyz the points)
-    int ids[5];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) ids[j] = D.knn_id[j * D.knn_stride + rb + ridx];
-    if (ids[0] >= 0) {
+    if (D.knn_id[rb + ridx] >= 0) {
       const float4* lin = carena_base(D, s, m, F.arena_active[m]);
       float nb[5][3];
 #pragma unroll
       for (int j = 0; j < 5; ++j) {
-        const float4 p = D.sharded ? D.nn_xyz[j * D.knn_stride + rb + ridx] : lin[ids[j]];
+        const float4 p = D.sharded ? D.nn_xyz[j * D.knn_stride + rb + ridx] : lin[D.knn_id[j * D.knn_stride + rb + ridx]];
         nb[j][0] = p.x;
         nb[j][1] = p.y;
         nb[j][2] = p.z;
